@@ -1,0 +1,174 @@
+"""Throughput benchmark: samples/s (whole node) of the flagship training step.
+
+Metric (BASELINE.json): "samples/sec (whole node) synthetic datamodule at 1/2/4/8 MI355X;
+p50 step ms".  One sample = one dataset window (100 stocks x 60-day lookback x 3
+features, 30-day target).  Config: the reference defaults (`configs/config.yaml`):
+``datamodule=synthetic model=small loss=mse trainer=fast`` — LSTM H=64 L=2
+(51,074 params), fp32 parameters/activations (trainer precision ``32-true``),
+Adam + grad-norm clip 5.0 — random-init weights, synthetic data from the
+reference DGP generated on the device.  Every timed step is the full training
+step: batch gather, forward, fused loss, backward, RCCL gradient all-reduce
+(N > 1), clip + Adam, metric accumulation — replayed from the captured HIP graph
+exactly as ``train.py`` runs it.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Weak scaling: ``--batch`` windows per GPU per step (global batch = B * N).
+Prints exactly one JSON line (rank 0) on stdout.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+
+REFERENCE_SAMPLES_PER_S = 59.0  # reference-equivalent replica, model=small, loss=mse, B=1
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("MTA_BENCH_BATCH", "1")),
+                    help="windows per GPU per step (reference datamodule default: 1)")
+    ap.add_argument("--model", default="small")
+    ap.add_argument("--loss", default="mse")
+    ap.add_argument("--trainer", default="fast")
+    ap.add_argument("--matmul-precision", default="high", choices=["highest", "high", "medium"])
+    ap.add_argument("--backend", default="auto", choices=["auto", "torch"],
+                    help="torch = reference-equivalent PyTorch eager path (MIOpen LSTM) for A/B")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--n-samples", type=int, default=1_000_000, help="synthetic DGP days (reference: 1e6)")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from masters_thesis_amd.config import compose
+    from masters_thesis_amd.data import FinancialLstmDataModule
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import get_model_class, model_params_from_config
+    from masters_thesis_amd.parallel import dist as pdist
+
+    denv = pdist.init_distributed()
+    world = denv.world_size
+    if args.gpus != world and world > 1:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    dev = denv.device
+    torch.manual_seed(1234 + denv.rank)
+
+    cfg, _, _ = compose(REPO / "configs", "config", [
+        f"model={args.model}", f"loss={args.loss}", f"trainer={args.trainer}",
+        f"datamodule.batch_size={args.batch}", f"datamodule.n_samples={args.n_samples}"])
+    if args.backend == "torch":
+        cfg.model["backend"] = "torch"
+    t_data = time.perf_counter()
+    dm = FinancialLstmDataModule.from_config(cfg.datamodule, cache=False, device=dev, rank=denv.rank,
+                                             world_size=world)
+    dm.setup("fit")
+    log(f"[bench] rank {denv.rank}: {dm.n_windows} windows built on {dev} in {time.perf_counter() - t_data:.1f}s")
+
+    ModelClass = get_model_class(cfg.loss.module_class, cfg.model.get("arch", "lstm"))
+    model = ModelClass(**model_params_from_config(cfg))
+    trainer = Trainer(max_epochs=1, gradient_clip_val=cfg.trainer.gradient_clip_val, precision=cfg.trainer.precision,
+                      enable_progress_bar=False, enable_model_summary=False, logger=None, callbacks=[],
+                      use_hip_graphs=not args.no_graphs, matmul_precision=args.matmul_precision)
+    trainer._setup_env()
+    trainer._setup_model(model)
+    trainer._configure_optimizers(model)
+    model.train()
+
+    loader = dm.train_dataloader()
+
+    def batches():
+        ep = 0
+        while True:
+            loader.set_epoch(ep)
+            for b in loader:
+                if b[0].shape[0] == args.batch:
+                    yield b
+            ep += 1
+
+    it = batches()
+    for i in range(args.warmup):
+        trainer._run_train_step(next(it), i)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    evs = []
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if dev.type == "cuda":
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        trainer._run_train_step(next(it), args.warmup + i)
+        if dev.type == "cuda":
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            evs.append((e0, e1))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.all_reduce_max(elapsed, dev)
+    step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs else [elapsed * 1e3 / args.steps]
+    p50 = pdist.all_reduce_max(step_ms[len(step_ms) // 2], dev)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = args.batch * world * args.steps / elapsed
+    nonfinite = float(trainer._nonfinite.item()) if trainer._nonfinite is not None else 0.0
+    if denv.rank == 0:
+        log(f"[bench] p50 step {p50:.3f} ms, mean {ms_per_step:.3f} ms, graphs={'on' if trainer._graphs else 'off'}, "
+            f"nonfinite={nonfinite}, last loss={float(trainer.callback_metrics.get('loss', float('nan'))):.4g}")
+        rec = {
+            "metric": "samples/sec (whole node) synthetic datamodule; p50 step ms",
+            "value": round(value, 3),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "p50_step_ms": round(p50, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / REFERENCE_SAMPLES_PER_S, 3),
+            "dtype": "fp32" if cfg.trainer.precision == "32-true" else "bf16",
+            "data": "synthetic (reference DGP, generated on device), random-init weights",
+            "config": {
+                "model": f"FinancialLstm{args.loss.capitalize()} model={args.model} "
+                         f"(LSTM H={cfg.model.hidden_size} L={cfg.model.num_layers})",
+                "global_batch": args.batch * world,
+                "seq_len": int(cfg.datamodule.lookback_window),
+                "parallelism": f"dp{world}",
+                "per_gpu_batch_windows": args.batch,
+                "sequences_per_window": 100,
+                "trainer": args.trainer,
+                "precision": cfg.trainer.precision,
+                "matmul_precision": args.matmul_precision,
+                "backend": "hip" if args.backend == "auto" else "torch-eager",
+                "hip_graphs": not args.no_graphs,
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+// Shared device helpers for the masters_thesis_amd CDNA4 (gfx950) kernels.
+//
+// Everything here is written for MI355X directly: wave64, MFMA fragments of
+// v_mfma_f32_16x16x32_bf16 / v_mfma_f32_16x16x4_f32, bf16 round-to-nearest-even
+// conversion via the __bf16 type (lowers to v_cvt_pk_bf16_f32 on gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Matmul precision for fp32 recurrences, mirroring torch.set_float32_matmul_precision:
+//   PREC_F32    'highest' : exact f32-input MFMA (v_mfma_f32_16x16x4_f32, fmaf-chain numerics)
+//   PREC_BF16X3 'high'    : x = hi + lo split into two bf16, a*b ~= hi*hi + hi*lo + lo*hi (3 bf16 MFMAs,
+//                           ~16 mantissa bits per product, fp32 accumulate; > TF32, which cuDNN uses)
+//   PREC_BF16   'medium'  : single bf16 MFMA pass, fp32 accumulate (the reference's own setting,
+//                           train.py:13 set_float32_matmul_precision('medium'))
+enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2 };
+
+#define MTA_WAVE 64
+
+__device__ __forceinline__ float mta_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float mta_tanh(float x) {
+  // 2*sigmoid(2x) - 1: one v_exp_f32 + one v_rcp_f32, saturates cleanly at +-1
+  return 2.0f / (1.0f + __expf(-2.0f * x)) - 1.0f;
+}
+
+__device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)x;
+  lo = (__bf16)(x - (float)hi);
+}
+
+__device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x16x4f32(float a, float b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Wave-level sum (64 lanes) via DPP-friendly shuffles.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block-level sum for blockDim.x <= 1024; `scratch` needs blockDim.x/64 floats.
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}

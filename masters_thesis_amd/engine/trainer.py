@@ -1,0 +1,547 @@
+"""Training engine: fit / validate / test loops with Lightning-equivalent semantics.
+
+Reference behaviour (Lightning ``Trainer`` as configured in `train.py:169-198`):
+sanity validation (2 batches), per-epoch training with ``gradient_clip_val`` norm
+clipping, validation every ``check_val_every_n_epoch``, ``ModelCheckpoint`` and
+``LearningRateMonitor`` callbacks, ``ReduceLROnPlateau`` stepped at the validation
+frequency on ``loss/total/val`` (`src/model.py:156-172`), epoch-level logging of
+``self.log(..., on_epoch=True)`` values, ``trainer.test`` on the current weights.
+
+MI355X execution model:
+
+* one process per GPU (``parallel.dist``), gradients in one flat buffer,
+  one RCCL all-reduce per step (``parallel.ddp.FlatDDP``), metrics synced with
+  one fused all-reduce per epoch (fixes the rank-local monitor of SURVEY Q2);
+* the optimizer is the fused clip+Adam HIP kernel pair (``ops.optim.FusedAdam``),
+  swapped in for ``torch.optim.Adam/AdamW`` returned by ``configure_optimizers``;
+* after ``graph_warmup_steps`` eager steps, the train step (zero-grad, forward,
+  loss, backward, [all-reduce], clip+Adam, device-side metric accumulation) is
+  captured into a HIP graph and replayed for every later full batch; validation
+  and test steps are captured the same way.  The per-step host cost becomes one
+  graph launch; nothing reads back to the host until the epoch ends.
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+from contextlib import nullcontext
+from pathlib import Path
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ..metrics import Metric, sync_metrics
+from ..ops.optim import FlatParameters, FusedAdam
+from ..parallel import dist as pdist
+from ..parallel.ddp import FlatDDP
+from .callbacks import Callback, LearningRateMonitor, ModelCheckpoint, StepTimer
+from .checkpoint import (LIGHTNING_COMPAT_VERSION, atomic_save, capture_rng_states, load_checkpoint,
+                         restore_rng_states)
+from .schedulers import PlateauScheduler
+
+
+def _batch_size(batch) -> int:
+    return int(batch[0].shape[0]) if isinstance(batch, (list, tuple)) else int(batch.shape[0])
+
+
+class _CapturedStep:
+    """A captured HIP graph with static input buffers."""
+
+    def __init__(self, graph: "torch.cuda.CUDAGraph", static_in: Sequence[torch.Tensor], static_out: Any):
+        self.graph = graph
+        self.static_in = list(static_in)
+        self.static_out = static_out
+
+    def run(self, batch: Sequence[torch.Tensor]):
+        for s, b in zip(self.static_in, batch):
+            if s.data_ptr() != b.data_ptr():
+                s.copy_(b, non_blocking=True)
+        self.graph.replay()
+        return self.static_out
+
+
+class Trainer:
+    def __init__(self, max_epochs: int = 1000, gradient_clip_val: Optional[float] = None,
+                 precision: str = "32-true", enable_progress_bar: bool = True, enable_model_summary: bool = True,
+                 logger=None, callbacks: Optional[List[Callback]] = None, check_val_every_n_epoch: int = 1,
+                 num_sanity_val_steps: int = 2, accelerator: str = "auto", devices: Any = "auto",
+                 use_hip_graphs: bool = True, graph_warmup_steps: int = 2, matmul_precision: str = "high",
+                 limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
+                 limit_test_batches: Optional[int] = None, default_root_dir: str = ".",
+                 max_steps: int = -1, fail_at_step: Optional[int] = None, deterministic: bool = False,
+                 log_every_n_steps: int = 50):
+        self.max_epochs = int(max_epochs)
+        self.max_steps = int(max_steps)
+        self.gradient_clip_val = float(gradient_clip_val or 0.0)
+        self.precision = str(precision)
+        self.enable_progress_bar = enable_progress_bar
+        self.enable_model_summary = enable_model_summary
+        self.logger = logger
+        self.callbacks: List[Callback] = list(callbacks or [])
+        self.check_val_every_n_epoch = int(check_val_every_n_epoch or 1)
+        self.num_sanity_val_steps = int(num_sanity_val_steps)
+        self.accelerator = accelerator
+        self.use_hip_graphs = use_hip_graphs
+        self.graph_warmup_steps = max(1, int(graph_warmup_steps))
+        self.matmul_precision = matmul_precision
+        self.limit_train_batches = limit_train_batches
+        self.limit_val_batches = limit_val_batches
+        self.limit_test_batches = limit_test_batches
+        self.default_root_dir = default_root_dir
+        env_fail = os.environ.get("MTA_FAIL_AT_STEP")
+        self.fail_at_step = int(env_fail) if env_fail else fail_at_step
+        self.deterministic = deterministic
+        # state
+        self.current_epoch = 0
+        self.global_step = 0
+        self.callback_metrics: Dict[str, torch.Tensor] = {}
+        self.logged_metrics: Dict[str, float] = {}
+        self.sanity_checking = False
+        self.should_stop = False
+        self.num_val_batches = 0
+        self.optimizer: Optional[FusedAdam] = None
+        self.optimizer_name = "Adam"
+        self.scheduler: Optional[PlateauScheduler] = None
+        self.scheduler_cfg: Dict[str, Any] = {}
+        self.flat: Optional[FlatParameters] = None
+        self.ddp: Optional[FlatDDP] = None
+        self.denv = pdist.get_env()
+        self.device = torch.device("cpu")
+        self.model = None
+        self.datamodule = None
+        self._graphs: Dict[Tuple[str, int], _CapturedStep] = {}
+        self._eager_counts: Dict[Tuple[str, int], int] = {}
+        self.step_timer = StepTimer()
+        self.perf: Dict[str, float] = {}
+        self._nonfinite: Optional[torch.Tensor] = None
+        self._ckpt_to_resume: Optional[Dict[str, Any]] = None
+        self._graph_mode_active = False
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def is_global_zero(self) -> bool:
+        return self.denv.rank == 0
+
+    @property
+    def world_size(self) -> int:
+        return self.denv.world_size
+
+    @property
+    def checkpoint_callback(self) -> Optional[ModelCheckpoint]:
+        for c in self.callbacks:
+            if isinstance(c, ModelCheckpoint):
+                return c
+        return None
+
+    def _print(self, *a, **k) -> None:
+        if self.is_global_zero:
+            print(*a, **k, flush=True)
+
+    # ------------------------------------------------------------------ setup
+    def _setup_env(self) -> None:
+        want_cpu = self.accelerator == "cpu" or not torch.cuda.is_available()
+        self.denv = pdist.init_distributed(device="cpu" if want_cpu else None)
+        self.device = self.denv.device
+        if self.logger is not None and hasattr(self.logger, "rank"):
+            self.logger.rank = self.denv.rank
+        for c in self.callbacks:
+            if isinstance(c, ModelCheckpoint) and c.dirpath is None and self.logger is not None:
+                c.dirpath = str(Path(self.logger.log_dir) / "checkpoints")
+        if self.device.type == "cuda":
+            torch.backends.cudnn.benchmark = False
+
+    def _setup_model(self, model) -> None:
+        model.trainer = self
+        model.to(self.device)
+        model.matmul_precision = self._effective_matmul_precision()
+        self.model = model
+
+    def _effective_matmul_precision(self) -> str:
+        if self.precision.startswith("bf16"):
+            return "medium"
+        return self.matmul_precision
+
+    def _configure_optimizers(self, model) -> None:
+        conf = model.configure_optimizers()
+        opt, sched_cfg = conf, None
+        if isinstance(conf, dict):
+            opt, sched_cfg = conf["optimizer"], conf.get("lr_scheduler")
+        elif isinstance(conf, (list, tuple)):
+            opt = conf[0]
+        self.flat = FlatParameters(model.parameters(), device=self.device)
+        g = opt.param_groups[0]
+        adamw = isinstance(opt, torch.optim.AdamW)
+        if not isinstance(opt, (torch.optim.Adam, torch.optim.AdamW)) or g.get("amsgrad"):
+            raise NotImplementedError("the fused engine supports Adam / AdamW optimizers")
+        self.optimizer = FusedAdam(self.flat, lr=g["lr"], betas=g["betas"], eps=g["eps"],
+                                   weight_decay=g["weight_decay"], adamw=adamw)
+        self.optimizer_name = "AdamW" if adamw else "Adam"
+        self.scheduler_cfg = {}
+        self.scheduler = None
+        if sched_cfg is not None:
+            sch = sched_cfg["scheduler"] if isinstance(sched_cfg, dict) else sched_cfg
+            if isinstance(sch, torch.optim.lr_scheduler.ReduceLROnPlateau):
+                self.scheduler = PlateauScheduler.from_torch(sch, self.optimizer)
+            else:
+                raise NotImplementedError("only ReduceLROnPlateau schedulers are supported")
+            self.scheduler_cfg = {
+                "monitor": sched_cfg.get("monitor", "loss/total/val") if isinstance(sched_cfg, dict) else None,
+                "interval": sched_cfg.get("interval", "epoch") if isinstance(sched_cfg, dict) else "epoch",
+                "frequency": int(sched_cfg.get("frequency", 1)) if isinstance(sched_cfg, dict) else 1,
+            }
+        self.ddp = FlatDDP(self.flat)
+        self.ddp.broadcast_parameters()
+        self._nonfinite = torch.zeros(1, device=self.device)
+
+    def _model_summary(self, model) -> None:
+        if not (self.enable_model_summary and self.is_global_zero):
+            return
+        rows = []
+        for name, mod in model.named_children():
+            n = sum(p.numel() for p in mod.parameters())
+            rows.append((name, type(mod).__name__, n))
+        total = sum(p.numel() for p in model.parameters())
+        train = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        print("  | Name" + " " * 12 + "| Type" + " " * 26 + "| Params")
+        for i, (n, t, c) in enumerate(rows):
+            print(f"{i} | {n:<16}| {t:<30}| {c:,}")
+        print(f"{train:,} Trainable params\n{total - train:,} Non-trainable params\n{total:,} Total params")
+        print(f"{total * 4 / 1e6:.3f} Total estimated model params size (MB)", flush=True)
+
+    # ------------------------------------------------------------------ step bodies
+    def _train_body(self, batch, batch_idx: int):
+        model, opt = self.model, self.optimizer
+        self.flat.grad.zero_()
+        loss = model.training_step(batch, batch_idx)
+        loss.backward()
+        if self._capture_allreduce():
+            self.ddp.allreduce_grads()
+        if not self._split_optimizer():
+            opt.step(self.gradient_clip_val, self.ddp.grad_scale)
+            self._nonfinite.add_((~torch.isfinite(opt.grad_norm)).float())
+        return loss
+
+    def _capture_allreduce(self) -> bool:
+        return self.ddp.world == 1 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1" or \
+            not self._graph_mode_active
+
+    def _split_optimizer(self) -> bool:
+        # with world > 1 the all-reduce runs eagerly between the fwd/bwd graph and the optimizer
+        return self._graph_mode_active and not self._capture_allreduce()
+
+    def _graphs_enabled(self) -> bool:
+        return self.use_hip_graphs and self.device.type == "cuda"
+
+    def _run_train_step(self, batch, batch_idx: int):
+        B = _batch_size(batch)
+        key = ("train", B)
+        self.model._current_batch_size = B
+        if not self._graphs_enabled():
+            self._graph_mode_active = False
+            return self._train_body(batch, batch_idx)
+        g = self._graphs.get(key)
+        if g is None:
+            n = self._eager_counts.get(key, 0)
+            if n < self.graph_warmup_steps:
+                self._eager_counts[key] = n + 1
+                self._graph_mode_active = False
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    out = self._train_body(batch, batch_idx)
+                torch.cuda.current_stream().wait_stream(side)
+                return out
+            g = self._capture("train", batch, lambda b: self._train_body(b, batch_idx))
+            self._graphs[key] = g
+        out = g.run(batch)
+        if self._split_optimizer():
+            self.ddp.allreduce_grads()
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
+            self._nonfinite.add_((~torch.isfinite(self.optimizer.grad_norm)).float())
+        return out
+
+    def _capture(self, stage: str, batch, body: Callable) -> _CapturedStep:
+        self._graph_mode_active = True
+        static_in = [t.clone() for t in batch]
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = body(static_in)
+        return _CapturedStep(graph, static_in, out)
+
+    def _run_eval_step(self, stage: str, batch, batch_idx: int):
+        model = self.model
+        B = _batch_size(batch)
+        model._current_batch_size = B
+        fn = model.validation_step if stage == "val" else model.test_step
+        if not self._graphs_enabled() or stage == "test_no_graph":
+            return fn(batch, batch_idx)
+        key = (stage, B)
+        g = self._graphs.get(key)
+        if g is None:
+            n = self._eager_counts.get(key, 0)
+            if n < 1:
+                self._eager_counts[key] = n + 1
+                return fn(batch, batch_idx)
+            g = self._capture(stage, batch, lambda b: fn(b, batch_idx))
+            self._graphs[key] = g
+        return g.run(batch)
+
+    # ------------------------------------------------------------------ epoch helpers
+    def _metrics_of(self, stage: str) -> Dict[str, Metric]:
+        return self.model.logged_metrics(stage)
+
+    def _compute_stage_metrics(self, stage: str) -> Dict[str, torch.Tensor]:
+        ms = self._metrics_of(stage)
+        sync_metrics(ms.values())
+        out = {}
+        for name, m in ms.items():
+            try:
+                out[name] = m.compute().detach().float().cpu()
+            except ZeroDivisionError:  # pragma: no cover
+                continue
+        return out
+
+    def _reset_stage_metrics(self, stage: str) -> None:
+        for m in self._metrics_of(stage).values():
+            m.reset()
+
+    def log_metrics(self, metrics: Dict[str, float], step: int) -> None:
+        vals = {k: float(v) for k, v in metrics.items()}
+        self.logged_metrics.update(vals)
+        if self.logger is not None and self.is_global_zero:
+            self.logger.log_metrics(vals, step)
+
+    def _limit(self, n: int, lim) -> int:
+        if lim is None:
+            return n
+        if isinstance(lim, float) and lim <= 1.0:
+            return max(1, int(n * lim))
+        return min(n, int(lim))
+
+    # ------------------------------------------------------------------ loops
+    def _run_eval(self, stage: str, loader, limit=None) -> Dict[str, torch.Tensor]:
+        model = self.model
+        model.eval()
+        model._stage = "val" if stage == "sanity" else stage
+        n = self._limit(len(loader), limit)
+        with torch.no_grad():
+            for i, batch in enumerate(loader):
+                if i >= n:
+                    break
+                self._run_eval_step(model._stage, batch, i)
+        res = self._compute_stage_metrics(model._stage)
+        self._reset_stage_metrics(model._stage)
+        model.train()
+        model._stage = "train"
+        return res
+
+    def fit(self, model, datamodule=None, ckpt_path: Optional[str] = None, train_dataloaders=None,
+            val_dataloaders=None) -> None:
+        self._setup_env()
+        dm = datamodule
+        self.datamodule = dm
+        if dm is not None:
+            dm.rank, dm.world_size, dm.device = self.denv.rank, self.denv.world_size, self.device
+            if self.denv.local_rank == 0:
+                dm.prepare_data()
+            pdist.barrier()
+            dm.setup("fit")
+        self._setup_model(model)
+        self._model_summary(model)
+        self._configure_optimizers(model)
+        start_epoch = 0
+        if ckpt_path:
+            start_epoch = self._restore(ckpt_path)
+        for c in self.callbacks:
+            c.on_fit_start(self, model)
+        train_loader = train_dataloaders or dm.train_dataloader()
+        val_loader = val_dataloaders or dm.val_dataloader()
+        self.num_val_batches = self._limit(len(val_loader), self.limit_val_batches)
+
+        # sanity check (Lightning default num_sanity_val_steps=2)
+        if self.num_sanity_val_steps > 0 and start_epoch == 0:
+            self.sanity_checking = True
+            self._run_eval("sanity", val_loader, limit=self.num_sanity_val_steps)
+            self.sanity_checking = False
+
+        samples_per_batch = None
+        for epoch in range(start_epoch, self.max_epochs):
+            self.current_epoch = epoch
+            model._stage = "train"
+            model.train()
+            model.on_train_epoch_start()
+            for c in self.callbacks:
+                c.on_train_epoch_start(self, model)
+            if hasattr(train_loader, "set_epoch"):
+                train_loader.set_epoch(epoch)
+            n_batches = self._limit(len(train_loader), self.limit_train_batches)
+            t_epoch = time.perf_counter()
+            ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
+            host_ms: List[float] = []
+            for i, batch in enumerate(train_loader):
+                if i >= n_batches or (0 <= self.max_steps <= self.global_step):
+                    break
+                if self.fail_at_step is not None and self.global_step == self.fail_at_step:
+                    raise RuntimeError(f"fault injection: MTA_FAIL_AT_STEP={self.fail_at_step}")
+                samples_per_batch = _batch_size(batch)
+                if self.device.type == "cuda":
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                else:
+                    t0 = time.perf_counter()
+                self._run_train_step(batch, i)
+                if self.device.type == "cuda":
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e1.record()
+                    ev.append((e0, e1))
+                else:
+                    host_ms.append((time.perf_counter() - t0) * 1e3)
+                self.global_step += 1
+                if self.enable_progress_bar and self.is_global_zero and (i % 500 == 0 or i == n_batches - 1):
+                    sys.stdout.write(f"\rEpoch {epoch}: {i + 1}/{n_batches}")
+                    sys.stdout.flush()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+                host_ms = [a.elapsed_time(b) for a, b in ev[self.graph_warmup_steps + 1:]] or \
+                    [a.elapsed_time(b) for a, b in ev]
+            wall = time.perf_counter() - t_epoch
+            if self.enable_progress_bar and self.is_global_zero:
+                sys.stdout.write("\n")
+            perf = self.step_timer.summarize(host_ms, samples_per_batch or 1, self.world_size)
+            perf["perf/epoch_wall_s"] = wall
+            self.perf = perf
+            if self._nonfinite is not None and float(self._nonfinite.item()) > 0:
+                self._print(f"WARNING: {int(self._nonfinite.item())} step(s) with a non-finite gradient norm")
+                self._nonfinite.zero_()
+
+            train_metrics = self._compute_stage_metrics("train")
+            self._reset_stage_metrics("train")
+            self.callback_metrics.update(train_metrics)
+            log = {k: float(v) for k, v in train_metrics.items()}
+            log["epoch"] = float(epoch)
+            log.update(perf)
+            self.log_metrics(log, step=max(self.global_step - 1, 0))
+
+            if (epoch + 1) % self.check_val_every_n_epoch == 0 and self.num_val_batches > 0:
+                val_metrics = self._run_eval("val", val_loader, limit=self.limit_val_batches)
+                self.callback_metrics.update(val_metrics)
+                vlog = {k: float(v) for k, v in val_metrics.items()}
+                vlog["epoch"] = float(epoch)
+                self.log_metrics(vlog, step=max(self.global_step - 1, 0))
+                for c in self.callbacks:
+                    c.on_validation_end(self, model)
+            model.on_train_epoch_end()
+            for c in self.callbacks:
+                c.on_train_epoch_end(self, model)
+            self._step_scheduler(epoch)
+            summary = " ".join(f"{k}={float(v):.6g}" for k, v in self.callback_metrics.items())
+            self._print(f"[epoch {epoch}] {summary} | step p50 {perf.get('perf/step_ms_p50', 0):.3f} ms, "
+                        f"{perf.get('perf/samples_per_s', 0):.1f} samples/s")
+            if self.should_stop or (0 <= self.max_steps <= self.global_step):
+                break
+        for c in self.callbacks:
+            c.on_fit_end(self, model)
+        if self.logger is not None:
+            self.logger.finalize()
+
+    def _step_scheduler(self, epoch: int) -> None:
+        if self.scheduler is None:
+            return
+        freq = self.scheduler_cfg.get("frequency", 1)
+        if (epoch + 1) % freq != 0:
+            return
+        mon = self.scheduler_cfg.get("monitor")
+        if mon not in self.callback_metrics:
+            raise KeyError(f"ReduceLROnPlateau conditioned on metric {mon} which is not available. "
+                           f"Available metrics are: {sorted(self.callback_metrics)}")
+        self.scheduler.step(float(self.callback_metrics[mon]))
+
+    def validate(self, model, datamodule=None) -> Dict[str, float]:
+        if self.model is None:
+            self._setup_env()
+            self._setup_model(model)
+        dm = datamodule or self.datamodule
+        if not dm.splits:
+            dm.setup("fit")
+        res = self._run_eval("val", dm.val_dataloader(), self.limit_val_batches)
+        return {k: float(v) for k, v in res.items()}
+
+    def test(self, model, datamodule=None) -> List[Dict[str, float]]:
+        if self.model is None or self.model is not model:
+            self._setup_env()
+            self._setup_model(model)
+        dm = datamodule or self.datamodule
+        if dm is not None:
+            dm.rank, dm.world_size, dm.device = self.denv.rank, self.denv.world_size, self.device
+            if not dm.splits or dm.dataset is None:
+                dm.setup("test")
+        loader = dm.test_dataloader()
+        model.eval()
+        model._stage = "test"
+        model.on_test_start()
+        n = self._limit(len(loader), self.limit_test_batches)
+        with torch.no_grad():
+            for i, batch in enumerate(loader):
+                if i >= n:
+                    break
+                self._run_eval_step("test", batch, i)
+        # sync every test-time Metric (logged or attribute) across ranks before on_test_end
+        test_metrics = list(self._metrics_of("test").values())
+        test_metrics += [m for name, m in model.named_children() if isinstance(m, Metric) and name.startswith("test")]
+        sync_metrics(test_metrics)
+        model.on_test_end()
+        res = {k: float(v) for k, v in self._compute_stage_metrics("test").items()}
+        self._reset_stage_metrics("test")
+        model._stage = "train"
+        if res:
+            self.log_metrics(res, step=self.global_step)
+        return [res]
+
+    # ------------------------------------------------------------------ checkpointing
+    def checkpoint_dict(self) -> Dict[str, Any]:
+        model = self.model
+        sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+        ck = {
+            "epoch": self.current_epoch,
+            "global_step": self.global_step,
+            "pytorch-lightning_version": LIGHTNING_COMPAT_VERSION,
+            "state_dict": sd,
+            "loops": {"fit_loop": {"epoch_progress": {"current": {"completed": self.current_epoch + 1}},
+                                   "epoch_loop.state_dict": {"_batches_that_stepped": self.global_step}}},
+            "callbacks": {c.state_key: c.state_dict() for c in self.callbacks},
+            "optimizer_states": [self.optimizer.state_dict()] if self.optimizer else [],
+            "lr_schedulers": [self.scheduler.state_dict()] if self.scheduler else [],
+            "hparams_name": "kwargs",
+            "hyper_parameters": dict(model.hparams),
+            "rng_states": capture_rng_states(),
+            "mta": {"world_size": self.world_size, "precision": self.precision,
+                    "matmul_precision": self._effective_matmul_precision()},
+        }
+        model.on_save_checkpoint(ck)
+        return ck
+
+    def save_checkpoint(self, path) -> None:
+        ck = self.checkpoint_dict() if self.is_global_zero else None
+        if self.is_global_zero:
+            atomic_save(ck, path)
+        pdist.barrier()
+
+    def _restore(self, path) -> int:
+        ck = load_checkpoint(path, map_location="cpu")
+        self.model.load_state_dict(ck["state_dict"])
+        if ck.get("optimizer_states"):
+            self.optimizer.load_state_dict(ck["optimizer_states"][0])
+        if ck.get("lr_schedulers") and self.scheduler is not None:
+            self.scheduler.load_state_dict(ck["lr_schedulers"][0])
+        cbs = ck.get("callbacks", {})
+        for c in self.callbacks:
+            if c.state_key in cbs:
+                c.load_state_dict(cbs[c.state_key])
+        if "rng_states" in ck:
+            restore_rng_states(ck["rng_states"])
+        self.global_step = int(ck.get("global_step", 0))
+        self._print(f"Restored training state from {path} (epoch {ck['epoch']}, step {self.global_step})")
+        return int(ck["epoch"]) + 1

@@ -1,0 +1,229 @@
+"""LSTM alpha/beta encoder models (reference: `src/model.py:72-331`).
+
+``FinancialLstm{Mse,Nll,Combined}`` keep the reference constructor signature,
+hyper-parameters, ``state_dict`` keys (``lstm.weight_ih_l{k}`` ... ``beta_head.bias``),
+logged tags (``loss/{mse,nll,total}/{train,val}``), optimizer (Adam with coupled
+L2, ReduceLROnPlateau(min, 0.5, 2) monitored on ``loss/total/val`` at the
+validation frequency) and test hooks (MAE + NLL, `src/model.py:111-147`).
+
+What changes is the compute path on MI355X: the encoder is the persistent HIP
+LSTM (``ops.lstm``), the two heads produce one (N, 2) ``[alpha | beta]`` tile, and
+every decoder/loss variant is ONE fused HIP kernel (``ops.losses``) that returns
+the MSE, NLL and MAE plus their analytic gradients — no K x K Woodbury matrix, no
+LU ``logdet``.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+from torch import Tensor
+
+from ..data.common import inverse_returns_covariance
+from ..engine.module import LightningModule
+from ..metrics import MeanAbsoluteError, MeanSquaredError, MultivariateGaussianNLLLoss
+from ..ops import lstm as lstm_op
+from ..ops.losses import decoder_losses
+
+
+class LSTMStack(torch.nn.Module):
+    """Parameter container with ``torch.nn.LSTM``'s names/shapes/init (batch_first)."""
+
+    def __init__(self, input_size: int, hidden_size: int, num_layers: int = 1, dropout: float = 0.0):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        self.dropout = float(dropout)
+        self.batch_first = True
+        self._flat_names = []
+        for l in range(num_layers):
+            fin = input_size if l == 0 else hidden_size
+            for name, shape in ((f"weight_ih_l{l}", (4 * hidden_size, fin)), (f"weight_hh_l{l}", (4 * hidden_size, hidden_size)),
+                                (f"bias_ih_l{l}", (4 * hidden_size,)), (f"bias_hh_l{l}", (4 * hidden_size,))):
+                self.register_parameter(name, torch.nn.Parameter(torch.empty(shape)))
+                self._flat_names.append(name)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        # nn.LSTM init: U(-1/sqrt(H), 1/sqrt(H)) for every weight and bias
+        k = 1.0 / self.hidden_size ** 0.5
+        for name in self._flat_names:
+            torch.nn.init.uniform_(getattr(self, name), -k, k)
+
+    @property
+    def flat_weights(self):
+        return [getattr(self, n) for n in self._flat_names]
+
+    def extra_repr(self) -> str:
+        return (f"{self.input_size}, {self.hidden_size}, num_layers={self.num_layers}, batch_first=True, "
+                f"dropout={self.dropout}")
+
+    def last_hidden(self, x: Tensor, precision=None, backend: str = "auto") -> Tensor:
+        if backend == "torch" and x.is_cuda:
+            H, N = self.hidden_size, x.shape[0]
+            h0 = x.new_zeros(self.num_layers, N, H)
+            out, _, _ = torch._VF.lstm(x, (h0, h0), self.flat_weights, True, self.num_layers, self.dropout,
+                                       self.training, False, True)
+            return out[:, -1, :]
+        return lstm_op.lstm_last_hidden(x, self.flat_weights, self.num_layers, self.dropout if self.num_layers > 1
+                                        else 0.0, self.training, precision)
+
+
+class FinancialLstm(LightningModule):
+    def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
+                 learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
+                 nll_mode: str = "reference", optimizer: str = "adam"):
+        super().__init__()
+        self.lstm = LSTMStack(input_size, hidden_size, num_layers, dropout if num_layers > 1 else 0)
+        self.alpha_head = torch.nn.Linear(hidden_size, 1)
+        self.beta_head = torch.nn.Linear(hidden_size, 1)
+        self.test_mae = MeanAbsoluteError()
+        self.test_nll = MultivariateGaussianNLLLoss()
+        self.test_results = None
+        self.backend = backend
+        self.nll_mode = nll_mode
+        self.optimizer_kind = optimizer
+        self.matmul_precision = "high"
+        # defaults for direct (non-subclass) use; subclasses overwrite via save_hyperparameters
+        self._hparams.update(dict(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers,
+                                  dropout=dropout, learning_rate=learning_rate, weight_decay=weight_decay))
+
+    # ---- forward ---------------------------------------------------------------------
+    def encode(self, x: Tensor) -> Tensor:
+        return self.lstm.last_hidden(x, self.matmul_precision, self.backend)
+
+    def heads(self, h: Tensor) -> Tensor:
+        """``[alpha | beta]`` as one (N, 2) tile (two Linear(H,1) heads, `src/model.py:96-97,107-108`)."""
+        w = torch.cat([self.alpha_head.weight, self.beta_head.weight], 0)
+        b = torch.cat([self.alpha_head.bias, self.beta_head.bias], 0)
+        return torch.addmm(b, h, w.t())
+
+    def forward(self, lstm_input: Tensor) -> Tuple[Tensor, Tensor]:
+        ab = self.heads(self.encode(lstm_input))
+        return ab[:, 0:1], ab[:, 1:2]
+
+    # ---- batch plumbing (`src/model.py:120-128`) ------------------------------------------
+    @staticmethod
+    def _unpack(batch):
+        context = batch[0].flatten(0, 1)  # (B*K, T, F)
+        target = batch[1].flatten(0, 1)   # (B*K, n, 4)
+        factor = batch[2]                 # (B, 2)
+        inv_psi = batch[3].flatten(0, 1)  # (B*K,)
+        return context, target, factor, inv_psi, int(batch[0].shape[0])
+
+    def _losses(self, batch, want_nll: bool):
+        context, target, factor, inv_psi, B = self._unpack(batch)
+        ab = self.heads(self.encode(context))
+        mse, nll, mae = decoder_losses(ab, target, factor, inv_psi, batch_windows=B, want_nll=want_nll,
+                                       nll_mode=self.nll_mode)
+        return mse, nll, mae, target.shape[0] * target.shape[1]
+
+    # ---- test hooks (`src/model.py:111-147`) ---------------------------------------------
+    def on_test_start(self):
+        self.test_results = {"test_loss": {"mae": None, "nll": None}}
+        self.test_mae.reset()
+        self.test_nll.reset()
+
+    def test_step(self, batch, batch_idx):
+        mse, nll, mae, count = self._losses(batch, want_nll=True)
+        self.test_mae.update_from(mae * count, count)
+        self.test_nll.update_from(nll)
+
+    def on_test_end(self):
+        self.test_results["test_loss"]["mae"] = float(self.test_mae.compute().cpu().item())
+        self.test_results["test_loss"]["nll"] = float(self.test_nll.compute().cpu().item())
+
+    # ---- optimisation (`src/model.py:149-173`) ------------------------------------------------
+    def configure_optimizers(self):
+        cls = torch.optim.AdamW if self.optimizer_kind == "adamw" else torch.optim.Adam
+        optimizer = cls(self.parameters(), lr=self.hparams.learning_rate, weight_decay=self.hparams.weight_decay)
+        scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=0.5, patience=2)
+        frequency = getattr(self.trainer, "check_val_every_n_epoch", 1) if self.trainer is not None else 1
+        return {"optimizer": optimizer,
+                "lr_scheduler": {"scheduler": scheduler, "monitor": "loss/total/val", "interval": "epoch",
+                                 "frequency": frequency}}
+
+    # ---- dense reference path (parity oracle: the reference's exact math) ------------------------
+    def reference_nll(self, batch) -> Tensor:
+        context, target, factor, inv_psi, _ = self._unpack(batch)
+        alpha, beta = self(context)
+        fac = factor.flatten(0, 1)
+        r_mean = alpha + beta * fac[0]
+        r_inv_cov = inverse_returns_covariance(beta, torch.diag(inv_psi), fac[1])
+        return MultivariateGaussianNLLLoss.multivariate_gaussian_nll_loss(r_mean, r_inv_cov, target[:, :, 0])
+
+
+class FinancialLstmMse(FinancialLstm):
+    def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
+                 learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
+                 nll_mode: str = "reference", optimizer: str = "adam"):
+        super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
+                         nll_mode=nll_mode, optimizer=optimizer)
+        self.save_hyperparameters()
+        self.train_metric = MeanSquaredError()
+        self.val_metric = MeanSquaredError()
+
+    def training_step(self, batch, batch_idx):
+        mse, _, _, count = self._losses(batch, want_nll=False)
+        self.train_metric.update_from(mse.detach() * count, count)
+        self.log("loss/mse/train", self.train_metric, on_step=False, on_epoch=True)
+        self.log("loss/total/train", mse, on_step=False, on_epoch=True)
+        return mse
+
+    def validation_step(self, batch, batch_idx):
+        mse, _, _, count = self._losses(batch, want_nll=False)
+        self.val_metric.update_from(mse.detach() * count, count)
+        self.log("loss/mse/val", self.val_metric, on_step=False, on_epoch=True)
+        self.log("loss/total/val", mse, on_step=False, on_epoch=True)
+
+
+class FinancialLstmNll(FinancialLstm):
+    def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
+                 learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
+                 nll_mode: str = "reference", optimizer: str = "adam"):
+        super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
+                         nll_mode=nll_mode, optimizer=optimizer)
+        self.save_hyperparameters()
+        self.train_metric = MultivariateGaussianNLLLoss()
+        self.val_metric = MultivariateGaussianNLLLoss()
+
+    def training_step(self, batch, batch_idx):
+        _, nll, _, _ = self._losses(batch, want_nll=True)
+        self.train_metric.update_from(nll)
+        self.log("loss/nll/train", self.train_metric, on_step=False, on_epoch=True)
+        self.log("loss/total/train", nll, on_step=False, on_epoch=True)
+        return nll
+
+    def validation_step(self, batch, batch_idx):
+        _, nll, _, _ = self._losses(batch, want_nll=True)
+        self.val_metric.update_from(nll)
+        self.log("loss/nll/val", self.val_metric, on_step=False, on_epoch=True)
+        self.log("loss/total/val", nll, on_step=False, on_epoch=True)
+
+
+class FinancialLstmCombined(FinancialLstm):
+    def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
+                 learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,
+                 backend: str = "auto", nll_mode: str = "reference", optimizer: str = "adam"):
+        super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
+                         nll_mode=nll_mode, optimizer=optimizer)
+        self.save_hyperparameters()
+        self.train_mse = MeanSquaredError()
+        self.train_nll = MultivariateGaussianNLLLoss()
+        self.val_mse = MeanSquaredError()
+        self.val_nll = MultivariateGaussianNLLLoss()
+
+    def _step(self, batch, mse_m, nll_m, stage: str):
+        mse, nll, _, count = self._losses(batch, want_nll=True)
+        mse_m.update_from(mse.detach() * count, count)
+        nll_m.update_from(nll)
+        self.log(f"loss/mse/{stage}", mse_m, on_step=False, on_epoch=True)
+        self.log(f"loss/nll/{stage}", nll_m, on_step=False, on_epoch=True)
+        loss = nll + self.hparams.mse_weight * mse
+        self.log(f"loss/total/{stage}", loss, on_step=False, on_epoch=True)
+        return loss
+
+    def training_step(self, batch, batch_idx):
+        return self._step(batch, self.train_mse, self.train_nll, "train")
+
+    def validation_step(self, batch, batch_idx):
+        self._step(batch, self.val_mse, self.val_nll, "val")

@@ -1,0 +1,167 @@
+"""Numerics of the HIP kernels against plain PyTorch fp64 references (run on the MI355X box).
+
+Every test asserts that the native extension is the code path that ran (no silent
+eager fallback): ``masters_thesis_amd._C`` must be importable and the ops must be
+dispatched to it for CUDA tensors.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from masters_thesis_amd.ops import _lib
+
+    assert _lib.lib(required=True) is not None
+    assert not _lib.fallback_allowed()
+
+
+def _lstm_weights(F, H, L, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    k = 1.0 / math.sqrt(H)
+    ws = []
+    for l in range(L):
+        fin = F if l == 0 else H
+        for shape in ((4 * H, fin), (4 * H, H), (4 * H,), (4 * H,)):
+            ws.append((torch.rand(shape, generator=g) * 2 - 1) * k)
+    return ws
+
+
+def _ref_lstm(x, ws, L):
+    """fp64 CPU reference via the nn.LSTM kernel."""
+    x64 = x.detach().double().cpu().requires_grad_(True)
+    w64 = [w.detach().double().cpu().requires_grad_(True) for w in ws]
+    N, H = x.shape[0], ws[1].shape[1]
+    h0 = torch.zeros(L, N, H, dtype=torch.float64)
+    out, _, _ = torch._VF.lstm(x64, (h0, h0), w64, True, L, 0.0, False, False, True)
+    return out[:, -1], x64, w64
+
+
+TOLS = {"highest": 2e-5, "high": 3e-4, "medium": 3e-2}
+
+
+@pytest.mark.parametrize("prec", ["highest", "high", "medium"])
+@pytest.mark.parametrize("N,T,F,H,L", [(100, 60, 3, 64, 2), (37, 20, 5, 64, 1), (40, 15, 3, 32, 3),
+                                       (33, 12, 64, 128, 2), (300, 60, 3, 64, 4)])
+def test_lstm_forward_backward(prec, N, T, F, H, L):
+    from masters_thesis_amd.ops.lstm import lstm_last_hidden
+
+    torch.manual_seed(1)
+    x = torch.randn(N, T, F)
+    ws = _lstm_weights(F, H, L)
+    R = torch.randn(N, H)
+    ref, x64, w64 = _ref_lstm(x, ws, L)
+    (ref * R.double()).sum().backward()
+
+    xg = x.to(DEV).requires_grad_(True)
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    out = lstm_last_hidden(xg, wg, L, 0.0, True, prec)
+    (out * R.to(DEV)).sum().backward()
+    tol = TOLS[prec]
+    scale = ref.abs().max().item()
+    err = (out.double().cpu() - ref.detach()).abs().max().item()
+    assert err <= tol * max(scale, 1.0), f"forward err {err} (scale {scale})"
+    for name, a, b in [("x", xg.grad, x64.grad)] + [(f"w{i}", wg[i].grad, w64[i].grad) for i in range(len(ws))]:
+        sc = b.abs().max().item()
+        e = (a.double().cpu() - b).abs().max().item()
+        assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad {name}: err {e} (scale {sc})"
+
+
+def test_lstm_dropout_path():
+    from masters_thesis_amd.ops.lstm import lstm_last_hidden
+
+    torch.manual_seed(2)
+    x = torch.randn(64, 30, 3, device=DEV, requires_grad=True)
+    ws = [w.to(DEV).requires_grad_(True) for w in _lstm_weights(3, 64, 3)]
+    out_eval = lstm_last_hidden(x, ws, 3, 0.3, False, "highest")
+    out_nodrop = lstm_last_hidden(x, ws, 3, 0.0, True, "highest")
+    torch.testing.assert_close(out_eval, out_nodrop, rtol=0, atol=0)
+    out = lstm_last_hidden(x, ws, 3, 0.3, True, "highest")
+    assert not torch.allclose(out, out_eval)
+    out.sum().backward()
+    assert all(torch.isfinite(w.grad).all() for w in ws)
+
+
+@pytest.mark.parametrize("B,mode", [(1, "reference"), (3, "reference"), (3, "per_window")])
+def test_decoder_losses_match_dense_reference(B, mode):
+    from masters_thesis_amd.data.common import gaussian_nll_dense, inverse_returns_covariance
+    from masters_thesis_amd.ops.losses import decoder_losses
+
+    torch.manual_seed(3)
+    K, n = 100, 30
+    N = B * K
+    ab = torch.randn(N, 2, dtype=torch.float64) * 0.3 + torch.tensor([0.0, 1.0], dtype=torch.float64)
+    y = torch.randn(N, n, 4, dtype=torch.float64)
+    factor = torch.stack([torch.randn(B) * 0.1, torch.rand(B) * 0.5 + 0.2], -1).double()
+    inv_psi = (torch.rand(N) * 5 + 1).double()
+
+    # fp64 dense reference (exactly the reference's math, src/model.py:45-69)
+    ab_r = ab.clone().requires_grad_(True)
+    r, rm = y[..., 0], y[..., 1]
+    pred = ab_r[:, :1] + ab_r[:, 1:] * rm
+    mse_r = ((pred - r) ** 2).mean()
+    if mode == "reference":
+        fm, fv = factor.flatten()[0], factor.flatten()[1]
+        nll_r = gaussian_nll_dense(ab_r[:, :1] + ab_r[:, 1:] * fm,
+                                   inverse_returns_covariance(ab_r[:, 1:], torch.diag(inv_psi), fv), r)
+    else:
+        nll_r = 0
+        for w in range(B):
+            sl = slice(w * K, (w + 1) * K)
+            fm, fv = factor[w, 0], factor[w, 1]
+            nll_r = nll_r + gaussian_nll_dense(ab_r[sl, :1] + ab_r[sl, 1:] * fm,
+                                               inverse_returns_covariance(ab_r[sl, 1:], torch.diag(inv_psi[sl]), fv),
+                                               r[sl])
+    (g_ref,) = torch.autograd.grad(mse_r * 0.7 + nll_r * 1.3, ab_r)
+
+    abg = ab.float().to(DEV).requires_grad_(True)
+    mse, nll, mae = decoder_losses(abg, y.float().to(DEV), factor.float().to(DEV), inv_psi.float().to(DEV),
+                                   batch_windows=B, nll_mode=mode)
+    (mse * 0.7 + nll * 1.3).backward()
+    assert abs(mse.item() - mse_r.item()) <= 1e-5 * abs(mse_r.item())
+    assert abs(nll.item() - nll_r.item()) <= 2e-5 * abs(nll_r.item()) + 1e-3
+    assert abs(mae.item() - (pred - r).abs().mean().item()) <= 1e-5
+    err = (abg.grad.double().cpu() - g_ref).abs().max().item()
+    assert err <= 2e-4 * g_ref.abs().max().item(), err
+
+
+def test_fused_adam_matches_torch_adam_with_clipping():
+    from masters_thesis_amd.ops.optim import FlatParameters, FusedAdam
+
+    torch.manual_seed(4)
+    shapes = [(256, 3), (256, 64), (256,), (1, 64), (1,)]
+    ref = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+    mine = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    opt_ref = torch.optim.Adam(ref, lr=3e-3, weight_decay=1e-2)
+    flat = FlatParameters(mine)
+    opt = FusedAdam(flat, lr=3e-3, weight_decay=1e-2)
+    for step in range(5):
+        grads = [torch.randn(s, device=DEV) * (10 if step % 2 else 0.1) for s in shapes]
+        for p, g in zip(ref, grads):
+            p.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt_ref.step()
+        flat.zero_grad()
+        for p, g in zip(mine, grads):
+            p.grad.copy_(g)
+        opt.step(max_norm=1.0)
+    for a, b in zip(mine, ref):
+        torch.testing.assert_close(a.detach(), b.detach(), rtol=2e-5, atol=2e-6)
+    assert float(opt.step_t.item()) == 5.0
+
+
+def test_flat_grads_survive_backward():
+    from masters_thesis_amd.ops.optim import FlatParameters
+
+    lin = torch.nn.Linear(8, 4).to(DEV)
+    flat = FlatParameters(lin.parameters())
+    ptr = lin.weight.grad.data_ptr()
+    lin(torch.randn(3, 8, device=DEV)).sum().backward()
+    assert lin.weight.grad.data_ptr() == ptr
+    assert flat.grad.abs().sum() > 0
