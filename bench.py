@@ -93,19 +93,9 @@ def main(argv=None):
     model.train()
 
     loader = dm.train_dataloader()
-
-    def batches():
-        ep = 0
-        while True:
-            loader.set_epoch(ep)
-            for b in loader:
-                if b[0].shape[0] == args.batch:
-                    yield b
-            ep += 1
-
-    it = batches()
-    for i in range(args.warmup):
-        trainer._run_train_step(next(it), i)
+    step = trainer.make_train_stepper(loader)  # full batches; epoch roll-over reshuffles like fit()
+    for _ in range(args.warmup):
+        step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     pdist.barrier()
@@ -117,7 +107,7 @@ def main(argv=None):
         if dev.type == "cuda":
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
-        trainer._run_train_step(next(it), args.warmup + i)
+        step()
         if dev.type == "cuda":
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record()
@@ -133,10 +123,10 @@ def main(argv=None):
     p50 = pdist.all_reduce_max(step_ms[len(step_ms) // 2], dev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = args.batch * world * args.steps / elapsed
-    nonfinite = float(trainer._nonfinite.item()) if trainer._nonfinite is not None else 0.0
+    nonfinite = float(trainer.optimizer.nonfinite.item())
     if denv.rank == 0:
         log(f"[bench] p50 step {p50:.3f} ms, mean {ms_per_step:.3f} ms, graphs={'on' if trainer._graphs else 'off'}, "
-            f"nonfinite={nonfinite}, last loss={float(trainer.callback_metrics.get('loss', float('nan'))):.4g}")
+            f"nonfinite={nonfinite}, static_batches={trainer._static_ok(loader)}")
         rec = {
             "metric": "samples/sec (whole node) synthetic datamodule; p50 step ms",
             "value": round(value, 3),

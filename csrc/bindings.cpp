@@ -3,141 +3,258 @@
 // validates tensors and forwards the current PyTorch HIP stream, so every op is stream-ordered
 // with PyTorch and capturable into a HIP graph.
 #include <torch/extension.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
 extern "C" {
 int mta_lstm_fwd_layer(int H, int prec, const float* x, const float* w_ih, const float* b_ih, const float* b_hh,
-                       int fin, const float* gx, float* gates, const float* w_hh, float* hseq, float* cseq, int N,
-                       int T, hipStream_t st);
-int mta_lstm_bwd_layer(int H, int prec, float* gates, const float* cseq, const float* w_hh, const float* dH,
-                       const float* dh_last, int N, int T, hipStream_t st);
+                       int fin, const float* gx, float* stash, const float* w_hh, float* hseq, int N, int Np, int T,
+                       hipStream_t st);
+int mta_lstm_bwd_layer(int H, int prec, const float* stash, const float* w_hh, const float* dH, const float* dh_last,
+                       float* dG, int N, int Np, int T, hipStream_t st);
+void mta_lstm_wgrad(const float* dG, const float* hseq, const float* inp, int inp_batch_first, int N, int Np, int T,
+                    int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, hipStream_t st);
+void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
+                   hipStream_t st);
+void mta_gather_batch(const float* const* src, float* const* dst, const long* row_floats, int ntensors,
+                      const int* perm, int* cursor, int* arrive, int B, int row_offset, hipStream_t st);
 void mta_decoder_losses(const float* ab, const float* y, const float* factor, const float* inv_psi, int N, int n,
-                        int C, int windows, int kwin, int factor_stride, int want_nll, float* out, float* gmse,
-                        float* gnll, hipStream_t st);
-void mta_decoder_losses_bwd(const float* gout, const float* gmse, const float* gnll, float* dab, int N, int has_nll,
-                            hipStream_t st);
+                        int C, int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
+                        float batch_weight, float* out, float* gmse, float* gnll, double* acc, hipStream_t st);
+void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb, const float* bb,
+                      float* ab_out, const float* y, const float* factor, const float* inv_psi, int N, int n, int C,
+                      int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
+                      float batch_weight, float* out, float* gmse, float* gnll, double* acc, hipStream_t st);
+void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g_total, float c_nll, float c_mse, const float* gmse, const float* gnll,
+                          int has_nll, const float* h, int N, int H, const float* wa, const float* wb, float* dh,
+                          float* dab, float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st);
 int mta_optim_num_partials(long n);
 void mta_grad_sqnorm(const float* g, long n, float scale, float* partials, float* step, hipStream_t st);
 void mta_adam(float* p, float* g, float* m, float* v, long n, const float* partials, const float* lr,
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
-              float* norm_out, hipStream_t st);
+              float* norm_out, float* nonfinite, hipStream_t st);
 void mta_scale(float* x, long n, float s, hipStream_t st);
 }
 
 namespace {
 
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
 #define MTA_CHECK_F32(t)                                                                            \
   TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor");                                           \
   TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32");                              \
   TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 
-const float* opt_ptr(const c10::optional<at::Tensor>& t) {
-  if (!t.has_value() || !t->defined()) return nullptr;
+using OptT = c10::optional<at::Tensor>;
+
+bool has(const OptT& t) { return t.has_value() && t->defined(); }
+
+const float* opt_ptr(const OptT& t) {
+  if (!has(t)) return nullptr;
   MTA_CHECK_F32(*t);
   return t->data_ptr<float>();
 }
 
-void lstm_fwd_layer(int64_t H, int64_t prec, const c10::optional<at::Tensor>& x, const c10::optional<at::Tensor>& w_ih,
-                    const c10::optional<at::Tensor>& b_ih, const c10::optional<at::Tensor>& b_hh,
-                    const c10::optional<at::Tensor>& gx, at::Tensor gates, at::Tensor w_hh, at::Tensor hseq,
-                    at::Tensor cseq, int64_t N, int64_t T) {
-  MTA_CHECK_F32(gates);
+float* opt_mut(const OptT& t) { return const_cast<float*>(opt_ptr(t)); }
+
+// ------------------------------------------------------------------------------------------- LSTM
+void lstm_fwd_layer(int64_t H, int64_t prec, const OptT& x, const OptT& w_ih, const OptT& b_ih, const OptT& b_hh,
+                    const OptT& gx, const OptT& stash, at::Tensor w_hh, at::Tensor hseq, int64_t N, int64_t Np,
+                    int64_t T) {
   MTA_CHECK_F32(w_hh);
   MTA_CHECK_F32(hseq);
-  MTA_CHECK_F32(cseq);
-  TORCH_CHECK(gates.numel() == T * N * 4 * H, "gates must be (T, N, 4H)");
-  TORCH_CHECK(hseq.numel() == T * N * H && cseq.numel() == T * N * H, "hseq/cseq must be (T, N, H)");
+  TORCH_CHECK(Np % 16 == 0 && N <= Np && N >= 1, "Np must be a multiple of 16 and >= N");
+  TORCH_CHECK(hseq.numel() == T * Np * H, "hseq must be (T, Np, H)");
   TORCH_CHECK(w_hh.numel() == 4 * H * H, "w_hh must be (4H, H)");
+  if (has(stash)) TORCH_CHECK(stash->numel() == T * Np * 5 * H, "stash must hold T*Np*5H floats");
   int fin = 0;
-  if (x.has_value() && x->defined()) {
+  if (has(x)) {
     TORCH_CHECK(x->dim() == 3 && x->size(0) == N && x->size(1) == T, "x must be (N, T, F)");
     fin = (int)x->size(2);
-    TORCH_CHECK(fin >= 1 && fin <= 5, "fused input projection supports 1 <= F <= 5");
-    TORCH_CHECK(w_ih.has_value() && w_ih->numel() == 4 * H * fin, "w_ih must be (4H, F)");
-    TORCH_CHECK(b_ih.has_value() && b_hh.has_value(), "fused input projection needs b_ih and b_hh");
+    TORCH_CHECK(fin == 3 || fin == 5, "fused input projection supports F in {3, 5}");
+    TORCH_CHECK(has(w_ih) && w_ih->numel() == 4 * H * fin, "w_ih must be (4H, F)");
+    TORCH_CHECK(has(b_ih) && has(b_hh), "fused input projection needs b_ih and b_hh");
   } else {
-    TORCH_CHECK(gx.has_value() && gx->numel() == T * N * 4 * H, "gx must be (T, N, 4H)");
+    TORCH_CHECK(has(gx) && gx->numel() == T * Np * 4 * H, "gx must be (T, Np, 4H)");
   }
-  c10::hip::HIPGuard guard(gates.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(hseq.device());
   int rc = mta_lstm_fwd_layer((int)H, (int)prec, opt_ptr(x), opt_ptr(w_ih), opt_ptr(b_ih), opt_ptr(b_hh), fin,
-                              opt_ptr(gx), gates.data_ptr<float>(), w_hh.data_ptr<float>(), hseq.data_ptr<float>(),
-                              cseq.data_ptr<float>(), (int)N, (int)T, cur_stream());
-  TORCH_CHECK(rc == 0, "lstm_fwd_layer: unsupported hidden size ", H, " (supported: 32, 64, 128)");
+                              opt_ptr(gx), opt_mut(stash), w_hh.data_ptr<float>(), hseq.data_ptr<float>(), (int)N,
+                              (int)Np, (int)T, cur_stream());
+  TORCH_CHECK(rc == 0, "lstm_fwd_layer: unsupported configuration (H must be 32, 64 or 128)");
 }
 
-void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor gates, at::Tensor cseq, at::Tensor w_hh,
-                    const c10::optional<at::Tensor>& dH, const c10::optional<at::Tensor>& dh_last, int64_t N,
-                    int64_t T) {
-  MTA_CHECK_F32(gates);
-  MTA_CHECK_F32(cseq);
+void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor stash, at::Tensor w_hh, const OptT& dH, const OptT& dh_last,
+                    at::Tensor dG, int64_t N, int64_t Np, int64_t T) {
+  MTA_CHECK_F32(stash);
   MTA_CHECK_F32(w_hh);
-  TORCH_CHECK(gates.numel() == T * N * 4 * H && cseq.numel() == T * N * H, "bad gates/cseq shape");
-  if (dH.has_value() && dH->defined()) TORCH_CHECK(dH->numel() == T * N * H, "dH must be (T, N, H)");
-  if (dh_last.has_value() && dh_last->defined()) TORCH_CHECK(dh_last->numel() == N * H, "dh_last must be (N, H)");
-  c10::hip::HIPGuard guard(gates.device());
-  int rc = mta_lstm_bwd_layer((int)H, (int)prec, gates.data_ptr<float>(), cseq.data_ptr<float>(),
-                              w_hh.data_ptr<float>(), opt_ptr(dH), opt_ptr(dh_last), (int)N, (int)T, cur_stream());
-  TORCH_CHECK(rc == 0, "lstm_bwd_layer: unsupported hidden size ", H);
+  MTA_CHECK_F32(dG);
+  TORCH_CHECK(stash.numel() == T * Np * 5 * H && dG.numel() == T * Np * 4 * H, "bad stash/dG shape");
+  const bool has_dh = has(dH);
+  if (has_dh) {
+    TORCH_CHECK(dH->numel() == T * Np * H, "dH must be (T, Np, H)");
+  } else {
+    TORCH_CHECK(has(dh_last) && dh_last->numel() == N * H, "dh_last must be (N, H)");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dG.device());
+  int rc = mta_lstm_bwd_layer((int)H, (int)prec, stash.data_ptr<float>(), w_hh.data_ptr<float>(), opt_ptr(dH),
+                              has_dh ? nullptr : opt_ptr(dh_last), dG.data_ptr<float>(), (int)N, (int)Np, (int)T,
+                              cur_stream());
+  TORCH_CHECK(rc == 0, "lstm_bwd_layer: unsupported configuration");
 }
 
-void decoder_losses(at::Tensor ab, at::Tensor y, at::Tensor factor, at::Tensor inv_psi, int64_t windows,
-                    int64_t kwin, int64_t factor_stride, bool want_nll, at::Tensor out, at::Tensor gmse,
-                    at::Tensor gnll) {
-  MTA_CHECK_F32(ab);
+void lstm_wgrad(at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_first, int64_t N, int64_t Np,
+                int64_t T, int64_t H, at::Tensor g_wih, at::Tensor g_whh, at::Tensor g_bih, at::Tensor g_bhh) {
+  MTA_CHECK_F32(dG);
+  MTA_CHECK_F32(hseq);
+  MTA_CHECK_F32(inp);
+  MTA_CHECK_F32(g_wih);
+  MTA_CHECK_F32(g_whh);
+  MTA_CHECK_F32(g_bih);
+  MTA_CHECK_F32(g_bhh);
+  const int64_t F = g_wih.numel() / (4 * H);
+  TORCH_CHECK(dG.numel() == T * Np * 4 * H && hseq.numel() == T * Np * H, "bad dG/hseq shape");
+  TORCH_CHECK(inp.numel() == (inp_batch_first ? N * T * F : T * Np * F), "bad layer-input shape");
+  TORCH_CHECK(g_whh.numel() == 4 * H * H && g_bih.numel() == 4 * H && g_bhh.numel() == 4 * H, "bad grad shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dG.device());
+  mta_lstm_wgrad(dG.data_ptr<float>(), hseq.data_ptr<float>(), inp.data_ptr<float>(), inp_batch_first ? 1 : 0,
+                 (int)N, (int)Np, (int)T, (int)H, (int)F, g_wih.data_ptr<float>(), g_whh.data_ptr<float>(),
+                 g_bih.data_ptr<float>(), g_bhh.data_ptr<float>(), cur_stream());
+}
+
+void lstm_prep(at::Tensor w_ih, at::Tensor b_ih, at::Tensor b_hh, int64_t H, at::Tensor w_um, at::Tensor b_um) {
+  MTA_CHECK_F32(w_ih);
+  MTA_CHECK_F32(b_ih);
+  MTA_CHECK_F32(b_hh);
+  MTA_CHECK_F32(w_um);
+  MTA_CHECK_F32(b_um);
+  const int64_t F = w_ih.numel() / (4 * H);
+  TORCH_CHECK(w_um.numel() == w_ih.numel() && b_um.numel() == 4 * H, "bad prep shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(w_ih.device());
+  mta_lstm_prep(w_ih.data_ptr<float>(), b_ih.data_ptr<float>(), b_hh.data_ptr<float>(), (int)H, (int)F,
+                w_um.data_ptr<float>(), b_um.data_ptr<float>(), cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------- data
+void gather_batch(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::Tensor perm, at::Tensor cursor,
+                  at::Tensor arrive, int64_t B, int64_t row_offset) {
+  TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 tensors");
+  TORCH_CHECK(perm.scalar_type() == at::kInt && cursor.scalar_type() == at::kInt && arrive.scalar_type() == at::kInt,
+              "perm/cursor/arrive must be int32");
+  const float* s[4];
+  float* d[4];
+  long rf[4];
+  for (size_t k = 0; k < src.size(); ++k) {
+    MTA_CHECK_F32(src[k]);
+    MTA_CHECK_F32(dst[k]);
+    rf[k] = (long)(src[k].numel() / src[k].size(0));
+    TORCH_CHECK(dst[k].numel() == B * rf[k], "dst ", k, " must hold B rows");
+    s[k] = src[k].data_ptr<float>();
+    d[k] = dst[k].data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(perm.device());
+  mta_gather_batch(s, d, rf, (int)src.size(), perm.data_ptr<int>(), cursor.data_ptr<int>(), arrive.data_ptr<int>(),
+                   (int)B, (int)row_offset, cur_stream());
+}
+
+// ------------------------------------------------------------------------------------------- losses
+double* opt_acc(const OptT& acc) {
+  if (!has(acc)) return nullptr;
+  TORCH_CHECK(acc->is_cuda() && acc->scalar_type() == at::kDouble && acc->is_contiguous() && acc->numel() >= 8,
+              "acc must be a contiguous float64 GPU tensor of >= 8 elements");
+  return acc->data_ptr<double>();
+}
+
+void check_loss_inputs(int64_t N, const at::Tensor& y, const at::Tensor& factor, const at::Tensor& inv_psi,
+                       int64_t windows, int64_t kwin, int64_t factor_stride, const at::Tensor& out,
+                       const at::Tensor& gmse, const at::Tensor& gnll) {
   MTA_CHECK_F32(y);
   MTA_CHECK_F32(factor);
   MTA_CHECK_F32(inv_psi);
   MTA_CHECK_F32(out);
   MTA_CHECK_F32(gmse);
   MTA_CHECK_F32(gnll);
-  const int64_t N = ab.size(0);
-  TORCH_CHECK(ab.dim() == 2 && ab.size(1) == 2, "ab must be (N, 2)");
   TORCH_CHECK(y.dim() == 3 && y.size(0) == N && y.size(2) >= 2, "y must be (N, n, C>=2)");
   TORCH_CHECK(inv_psi.numel() == N, "inv_psi must be (N,)");
   TORCH_CHECK(windows * kwin == N, "windows * kwin must equal N");
   TORCH_CHECK(factor.numel() >= 2 + (windows - 1) * factor_stride, "factor too small");
   TORCH_CHECK(out.numel() >= 4 && gmse.numel() == 2 * N && gnll.numel() == 2 * N, "bad output shapes");
-  c10::hip::HIPGuard guard(ab.device());
+}
+
+void decoder_losses(at::Tensor ab, at::Tensor y, at::Tensor factor, at::Tensor inv_psi, int64_t windows, int64_t kwin,
+                    int64_t factor_stride, bool want_nll, double c_nll, double c_mse, double batch_weight,
+                    at::Tensor out, at::Tensor gmse, at::Tensor gnll, const OptT& acc) {
+  MTA_CHECK_F32(ab);
+  const int64_t N = ab.size(0);
+  TORCH_CHECK(ab.dim() == 2 && ab.size(1) == 2, "ab must be (N, 2)");
+  check_loss_inputs(N, y, factor, inv_psi, windows, kwin, factor_stride, out, gmse, gnll);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(ab.device());
   mta_decoder_losses(ab.data_ptr<float>(), y.data_ptr<float>(), factor.data_ptr<float>(), inv_psi.data_ptr<float>(),
                      (int)N, (int)y.size(1), (int)y.size(2), (int)windows, (int)kwin, (int)factor_stride,
-                     want_nll ? 1 : 0, out.data_ptr<float>(), gmse.data_ptr<float>(), gnll.data_ptr<float>(),
-                     cur_stream());
+                     want_nll ? 1 : 0, (float)c_nll, (float)c_mse, (float)batch_weight, out.data_ptr<float>(),
+                     gmse.data_ptr<float>(), gnll.data_ptr<float>(), opt_acc(acc), cur_stream());
 }
 
-void decoder_losses_bwd(at::Tensor gout, at::Tensor gmse, at::Tensor gnll, at::Tensor dab, bool has_nll) {
-  MTA_CHECK_F32(gout);
+void heads_losses(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor wb, at::Tensor bb, at::Tensor ab_out,
+                  at::Tensor y, at::Tensor factor, at::Tensor inv_psi, int64_t windows, int64_t kwin,
+                  int64_t factor_stride, bool want_nll, double c_nll, double c_mse, double batch_weight,
+                  at::Tensor out, at::Tensor gmse, at::Tensor gnll, const OptT& acc) {
+  MTA_CHECK_F32(h);
+  MTA_CHECK_F32(wa);
+  MTA_CHECK_F32(ba);
+  MTA_CHECK_F32(wb);
+  MTA_CHECK_F32(bb);
+  MTA_CHECK_F32(ab_out);
+  TORCH_CHECK(h.dim() == 2, "h must be (N, H)");
+  const int64_t N = h.size(0), H = h.size(1);
+  TORCH_CHECK(wa.numel() == H && wb.numel() == H && ba.numel() == 1 && bb.numel() == 1, "bad head shapes");
+  TORCH_CHECK(ab_out.numel() == 2 * N, "ab_out must be (N, 2)");
+  check_loss_inputs(N, y, factor, inv_psi, windows, kwin, factor_stride, out, gmse, gnll);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  mta_heads_losses(h.data_ptr<float>(), (int)H, wa.data_ptr<float>(), ba.data_ptr<float>(), wb.data_ptr<float>(),
+                   bb.data_ptr<float>(), ab_out.data_ptr<float>(), y.data_ptr<float>(), factor.data_ptr<float>(),
+                   inv_psi.data_ptr<float>(), (int)N, (int)y.size(1), (int)y.size(2), (int)windows, (int)kwin,
+                   (int)factor_stride, want_nll ? 1 : 0, (float)c_nll, (float)c_mse, (float)batch_weight,
+                   out.data_ptr<float>(), gmse.data_ptr<float>(), gnll.data_ptr<float>(), opt_acc(acc),
+                   cur_stream());
+}
+
+void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total, double c_nll, double c_mse,
+                      at::Tensor gmse, at::Tensor gnll, bool has_nll, const OptT& h, const OptT& wa, const OptT& wb, const OptT& dh, const OptT& dab,
+                      const OptT& g_wa, const OptT& g_ba, const OptT& g_wb, const OptT& g_bb) {
   MTA_CHECK_F32(gmse);
   MTA_CHECK_F32(gnll);
-  MTA_CHECK_F32(dab);
-  TORCH_CHECK(gout.numel() >= 2, "gout must hold [g_mse, g_nll]");
-  c10::hip::HIPGuard guard(dab.device());
-  mta_decoder_losses_bwd(gout.data_ptr<float>(), gmse.data_ptr<float>(), gnll.data_ptr<float>(),
-                         dab.data_ptr<float>(), (int)(dab.numel() / 2), has_nll ? 1 : 0, cur_stream());
+  const int64_t N = gmse.numel() / 2;
+  int64_t H = 0;
+  if (has(h)) {
+    H = h->size(1);
+    TORCH_CHECK(h->size(0) == N && has(wa) && has(wb), "heads backward needs h, wa, wb");
+    if (has(dh)) TORCH_CHECK(dh->numel() == N * H, "dh must be (N, H)");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(gmse.device());
+  mta_heads_losses_bwd(opt_ptr(g_mse), opt_ptr(g_nll), opt_ptr(g_total), (float)c_nll, (float)c_mse, gmse.data_ptr<float>(),
+                       gnll.data_ptr<float>(), has_nll ? 1 : 0, opt_ptr(h), (int)N, (int)H, opt_ptr(wa), opt_ptr(wb),
+                       opt_mut(dh), opt_mut(dab), opt_mut(g_wa), opt_mut(g_ba), opt_mut(g_wb), opt_mut(g_bb),
+                       cur_stream());
 }
 
+// ------------------------------------------------------------------------------------------- optimizer
 int64_t optim_num_partials(int64_t n) { return mta_optim_num_partials((long)n); }
 
-void grad_sqnorm(at::Tensor g, double scale, at::Tensor partials, const c10::optional<at::Tensor>& step) {
+void grad_sqnorm(at::Tensor g, double scale, at::Tensor partials, const OptT& step) {
   MTA_CHECK_F32(g);
   MTA_CHECK_F32(partials);
   TORCH_CHECK(g.numel() % 4 == 0, "flat buffers must be padded to a multiple of 4");
   TORCH_CHECK(partials.numel() >= mta_optim_num_partials((long)g.numel()), "partials too small");
-  c10::hip::HIPGuard guard(g.device());
-  float* stp = nullptr;
-  if (step.has_value() && step->defined()) {
-    MTA_CHECK_F32(*step);
-    stp = step->data_ptr<float>();
-  }
-  mta_grad_sqnorm(g.data_ptr<float>(), (long)g.numel(), (float)scale, partials.data_ptr<float>(), stp, cur_stream());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  mta_grad_sqnorm(g.data_ptr<float>(), (long)g.numel(), (float)scale, partials.data_ptr<float>(), opt_mut(step),
+                  cur_stream());
 }
 
 void adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor partials, at::Tensor lr, at::Tensor step,
           double beta1, double beta2, double eps, double wd, double max_norm, double scale, bool adamw,
-          const c10::optional<at::Tensor>& norm_out) {
+          const OptT& norm_out, const OptT& nonfinite) {
   MTA_CHECK_F32(p);
   MTA_CHECK_F32(g);
   MTA_CHECK_F32(m);
@@ -147,21 +264,17 @@ void adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor par
   MTA_CHECK_F32(step);
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "flat buffer size mismatch");
-  c10::hip::HIPGuard guard(p.device());
-  float* no = nullptr;
-  if (norm_out.has_value() && norm_out->defined()) {
-    MTA_CHECK_F32(*norm_out);
-    no = norm_out->data_ptr<float>();
-  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   mta_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (long)n,
            partials.data_ptr<float>(), lr.data_ptr<float>(), step.data_ptr<float>(), (float)beta1, (float)beta2,
-           (float)eps, (float)wd, (float)max_norm, (float)scale, adamw ? 1 : 0, no, cur_stream());
+           (float)eps, (float)wd, (float)max_norm, (float)scale, adamw ? 1 : 0, opt_mut(norm_out), opt_mut(nonfinite),
+           cur_stream());
 }
 
 void scale_(at::Tensor x, double s) {
   MTA_CHECK_F32(x);
   TORCH_CHECK(x.numel() % 4 == 0, "flat buffers must be padded to a multiple of 4");
-  c10::hip::HIPGuard guard(x.device());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mta_scale(x.data_ptr<float>(), (long)x.numel(), (float)s, cur_stream());
 }
 
@@ -171,8 +284,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
   m.def("lstm_fwd_layer", &lstm_fwd_layer);
   m.def("lstm_bwd_layer", &lstm_bwd_layer);
+  m.def("lstm_wgrad", &lstm_wgrad);
+  m.def("lstm_prep", &lstm_prep);
+  m.def("gather_batch", &gather_batch);
   m.def("decoder_losses", &decoder_losses);
-  m.def("decoder_losses_bwd", &decoder_losses_bwd);
+  m.def("heads_losses", &heads_losses);
+  m.def("heads_losses_bwd", &heads_losses_bwd);
   m.def("optim_num_partials", &optim_num_partials);
   m.def("grad_sqnorm", &grad_sqnorm);
   m.def("adam", &adam);

@@ -22,10 +22,13 @@ enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2 };
 
 #define MTA_WAVE 64
 
-__device__ __forceinline__ float mta_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// Activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (1 ulp) instead of the ~10-instruction
+// IEEE division sequence a plain '1.0f / x' compiles to.
+__device__ __forceinline__ float mta_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float mta_sigmoid(float x) { return mta_rcp(1.0f + __expf(-x)); }
 __device__ __forceinline__ float mta_tanh(float x) {
-  // 2*sigmoid(2x) - 1: one v_exp_f32 + one v_rcp_f32, saturates cleanly at +-1
-  return 2.0f / (1.0f + __expf(-2.0f * x)) - 1.0f;
+  // 2*sigmoid(2x) - 1: saturates cleanly at +-1
+  return fmaf(2.0f, mta_rcp(1.0f + __expf(-2.0f * x)), -1.0f);
 }
 
 __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
@@ -63,3 +66,7 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   for (int i = 0; i < nw; ++i) r += scratch[i];
   return r;
 }
+
+// s_waitcnt vmcnt(0) as a builtin (the compiler's waitcnt pass sees it, unlike inline asm).
+// gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]=0  ->  0x0F70
+__device__ __forceinline__ void mta_wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }

@@ -1,12 +1,15 @@
-// Fused decoder losses: MSE decoder, Woodbury Gaussian NLL and MAE in one pass, with analytic
-// gradients w.r.t. (alpha, beta) produced in the same pass.
+// Fused decoder losses: alpha/beta heads, MSE decoder, Woodbury Gaussian NLL and MAE in one pass, with
+// the analytic gradients w.r.t. (alpha, beta) produced in the same pass and the epoch metrics
+// accumulated in place.
 //
 // Reference semantics:
-//   MSE : r_hat = alpha + beta * r_mkt ; mean((r_hat - r)^2) over all N*n   (src/model.py:192-206)
+//   heads: alpha = h_T w_a + b_a, beta = h_T w_b + b_b                          (src/model.py:96-97,105-108)
+//   MSE : r_hat = alpha + beta * r_mkt ; mean((r_hat - r)^2) over all N*n         (src/model.py:192-206)
 //   NLL : mu = alpha + beta * f_mean ; Sigma^-1 = Woodbury(beta, Psi^-1, f_var) built DENSE (K x K)
 //         and 0.5 * (n (K ln 2pi - logdet Sigma^-1) + tr(D^T Sigma^-1 D))  (src/model.py:45-69,
 //         src/common.py:50-78) -> here the O(K n) closed form of SURVEY.md A.1 (no K x K matrix, no LU).
-//   MAE : mean |r_hat - r|                                                     (src/model.py:139)
+//   MAE : mean |r_hat - r|                                                          (src/model.py:139)
+//   total = c_nll * NLL + c_mse * MSE  (mse model: (0,1); nll: (1,0); combined: (1, mse_weight))
 // `windows` x `kwin` sequences: the reference's batch semantics (one Gaussian over all B*K
 // sequences with window 0's factor) is windows=1, kwin=N, factor_stride=0; the
 // corrected per-window batched NLL is windows=B, kwin=K, factor_stride=2.
@@ -15,32 +18,36 @@
 namespace {
 
 constexpr int TPB = 1024;
+constexpr int NWAVES = TPB / 64;
 constexpr double LOG2PI = 1.8378770664093453;
 
-__global__ __launch_bounds__(TPB) void decoder_losses_kernel(
-    const float* __restrict__ ab,      // (N, 2): [alpha, beta]
-    const float* __restrict__ y,       // (N, n, C): channel 0 = r_target, 1 = r_mkt
-    const float* __restrict__ factor,  // (W', 2): [f_mean, f_var]
-    const float* __restrict__ inv_psi, // (N)
-    int N, int n, int C, int windows, int kwin, int factor_stride, int want_nll,
-    float* __restrict__ out,           // [mse, nll, mae, sse]
-    float* __restrict__ gmse,          // (N, 2) d mse / d (alpha, beta)
-    float* __restrict__ gnll) {        // (N, 2) d nll / d (alpha, beta)
-  extern __shared__ __attribute__((aligned(16))) float ut[];  // n floats
-  __shared__ double red[TPB / 64][6];
+struct LossArgs {
+  const float* y;        // (N, n, C): channel 0 = r_target, 1 = r_mkt
+  const float* factor;   // (W', 2): [f_mean, f_var]
+  const float* inv_psi;  // (N)
+  int N, n, C, windows, kwin, factor_stride, want_nll;
+  float c_nll, c_mse, batch_weight;
+  float* out;            // [mse, nll, mae, total]
+  float* gmse;           // (N, 2) d mse / d (alpha, beta)
+  float* gnll;           // (N, 2) d nll / d (alpha, beta)
+  double* acc;           // optional metric accumulator (8 doubles) or nullptr
+};
+
+// Work split: one wave per sequence, lanes over the n target days (looping when n > 64);
+// every per-sequence sum is a wave reduction, u_t accumulates with LDS atomics whose
+// addresses are distinct within a wave instruction.  `ab` may live in LDS or global memory.
+__device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
+  __shared__ double red[NWAVES][6];
   __shared__ double bcast[6];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int N = A.N, n = A.n, C = A.C;
   const float inv_cnt = 1.0f / ((float)N * (float)n);
 
-  // Work split: one wave per sequence, lanes over the n target days (looping when n > 64);
-  // every per-sequence sum is a wave reduction, u_t accumulates with LDS atomics whose
-  // addresses are distinct within a wave instruction.
-  const int nwaves = TPB / 64;
   // ---------------- MSE / MAE over all sequences -------------------------------------------
   double sse = 0.0, sae = 0.0;
-  for (int i = wid; i < N; i += nwaves) {
+  for (int i = wid; i < N; i += NWAVES) {
     const float a = ab[2 * i], b = ab[2 * i + 1];
-    const float* yi = y + (size_t)i * n * C;
+    const float* yi = A.y + (size_t)i * n * C;
     float se = 0.f, serm = 0.f, ss = 0.f, sa = 0.f;
     for (int t = lane; t < n; t += 64) {
       const float r = yi[t * C], rm = yi[t * C + 1];
@@ -55,119 +62,230 @@ __global__ __launch_bounds__(TPB) void decoder_losses_kernel(
     sse += (double)wave_sum(ss);
     sae += (double)wave_sum(sa);
     if (lane == 0) {
-      gmse[2 * i] = 2.f * se * inv_cnt;
-      gmse[2 * i + 1] = 2.f * serm * inv_cnt;
+      A.gmse[2 * i] = 2.f * se * inv_cnt;
+      A.gmse[2 * i + 1] = 2.f * serm * inv_cnt;
     }
   }
   if (lane == 0) { red[wid][0] = sse; red[wid][1] = sae; }
   __syncthreads();
-  if (tid == 0) {
-    double s0 = 0, s1 = 0;
-    for (int k = 0; k < nwaves; ++k) { s0 += red[k][0]; s1 += red[k][1]; }
-    out[0] = (float)(s0 / ((double)N * n));
-    out[2] = (float)(s1 / ((double)N * n));
-    out[3] = (float)s0;
-  }
-  if (!want_nll) { if (tid == 0) out[1] = 0.f; return; }
+  double s_sse = 0, s_sae = 0;
+  for (int k = 0; k < NWAVES; ++k) { s_sse += red[k][0]; s_sae += red[k][1]; }
+  const double mse = s_sse / ((double)N * n);
 
   // ---------------- Woodbury NLL, window by window -------------------------------------------
   double nll_total = 0.0;
-  for (int wdw = 0; wdw < windows; ++wdw) {
-    const float fm = factor[wdw * factor_stride], fv = factor[wdw * factor_stride + 1];
-    const int i0 = wdw * kwin;
-    for (int t = tid; t < n; t += TPB) ut[t] = 0.f;
-    __syncthreads();
-    // pass 1: u_t = sum_i w_i b_i D_it ; partials of s = sum w b^2, sum log w, sum w D^2
-    double s_wbb = 0.0, s_logw = 0.0, s_wdd = 0.0;
-    for (int k = wid; k < kwin; k += nwaves) {
-      const int i = i0 + k;
-      const float a = ab[2 * i], b = ab[2 * i + 1], w = inv_psi[i];
-      const float mu = fmaf(b, fm, a), wb = w * b;
-      const float* yi = y + (size_t)i * n * C;
-      float sdd = 0.f;
-      for (int t = lane; t < n; t += 64) {
-        const float D = yi[t * C] - mu;
-        sdd = fmaf(D, D, sdd);
-        atomicAdd(&ut[t], wb * D);
+  if (A.want_nll) {
+    for (int wdw = 0; wdw < A.windows; ++wdw) {
+      const float fm = A.factor[wdw * A.factor_stride], fv = A.factor[wdw * A.factor_stride + 1];
+      const int i0 = wdw * A.kwin;
+      __syncthreads();
+      for (int t = tid; t < n; t += TPB) ut[t] = 0.f;
+      __syncthreads();
+      // pass 1: u_t = sum_i w_i b_i D_it ; partials of s = sum w b^2, sum log w, sum w D^2
+      double s_wbb = 0.0, s_logw = 0.0, s_wdd = 0.0;
+      for (int k = wid; k < A.kwin; k += NWAVES) {
+        const int i = i0 + k;
+        const float a = ab[2 * i], b = ab[2 * i + 1], w = A.inv_psi[i];
+        const float mu = fmaf(b, fm, a), wb = w * b;
+        const float* yi = A.y + (size_t)i * n * C;
+        float sdd = 0.f;
+        for (int t = lane; t < n; t += 64) {
+          const float D = yi[t * C] - mu;
+          sdd = fmaf(D, D, sdd);
+          atomicAdd(&ut[t], wb * D);
+        }
+        sdd = wave_sum(sdd);
+        if (lane == 0) {
+          s_wbb += (double)wb * b;
+          s_logw += log((double)w);
+          s_wdd += (double)w * sdd;
+        }
       }
-      sdd = wave_sum(sdd);
-      if (lane == 0) {
-        s_wbb += (double)wb * b;
-        s_logw += log((double)w);
-        s_wdd += (double)w * sdd;
-      }
-    }
-    __syncthreads();
-    // U1 = sum_t u_t, U2 = sum_t u_t^2
-    double s_u1 = 0.0, s_u2 = 0.0;
-    for (int t = tid; t < n; t += TPB) { s_u1 += ut[t]; s_u2 += (double)ut[t] * ut[t]; }
-    double v[5] = {s_wbb, s_logw, s_wdd, s_u1, s_u2};
+      __syncthreads();
+      double s_u1 = 0.0, s_u2 = 0.0;
+      for (int t = tid; t < n; t += TPB) { s_u1 += ut[t]; s_u2 += (double)ut[t] * ut[t]; }
+      double v[5] = {s_wbb, s_logw, s_wdd, s_u1, s_u2};
 #pragma unroll
-    for (int m = 0; m < 5; ++m) v[m] = wave_sum_d(v[m]);
-    if (lane == 0)
-      for (int m = 0; m < 5; ++m) red[wid][m] = v[m];
-    __syncthreads();
-    if (tid == 0) {
-      double acc[5] = {0, 0, 0, 0, 0};
-      for (int k = 0; k < nwaves; ++k)
-        for (int m = 0; m < 5; ++m) acc[m] += red[k][m];
-      for (int m = 0; m < 5; ++m) bcast[m] = acc[m];
-    }
-    __syncthreads();
-    const double den = 1.0 / (double)fv + bcast[0];
-    const double logdet = bcast[1] - log((double)fv * den);
-    const double U1 = bcast[3], U2 = bcast[4];
-    const double quad = bcast[2] - U2 / den;
-    nll_total += 0.5 * ((double)n * ((double)kwin * LOG2PI - logdet) + quad);
-    // pass 2: gradients (derivation in masters_thesis_amd/ops/losses.py)
-    const float fden = (float)den, fU1 = (float)U1, fU2 = (float)U2;
-    for (int k = wid; k < kwin; k += nwaves) {
-      const int i = i0 + k;
-      const float a = ab[2 * i], b = ab[2 * i + 1], w = inv_psi[i];
-      const float mu = fmaf(b, fm, a);
-      const float* yi = y + (size_t)i * n * C;
-      float sd = 0.f, ud = 0.f;
-      for (int t = lane; t < n; t += 64) {
-        const float D = yi[t * C] - mu;
-        sd += D;
-        ud = fmaf(ut[t], D, ud);
+      for (int m = 0; m < 5; ++m) v[m] = wave_sum_d(v[m]);
+      if (lane == 0)
+        for (int m = 0; m < 5; ++m) red[wid][m] = v[m];
+      __syncthreads();
+      if (tid == 0) {
+        double acc[5] = {0, 0, 0, 0, 0};
+        for (int k = 0; k < NWAVES; ++k)
+          for (int m = 0; m < 5; ++m) acc[m] += red[k][m];
+        for (int m = 0; m < 5; ++m) bcast[m] = acc[m];
       }
-      sd = wave_sum(sd);
-      ud = wave_sum(ud);
-      if (lane == 0) {
-        const float wb = w * b;
-        gnll[2 * i] = -w * sd + wb * fU1 / fden;
-        gnll[2 * i + 1] = (float)n * wb / fden - fm * (w * sd - wb * fU1 / fden) - w * ud / fden +
-                          fU2 * wb / (fden * fden);
+      __syncthreads();
+      const double den = 1.0 / (double)fv + bcast[0];
+      const double logdet = bcast[1] - log((double)fv * den);
+      const double U1 = bcast[3], U2 = bcast[4];
+      const double quad = bcast[2] - U2 / den;
+      nll_total += 0.5 * ((double)n * ((double)A.kwin * LOG2PI - logdet) + quad);
+      // pass 2: gradients (derivation in masters_thesis_amd/ops/losses.py)
+      const float fden = (float)den, fU1 = (float)U1, fU2 = (float)U2;
+      for (int k = wid; k < A.kwin; k += NWAVES) {
+        const int i = i0 + k;
+        const float a = ab[2 * i], b = ab[2 * i + 1], w = A.inv_psi[i];
+        const float mu = fmaf(b, fm, a);
+        const float* yi = A.y + (size_t)i * n * C;
+        float sd = 0.f, ud = 0.f;
+        for (int t = lane; t < n; t += 64) {
+          const float D = yi[t * C] - mu;
+          sd += D;
+          ud = fmaf(ut[t], D, ud);
+        }
+        sd = wave_sum(sd);
+        ud = wave_sum(ud);
+        if (lane == 0) {
+          const float wb = w * b;
+          A.gnll[2 * i] = -w * sd + wb * fU1 / fden;
+          A.gnll[2 * i + 1] = (float)n * wb / fden - fm * (w * sd - wb * fU1 / fden) - w * ud / fden +
+                              fU2 * wb / (fden * fden);
+        }
       }
     }
-    __syncthreads();
   }
-  if (tid == 0) out[1] = (float)nll_total;
+  if (tid == 0) {
+    const double total = (double)A.c_nll * nll_total + (double)A.c_mse * mse;
+    A.out[0] = (float)mse;
+    A.out[1] = (float)nll_total;
+    A.out[2] = (float)(s_sae / ((double)N * n));
+    A.out[3] = (float)total;
+    if (A.acc) {
+      const double cnt = (double)N * n;
+      A.acc[0] += s_sse;        // MSE: sum of squared errors
+      A.acc[1] += cnt;          //      element count
+      A.acc[2] += nll_total;    // NLL: loss sum
+      A.acc[3] += 1.0;          //      update count (src/model.py:38-39)
+      A.acc[4] += total * A.batch_weight;  // loss/total: batch-size weighted mean
+      A.acc[5] += A.batch_weight;
+      A.acc[6] += s_sae;        // MAE
+      A.acc[7] += cnt;
+    }
+  }
 }
 
-// d(alpha, beta) = g_mse * gmse + g_nll * gnll + g_mae * sign-term (MAE is eval-only: no grad)
-__global__ void decoder_losses_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ gmse,
-                                          const float* __restrict__ gnll, float* __restrict__ dab, int N2,
-                                          int has_nll) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= N2) return;
-  float v = gout[0] * gmse[k];
-  if (has_nll) v = fmaf(gout[1], gnll[k], v);
-  dab[k] = v;
+__global__ __launch_bounds__(TPB) void decoder_losses_kernel(const float* __restrict__ ab, LossArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // n floats
+  losses_body(ab, A, smem);
+}
+
+// heads (two Linear(H,1)) computed in-kernel from h_T, then the losses
+__global__ __launch_bounds__(TPB) void heads_losses_kernel(const float* __restrict__ h, int H,
+                                                           const float* __restrict__ wa, const float* __restrict__ ba,
+                                                           const float* __restrict__ wb, const float* __restrict__ bb,
+                                                           float* __restrict__ ab_out, LossArgs A) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // 2N (ab) + n (u_t) floats
+  float* ab = smem;
+  float* ut = smem + 2 * ((A.N + 1) & ~1) + 4;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int i = wid; i < A.N; i += NWAVES) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = lane; k < H; k += 64) {
+      const float hv = h[(size_t)i * H + k];
+      sa = fmaf(hv, wa[k], sa);
+      sb = fmaf(hv, wb[k], sb);
+    }
+    sa = wave_sum(sa) + ba[0];
+    sb = wave_sum(sb) + bb[0];
+    if (lane == 0) {
+      ab[2 * i] = sa;
+      ab[2 * i + 1] = sb;
+      ab_out[2 * i] = sa;
+      ab_out[2 * i + 1] = sb;
+    }
+  }
+  __syncthreads();
+  losses_body(ab, A, ut);
+}
+
+// backward: d(alpha, beta) from the saved per-sequence gradients, then dh_T and the head weight
+// gradients (accumulated into the parameters' gradient views)
+__global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
+    const float* __restrict__ g_mse, const float* __restrict__ g_nll, const float* __restrict__ g_total,  // nullable
+    float c_nll, float c_mse, const float* __restrict__ gmse, const float* __restrict__ gnll, int has_nll,
+    const float* __restrict__ h, int N, int H, const float* __restrict__ wa, const float* __restrict__ wb,
+    float* __restrict__ dh, float* __restrict__ dab, float* __restrict__ g_wa, float* __restrict__ g_ba,
+    float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  extern __shared__ __attribute__((aligned(16))) float d[];  // 2N
+  __shared__ float part[NWAVES][2][64 + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float gt = g_total ? g_total[0] : 0.f;
+  const float gm = (g_mse ? g_mse[0] : 0.f) + gt * c_mse;
+  const float gn = has_nll ? (g_nll ? g_nll[0] : 0.f) + gt * c_nll : 0.f;
+  for (int k = tid; k < 2 * N; k += TPB) {
+    float v = gm * gmse[k];
+    if (has_nll) v = fmaf(gn, gnll[k], v);
+    d[k] = v;
+    if (dab) dab[k] = v;
+  }
+  __syncthreads();
+  if (dh) {
+    for (int e = tid; e < N * H; e += TPB) {
+      const int i = e / H, k = e % H;
+      dh[e] = d[2 * i] * wa[k] + d[2 * i + 1] * wb[k];
+    }
+  }
+  if (g_wa) {
+    // wave w sums rows i = w, w+16, ... ; lane = column k (H <= 64 per pass)
+    for (int k0 = 0; k0 < H; k0 += 64) {
+      const int k = k0 + lane;
+      float sa = 0.f, sb = 0.f, da = 0.f, db = 0.f;
+      for (int i = wid; i < N; i += NWAVES) {
+        const float hv = k < H ? h[(size_t)i * H + k] : 0.f;
+        sa = fmaf(d[2 * i], hv, sa);
+        sb = fmaf(d[2 * i + 1], hv, sb);
+        da += d[2 * i];
+        db += d[2 * i + 1];
+      }
+      part[wid][0][lane] = sa;
+      part[wid][1][lane] = sb;
+      if (lane == 0) { part[wid][0][64] = da; part[wid][1][64] = db; }
+      __syncthreads();
+      if (wid == 0) {
+        float ta = 0.f, tb = 0.f;
+        for (int w = 0; w < NWAVES; ++w) { ta += part[w][0][lane]; tb += part[w][1][lane]; }
+        if (k < H) { g_wa[k] += ta; g_wb[k] += tb; }
+        if (k0 == 0 && lane == 0) {
+          float pa = 0.f, pb = 0.f;
+          for (int w = 0; w < NWAVES; ++w) { pa += part[w][0][64]; pb += part[w][1][64]; }
+          g_ba[0] += pa;
+          g_bb[0] += pb;
+        }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 }  // namespace
 
 extern "C" void mta_decoder_losses(const float* ab, const float* y, const float* factor, const float* inv_psi, int N,
-                                   int n, int C, int windows, int kwin, int factor_stride, int want_nll, float* out,
-                                   float* gmse, float* gnll, hipStream_t st) {
-  decoder_losses_kernel<<<1, TPB, (size_t)((n + 3) & ~3) * sizeof(float), st>>>(
-      ab, y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, out, gmse, gnll);
+                                   int n, int C, int windows, int kwin, int factor_stride, int want_nll, float c_nll,
+                                   float c_mse, float batch_weight, float* out, float* gmse, float* gnll, double* acc,
+                                   hipStream_t st) {
+  LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
+             out, gmse, gnll, acc};
+  decoder_losses_kernel<<<1, TPB, (size_t)((n + 3) & ~3) * sizeof(float), st>>>(ab, A);
 }
 
-extern "C" void mta_decoder_losses_bwd(const float* gout, const float* gmse, const float* gnll, float* dab, int N,
-                                       int has_nll, hipStream_t st) {
-  const int N2 = 2 * N;
-  decoder_losses_bwd_kernel<<<(N2 + 255) / 256, 256, 0, st>>>(gout, gmse, gnll, dab, N2, has_nll);
+extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb,
+                                 const float* bb, float* ab_out, const float* y, const float* factor,
+                                 const float* inv_psi, int N, int n, int C, int windows, int kwin, int factor_stride,
+                                 int want_nll, float c_nll, float c_mse, float batch_weight, float* out, float* gmse,
+                                 float* gnll, double* acc, hipStream_t st) {
+  LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
+             out, gmse, gnll, acc};
+  const size_t lds = (size_t)(2 * ((N + 1) & ~1) + 4 + ((n + 3) & ~3)) * sizeof(float);
+  heads_losses_kernel<<<1, TPB, lds, st>>>(h, H, wa, ba, wb, bb, ab_out, A);
+}
+
+extern "C" void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g_total, float c_nll, float c_mse, const float* gmse,
+                                     const float* gnll, int has_nll, const float* h, int N, int H, const float* wa,
+                                     const float* wb, float* dh, float* dab, float* g_wa, float* g_ba, float* g_wb,
+                                     float* g_bb, hipStream_t st) {
+  heads_losses_bwd_kernel<<<1, TPB, (size_t)(2 * N) * sizeof(float), st>>>(g_mse, g_nll, g_total, c_nll, c_mse, gmse, gnll, has_nll, h,
+                                                                           N, H, wa, wb, dh, dab, g_wa, g_ba, g_wb,
+                                                                           g_bb);
 }

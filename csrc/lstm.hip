@@ -2,7 +2,9 @@
 //
 // Replaces the reference's cuDNN LSTM (src/model.py:88-94,104).
 // Design (one workgroup = 16 sequences = one MFMA M-tile, one wave per 16 hidden units):
-//   * time-major activations (T, N, .) so each step's 16-sequence slab is contiguous and the
+//   * time-major activations (T, Np, .) with Np = N rounded up to 16, so every load/store in
+//     the recurrence is unconditional (no per-lane guards: hipcc turns a guarded load into a
+//     branch + s_waitcnt vmcnt(0), which serialises the memory pipeline) and the
 //     weight-gradient GEMMs need no copies (h_{t-1} is a contiguous prefix);
 //   * W_hh lives in VGPRs for the whole sequence as MFMA B fragments (hi/lo bf16 for 'high',
 //     f32 for 'highest'); the recurrent state crosses waves through a double-buffered LDS
@@ -10,48 +12,83 @@
 //   * wave w owns units [16w, 16w+16) for all four gates, so the MFMA C/D layout
 //     (col = lane&15 -> unit, row = 4*(lane>>4)+reg -> sequence) puts i,f,g,o of one
 //     (sequence, unit) in one lane: the cell update is lane-local;
-//   * forward stores the activated gates (overwriting the input projection in place) and c_t
-//     for BPTT; backward overwrites the gates with dG (pre-activation gradients) which the
-//     weight-gradient GEMMs consume.
+//   * the BPTT stash (activated gates + c_t) is written in the lanes' own fragment order,
+//     5 x 16-byte stores per lane per step (1 KiB per wave instruction), and read back the
+//     same way by the backward kernel, which emits dG (pre-activation gradients) as (T, Np, 4H)
+//     for the time-parallel weight-gradient GEMMs;
+//   * gate columns of gx (input) and dG (output) are UNIT-MAJOR (col = 4u + g), so a lane's
+//     four gates of one sequence are one 16-byte access.
 #include "common.h"
+
+#ifndef MTA_LSTM_STAMPS
+#define MTA_LSTM_STAMPS 0
+#endif
+#if MTA_LSTM_STAMPS
+// Diagnostic build only (csrc/tools/lstm_probe.hip): per-segment s_memtime sums of block 0 / lane 0.
+__device__ unsigned long long mta_stamp_acc[2][8];
+#define STAMP_DECL unsigned long long _ts_prev = 0, _ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(k)                                                                   \
+  {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();                    \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
+    if ((k) > 0) _ts_acc[(k)] += _n - _ts_prev;                                    \
+    _ts_prev = _n;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+  }
+#define STAMP_FLUSH(which)                                                         \
+  if (blockIdx.x == 0 && threadIdx.x == 0)                                         \
+    for (int _k = 0; _k < 8; ++_k) mta_stamp_acc[(which)][_k] = _ts_acc[_k];
+#else
+#define STAMP_DECL
+#define STAMP(k)
+#define STAMP_FLUSH(which)
+#endif
 
 namespace {
 
-constexpr int S = 16;  // sequences per workgroup (MFMA M tile)
+constexpr int S = 16;       // sequences per workgroup (MFMA M tile)
+constexpr int STASH = 5;    // float4 per lane per step: i, f, g, o (4 seqs each), c (4 seqs)
+
+__device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
+  return ((((size_t)t * ntiles + tile) * nw + w) * 64 + lane) * STASH;
+}
 
 // ---------------------------------------------------------------------------------------------
 // forward
 // ---------------------------------------------------------------------------------------------
-template <int H, int PREC, int FIN>
+template <int H, int PREC, int FIN, bool WSTASH>
 __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
-    const float* __restrict__ x,     // FIN > 0: (N, T, FIN) batch-first layer input
+    const float* __restrict__ x,     // FIN > 0: (N, T, FIN) batch-first layer input (N valid rows)
     const float* __restrict__ w_ih,  // FIN > 0: (4H, FIN)
     const float* __restrict__ b_ih,  // FIN > 0: (4H)
     const float* __restrict__ b_hh,  // FIN > 0: (4H)
-    const float* gx,                 // FIN == 0: (T, N, 4H) input projection incl. both biases
-    float* gates,                    // (T, N, 4H) out: activated [i, f, g, o]; may alias gx
+    const float* __restrict__ gx,    // FIN == 0: (T, Np, 4H) input projection incl. both biases, columns
+                                     //   UNIT-MAJOR (col = 4u + g: the caller permutes W_ih / bias rows)
+    float4* __restrict__ stash,      // (T, Np/16, H/16, 64, 5) float4 (may be null: inference)
     const float* __restrict__ w_hh,  // (4H, H)
-    float* __restrict__ hseq,        // (T, N, H)
-    float* __restrict__ cseq,        // (T, N, H)
-    int N, int T) {
+    float* __restrict__ hseq,        // (T, Np, H)
+    int N, int Np, int T) {
   constexpr int G4 = 4 * H;
-  constexpr int KB = H / 32;  // bf16 k-blocks of 32
-  constexpr int KF = H / 4;   // f32 k-steps of 4
-  constexpr int ROWB = H + 8; // padded bf16 row (16 B pad)
-  constexpr int ROWF = H + 4; // padded f32 row
+  constexpr int NW = H / 16;
+  constexpr int KB = H / 32;   // bf16 k-blocks of 32
+  constexpr int KF = H / 4;    // f32 k-steps of 4
+  constexpr int ROWB = H + 8;  // padded bf16 row (16 B pad)
+  constexpr int ROWF = H + 4;  // padded f32 row
 
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
-  const int n0 = blockIdx.x * S;
+  const int tile = blockIdx.x, ntiles = gridDim.x;
+  const int n0 = tile * S;
 
-  __shared__ __attribute__((aligned(16))) __bf16 h_hi[2][S][ROWB];
-  __shared__ __attribute__((aligned(16))) __bf16 h_lo[2][S][ROWB];
-  __shared__ __attribute__((aligned(16))) float h_f[2][S][ROWF];
+  __shared__ __attribute__((aligned(16))) __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __shared__ __attribute__((aligned(16))) __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  __shared__ __attribute__((aligned(16))) float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
 
   // ---- weights -> registers -------------------------------------------------------------
-  bf16x8 Bhi[4][KB > 0 ? KB : 1], Blo[4][KB > 0 ? KB : 1];
+  bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
   float Bf[4][PREC == PREC_F32 ? KF : 1];
   if constexpr (PREC == PREC_F32) {
 #pragma unroll
@@ -65,11 +102,10 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float v = w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e];
           __bf16 hi, lo;
-          split_bf16(v, hi, lo);
+          split_bf16(w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
           Bhi[g][kb][e] = hi;
-          Blo[g][kb][e] = lo;
+          if constexpr (PREC == PREC_BF16X3) Blo[g][kb][e] = lo;
         }
   }
   float wi[4][FIN > 0 ? FIN : 1], bias[4];
@@ -83,31 +119,41 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
   }
 
   // ---- zero initial state (buffer 0) ------------------------------------------------------
-  for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) {
-    (&h_hi[0][0][0])[idx] = (__bf16)0.f;
-    (&h_lo[0][0][0])[idx] = (__bf16)0.f;
+  if constexpr (PREC == PREC_F32) {
+    for (int idx = threadIdx.x; idx < S * ROWF; idx += blockDim.x) (&h_f[0][0][0])[idx] = 0.f;
+  } else {
+    for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_hi[0][0][0])[idx] = (__bf16)0.f;
+    if constexpr (PREC == PREC_BF16X3)
+      for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
   }
-  for (int idx = threadIdx.x; idx < S * ROWF; idx += blockDim.x) (&h_f[0][0][0])[idx] = 0.f;
   __syncthreads();
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  bool valid[4];
+  // rows beyond N (padding) read a clamped valid row and are masked to zero input
+  int nrow[4];
+  float nmask[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) valid[i] = (n0 + 4 * q + i) < N;
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 4 * q + i;
+    nrow[i] = n < N ? n : N - 1;
+    nmask[i] = n < N ? 1.f : 0.f;
+  }
 
-  // prefetch input contribution for t = 0
   float nxt[4][4];
   auto load_in = [&](int t, float (&dst)[4][4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int n = n0 + 4 * q + i;
       if constexpr (FIN == 0) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) dst[g][i] = valid[i] ? gx[((size_t)t * N + n) * G4 + g * H + u] : 0.f;
+        const float4 v = *reinterpret_cast<const float4*>(gx + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u);
+        dst[0][i] = v.x;
+        dst[1][i] = v.y;
+        dst[2][i] = v.z;
+        dst[3][i] = v.w;
       } else {
+        const float* xs = x + ((size_t)nrow[i] * T + t) * FIN;
         float xv[FIN];
 #pragma unroll
-        for (int f = 0; f < FIN; ++f) xv[f] = valid[i] ? x[((size_t)n * T + t) * FIN + f] : 0.f;
+        for (int f = 0; f < FIN; ++f) xv[f] = xs[f] * nmask[i];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           float a = bias[g];
@@ -120,12 +166,38 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
   };
   load_in(0, nxt);
 
+  // Outputs of step t are held in registers and stored at the top of step t+1, BEFORE the
+  // prefetch of step t+2's input: the loop-head wait for that prefetch (hipcc emits it as a
+  // vmcnt count that ignores stores; the hardware counter does not) then covers stores that
+  // have had a whole step to drain instead of stores issued just before the barrier.
+  f32x4 pgi, pgf, pgg, pgo, pcc;
+  float ph[4];
+  auto store_step = [&](int t) {
+    if constexpr (WSTASH) {
+      float4* st = stash + stash_index(t, tile, ntiles, w, NW, lane);
+      st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
+      st[1] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      st[2] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      st[3] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      st[4] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) hseq[((size_t)t * Np + n0 + 4 * q + i) * H + u] = ph[i];
+  };
+
+  STAMP_DECL
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1;
+    STAMP(0)
     f32x4 acc[4];
 #pragma unroll
     for (int g = 0; g < 4; ++g) acc[g] = f32x4{nxt[g][0], nxt[g][1], nxt[g][2], nxt[g][3]};
-    if (t + 1 < T) load_in(t + 1, nxt);
+    STAMP(1)
+    mta_wait_vmem();  // retire this step's prefetch (and last step's stores) before new stores
+    if (t > 0) store_step(t - 1);
+    load_in(t + 1 < T ? t + 1 : t, nxt);  // prefetch (last step re-reads a valid slab)
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(2)
 
     // ---- recurrent MFMA: acc[g] += h_{t-1} (16 x H) . W_hh[g]^T (H x 16) -----------------
     if constexpr (PREC == PREC_F32) {
@@ -154,38 +226,38 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
     }
 
     // ---- gates + cell update (lane-local) ------------------------------------------------
+    STAMP(3)
     const int nb = (t + 1) & 1;
+    float h[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float ig = mta_sigmoid(acc[0][i]);
-      const float fg = mta_sigmoid(acc[1][i]);
-      const float gg = mta_tanh(acc[2][i]);
-      const float og = mta_sigmoid(acc[3][i]);
-      c[i] = fmaf(fg, c[i], ig * gg);
-      const float h = og * mta_tanh(c[i]);
+      pgi[i] = mta_sigmoid(acc[0][i]);
+      pgf[i] = mta_sigmoid(acc[1][i]);
+      pgg[i] = mta_tanh(acc[2][i]);
+      pgo[i] = mta_sigmoid(acc[3][i]);
+      c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
+      pcc[i] = c[i];
+      h[i] = pgo[i] * mta_tanh(c[i]);
+      ph[i] = h[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
       const int s = 4 * q + i;
-      const int n = n0 + s;
-      if (valid[i]) {
-        const size_t gb = ((size_t)t * N + n) * G4 + u;
-        gates[gb] = ig;
-        gates[gb + H] = fg;
-        gates[gb + 2 * H] = gg;
-        gates[gb + 3 * H] = og;
-        const size_t hb = ((size_t)t * N + n) * H + u;
-        cseq[hb] = c[i];
-        hseq[hb] = h;
-      }
       if constexpr (PREC == PREC_F32) {
-        h_f[nb][s][(u & 3) * KF + (u >> 2)] = h;
+        h_f[nb][s][(u & 3) * KF + (u >> 2)] = h[i];
       } else {
         __bf16 hi, lo;
-        split_bf16(h, hi, lo);
+        split_bf16(h[i], hi, lo);
         h_hi[nb][s][u] = hi;
         if constexpr (PREC == PREC_BF16X3) h_lo[nb][s][u] = lo;
       }
     }
+    STAMP(4)
     __syncthreads();
+    STAMP(5)
   }
+  STAMP_FLUSH(0)
+  store_step(T - 1);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -202,17 +274,18 @@ __device__ __forceinline__ int rperm_to_r(int rp) {
   return g * H + uu;
 }
 
-template <int H, int PREC>
+template <int H, int PREC, bool HAS_DH>
 __global__ __launch_bounds__((H / 16) * 64) void lstm_bwd_kernel(
-    float* gates,                     // (T, N, 4H) in: activated gates; out: dG (pre-activation)
-    const float* __restrict__ cseq,   // (T, N, H)
-    const float* __restrict__ w_hh,   // (4H, H)
-    const float* __restrict__ dH,     // (T, N, H) grad wrt this layer's outputs, or nullptr
-    const float* __restrict__ dh_last,// (N, H) grad wrt h_{T-1} only, or nullptr
-    int N, int T) {
+    const float4* __restrict__ stash,  // forward stash (fragment order)
+    const float* __restrict__ w_hh,    // (4H, H)
+    const float* __restrict__ dH,      // HAS_DH: (T, Np, H) grad wrt this layer's outputs
+    const float* __restrict__ dh_last, // !HAS_DH: (N, H) grad wrt h_{T-1} only
+    float* __restrict__ dG,            // (T, Np, 4H) out: pre-activation gate gradients, UNIT-MAJOR columns
+    int N, int Np, int T) {
   constexpr int G4 = 4 * H;
-  constexpr int KB = G4 / 32;       // bf16 k-blocks
-  constexpr int KF = G4 / 4;        // f32 k-steps
+  constexpr int NW = H / 16;
+  constexpr int KB = G4 / 32;  // bf16 k-blocks
+  constexpr int KF = G4 / 4;   // f32 k-steps
   constexpr int ROWB = G4 + 8;
   constexpr int ROWF = G4 + 4;
 
@@ -220,7 +293,8 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_bwd_kernel(
   const int w = threadIdx.x >> 6;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
-  const int n0 = blockIdx.x * S;
+  const int tile = blockIdx.x, ntiles = gridDim.x;
+  const int n0 = tile * S;
 
   __shared__ __attribute__((aligned(16))) __bf16 g_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __shared__ __attribute__((aligned(16))) __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
@@ -245,92 +319,109 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_bwd_kernel(
       }
   }
 
-  bool valid[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) valid[i] = (n0 + 4 * q + i) < N;
-
   float dc[4] = {0.f, 0.f, 0.f, 0.f};
-  float dhr[4] = {0.f, 0.f, 0.f, 0.f};  // recurrent dh from step t+1
+  float dhr[4];  // recurrent dh (from step t+1); seeded with dL/dh_{T-1} when there is no dH
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 4 * q + i;
+    if constexpr (HAS_DH) {
+      dhr[i] = 0.f;
+    } else {
+      const float v = dh_last[(size_t)(n < N ? n : N - 1) * H + u];
+      dhr[i] = n < N ? v : 0.f;
+    }
+  }
 
-  // per-step inputs (prefetched one step ahead)
-  float ga[4][4], ct[4], cp[4], dho[4];
-  auto load_step = [&](int t, float (&gdst)[4][4], float (&cdst)[4], float (&cpdst)[4], float (&ddst)[4]) {
+  // per-step inputs, prefetched one step ahead
+  // Everything step t needs (its stash slot, c_{t-1}, dH_t) is prefetched during step t+1, and
+  // dG_t is stored at the top of step t-1 (see the forward kernel for why stores are delayed).
+  float4 st_nxt[STASH], cp_nxt;
+  float dh_nxt[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_step = [&](int t, float4 (&sdst)[STASH], float4& cdst, float (&ddst)[4]) {
+    const float4* src = stash + stash_index(t, tile, ntiles, w, NW, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = n0 + 4 * q + i;
-      const size_t hb = ((size_t)t * N + n) * H + u;
-      const size_t gb = ((size_t)t * N + n) * G4 + u;
+    for (int k = 0; k < STASH; ++k) sdst[k] = src[k];
+    cdst = stash[stash_index(t > 0 ? t - 1 : 0, tile, ntiles, w, NW, lane) + 4];
+    if constexpr (HAS_DH) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) gdst[g][i] = valid[i] ? gates[gb + g * H] : 0.f;
-      cdst[i] = valid[i] ? cseq[hb] : 0.f;
-      cpdst[i] = (valid[i] && t > 0) ? cseq[hb - (size_t)N * H] : 0.f;
-      float d = 0.f;
-      if (valid[i]) {
-        if (dH) d = dH[hb];
-        else if (dh_last && t == T - 1) d = dh_last[(size_t)n * H + u];
-      }
-      ddst[i] = d;
+      for (int i = 0; i < 4; ++i) ddst[i] = dH[((size_t)t * Np + n0 + 4 * q + i) * H + u];
     }
   };
-  load_step(T - 1, ga, ct, cp, dho);
-
-  for (int t = T - 1; t >= 0; --t) {
-    float g_cur[4][4], c_cur[4], cp_cur[4], dh_cur[4];
+  float pdG[4][4];
+  auto store_step = [&](int t) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) g_cur[g][i] = ga[g][i];
-      c_cur[i] = ct[i];
-      cp_cur[i] = cp[i];
-      dh_cur[i] = dho[i];
+      *reinterpret_cast<float4*>(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u) =
+          make_float4(pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]);
     }
-    if (t > 0) load_step(t - 1, ga, ct, cp, dho);
+  };
+  load_step(T - 1, st_nxt, cp_nxt, dh_nxt);
+
+  STAMP_DECL
+  for (int t = T - 1; t >= 0; --t) {
+    STAMP(0)
+    float4 st[STASH];
+    float dho[4];
+#pragma unroll
+    for (int k = 0; k < STASH; ++k) st[k] = st_nxt[k];
+    const float cpm = t > 0 ? 1.f : 0.f;  // c_{-1} = 0
+    const float cp4[4] = {cp_nxt.x * cpm, cp_nxt.y * cpm, cp_nxt.z * cpm, cp_nxt.w * cpm};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dho[i] = dh_nxt[i];
+    STAMP(1)
+    mta_wait_vmem();
+    if (t < T - 1) store_step(t + 1);
+    load_step(t > 0 ? t - 1 : 0, st_nxt, cp_nxt, dh_nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    STAMP(2)
+    const float ig4[4] = {st[0].x, st[0].y, st[0].z, st[0].w};
+    const float fg4[4] = {st[1].x, st[1].y, st[1].z, st[1].w};
+    const float gg4[4] = {st[2].x, st[2].y, st[2].z, st[2].w};
+    const float og4[4] = {st[3].x, st[3].y, st[3].z, st[3].w};
+    const float ct4[4] = {st[4].x, st[4].y, st[4].z, st[4].w};
 
     const int buf = t & 1;
-    float dG[4][4];
+    float (&dGv)[4][4] = pdG;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float ig = g_cur[0][i], fg = g_cur[1][i], gg = g_cur[2][i], og = g_cur[3][i];
-      const float dh = dh_cur[i] + dhr[i];
-      const float tc = mta_tanh(c_cur[i]);
+      const float ig = ig4[i], fg = fg4[i], gg = gg4[i], og = og4[i];
+      const float dh = dho[i] + dhr[i];
+      const float tc = mta_tanh(ct4[i]);
       const float d_o = dh * tc * og * (1.f - og);
       const float dcc = fmaf(dh * og, 1.f - tc * tc, dc[i]);
-      dG[0][i] = dcc * gg * ig * (1.f - ig);
-      dG[1][i] = dcc * cp_cur[i] * fg * (1.f - fg);
-      dG[2][i] = dcc * ig * (1.f - gg * gg);
-      dG[3][i] = d_o;
+      dGv[0][i] = dcc * gg * ig * (1.f - ig);
+      dGv[1][i] = dcc * cp4[i] * fg * (1.f - fg);
+      dGv[2][i] = dcc * ig * (1.f - gg * gg);
+      dGv[3][i] = d_o;
       dc[i] = dcc * fg;
       const int s = 4 * q + i;
-      const int n = n0 + s;
-      if (valid[i]) {
-        const size_t gb = ((size_t)t * N + n) * G4 + u;
+      if constexpr (PREC == PREC_F32) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) gates[gb + g * H] = dG[g][i];
-      }
-      if (t > 0) {
-        if constexpr (PREC == PREC_F32) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int r = g * H + u;  // identity r' for f32; stored at (r&3)*KF + (r>>2)
-            g_f[buf][s][(r & 3) * KF + (r >> 2)] = dG[g][i];
-          }
-        } else {
-          bf16x4 hi4, lo4;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            __bf16 hi, lo;
-            split_bf16(dG[g][i], hi, lo);
-            hi4[g] = hi;
-            lo4[g] = lo;
-          }
-          const int rp = 8 * (u >> 1) + 4 * (u & 1);
-          *reinterpret_cast<bf16x4*>(&g_hi[buf][s][rp]) = hi4;
-          if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s][rp]) = lo4;
+        for (int g = 0; g < 4; ++g) {
+          const int r = g * H + u;  // identity r' for f32; stored at (r&3)*KF + (r>>2)
+          g_f[buf][s][(r & 3) * KF + (r >> 2)] = dGv[g][i];
         }
+      } else {
+        bf16x4 hi4, lo4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          __bf16 hi, lo;
+          split_bf16(dGv[g][i], hi, lo);
+          hi4[g] = hi;
+          lo4[g] = lo;
+        }
+        const int rp = 8 * (u >> 1) + 4 * (u & 1);
+        *reinterpret_cast<bf16x4*>(&g_hi[buf][s][rp]) = hi4;
+        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s][rp]) = lo4;
       }
     }
-    if (t == 0) break;
+    STAMP(3)
+    if (t == 0) {
+      store_step(0);
+      break;
+    }
     __syncthreads();
+    STAMP(4)
 
     // ---- dh_{t-1} = dG_t (16 x 4H) . W_hh (4H x 16 cols of this wave) -----------------------
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -355,63 +446,77 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_bwd_kernel(
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) dhr[i] = acc0[i] + acc1[i];
+    STAMP(5)
   }
+  STAMP_FLUSH(1)
 }
 
 template <int H, int PREC>
 void launch_fwd(const float* x, const float* w_ih, const float* b_ih, const float* b_hh, int fin, const float* gx,
-                float* gates, const float* w_hh, float* hseq, float* cseq, int N, int T, hipStream_t st) {
-  dim3 grid((N + S - 1) / S), block((H / 16) * 64);
+                float* stash, const float* w_hh, float* hseq, int N, int Np, int T, hipStream_t st) {
+  dim3 grid(Np / S), block((H / 16) * 64);
+  float4* s4 = reinterpret_cast<float4*>(stash);
+#define MTA_FWD(F)                                                                                           \
+  if (s4) lstm_fwd_kernel<H, PREC, F, true><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, s4, w_hh, hseq, N, Np, T); \
+  else lstm_fwd_kernel<H, PREC, F, false><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, s4, w_hh, hseq, N, Np, T)
+  // layer 0 of the configs has F = 3 (interaction_only) or 5; other widths go through the GEMM path
   switch (fin) {
-    case 0: lstm_fwd_kernel<H, PREC, 0><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
-    case 1: lstm_fwd_kernel<H, PREC, 1><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
-    case 2: lstm_fwd_kernel<H, PREC, 2><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
-    case 3: lstm_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
-    case 4: lstm_fwd_kernel<H, PREC, 4><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
-    case 5: lstm_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, gates, w_hh, hseq, cseq, N, T); break;
+    case 0: MTA_FWD(0); break;
+    case 3: MTA_FWD(3); break;
+    case 5: MTA_FWD(5); break;
     default: break;
   }
+#undef MTA_FWD
 }
 
 template <int H>
 void dispatch_fwd(int prec, const float* x, const float* w_ih, const float* b_ih, const float* b_hh, int fin,
-                  const float* gx, float* gates, const float* w_hh, float* hseq, float* cseq, int N, int T,
+                  const float* gx, float* stash, const float* w_hh, float* hseq, int N, int Np, int T,
                   hipStream_t st) {
-  if (prec == PREC_F32) launch_fwd<H, PREC_F32>(x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st);
-  else if (prec == PREC_BF16X3) launch_fwd<H, PREC_BF16X3>(x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st);
-  else launch_fwd<H, PREC_BF16>(x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st);
+  if (prec == PREC_F32) launch_fwd<H, PREC_F32>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
+  else if (prec == PREC_BF16X3) launch_fwd<H, PREC_BF16X3>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
+  else launch_fwd<H, PREC_BF16>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
+}
+
+template <int H, int PREC>
+void launch_bwd(const float* stash, const float* w_hh, const float* dH, const float* dh_last, float* dG, int N,
+                int Np, int T, hipStream_t st) {
+  dim3 grid(Np / S), block((H / 16) * 64);
+  const float4* s4 = reinterpret_cast<const float4*>(stash);
+  if (dH) lstm_bwd_kernel<H, PREC, true><<<grid, block, 0, st>>>(s4, w_hh, dH, dh_last, dG, N, Np, T);
+  else lstm_bwd_kernel<H, PREC, false><<<grid, block, 0, st>>>(s4, w_hh, dH, dh_last, dG, N, Np, T);
 }
 
 template <int H>
-void dispatch_bwd(int prec, float* gates, const float* cseq, const float* w_hh, const float* dH,
-                  const float* dh_last, int N, int T, hipStream_t st) {
-  dim3 grid((N + S - 1) / S), block((H / 16) * 64);
-  if (prec == PREC_F32) lstm_bwd_kernel<H, PREC_F32><<<grid, block, 0, st>>>(gates, cseq, w_hh, dH, dh_last, N, T);
-  else if (prec == PREC_BF16X3) lstm_bwd_kernel<H, PREC_BF16X3><<<grid, block, 0, st>>>(gates, cseq, w_hh, dH, dh_last, N, T);
-  else lstm_bwd_kernel<H, PREC_BF16><<<grid, block, 0, st>>>(gates, cseq, w_hh, dH, dh_last, N, T);
+void dispatch_bwd(int prec, const float* stash, const float* w_hh, const float* dH, const float* dh_last, float* dG,
+                  int N, int Np, int T, hipStream_t st) {
+  if (prec == PREC_F32) launch_bwd<H, PREC_F32>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);
+  else if (prec == PREC_BF16X3) launch_bwd<H, PREC_BF16X3>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);
+  else launch_bwd<H, PREC_BF16>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);
 }
 
 }  // namespace
 
 // Returns 0 on success, -1 for an unsupported (H, fin) combination.
 extern "C" int mta_lstm_fwd_layer(int H, int prec, const float* x, const float* w_ih, const float* b_ih,
-                                  const float* b_hh, int fin, const float* gx, float* gates, const float* w_hh,
-                                  float* hseq, float* cseq, int N, int T, hipStream_t st) {
-  if (fin < 0 || fin > 5) return -1;
+                                  const float* b_hh, int fin, const float* gx, float* stash, const float* w_hh,
+                                  float* hseq, int N, int Np, int T, hipStream_t st) {
+  if (!(fin == 0 || fin == 3 || fin == 5) || Np % S != 0 || N > Np || N < 1) return -1;
   switch (H) {
-    case 32: dispatch_fwd<32>(prec, x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st); return 0;
-    case 64: dispatch_fwd<64>(prec, x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st); return 0;
-    case 128: dispatch_fwd<128>(prec, x, w_ih, b_ih, b_hh, fin, gx, gates, w_hh, hseq, cseq, N, T, st); return 0;
+    case 32: dispatch_fwd<32>(prec, x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st); return 0;
+    case 64: dispatch_fwd<64>(prec, x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st); return 0;
+    case 128: dispatch_fwd<128>(prec, x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st); return 0;
     default: return -1;
   }
 }
 
-extern "C" int mta_lstm_bwd_layer(int H, int prec, float* gates, const float* cseq, const float* w_hh,
-                                  const float* dH, const float* dh_last, int N, int T, hipStream_t st) {
+extern "C" int mta_lstm_bwd_layer(int H, int prec, const float* stash, const float* w_hh, const float* dH,
+                                  const float* dh_last, float* dG, int N, int Np, int T, hipStream_t st) {
+  if (Np % S != 0 || N > Np || N < 1 || (!dH && !dh_last)) return -1;
   switch (H) {
-    case 32: dispatch_bwd<32>(prec, gates, cseq, w_hh, dH, dh_last, N, T, st); return 0;
-    case 64: dispatch_bwd<64>(prec, gates, cseq, w_hh, dH, dh_last, N, T, st); return 0;
-    case 128: dispatch_bwd<128>(prec, gates, cseq, w_hh, dH, dh_last, N, T, st); return 0;
+    case 32: dispatch_bwd<32>(prec, stash, w_hh, dH, dh_last, dG, N, Np, T, st); return 0;
+    case 64: dispatch_bwd<64>(prec, stash, w_hh, dH, dh_last, dG, N, Np, T, st); return 0;
+    case 128: dispatch_bwd<128>(prec, stash, w_hh, dH, dh_last, dG, N, Np, T, st); return 0;
     default: return -1;
   }
 }

@@ -39,7 +39,8 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
                                                    const float* __restrict__ partials, int nparts,
                                                    const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr,
                                                    float beta1, float beta2, float eps, float wd, float max_norm,
-                                                   float scale, int adamw, float* __restrict__ norm_out) {
+                                                   float scale, int adamw, float* __restrict__ norm_out,
+                                                   float* __restrict__ nonfinite) {
   __shared__ float scratch[TPB / 64];
   float part = 0.f;
   for (int i = threadIdx.x; i < nparts; i += TPB) part += partials[i];
@@ -47,7 +48,10 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
   const float norm = sqrtf(sq);
   float clip = 1.0f;
   if (max_norm > 0.f) clip = fminf(1.0f, max_norm / (norm + 1e-6f));
-  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = norm;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[0] = norm;
+    if (nonfinite && !isfinite(norm)) nonfinite[0] += 1.0f;  // NaN/Inf guard, read once per epoch
+  }
   const float gs = scale * clip;
   const float lr = lr_ptr[0];
   const float t = step_ptr[0];
@@ -106,12 +110,12 @@ extern "C" void mta_grad_sqnorm(const float* g, long n, float scale, float* part
 
 extern "C" void mta_adam(float* p, float* g, float* m, float* v, long n, const float* partials, const float* lr,
                          const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale,
-                         int adamw, float* norm_out, hipStream_t st) {
+                         int adamw, float* norm_out, float* nonfinite, hipStream_t st) {
   const long n4 = n / 4;
   adam_kernel<<<grid_for(n4), TPB, 0, st>>>(reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g),
                                             reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4, partials,
                                             grid_for(n4), lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-                                            norm_out);
+                                            norm_out, nonfinite);
 }
 
 extern "C" void mta_scale(float* x, long n, float s, hipStream_t st) {

@@ -14,19 +14,19 @@ MI355X execution model:
   one fused all-reduce per epoch (fixes the rank-local monitor of SURVEY Q2);
 * the optimizer is the fused clip+Adam HIP kernel pair (``ops.optim.FusedAdam``),
   swapped in for ``torch.optim.Adam/AdamW`` returned by ``configure_optimizers``;
-* after ``graph_warmup_steps`` eager steps, the train step (zero-grad, forward,
-  loss, backward, [all-reduce], clip+Adam, device-side metric accumulation) is
-  captured into a HIP graph and replayed for every later full batch; validation
-  and test steps are captured the same way.  The per-step host cost becomes one
-  graph launch; nothing reads back to the host until the epoch ends.
+* with an HBM-resident dataset the batch is assembled on the device by one gather
+  kernel (indices from a per-epoch device permutation + device cursor), so after
+  ``graph_warmup_steps`` eager steps the WHOLE train step — gather, forward, fused
+  heads/losses/metrics, backward, [all-reduce], clip+Adam — is captured into one
+  HIP graph and replayed; validation/test steps are captured the same way.  The
+  per-step host cost is one ``hipGraphLaunch``; nothing reads back to the host
+  until the epoch ends.
 """
 from __future__ import annotations
 
-import math
 import os
 import sys
 import time
-from contextlib import nullcontext
 from pathlib import Path
 from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -36,7 +36,7 @@ from ..metrics import Metric, sync_metrics
 from ..ops.optim import FlatParameters, FusedAdam
 from ..parallel import dist as pdist
 from ..parallel.ddp import FlatDDP
-from .callbacks import Callback, LearningRateMonitor, ModelCheckpoint, StepTimer
+from .callbacks import Callback, ModelCheckpoint, StepTimer
 from .checkpoint import (LIGHTNING_COMPAT_VERSION, atomic_save, capture_rng_states, load_checkpoint,
                          restore_rng_states)
 from .schedulers import PlateauScheduler
@@ -46,20 +46,19 @@ def _batch_size(batch) -> int:
     return int(batch[0].shape[0]) if isinstance(batch, (list, tuple)) else int(batch.shape[0])
 
 
-class _CapturedStep:
-    """A captured HIP graph with static input buffers."""
+class _Graph:
+    """A captured HIP graph; ``static_in`` is set when inputs are copied in (non-static loaders)."""
 
-    def __init__(self, graph: "torch.cuda.CUDAGraph", static_in: Sequence[torch.Tensor], static_out: Any):
-        self.graph = graph
-        self.static_in = list(static_in)
-        self.static_out = static_out
+    def __init__(self, graph, out, static_in: Optional[Sequence[torch.Tensor]] = None):
+        self.graph, self.out, self.static_in = graph, out, static_in
 
-    def run(self, batch: Sequence[torch.Tensor]):
-        for s, b in zip(self.static_in, batch):
-            if s.data_ptr() != b.data_ptr():
-                s.copy_(b, non_blocking=True)
+    def replay(self, batch=None):
+        if self.static_in is not None and batch is not None:
+            for s, b in zip(self.static_in, batch):
+                if s.data_ptr() != b.data_ptr():
+                    s.copy_(b, non_blocking=True)
         self.graph.replay()
-        return self.static_out
+        return self.out
 
 
 class Trainer:
@@ -111,13 +110,11 @@ class Trainer:
         self.device = torch.device("cpu")
         self.model = None
         self.datamodule = None
-        self._graphs: Dict[Tuple[str, int], _CapturedStep] = {}
-        self._eager_counts: Dict[Tuple[str, int], int] = {}
+        self._graphs: Dict[Tuple, _Graph] = {}
+        self._eager_counts: Dict[Tuple, int] = {}
         self.step_timer = StepTimer()
         self.perf: Dict[str, float] = {}
-        self._nonfinite: Optional[torch.Tensor] = None
-        self._ckpt_to_resume: Optional[Dict[str, Any]] = None
-        self._graph_mode_active = False
+        self._in_graph = False
 
     # ------------------------------------------------------------------ properties
     @property
@@ -149,8 +146,6 @@ class Trainer:
         for c in self.callbacks:
             if isinstance(c, ModelCheckpoint) and c.dirpath is None and self.logger is not None:
                 c.dirpath = str(Path(self.logger.log_dir) / "checkpoints")
-        if self.device.type == "cuda":
-            torch.backends.cudnn.benchmark = False
 
     def _setup_model(self, model) -> None:
         model.trainer = self
@@ -193,7 +188,6 @@ class Trainer:
             }
         self.ddp = FlatDDP(self.flat)
         self.ddp.broadcast_parameters()
-        self._nonfinite = torch.zeros(1, device=self.device)
 
     def _model_summary(self, model) -> None:
         if not (self.enable_model_summary and self.is_global_zero):
@@ -210,84 +204,128 @@ class Trainer:
         print(f"{train:,} Trainable params\n{total - train:,} Non-trainable params\n{total:,} Total params")
         print(f"{total * 4 / 1e6:.3f} Total estimated model params size (MB)", flush=True)
 
-    # ------------------------------------------------------------------ step bodies
-    def _train_body(self, batch, batch_idx: int):
-        model, opt = self.model, self.optimizer
-        self.flat.grad.zero_()
-        loss = model.training_step(batch, batch_idx)
-        loss.backward()
-        if self._capture_allreduce():
-            self.ddp.allreduce_grads()
-        if not self._split_optimizer():
-            opt.step(self.gradient_clip_val, self.ddp.grad_scale)
-            self._nonfinite.add_((~torch.isfinite(opt.grad_norm)).float())
-        return loss
-
-    def _capture_allreduce(self) -> bool:
-        return self.ddp.world == 1 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1" or \
-            not self._graph_mode_active
-
-    def _split_optimizer(self) -> bool:
-        # with world > 1 the all-reduce runs eagerly between the fwd/bwd graph and the optimizer
-        return self._graph_mode_active and not self._capture_allreduce()
-
+    # ------------------------------------------------------------------ step machinery
     def _graphs_enabled(self) -> bool:
         return self.use_hip_graphs and self.device.type == "cuda"
 
-    def _run_train_step(self, batch, batch_idx: int):
-        B = _batch_size(batch)
-        key = ("train", B)
-        self.model._current_batch_size = B
+    def _allreduce_in_graph(self) -> bool:
+        return self.ddp.world == 1 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1"
+
+    def _train_body(self, batch, batch_idx: int):
+        """zero-grad, forward + fused loss, backward, [all-reduce], clip + Adam."""
+        self.flat.grad.zero_()
+        loss = self.model.training_step(batch, batch_idx)
+        loss.backward()
+        if not self._in_graph or self._allreduce_in_graph():
+            self.ddp.allreduce_grads()
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
+        return loss
+
+    def _after_graph(self) -> None:
+        # world > 1: the RCCL all-reduce and the optimizer run outside the captured fwd/bwd graph
+        if not self._allreduce_in_graph():
+            self.ddp.allreduce_grads()
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
+
+    def _run(self, key: Tuple, provider: Callable[[], Sequence[torch.Tensor]], body: Callable, static: bool,
+             warmup: int):
+        """Run one step: eager for the first ``warmup`` calls of ``key``, then capture once and replay.
+
+        ``provider`` returns the batch; when ``static`` it launches the in-graph gather into fixed
+        buffers, otherwise it returns fresh tensors that are copied into the graph's inputs.
+        """
         if not self._graphs_enabled():
-            self._graph_mode_active = False
-            return self._train_body(batch, batch_idx)
+            return body(provider())
         g = self._graphs.get(key)
         if g is None:
             n = self._eager_counts.get(key, 0)
-            if n < self.graph_warmup_steps:
+            if n < warmup:
                 self._eager_counts[key] = n + 1
-                self._graph_mode_active = False
                 side = torch.cuda.Stream()
                 side.wait_stream(torch.cuda.current_stream())
                 with torch.cuda.stream(side):
-                    out = self._train_body(batch, batch_idx)
+                    out = body(provider())
                 torch.cuda.current_stream().wait_stream(side)
                 return out
-            g = self._capture("train", batch, lambda b: self._train_body(b, batch_idx))
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            if static:
+                self._in_graph = True
+                try:
+                    with torch.cuda.graph(graph):
+                        out = body(provider())
+                finally:
+                    self._in_graph = False
+                g = _Graph(graph, out)
+            else:
+                batch = provider()
+                static_in = [t.clone() for t in batch]
+                self._in_graph = True
+                try:
+                    with torch.cuda.graph(graph):
+                        out = body(static_in)
+                finally:
+                    self._in_graph = False
+                g = _Graph(graph, out, static_in)
+                self._graphs[key] = g
+                out = g.replay(batch)
+                return out
             self._graphs[key] = g
-        out = g.run(batch)
-        if self._split_optimizer():
-            self.ddp.allreduce_grads()
-            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
-            self._nonfinite.add_((~torch.isfinite(self.optimizer.grad_norm)).float())
+        if g.static_in is None:
+            return g.replay()
+        return g.replay(provider())
+
+    def _train_step(self, loader, batch_idx: int, static: bool, batch=None):
+        if static:
+            B = loader.batch_size
+            self.model._current_batch_size = B
+            out = self._run(("train", B, True), loader.gather_static, lambda b: self._train_body(b, batch_idx), True,
+                            self.graph_warmup_steps)
+        else:
+            B = _batch_size(batch)
+            self.model._current_batch_size = B
+            out = self._run(("train", B, False), lambda: batch, lambda b: self._train_body(b, batch_idx), False,
+                            self.graph_warmup_steps)
+        if self._graphs_enabled() and (("train", B, static) in self._graphs):
+            self._after_graph()
         return out
 
-    def _capture(self, stage: str, batch, body: Callable) -> _CapturedStep:
-        self._graph_mode_active = True
-        static_in = [t.clone() for t in batch]
-        torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            out = body(static_in)
-        return _CapturedStep(graph, static_in, out)
-
-    def _run_eval_step(self, stage: str, batch, batch_idx: int):
+    def _eval_step(self, stage: str, loader, batch_idx: int, static: bool, batch=None):
         model = self.model
+        fn = model.validation_step if stage == "val" else model.test_step
+        if static:
+            B = loader.batch_size
+            model._current_batch_size = B
+            return self._run((stage, B, True), loader.gather_static, lambda b: fn(b, batch_idx), True, 1)
         B = _batch_size(batch)
         model._current_batch_size = B
-        fn = model.validation_step if stage == "val" else model.test_step
-        if not self._graphs_enabled() or stage == "test_no_graph":
-            return fn(batch, batch_idx)
-        key = (stage, B)
-        g = self._graphs.get(key)
-        if g is None:
-            n = self._eager_counts.get(key, 0)
-            if n < 1:
-                self._eager_counts[key] = n + 1
-                return fn(batch, batch_idx)
-            g = self._capture(stage, batch, lambda b: fn(b, batch_idx))
-            self._graphs[key] = g
-        return g.run(batch)
+        return self._run((stage, B, False), lambda: batch, lambda b: fn(b, batch_idx), False, 1)
+
+    def _static_ok(self, loader) -> bool:
+        return hasattr(loader, "supports_static") and loader.supports_static()
+
+    def make_train_stepper(self, loader):
+        """Callable running one training step per call on the loader's stream of batches (bench.py)."""
+        static = self._static_ok(loader)
+        state = {"epoch": -1, "left": 0, "i": 0, "it": None}
+
+        def step():
+            if state["left"] == 0:
+                state["epoch"] += 1
+                if static:
+                    state["left"] = loader.begin_epoch(state["epoch"])
+                else:
+                    loader.set_epoch(state["epoch"])
+                    batches = [b for b in loader if _batch_size(b) == loader.batch_size]
+                    state["it"] = iter(batches)
+                    state["left"] = len(batches)
+            state["left"] -= 1
+            state["i"] += 1
+            if static:
+                return self._train_step(loader, state["i"], True)
+            return self._train_step(loader, state["i"], False, next(state["it"]))
+
+        return step
 
     # ------------------------------------------------------------------ epoch helpers
     def _metrics_of(self, stage: str) -> Dict[str, Metric]:
@@ -298,10 +336,7 @@ class Trainer:
         sync_metrics(ms.values())
         out = {}
         for name, m in ms.items():
-            try:
-                out[name] = m.compute().detach().float().cpu()
-            except ZeroDivisionError:  # pragma: no cover
-                continue
+            out[name] = m.compute().detach().float().cpu()
         return out
 
     def _reset_stage_metrics(self, stage: str) -> None:
@@ -322,21 +357,94 @@ class Trainer:
         return min(n, int(lim))
 
     # ------------------------------------------------------------------ loops
+    def _eval_loop(self, stage: str, loader, limit=None, epoch: int = 0) -> None:
+        n_total = self._limit(len(loader), limit)
+        if self._static_ok(loader):
+            nfull = loader.begin_epoch(epoch)
+            for i in range(min(nfull, n_total)):
+                self._eval_step(stage, loader, i, True)
+            if n_total > nfull:
+                tail = loader.tail_batch()
+                if tail is not None:
+                    self._eval_step(stage, loader, nfull, False, tail)
+            return
+        for i, batch in enumerate(loader):
+            if i >= n_total:
+                break
+            self._eval_step(stage, loader, i, False, batch)
+
     def _run_eval(self, stage: str, loader, limit=None) -> Dict[str, torch.Tensor]:
         model = self.model
         model.eval()
         model._stage = "val" if stage == "sanity" else stage
-        n = self._limit(len(loader), limit)
         with torch.no_grad():
-            for i, batch in enumerate(loader):
-                if i >= n:
-                    break
-                self._run_eval_step(model._stage, batch, i)
+            self._eval_loop(model._stage, loader, limit)
         res = self._compute_stage_metrics(model._stage)
         self._reset_stage_metrics(model._stage)
         model.train()
         model._stage = "train"
         return res
+
+    def _train_epoch(self, loader, epoch: int) -> Tuple[List[float], int]:
+        """One epoch of training steps; returns per-step device times (ms) and samples per batch."""
+        static = self._static_ok(loader)
+        n_batches = self._limit(len(loader), self.limit_train_batches)
+        cuda = self.device.type == "cuda"
+        events: List[Tuple[Any, Any]] = []
+        host_ms: List[float] = []
+        B = loader.batch_size
+
+        def timed(fn):
+            if cuda:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                events.append((e0, e1))
+            else:
+                t0 = time.perf_counter()
+                fn()
+                host_ms.append((time.perf_counter() - t0) * 1e3)
+
+        def pre_step(i):
+            if self.fail_at_step is not None and self.global_step == self.fail_at_step:
+                raise RuntimeError(f"fault injection: MTA_FAIL_AT_STEP={self.fail_at_step}")
+            if self.enable_progress_bar and self.is_global_zero and (i % 500 == 0 or i == n_batches - 1):
+                sys.stdout.write(f"\rEpoch {epoch}: {i + 1}/{n_batches}")
+                sys.stdout.flush()
+
+        if static:
+            nfull = loader.begin_epoch(epoch)
+            for i in range(min(nfull, n_batches)):
+                if 0 <= self.max_steps <= self.global_step:
+                    break
+                pre_step(i)
+                timed(lambda: self._train_step(loader, i, True))
+                self.global_step += 1
+            if n_batches > nfull and not (0 <= self.max_steps <= self.global_step):
+                tail = loader.tail_batch()
+                if tail is not None:
+                    pre_step(nfull)
+                    timed(lambda: self._train_step(loader, nfull, False, tail))
+                    self.global_step += 1
+        else:
+            if hasattr(loader, "set_epoch"):
+                loader.set_epoch(epoch)
+            for i, batch in enumerate(loader):
+                if i >= n_batches or (0 <= self.max_steps <= self.global_step):
+                    break
+                pre_step(i)
+                B = _batch_size(batch)
+                timed(lambda: self._train_step(loader, i, False, batch))
+                self.global_step += 1
+        if cuda:
+            torch.cuda.synchronize()
+            skip = self.graph_warmup_steps + 1
+            host_ms = [a.elapsed_time(b) for a, b in (events[skip:] if len(events) > skip else events)]
+        if self.enable_progress_bar and self.is_global_zero:
+            sys.stdout.write("\n")
+        return host_ms, B
 
     def fit(self, model, datamodule=None, ckpt_path: Optional[str] = None, train_dataloaders=None,
             val_dataloaders=None) -> None:
@@ -361,13 +469,11 @@ class Trainer:
         val_loader = val_dataloaders or dm.val_dataloader()
         self.num_val_batches = self._limit(len(val_loader), self.limit_val_batches)
 
-        # sanity check (Lightning default num_sanity_val_steps=2)
         if self.num_sanity_val_steps > 0 and start_epoch == 0:
             self.sanity_checking = True
             self._run_eval("sanity", val_loader, limit=self.num_sanity_val_steps)
             self.sanity_checking = False
 
-        samples_per_batch = None
         for epoch in range(start_epoch, self.max_epochs):
             self.current_epoch = epoch
             model._stage = "train"
@@ -375,47 +481,16 @@ class Trainer:
             model.on_train_epoch_start()
             for c in self.callbacks:
                 c.on_train_epoch_start(self, model)
-            if hasattr(train_loader, "set_epoch"):
-                train_loader.set_epoch(epoch)
-            n_batches = self._limit(len(train_loader), self.limit_train_batches)
             t_epoch = time.perf_counter()
-            ev: List[Tuple[torch.cuda.Event, torch.cuda.Event]] = []
-            host_ms: List[float] = []
-            for i, batch in enumerate(train_loader):
-                if i >= n_batches or (0 <= self.max_steps <= self.global_step):
-                    break
-                if self.fail_at_step is not None and self.global_step == self.fail_at_step:
-                    raise RuntimeError(f"fault injection: MTA_FAIL_AT_STEP={self.fail_at_step}")
-                samples_per_batch = _batch_size(batch)
-                if self.device.type == "cuda":
-                    e0 = torch.cuda.Event(enable_timing=True)
-                    e0.record()
-                else:
-                    t0 = time.perf_counter()
-                self._run_train_step(batch, i)
-                if self.device.type == "cuda":
-                    e1 = torch.cuda.Event(enable_timing=True)
-                    e1.record()
-                    ev.append((e0, e1))
-                else:
-                    host_ms.append((time.perf_counter() - t0) * 1e3)
-                self.global_step += 1
-                if self.enable_progress_bar and self.is_global_zero and (i % 500 == 0 or i == n_batches - 1):
-                    sys.stdout.write(f"\rEpoch {epoch}: {i + 1}/{n_batches}")
-                    sys.stdout.flush()
-            if self.device.type == "cuda":
-                torch.cuda.synchronize()
-                host_ms = [a.elapsed_time(b) for a, b in ev[self.graph_warmup_steps + 1:]] or \
-                    [a.elapsed_time(b) for a, b in ev]
+            step_ms, samples_per_batch = self._train_epoch(train_loader, epoch)
             wall = time.perf_counter() - t_epoch
-            if self.enable_progress_bar and self.is_global_zero:
-                sys.stdout.write("\n")
-            perf = self.step_timer.summarize(host_ms, samples_per_batch or 1, self.world_size)
+            perf = self.step_timer.summarize(step_ms, samples_per_batch, self.world_size)
             perf["perf/epoch_wall_s"] = wall
             self.perf = perf
-            if self._nonfinite is not None and float(self._nonfinite.item()) > 0:
-                self._print(f"WARNING: {int(self._nonfinite.item())} step(s) with a non-finite gradient norm")
-                self._nonfinite.zero_()
+            nonfinite = float(self.optimizer.nonfinite.item())
+            if nonfinite > 0:
+                self._print(f"WARNING: {int(nonfinite)} step(s) with a non-finite gradient norm")
+                self.optimizer.nonfinite.zero_()
 
             train_metrics = self._compute_stage_metrics("train")
             self._reset_stage_metrics("train")
@@ -482,12 +557,8 @@ class Trainer:
         model.eval()
         model._stage = "test"
         model.on_test_start()
-        n = self._limit(len(loader), self.limit_test_batches)
         with torch.no_grad():
-            for i, batch in enumerate(loader):
-                if i >= n:
-                    break
-                self._run_eval_step("test", batch, i)
+            self._eval_loop("test", loader, self.limit_test_batches)
         # sync every test-time Metric (logged or attribute) across ranks before on_test_end
         test_metrics = list(self._metrics_of("test").values())
         test_metrics += [m for name, m in model.named_children() if isinstance(m, Metric) and name.startswith("test")]

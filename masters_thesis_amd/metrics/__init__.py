@@ -136,6 +136,56 @@ class MeanAccumulator(Metric):
         return (self.value_sum / self.weight).float()
 
 
+class MetricAccumulator(Metric):
+    """One float64[8] device buffer that the fused loss kernel adds into every step
+    (``ops.losses.heads_losses(acc=...)``): [sse, count, nll_sum, nll_updates,
+    total_sum, total_weight, sae, count].  The epoch metrics below are views of it, so
+    the whole per-step metric bookkeeping costs zero extra kernels."""
+
+    SSE, CNT, NLL, NLL_N, TOT, TOT_W, SAE, CNT2 = range(8)
+
+    def __init__(self):
+        super().__init__()
+        self.add_state("acc", torch.zeros(8, dtype=torch.float64))
+
+
+class _Linked(Metric):
+    def __init__(self, source: MetricAccumulator, num: int, den: int):
+        super().__init__()
+        object.__setattr__(self, "_source", source)  # not a submodule: no duplicate state_dict/buffers
+        self._num, self._den = num, den
+
+    def state_tensors(self) -> List[Tensor]:
+        return self._source.state_tensors()
+
+    def reset(self) -> None:
+        self._source.reset()
+
+    def compute(self) -> Tensor:
+        a = self._source.acc
+        return (a[self._num] / a[self._den]).float()
+
+
+class LinkedMSE(_Linked):
+    def __init__(self, source: MetricAccumulator):
+        super().__init__(source, MetricAccumulator.SSE, MetricAccumulator.CNT)
+
+
+class LinkedNLL(_Linked):
+    def __init__(self, source: MetricAccumulator):
+        super().__init__(source, MetricAccumulator.NLL, MetricAccumulator.NLL_N)
+
+
+class LinkedTotal(_Linked):
+    def __init__(self, source: MetricAccumulator):
+        super().__init__(source, MetricAccumulator.TOT, MetricAccumulator.TOT_W)
+
+
+class LinkedMAE(_Linked):
+    def __init__(self, source: MetricAccumulator):
+        super().__init__(source, MetricAccumulator.SAE, MetricAccumulator.CNT2)
+
+
 def sync_metrics(metrics: Iterable[Metric], group=None) -> None:
     """All-reduce (sum) every state of every metric in one flat collective."""
     import torch.distributed as dist
@@ -143,7 +193,13 @@ def sync_metrics(metrics: Iterable[Metric], group=None) -> None:
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
     ms = list(metrics)
-    states = [s for m in ms for s in m.state_tensors()]
+    seen = set()
+    states = []
+    for m in ms:
+        for s in m.state_tensors():
+            if s.data_ptr() not in seen:
+                seen.add(s.data_ptr())
+                states.append(s)
     if not states:
         return
     flat = torch.cat([s.reshape(-1).to(torch.float64) for s in states])
@@ -158,4 +214,4 @@ def sync_metrics(metrics: Iterable[Metric], group=None) -> None:
 
 
 __all__ = ["Metric", "MeanSquaredError", "MeanAbsoluteError", "MultivariateGaussianNLLLoss", "MeanAccumulator",
-           "sync_metrics"]
+           "MetricAccumulator", "LinkedMSE", "LinkedNLL", "LinkedTotal", "LinkedMAE", "sync_metrics"]

@@ -7,10 +7,11 @@ L2, ReduceLROnPlateau(min, 0.5, 2) monitored on ``loss/total/val`` at the
 validation frequency) and test hooks (MAE + NLL, `src/model.py:111-147`).
 
 What changes is the compute path on MI355X: the encoder is the persistent HIP
-LSTM (``ops.lstm``), the two heads produce one (N, 2) ``[alpha | beta]`` tile, and
-every decoder/loss variant is ONE fused HIP kernel (``ops.losses``) that returns
-the MSE, NLL and MAE plus their analytic gradients — no K x K Woodbury matrix, no
-LU ``logdet``.
+LSTM (``ops.lstm``); the two heads, every decoder/loss variant, their gradients and
+the epoch-metric bookkeeping are ONE fused HIP kernel (``ops.losses.heads_losses``)
+— no K x K Woodbury matrix, no LU ``logdet``, no per-step metric kernels.  The
+epoch metrics (``train_metric``/``val_metric``/... as in the reference) are views of
+a per-stage float64 accumulator that the kernel updates in place.
 """
 from __future__ import annotations
 
@@ -21,9 +22,10 @@ from torch import Tensor
 
 from ..data.common import inverse_returns_covariance
 from ..engine.module import LightningModule
-from ..metrics import MeanAbsoluteError, MeanSquaredError, MultivariateGaussianNLLLoss
+from ..metrics import (LinkedMAE, LinkedMSE, LinkedNLL, LinkedTotal, MeanAbsoluteError, MetricAccumulator,
+                       MultivariateGaussianNLLLoss)
 from ..ops import lstm as lstm_op
-from ..ops.losses import decoder_losses
+from ..ops.losses import heads_losses
 
 
 class LSTMStack(torch.nn.Module):
@@ -37,7 +39,8 @@ class LSTMStack(torch.nn.Module):
         self._flat_names = []
         for l in range(num_layers):
             fin = input_size if l == 0 else hidden_size
-            for name, shape in ((f"weight_ih_l{l}", (4 * hidden_size, fin)), (f"weight_hh_l{l}", (4 * hidden_size, hidden_size)),
+            for name, shape in ((f"weight_ih_l{l}", (4 * hidden_size, fin)),
+                                (f"weight_hh_l{l}", (4 * hidden_size, hidden_size)),
                                 (f"bias_ih_l{l}", (4 * hidden_size,)), (f"bias_hh_l{l}", (4 * hidden_size,))):
                 self.register_parameter(name, torch.nn.Parameter(torch.empty(shape)))
                 self._flat_names.append(name)
@@ -64,11 +67,15 @@ class LSTMStack(torch.nn.Module):
             out, _, _ = torch._VF.lstm(x, (h0, h0), self.flat_weights, True, self.num_layers, self.dropout,
                                        self.training, False, True)
             return out[:, -1, :]
-        return lstm_op.lstm_last_hidden(x, self.flat_weights, self.num_layers, self.dropout if self.num_layers > 1
-                                        else 0.0, self.training, precision)
+        return lstm_op.lstm_last_hidden(x, self.flat_weights, self.num_layers,
+                                        self.dropout if self.num_layers > 1 else 0.0, self.training, precision)
 
 
 class FinancialLstm(LightningModule):
+    # (c_nll, c_mse) of the training loss; subclasses override
+    loss_coefficients = (0.0, 1.0)
+    want_nll = False
+
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
                  nll_mode: str = "reference", optimizer: str = "adam"):
@@ -76,14 +83,17 @@ class FinancialLstm(LightningModule):
         self.lstm = LSTMStack(input_size, hidden_size, num_layers, dropout if num_layers > 1 else 0)
         self.alpha_head = torch.nn.Linear(hidden_size, 1)
         self.beta_head = torch.nn.Linear(hidden_size, 1)
-        self.test_mae = MeanAbsoluteError()
-        self.test_nll = MultivariateGaussianNLLLoss()
+        # per-stage device accumulators updated inside the fused loss kernel
+        self.train_acc = MetricAccumulator()
+        self.val_acc = MetricAccumulator()
+        self.test_acc = MetricAccumulator()
+        self.test_mae = LinkedMAE(self.test_acc)
+        self.test_nll = LinkedNLL(self.test_acc)
         self.test_results = None
         self.backend = backend
         self.nll_mode = nll_mode
         self.optimizer_kind = optimizer
         self.matmul_precision = "high"
-        # defaults for direct (non-subclass) use; subclasses overwrite via save_hyperparameters
         self._hparams.update(dict(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers,
                                   dropout=dropout, learning_rate=learning_rate, weight_decay=weight_decay))
 
@@ -110,23 +120,24 @@ class FinancialLstm(LightningModule):
         inv_psi = batch[3].flatten(0, 1)  # (B*K,)
         return context, target, factor, inv_psi, int(batch[0].shape[0])
 
-    def _losses(self, batch, want_nll: bool):
+    def _losses(self, batch, want_nll: bool, acc: MetricAccumulator, coeffs=None):
+        """Encoder + fused heads/losses; returns (mse, nll, mae, total) and accumulates ``acc``."""
         context, target, factor, inv_psi, B = self._unpack(batch)
-        ab = self.heads(self.encode(context))
-        mse, nll, mae = decoder_losses(ab, target, factor, inv_psi, batch_windows=B, want_nll=want_nll,
-                                       nll_mode=self.nll_mode)
-        return mse, nll, mae, target.shape[0] * target.shape[1]
+        h = self.encode(context)
+        c_nll, c_mse = coeffs if coeffs is not None else self.loss_coefficients
+        _, mse, nll, mae, total = heads_losses(
+            h, self.alpha_head.weight, self.alpha_head.bias, self.beta_head.weight, self.beta_head.bias, target,
+            factor, inv_psi, batch_windows=B, want_nll=want_nll, nll_mode=self.nll_mode, c_nll=c_nll, c_mse=c_mse,
+            acc=acc.acc)
+        return mse, nll, mae, total
 
     # ---- test hooks (`src/model.py:111-147`) ---------------------------------------------
     def on_test_start(self):
         self.test_results = {"test_loss": {"mae": None, "nll": None}}
-        self.test_mae.reset()
-        self.test_nll.reset()
+        self.test_acc.reset()
 
     def test_step(self, batch, batch_idx):
-        mse, nll, mae, count = self._losses(batch, want_nll=True)
-        self.test_mae.update_from(mae * count, count)
-        self.test_nll.update_from(nll)
+        self._losses(batch, want_nll=True, acc=self.test_acc)
 
     def on_test_end(self):
         self.test_results["test_loss"]["mae"] = float(self.test_mae.compute().cpu().item())
@@ -151,79 +162,87 @@ class FinancialLstm(LightningModule):
         r_inv_cov = inverse_returns_covariance(beta, torch.diag(inv_psi), fac[1])
         return MultivariateGaussianNLLLoss.multivariate_gaussian_nll_loss(r_mean, r_inv_cov, target[:, :, 0])
 
+    def _log_stage(self, stage: str, acc: MetricAccumulator, names) -> None:
+        linked = {"mse": LinkedMSE, "nll": LinkedNLL}
+        for n in names:
+            m = getattr(self, f"_{stage}_{n}_view", None)
+            if m is None:
+                m = linked[n](acc)
+                object.__setattr__(self, f"_{stage}_{n}_view", m)
+            self.log(f"loss/{n}/{stage}", m, on_step=False, on_epoch=True)
+        tot = getattr(self, f"_{stage}_total_view", None)
+        if tot is None:
+            tot = LinkedTotal(acc)
+            object.__setattr__(self, f"_{stage}_total_view", tot)
+        self.log(f"loss/total/{stage}", tot, on_step=False, on_epoch=True)
+
 
 class FinancialLstmMse(FinancialLstm):
+    loss_coefficients = (0.0, 1.0)
+    want_nll = False
+
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
                  nll_mode: str = "reference", optimizer: str = "adam"):
         super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
                          nll_mode=nll_mode, optimizer=optimizer)
         self.save_hyperparameters()
-        self.train_metric = MeanSquaredError()
-        self.val_metric = MeanSquaredError()
+        self.train_metric = LinkedMSE(self.train_acc)
+        self.val_metric = LinkedMSE(self.val_acc)
 
     def training_step(self, batch, batch_idx):
-        mse, _, _, count = self._losses(batch, want_nll=False)
-        self.train_metric.update_from(mse.detach() * count, count)
-        self.log("loss/mse/train", self.train_metric, on_step=False, on_epoch=True)
-        self.log("loss/total/train", mse, on_step=False, on_epoch=True)
-        return mse
+        _, _, _, loss = self._losses(batch, want_nll=False, acc=self.train_acc)
+        self._log_stage("train", self.train_acc, ("mse",))
+        return loss
 
     def validation_step(self, batch, batch_idx):
-        mse, _, _, count = self._losses(batch, want_nll=False)
-        self.val_metric.update_from(mse.detach() * count, count)
-        self.log("loss/mse/val", self.val_metric, on_step=False, on_epoch=True)
-        self.log("loss/total/val", mse, on_step=False, on_epoch=True)
+        self._losses(batch, want_nll=False, acc=self.val_acc)
+        self._log_stage("val", self.val_acc, ("mse",))
 
 
 class FinancialLstmNll(FinancialLstm):
+    loss_coefficients = (1.0, 0.0)
+    want_nll = True
+
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
                  nll_mode: str = "reference", optimizer: str = "adam"):
         super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
                          nll_mode=nll_mode, optimizer=optimizer)
         self.save_hyperparameters()
-        self.train_metric = MultivariateGaussianNLLLoss()
-        self.val_metric = MultivariateGaussianNLLLoss()
+        self.train_metric = LinkedNLL(self.train_acc)
+        self.val_metric = LinkedNLL(self.val_acc)
 
     def training_step(self, batch, batch_idx):
-        _, nll, _, _ = self._losses(batch, want_nll=True)
-        self.train_metric.update_from(nll)
-        self.log("loss/nll/train", self.train_metric, on_step=False, on_epoch=True)
-        self.log("loss/total/train", nll, on_step=False, on_epoch=True)
-        return nll
+        _, _, _, loss = self._losses(batch, want_nll=True, acc=self.train_acc)
+        self._log_stage("train", self.train_acc, ("nll",))
+        return loss
 
     def validation_step(self, batch, batch_idx):
-        _, nll, _, _ = self._losses(batch, want_nll=True)
-        self.val_metric.update_from(nll)
-        self.log("loss/nll/val", self.val_metric, on_step=False, on_epoch=True)
-        self.log("loss/total/val", nll, on_step=False, on_epoch=True)
+        self._losses(batch, want_nll=True, acc=self.val_acc)
+        self._log_stage("val", self.val_acc, ("nll",))
 
 
 class FinancialLstmCombined(FinancialLstm):
+    want_nll = True
+
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,
                  backend: str = "auto", nll_mode: str = "reference", optimizer: str = "adam"):
         super().__init__(input_size, hidden_size, num_layers, dropout, learning_rate, weight_decay, backend=backend,
                          nll_mode=nll_mode, optimizer=optimizer)
         self.save_hyperparameters()
-        self.train_mse = MeanSquaredError()
-        self.train_nll = MultivariateGaussianNLLLoss()
-        self.val_mse = MeanSquaredError()
-        self.val_nll = MultivariateGaussianNLLLoss()
-
-    def _step(self, batch, mse_m, nll_m, stage: str):
-        mse, nll, _, count = self._losses(batch, want_nll=True)
-        mse_m.update_from(mse.detach() * count, count)
-        nll_m.update_from(nll)
-        self.log(f"loss/mse/{stage}", mse_m, on_step=False, on_epoch=True)
-        self.log(f"loss/nll/{stage}", nll_m, on_step=False, on_epoch=True)
-        loss = nll + self.hparams.mse_weight * mse
-        self.log(f"loss/total/{stage}", loss, on_step=False, on_epoch=True)
-        return loss
+        self.loss_coefficients = (1.0, float(mse_weight))  # loss = nll + mse_weight * mse (src/model.py:317)
+        self.train_mse = LinkedMSE(self.train_acc)
+        self.train_nll = LinkedNLL(self.train_acc)
+        self.val_mse = LinkedMSE(self.val_acc)
+        self.val_nll = LinkedNLL(self.val_acc)
 
     def training_step(self, batch, batch_idx):
-        return self._step(batch, self.train_mse, self.train_nll, "train")
+        _, _, _, loss = self._losses(batch, want_nll=True, acc=self.train_acc)
+        self._log_stage("train", self.train_acc, ("mse", "nll"))
+        return loss
 
     def validation_step(self, batch, batch_idx):
-        self._step(batch, self.val_mse, self.val_nll, "val")
+        self._losses(batch, want_nll=True, acc=self.val_acc)
+        self._log_stage("val", self.val_acc, ("mse", "nll"))

@@ -1,8 +1,10 @@
-"""Fused decoder losses (reference K5-K9: `src/model.py:45-69,176-331`, `src/common.py:50-78`).
+"""Fused alpha/beta heads + decoder losses (reference K4-K9: `src/model.py:45-69,96-108,176-331`,
+`src/common.py:50-78`).
 
-``decoder_losses(ab, y, factor, inv_psi)`` returns ``(mse, nll, mae)`` for
-``ab = [alpha | beta]`` (N, 2) and target windows ``y`` (N, n, C) with channel 0
-the stock and channel 1 the market return:
+``heads_losses(h, wa, ba, wb, bb, y, factor, inv_psi)`` evaluates the two
+``Linear(H, 1)`` heads on the encoder state ``h`` (N, H) and returns
+``(ab, mse, nll, mae, total)`` for target windows ``y`` (N, n, C) (channel 0 the
+stock, channel 1 the market return):
 
 * MSE decoder ``r_hat = alpha + beta * r_mkt``, mean over all N*n elements;
 * Gaussian NLL with ``mu = alpha + beta * f_mean`` and the Woodbury inverse
@@ -20,18 +22,23 @@ the stock and channel 1 the market return:
       dNLL/db_i = n w_i b_i / den - f_mean (w_i SD_i - w_i b_i U1 / den)
                   - w_i UD_i / den + U2 w_i b_i / den^2
 
-* MAE (test metric, `src/model.py:139`), no gradient.
+* MAE (test metric, `src/model.py:139`), no gradient;
+* ``total = c_nll * NLL + c_mse * MSE`` (the model's training loss).
 
 Batch semantics: ``nll_mode='reference'`` reproduces the reference exactly (one
 Gaussian over all B*K sequences using window 0's factor, SURVEY Q1);
 ``'per_window'`` sums the per-window NLLs (the statistically correct batched loss).
-The GPU path is one HIP kernel (``csrc/losses.hip``) that also emits the
-gradients, so backward is a single tiny elementwise kernel.
+
+GPU path: ONE HIP kernel (``csrc/losses.hip``) computes the heads, every loss, the
+per-sequence gradients and adds the epoch metric sums into ``acc`` (8 float64:
+sse, count, nll_sum, nll_updates, total_sum, total_weight, sae, count); backward is
+one kernel producing dh and accumulating the head weight gradients directly into
+the parameters' ``.grad`` views.
 """
 from __future__ import annotations
 
 import math
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 from torch import Tensor
@@ -41,41 +48,84 @@ from ._lib import lib, use_hip
 LOG2PI = math.log(2 * math.pi)
 
 
-def _windows(N: int, K: int, B: int, nll_mode: str) -> Tuple[int, int, int]:
+def _windows(N: int, B: int, nll_mode: str) -> Tuple[int, int, int]:
     if nll_mode == "per_window":
-        return B, K, 2
+        return B, N // B, 2
     return 1, N, 0
 
 
-class _DecoderLossesFn(torch.autograd.Function):
+def _c(t: Optional[Tensor]) -> Optional[Tensor]:
+    return None if t is None else t.contiguous().float()
+
+
+def _grad_buffer(p: Tensor) -> Tensor:
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+class _HeadsLossesFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, windows: int, kwin: int,
-                factor_stride: int, want_nll: bool):
+    def forward(ctx, h: Tensor, wa: Tensor, ba: Tensor, wb: Tensor, bb: Tensor, y: Tensor, factor: Tensor,
+                inv_psi: Tensor, windows: int, kwin: int, fstride: int, want_nll: bool, c_nll: float, c_mse: float,
+                batch_weight: float, acc: Optional[Tensor]):
+        C = lib()
+        N = h.shape[0]
+        dev = h.device
+        out = torch.empty(4, device=dev, dtype=torch.float32)
+        g = torch.empty((2, N, 2), device=dev, dtype=torch.float32)
+        ab = torch.empty((N, 2), device=dev, dtype=torch.float32)
+        C.heads_losses(h, wa, ba, wb, bb, ab, y, factor, inv_psi, windows, kwin, fstride, bool(want_nll),
+                       float(c_nll), float(c_mse), float(batch_weight), out, g[0], g[1], acc)
+        ctx.save_for_backward(g, h)
+        ctx.params = (wa, ba, wb, bb)
+        ctx.want_nll, ctx.c_nll, ctx.c_mse = bool(want_nll), float(c_nll), float(c_mse)
+        mse, nll, mae, total = out[0], out[1], out[2], out[3]
+        ctx.mark_non_differentiable(ab, mae)
+        ctx.set_materialize_grads(False)
+        return ab, mse, nll, mae, total
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_ab, g_mse, g_nll, g_mae, g_total):
+        g, h = ctx.saved_tensors
+        wa, ba, wb, bb = ctx.params
+        dh = torch.empty_like(h) if ctx.needs_input_grad[0] else None
+        lib().heads_losses_bwd(_c(g_mse), _c(g_nll), _c(g_total), ctx.c_nll, ctx.c_mse, g[0], g[1], ctx.want_nll, h, wa, wb, dh, None,
+                               _grad_buffer(wa), _grad_buffer(ba), _grad_buffer(wb), _grad_buffer(bb))
+        return (dh,) + (None,) * 15
+
+
+class _DecoderLossesFn(torch.autograd.Function):
+    """Losses from a precomputed ``ab`` (N, 2) — for encoders whose heads are not fused."""
+
+    @staticmethod
+    def forward(ctx, ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, windows: int, kwin: int, fstride: int,
+                want_nll: bool, c_nll: float, c_mse: float, batch_weight: float, acc: Optional[Tensor]):
         C = lib()
         N = ab.shape[0]
         out = torch.empty(4, device=ab.device, dtype=torch.float32)
         g = torch.empty((2, N, 2), device=ab.device, dtype=torch.float32)
-        C.decoder_losses(ab.contiguous(), y, factor, inv_psi, windows, kwin, factor_stride, bool(want_nll), out, g[0],
-                         g[1])
+        C.decoder_losses(ab.contiguous(), y, factor, inv_psi, windows, kwin, fstride, bool(want_nll), float(c_nll),
+                         float(c_mse), float(batch_weight), out, g[0], g[1], acc)
         ctx.save_for_backward(g)
-        ctx.want_nll = bool(want_nll)
-        mse, nll, mae = out[0], out[1], out[2]
+        ctx.want_nll, ctx.c_nll, ctx.c_mse = bool(want_nll), float(c_nll), float(c_mse)
+        mse, nll, mae, total = out[0], out[1], out[2], out[3]
         ctx.mark_non_differentiable(mae)
-        return mse, nll, mae
+        ctx.set_materialize_grads(False)
+        return mse, nll, mae, total
 
     @staticmethod
     @torch.autograd.function.once_differentiable
-    def backward(ctx, g_mse: Tensor, g_nll: Tensor, g_mae: Tensor):
+    def backward(ctx, g_mse, g_nll, g_mae, g_total):
         (g,) = ctx.saved_tensors
-        gout = torch.stack([
-            g_mse if g_mse is not None else g.new_zeros(()),
-            g_nll if g_nll is not None else g.new_zeros(()),
-        ]).contiguous()
         dab = torch.empty_like(g[0])
-        lib().decoder_losses_bwd(gout, g[0], g[1], dab, ctx.want_nll and g_nll is not None)
-        return dab, None, None, None, None, None, None, None
+        lib().heads_losses_bwd(_c(g_mse), _c(g_nll), _c(g_total), ctx.c_nll, ctx.c_mse, g[0], g[1], ctx.want_nll, None, None, None, None, dab,
+                               None, None, None, None)
+        return (dab,) + (None,) * 11
 
 
+# --------------------------------------------------------------------------- CPU (PyTorch) path
 def woodbury_nll_torch(alpha: Tensor, beta: Tensor, f_mean: Tensor, f_var: Tensor, inv_psi: Tensor,
                        r: Tensor) -> Tensor:
     """Closed-form NLL in PyTorch ops (CPU path; autograd supplies the gradients)."""
@@ -89,29 +139,56 @@ def woodbury_nll_torch(alpha: Tensor, beta: Tensor, f_mean: Tensor, f_var: Tenso
     return 0.5 * (n * (K * LOG2PI - logdet) + quad)
 
 
-def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, batch_windows: int = 1,
-                   want_nll: bool = True, nll_mode: str = "reference") -> Tuple[Tensor, Tensor, Tensor]:
-    """(mse, nll, mae) for ``ab (N,2)``, ``y (N, n, C)``, ``factor (B, 2)``, ``inv_psi (N,)``.
-
-    ``batch_windows`` = B, the number of windows flattened into N (N = B*K).
-    """
-    N = ab.shape[0]
-    K = N // batch_windows
-    windows, kwin, fstride = _windows(N, K, batch_windows, nll_mode)
-    if use_hip(ab):
-        return _DecoderLossesFn.apply(ab, y.contiguous(), factor.contiguous(), inv_psi.contiguous(), windows, kwin,
-                                      fstride, want_nll)
+def _losses_torch(ab, y, factor, inv_psi, windows, kwin, fstride, want_nll, c_nll, c_mse, batch_weight, acc):
     alpha, beta = ab[:, 0], ab[:, 1]
     r, rm = y[..., 0], y[..., 1]
     e = alpha.unsqueeze(-1) + beta.unsqueeze(-1) * rm - r
     mse = (e * e).mean()
     mae = e.detach().abs().mean()
-    if not want_nll:
-        return mse, torch.zeros((), dtype=mse.dtype, device=mse.device), mae
-    fac = factor.reshape(-1)
-    nll = 0.0
-    for wdw in range(windows):
-        sl = slice(wdw * kwin, (wdw + 1) * kwin)
-        fm, fv = fac[wdw * fstride], fac[wdw * fstride + 1]
-        nll = nll + woodbury_nll_torch(alpha[sl], beta[sl], fm, fv, inv_psi.reshape(-1)[sl], r[sl])
-    return mse, nll, mae
+    nll = torch.zeros((), dtype=mse.dtype, device=mse.device)
+    if want_nll:
+        fac = factor.reshape(-1)
+        ip = inv_psi.reshape(-1)
+        for wdw in range(windows):
+            sl = slice(wdw * kwin, (wdw + 1) * kwin)
+            nll = nll + woodbury_nll_torch(alpha[sl], beta[sl], fac[wdw * fstride], fac[wdw * fstride + 1], ip[sl],
+                                           r[sl])
+    total = c_nll * nll + c_mse * mse
+    if acc is not None:
+        with torch.no_grad():
+            cnt = float(e.numel())
+            acc += torch.tensor([float((e * e).sum()), cnt, float(nll), 1.0, float(total) * batch_weight,
+                                 batch_weight, float(e.abs().sum()), cnt], dtype=acc.dtype, device=acc.device)
+    return mse, nll, mae, total
+
+
+# --------------------------------------------------------------------------- public API
+def heads_losses(h: Tensor, wa: Tensor, ba: Tensor, wb: Tensor, bb: Tensor, y: Tensor, factor: Tensor,
+                 inv_psi: Tensor, *, batch_windows: int = 1, want_nll: bool = True, nll_mode: str = "reference",
+                 c_nll: float = 0.0, c_mse: float = 1.0, acc: Optional[Tensor] = None):
+    """Returns ``(ab, mse, nll, mae, total)``; ``wa``/``wb`` are the (1, H) head weights, ``ba``/``bb`` (1,)."""
+    N = h.shape[0]
+    windows, kwin, fstride = _windows(N, batch_windows, nll_mode)
+    if use_hip(h):
+        return _HeadsLossesFn.apply(h.contiguous(), wa, ba, wb, bb, y.contiguous(), factor.contiguous(),
+                                    inv_psi.contiguous(), windows, kwin, fstride, want_nll, c_nll, c_mse,
+                                    float(batch_windows), acc)
+    ab = torch.addmm(torch.cat([ba, bb]), h, torch.cat([wa, wb], 0).t())
+    mse, nll, mae, total = _losses_torch(ab, y, factor, inv_psi, windows, kwin, fstride, want_nll, c_nll, c_mse,
+                                         float(batch_windows), acc)
+    return ab, mse, nll, mae, total
+
+
+def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, batch_windows: int = 1,
+                   want_nll: bool = True, nll_mode: str = "reference", c_nll: float = 0.0, c_mse: float = 1.0,
+                   acc: Optional[Tensor] = None, with_total: bool = False):
+    """(mse, nll, mae[, total]) for ``ab (N,2)``, ``y (N, n, C)``, ``factor (B, 2)``, ``inv_psi (N,)``."""
+    N = ab.shape[0]
+    windows, kwin, fstride = _windows(N, batch_windows, nll_mode)
+    if use_hip(ab):
+        res = _DecoderLossesFn.apply(ab, y.contiguous(), factor.contiguous(), inv_psi.contiguous(), windows, kwin,
+                                     fstride, want_nll, c_nll, c_mse, float(batch_windows), acc)
+    else:
+        res = _losses_torch(ab, y, factor, inv_psi, windows, kwin, fstride, want_nll, c_nll, c_mse,
+                            float(batch_windows), acc)
+    return res if with_total else res[:3]

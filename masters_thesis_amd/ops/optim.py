@@ -79,6 +79,7 @@ class FusedAdam:
         self.lr_t = torch.tensor([lr], device=dev, dtype=torch.float32)
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.grad_norm = torch.zeros(1, device=dev, dtype=torch.float32)
+        self.nonfinite = torch.zeros(1, device=dev, dtype=torch.float32)  # steps with a NaN/Inf grad norm
         self.betas = tuple(float(b) for b in betas)
         self.eps = float(eps)
         self.weight_decay = float(weight_decay)
@@ -119,7 +120,7 @@ class FusedAdam:
             C.grad_sqnorm(f.grad, float(grad_scale), self.partials, self.step_t)
             C.adam(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.lr_t, self.step_t, b1, b2,
                    self.eps, self.weight_decay, float(max_norm or 0.0), float(grad_scale), self.adamw,
-                   self.grad_norm)
+                   self.grad_norm, self.nonfinite)
             return
         self._step_torch(max_norm, grad_scale)
 
@@ -134,6 +135,8 @@ class FusedAdam:
         norms = torch.stack([v.norm() for v in f.views(g)])
         total = norms.norm()
         self.grad_norm.copy_(total.reshape(1))
+        if not torch.isfinite(total):
+            self.nonfinite += 1
         if max_norm and max_norm > 0:
             coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
             g.mul_(coef)

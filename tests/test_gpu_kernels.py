@@ -165,3 +165,86 @@ def test_flat_grads_survive_backward():
     lin(torch.randn(3, 8, device=DEV)).sum().backward()
     assert lin.weight.grad.data_ptr() == ptr
     assert flat.grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("coeffs", [(0.0, 1.0), (1.0, 0.0), (1.0, 100.0)])
+def test_heads_losses_grads_and_metric_accumulator(coeffs):
+    from masters_thesis_amd.ops.losses import heads_losses
+
+    torch.manual_seed(5)
+    N, H, n = 100, 64, 30
+    h = torch.randn(N, H, dtype=torch.float64) * 0.5
+    wa, ba = torch.randn(1, H, dtype=torch.float64) * 0.1, torch.randn(1, dtype=torch.float64) * 0.1
+    wb, bb = torch.randn(1, H, dtype=torch.float64) * 0.1, torch.ones(1, dtype=torch.float64)
+    y = torch.randn(N, n, 4, dtype=torch.float64)
+    factor = torch.tensor([[0.05, 0.3]], dtype=torch.float64)
+    inv_psi = torch.rand(N, dtype=torch.float64) * 3 + 1
+    ref_in = [t.clone().requires_grad_(True) for t in (h, wa, ba, wb, bb)]
+    ab, mse_r, nll_r, _, tot_r = heads_losses(*ref_in, y, factor, inv_psi, c_nll=coeffs[0], c_mse=coeffs[1])
+    tot_r.backward()
+    gin = [t.float().to(DEV).requires_grad_(True) for t in (h, wa, ba, wb, bb)]
+    acc = torch.zeros(8, dtype=torch.float64, device=DEV)
+    _, mse, nll, mae, tot = heads_losses(*gin, y.float().to(DEV), factor.float().to(DEV), inv_psi.float().to(DEV),
+                                        c_nll=coeffs[0], c_mse=coeffs[1], acc=acc)
+    tot.backward()
+    assert abs(tot.item() - tot_r.item()) <= 3e-5 * abs(tot_r.item()) + 1e-4
+    for a, b in zip(gin, ref_in):
+        torch.testing.assert_close(a.grad.double().cpu(), b.grad, rtol=5e-4, atol=5e-5)
+    a = acc.cpu()
+    assert abs(a[0] / a[1] - mse_r.item()) < 1e-5 and a[3] == 1 and abs(a[4] / a[5] - tot_r.item()) < 1e-3 * abs(
+        tot_r.item()) + 1e-3
+
+
+def test_gather_batch_kernel_and_cursor():
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+
+    W = 37
+    X = torch.randn(W, 5, 6, 3, device=DEV)
+    Y = torch.randn(W, 5, 4, 4, device=DEV)
+    Fc = torch.randn(W, 2, device=DEV)
+    P = torch.randn(W, 5, device=DEV)
+    ld = TensorBatchLoader([X, Y, Fc, P], 4, shuffle=True, seed=3, start=2, stop=33)
+    assert ld.supports_static()
+    nfull = ld.begin_epoch(1)
+    idx = ld._epoch_idx
+    for k in range(nfull):
+        bufs = ld.gather_static()
+        sel = idx[k * 4:(k + 1) * 4].to(DEV).long()
+        for s, b in zip((X, Y, Fc, P), bufs):
+            torch.testing.assert_close(b, s.index_select(0, sel), rtol=0, atol=0)
+    assert int(ld._cursor.item()) == nfull and int(ld._arrive.item()) == 0
+    tail = ld.tail_batch()
+    assert tail is not None and tail[0].shape[0] == idx.numel() - 4 * nfull
+
+
+def test_train_step_graph_matches_eager():
+    """A captured train step (gather + fwd + bwd + clip/Adam in one graph) equals eager steps."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import FinancialLstmCombined
+
+    def run(graphs):
+        torch.manual_seed(11)
+        model = FinancialLstmCombined(dropout=0.0)
+        W = 12
+        g = torch.Generator().manual_seed(0)
+        data = [torch.randn(W, 100, 60, 3, generator=g), torch.randn(W, 100, 30, 4, generator=g),
+                torch.stack([torch.randn(W, generator=g) * 0.1, torch.rand(W, generator=g) + 0.2], -1),
+                torch.rand(W, 100, generator=g) * 3 + 1]
+        ld = TensorBatchLoader([d.to(DEV) for d in data], 1, shuffle=True, seed=0)
+        tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=graphs, matmul_precision="highest")
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.train()
+        step = tr.make_train_stepper(ld)
+        for _ in range(8):
+            step()
+        torch.cuda.synchronize()
+        return tr.flat.data.clone(), model.train_acc.acc.clone()
+
+    p_eager, acc_eager = run(False)
+    p_graph, acc_graph = run(True)
+    torch.testing.assert_close(p_graph, p_eager, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(acc_graph, acc_eager, rtol=1e-6, atol=1e-6)
