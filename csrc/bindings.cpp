@@ -35,6 +35,15 @@ void mta_adam(float* p, float* g, float* m, float* v, long n, const float* parti
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
               float* norm_out, float* nonfinite, hipStream_t st);
 void mta_scale(float* x, long n, float s, hipStream_t st);
+// host/prefetch.cpp
+void* mta_prefetch_create(int ntensors, const void* const* host, const long* row_bytes, void* const* staging, int B,
+                          int R, int nthreads);
+void mta_prefetch_start(void* h, const long* idx, long n_idx, long n_batches);
+int mta_prefetch_wait(void* h, long batch, long timeout_ms);
+int mta_prefetch_ready(void* h, long batch);
+void mta_prefetch_release(void* h, long batch);
+void mta_prefetch_stop(void* h);
+void mta_prefetch_destroy(void* h);
 }
 
 namespace {
@@ -280,7 +289,74 @@ void scale_(at::Tensor x, double s) {
 
 }  // namespace
 
+// Native pinned-ring prefetcher (residency=stream).  Holds references to the host dataset and
+// staging tensors so their storage outlives the worker threads.
+class HostPrefetcher {
+ public:
+  HostPrefetcher(std::vector<at::Tensor> host, std::vector<at::Tensor> staging, int64_t B, int64_t R,
+                 int64_t nthreads)
+      : host_(std::move(host)), staging_(std::move(staging)) {
+    TORCH_CHECK(host_.size() == staging_.size() && !host_.empty(), "prefetch: host/staging tensor lists differ");
+    std::vector<const void*> hp;
+    std::vector<void*> sp;
+    std::vector<long> rb;
+    for (size_t t = 0; t < host_.size(); ++t) {
+      auto& h = host_[t];
+      auto& s = staging_[t];
+      TORCH_CHECK(!h.is_cuda() && h.is_contiguous(), "prefetch: host tensors must be contiguous CPU tensors");
+      TORCH_CHECK(!s.is_cuda() && s.is_contiguous() && s.dtype() == h.dtype(), "prefetch: bad staging tensor");
+      const long row = h.dim() > 1 ? (long)(h.numel() / h.size(0)) * (long)h.element_size() : (long)h.element_size();
+      TORCH_CHECK((long)s.numel() * (long)s.element_size() >= (long)(R * B) * row, "prefetch: staging too small");
+      hp.push_back(h.data_ptr());
+      sp.push_back(s.data_ptr());
+      rb.push_back(row);
+      rows_ = h.size(0);
+    }
+    h_ = mta_prefetch_create((int)host_.size(), hp.data(), rb.data(), sp.data(), (int)B, (int)R, (int)nthreads);
+  }
+  ~HostPrefetcher() { close(); }
+  void start(at::Tensor idx, int64_t n_batches) {
+    TORCH_CHECK(!idx.is_cuda() && idx.dtype() == at::kLong && idx.is_contiguous(), "prefetch: idx must be int64 CPU");
+    if (idx.numel()) {
+      TORCH_CHECK(idx.min().item<int64_t>() >= 0 && idx.max().item<int64_t>() < rows_, "prefetch: index out of range");
+    }
+    idx_ = idx;
+    mta_prefetch_start(h_, idx.data_ptr<int64_t>(), (long)idx.numel(), (long)n_batches);
+  }
+  int64_t wait(int64_t b, int64_t timeout_ms) {
+    py::gil_scoped_release nogil;
+    return mta_prefetch_wait(h_, (long)b, (long)timeout_ms);
+  }
+  bool ready(int64_t b) { return mta_prefetch_ready(h_, (long)b) != 0; }
+  void release(int64_t b) { mta_prefetch_release(h_, (long)b); }
+  void stop() {
+    py::gil_scoped_release nogil;
+    if (h_) mta_prefetch_stop(h_);
+  }
+  void close() {
+    if (h_) {
+      py::gil_scoped_release nogil;
+      mta_prefetch_destroy(h_);
+      h_ = nullptr;
+    }
+  }
+
+ private:
+  std::vector<at::Tensor> host_, staging_;
+  at::Tensor idx_;
+  int64_t rows_ = 0;
+  void* h_ = nullptr;
+};
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  py::class_<HostPrefetcher>(m, "HostPrefetcher")
+      .def(py::init<std::vector<at::Tensor>, std::vector<at::Tensor>, int64_t, int64_t, int64_t>())
+      .def("start", &HostPrefetcher::start)
+      .def("wait", &HostPrefetcher::wait, py::arg("batch"), py::arg("timeout_ms") = -1)
+      .def("ready", &HostPrefetcher::ready)
+      .def("release", &HostPrefetcher::release)
+      .def("stop", &HostPrefetcher::stop)
+      .def("close", &HostPrefetcher::close);
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
   m.def("lstm_fwd_layer", &lstm_fwd_layer);
   m.def("lstm_bwd_layer", &lstm_bwd_layer);

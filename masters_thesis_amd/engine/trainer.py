@@ -111,6 +111,7 @@ class Trainer:
         self.model = None
         self.datamodule = None
         self._graphs: Dict[Tuple, _Graph] = {}
+        self._graph_loaders: Dict[int, Any] = {}  # keeps loaders alive while graphs key on id(loader)
         self._eager_counts: Dict[Tuple, int] = {}
         self.step_timer = StepTimer()
         self.perf: Dict[str, float] = {}
@@ -275,18 +276,29 @@ class Trainer:
             return g.replay()
         return g.replay(provider())
 
+    def _static_hooks(self, loader):
+        """Streaming loaders stage batch ``s`` (H2D on their copy stream) before and fence after a step."""
+        self._graph_loaders[id(loader)] = loader
+        return getattr(loader, "before_static_step", None), getattr(loader, "after_static_step", None)
+
     def _train_step(self, loader, batch_idx: int, static: bool, batch=None):
         if static:
             B = loader.batch_size
             self.model._current_batch_size = B
-            out = self._run(("train", B, True), loader.gather_static, lambda b: self._train_body(b, batch_idx), True,
+            pre, post = self._static_hooks(loader)
+            if pre is not None:
+                pre()
+            out = self._run(("train", B, True, id(loader)), loader.gather_static, lambda b: self._train_body(b, batch_idx), True,
                             self.graph_warmup_steps)
+            if post is not None:
+                post()
         else:
             B = _batch_size(batch)
             self.model._current_batch_size = B
             out = self._run(("train", B, False), lambda: batch, lambda b: self._train_body(b, batch_idx), False,
                             self.graph_warmup_steps)
-        if self._graphs_enabled() and (("train", B, static) in self._graphs):
+        key = ("train", B, True, id(loader)) if static else ("train", B, False)
+        if self._graphs_enabled() and key in self._graphs:
             self._after_graph()
         return out
 
@@ -296,7 +308,13 @@ class Trainer:
         if static:
             B = loader.batch_size
             model._current_batch_size = B
-            return self._run((stage, B, True), loader.gather_static, lambda b: fn(b, batch_idx), True, 1)
+            pre, post = self._static_hooks(loader)
+            if pre is not None:
+                pre()
+            out = self._run((stage, B, True, id(loader)), loader.gather_static, lambda b: fn(b, batch_idx), True, 1)
+            if post is not None:
+                post()
+            return out
         B = _batch_size(batch)
         model._current_batch_size = B
         return self._run((stage, B, False), lambda: batch, lambda b: fn(b, batch_idx), False, 1)

@@ -67,6 +67,11 @@ def sources() -> List[Path]:
     return sorted(CSRC.glob("*.hip"))
 
 
+def host_sources() -> List[Path]:
+    """Host-only C++ runtime pieces (prefetcher, ...): plain C++17, no HIP, no torch."""
+    return sorted((CSRC / "host").glob("*.cpp"))
+
+
 def _compile(cmd: List[str], verbose: bool) -> None:
     if verbose:
         print(" ".join(cmd), flush=True)
@@ -94,6 +99,14 @@ def build(verbose: bool = False, force: bool = False, debug: bool = False, jobs:
         objs.append(obj)
         if force or not obj.exists():
             jobs_list.append(([hipcc, *kflags, "-c", str(src), "-o", str(obj)], obj))
+    hflags = ["-std=c++17", "-fPIC", "-O3", "-pthread", f"-I{CSRC}"]
+    cxx = shutil.which("g++") or shutil.which("c++") or hipcc
+    for src in host_sources():
+        key = _digest([src, *headers], hflags)
+        obj = BUILD / f"host_{src.stem}-{key}.o"
+        objs.append(obj)
+        if force or not obj.exists():
+            jobs_list.append(([cxx, *hflags, "-c", str(src), "-o", str(obj)], obj))
     bsrc = CSRC / "bindings.cpp"
     bkey = _digest([bsrc], bflags)
     bobj = BUILD / f"bindings-{bkey}.o"
@@ -115,7 +128,7 @@ def build(verbose: bool = False, force: bool = False, debug: bool = False, jobs:
         for f in cf.as_completed(futs):
             f.result()
     tmp = out.with_name(out.name + f".tmp{os.getpid()}")
-    _compile([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp), *libs],
+    _compile([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *[str(o) for o in objs], "-o", str(tmp), *libs, "-pthread"],
              verbose)
     os.replace(tmp, out)
     stamp.write_text(link_key)

@@ -1,0 +1,75 @@
+"""Data-parallel correctness without a cluster: 2 gloo ranks on the CPU.
+
+World-size-2 training with one window per rank must follow the same trajectory as a
+single process with a global batch of two windows (MSE: mean of per-rank means ==
+global mean; the sharded sampler hands rank r the windows idx[r::2]), and the epoch
+metrics must be synchronised across ranks.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data(W=12):
+    g = torch.Generator().manual_seed(0)
+    return [torch.randn(W, 100, 20, 3, generator=g), torch.randn(W, 100, 10, 4, generator=g),
+            torch.stack([torch.randn(W, generator=g) * 0.1, torch.rand(W, generator=g) + 0.2], -1),
+            torch.rand(W, 100, generator=g) * 3 + 1]
+
+
+def _train(rank, world, batch, steps, out):
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import FinancialLstmMse
+    from masters_thesis_amd.parallel import dist as pdist
+
+    torch.manual_seed(7 + rank)  # different init per rank: the DDP broadcast must fix it
+    model = FinancialLstmMse(hidden_size=16, num_layers=2, dropout=0.0, learning_rate=1e-2)
+    ld = TensorBatchLoader(_data(), batch, shuffle=True, seed=0, rank=rank, world_size=world)
+    tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False, accelerator="cpu")
+    tr._setup_env()
+    tr._setup_model(model)
+    tr._configure_optimizers(model)
+    model.train()
+    step = tr.make_train_stepper(ld)
+    for _ in range(steps):
+        step()
+    ms = tr._compute_stage_metrics("train")
+    torch.save({"params": tr.flat.data.clone(), "mse": float(ms["loss/mse/train"])}, out)
+    pdist.destroy()
+
+
+def _worker(rank, world, port, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from masters_thesis_amd.parallel import dist as pdist
+
+    pdist.init_distributed(backend="gloo", device="cpu")
+    _train(rank, world, 1, 5, os.path.join(tmp, f"rank{rank}.pt"))
+
+
+@pytest.mark.timeout(300)
+def test_ddp_two_ranks_equals_single_process_global_batch(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    r1 = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    torch.testing.assert_close(r0["params"], r1["params"], rtol=0, atol=0)  # replicas stay identical
+    assert r0["mse"] == r1["mse"]  # synced metric
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    torch.manual_seed(7)
+    _train(0, 1, 2, 5, str(tmp_path / "single.pt"))
+    s = torch.load(tmp_path / "single.pt", weights_only=True)
+    torch.testing.assert_close(r0["params"], s["params"], rtol=1e-5, atol=1e-6)
+    assert abs(r0["mse"] - s["mse"]) < 1e-5 * abs(s["mse"])
