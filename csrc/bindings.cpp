@@ -13,8 +13,8 @@ int mta_lstm_fwd_layer(int H, int prec, const float* x, const float* w_ih, const
                        hipStream_t st);
 int mta_lstm_bwd_layer(int H, int prec, const float* stash, const float* w_hh, const float* dH, const float* dh_last,
                        float* dG, int N, int Np, int T, hipStream_t st);
-void mta_lstm_wgrad(const float* dG, const float* hseq, const float* inp, int inp_batch_first, int N, int Np, int T,
-                    int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, hipStream_t st);
+int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* inp, int inp_batch_first, int N, int Np,
+                   int T, int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, hipStream_t st);
 void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
                    hipStream_t st);
 void mta_gather_batch(const float* const* src, float* const* dst, const long* row_floats, int ntensors,
@@ -113,7 +113,7 @@ void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor stash, at::Tensor w_hh, 
   TORCH_CHECK(rc == 0, "lstm_bwd_layer: unsupported configuration");
 }
 
-void lstm_wgrad(at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_first, int64_t N, int64_t Np,
+void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_first, int64_t N, int64_t Np,
                 int64_t T, int64_t H, at::Tensor g_wih, at::Tensor g_whh, at::Tensor g_bih, at::Tensor g_bhh) {
   MTA_CHECK_F32(dG);
   MTA_CHECK_F32(hseq);
@@ -127,9 +127,11 @@ void lstm_wgrad(at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_f
   TORCH_CHECK(inp.numel() == (inp_batch_first ? N * T * F : T * Np * F), "bad layer-input shape");
   TORCH_CHECK(g_whh.numel() == 4 * H * H && g_bih.numel() == 4 * H && g_bhh.numel() == 4 * H, "bad grad shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dG.device());
-  mta_lstm_wgrad(dG.data_ptr<float>(), hseq.data_ptr<float>(), inp.data_ptr<float>(), inp_batch_first ? 1 : 0,
-                 (int)N, (int)Np, (int)T, (int)H, (int)F, g_wih.data_ptr<float>(), g_whh.data_ptr<float>(),
-                 g_bih.data_ptr<float>(), g_bhh.data_ptr<float>(), cur_stream());
+  const int rc = mta_lstm_wgrad((int)prec, dG.data_ptr<float>(), hseq.data_ptr<float>(), inp.data_ptr<float>(),
+                                inp_batch_first ? 1 : 0, (int)N, (int)Np, (int)T, (int)H, (int)F,
+                                g_wih.data_ptr<float>(), g_whh.data_ptr<float>(), g_bih.data_ptr<float>(),
+                                g_bhh.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "lstm_wgrad: unsupported configuration (H=", H, ", F=", F, ")");
 }
 
 void lstm_prep(at::Tensor w_ih, at::Tensor b_ih, at::Tensor b_hh, int64_t H, at::Tensor w_um, at::Tensor b_um) {

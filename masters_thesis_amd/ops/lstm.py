@@ -112,7 +112,7 @@ class _LSTMStackFn(torch.autograd.Function):
             dG = torch.empty((T, Np, 4 * H), device=dh_last.device, dtype=torch.float32)
             C.lstm_bwd_layer(H, ctx.prec, stash, w_hh, dH, None if dH is not None else dh_last, dG, N, Np, T)
             fused0 = l == 0 and F in FUSED_F
-            C.lstm_wgrad(dG, hseq, inp, fused0, N, Np, T, H, _grad_buffer(w_ih), _grad_buffer(w_hh),
+            C.lstm_wgrad(ctx.prec, dG, hseq, inp, fused0, N, Np, T, H, _grad_buffer(w_ih), _grad_buffer(w_hh),
                          _grad_buffer(b_ih), _grad_buffer(b_hh))
             dG2 = dG.view(T * Np, 4 * H)
             if l > 0:

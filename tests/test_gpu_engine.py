@@ -63,4 +63,5 @@ def test_trainer_streaming_equals_resident():
         torch.cuda.synchronize()
         return tr.flat.data.clone()
 
-    torch.testing.assert_close(run(True), run(False), rtol=0, atol=0)
+    # float atomics in the weight-gradient kernel make runs differ in the last bits
+    torch.testing.assert_close(run(True), run(False), rtol=1e-4, atol=1e-6)
