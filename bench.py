@@ -142,8 +142,9 @@ def main(argv=None):
             "dtype": "fp32" if cfg.trainer.precision == "32-true" else "bf16",
             "data": "synthetic (reference DGP, generated on device), random-init weights",
             "config": {
-                "model": f"FinancialLstm{args.loss.capitalize()} model={args.model} "
-                         f"(LSTM H={cfg.model.hidden_size} L={cfg.model.num_layers})",
+                "model": f"{type(model).__name__} model={args.model} "
+                         f"({cfg.model.get('arch', 'lstm')} H={cfg.model.hidden_size} L={cfg.model.num_layers}, "
+                         f"{sum(p.numel() for p in model.parameters())} params)",
                 "global_batch": args.batch * world,
                 "seq_len": int(cfg.datamodule.lookback_window),
                 "parallelism": f"dp{world}",

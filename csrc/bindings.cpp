@@ -35,6 +35,19 @@ void mta_adam(float* p, float* g, float* m, float* v, long n, const float* parti
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
               float* norm_out, float* nonfinite, hipStream_t st);
 void mta_scale(float* x, long n, float s, hipStream_t st);
+// gemm.hip / norm.hip / attention.hip (MLP + transformer encoders)
+int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb, float alpha,
+                  int flags, const float* bias, const float* resid, const void* aux_in, const uint64_t* seed,
+                  float drop_p, void* out_bf16, float* out_f32, void* aux_pre, int ldc, int n_store, int ksplit,
+                  float* bias_grad, hipStream_t st);
+int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
+                 const int* rows_p, const int* cols_p, const int* ld_src, hipStream_t st);
+int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
+             const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
+             float drop_p, const float* dy, const float* dres, const void* pre, void* dx_bf16, float* dx_f32,
+             float* dgamma, float* dbeta, hipStream_t st);
+int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
+                  int D, int heads, float rope_base, hipStream_t st);
 // host/prefetch.cpp
 void* mta_prefetch_create(int ntensors, const void* const* host, const long* row_bytes, void* const* staging, int B,
                           int R, int nthreads);
@@ -291,6 +304,135 @@ void scale_(at::Tensor x, double s) {
 
 }  // namespace
 
+
+// ------------------------------------------------------------------------------- MLP / transformer extras
+#define MTA_CHECK_GPU(t, dt)                                                                        \
+  TORCH_CHECK((t).is_cuda() && (t).scalar_type() == (dt), #t " must be a GPU tensor of " #dt);     \
+  TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+
+template <class T>
+T* opt_typed(const OptT& t, at::ScalarType dt, const char* name) {
+  if (!has(t)) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == dt && t->is_contiguous(), name, ": bad tensor (device/dtype/layout)");
+  return static_cast<T*>(t->data_ptr());
+}
+
+void check_span(const at::Tensor& t, int64_t rows, int64_t ld, int64_t cols, const char* name) {
+  TORCH_CHECK(rows == 0 || t.numel() >= (rows - 1) * ld + cols, name, ": tensor too small for [", rows, "][", ld,
+              "] access of ", cols, " columns");
+}
+
+void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
+               double alpha, int64_t flags, const OptT& bias, const OptT& resid, const OptT& aux_in, const OptT& seed,
+               double drop_p, const OptT& out_bf16, const OptT& out_f32, const OptT& aux_pre, int64_t ldc,
+               int64_t n_store, int64_t ksplit, const OptT& bias_grad) {
+  const int64_t NS = (n_store <= 0 || n_store > N) ? N : n_store;
+  MTA_CHECK_GPU(A, at::kBFloat16);
+  MTA_CHECK_GPU(B, at::kBFloat16);
+  if (mode == 0) {
+    check_span(A, M, lda, K, "A");
+    check_span(B, N, ldb, K, "B");
+  } else if (mode == 1) {
+    check_span(A, M, lda, K, "A");
+    check_span(B, K, ldb, N, "B");
+  } else {
+    check_span(A, K, lda, M, "A");
+    check_span(B, K, ldb, N, "B");
+  }
+  for (const OptT* o : {&resid, &out_f32}) {
+    if (has(*o)) check_span(**o, M, ldc, NS, "out/resid");
+  }
+  for (const OptT* o : {&aux_in, &out_bf16, &aux_pre}) {
+    if (has(*o)) check_span(**o, M, ldc, NS, "bf16 out/aux");
+  }
+  if (has(bias)) TORCH_CHECK(bias->numel() >= N, "bias too small");
+  if (has(bias_grad)) TORCH_CHECK(bias_grad->numel() >= M, "bias_grad too small");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  const int rc = mta_gemm_bf16((int)mode, A.data_ptr(), B.data_ptr(), (int)M, (int)N, (int)K, (int)lda, (int)ldb,
+                               (float)alpha, (int)flags, opt_typed<float>(bias, at::kFloat, "bias"),
+                               opt_typed<float>(resid, at::kFloat, "resid"),
+                               opt_typed<void>(aux_in, at::kBFloat16, "aux_in"),
+                               reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
+                               (float)drop_p, opt_typed<void>(out_bf16, at::kBFloat16, "out_bf16"),
+                               opt_typed<float>(out_f32, at::kFloat, "out_f32"),
+                               opt_typed<void>(aux_pre, at::kBFloat16, "aux_pre"), (int)ldc, (int)NS, (int)ksplit,
+                               opt_typed<float>(bias_grad, at::kFloat, "bias_grad"), cur_stream());
+  TORCH_CHECK(rc == 0, "gemm_bf16: unsupported arguments (rc=", rc, ", M=", M, " N=", N, " K=", K, ")");
+}
+
+void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
+  TORCH_CHECK(src.size() == dst.size() && !src.empty() && src.size() <= 16, "cast_pad: 1..16 tensor pairs");
+  std::vector<const float*> sp;
+  std::vector<void*> dp;
+  std::vector<int> rows, cols, rows_p, cols_p, ld;
+  for (size_t i = 0; i < src.size(); ++i) {
+    auto s2 = src[i].dim() == 1 ? src[i].view({1, -1}) : src[i];
+    auto d2 = dst[i].dim() == 1 ? dst[i].view({1, -1}) : dst[i];
+    TORCH_CHECK(s2.dim() == 2 && d2.dim() == 2, "cast_pad: 1-D or 2-D tensors");
+    TORCH_CHECK(s2.is_cuda() && s2.scalar_type() == at::kFloat && s2.stride(1) == 1, "cast_pad: src fp32 rows");
+    MTA_CHECK_GPU(d2, at::kBFloat16);
+    TORCH_CHECK(d2.size(0) >= s2.size(0) && d2.size(1) >= s2.size(1), "cast_pad: dst smaller than src");
+    sp.push_back(s2.data_ptr<float>());
+    dp.push_back(d2.data_ptr());
+    rows.push_back((int)s2.size(0));
+    cols.push_back((int)s2.size(1));
+    rows_p.push_back((int)d2.size(0));
+    cols_p.push_back((int)d2.size(1));
+    ld.push_back((int)s2.stride(0));
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(src[0].device());
+  TORCH_CHECK(mta_cast_pad((int)src.size(), sp.data(), dp.data(), rows.data(), cols.data(), rows_p.data(),
+                           cols_p.data(), ld.data(), cur_stream()) == 0, "cast_pad failed");
+}
+
+void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, double eps, const OptT& gamma,
+          const OptT& beta, const OptT& y_bf16, const OptT& y_f32, const OptT& mean, at::Tensor rstd,
+          const OptT& seed, double drop_p, const OptT& dy, const OptT& dres, const OptT& pre, const OptT& dx_bf16,
+          const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be fp32 GPU");
+  check_span(x, M, ldx, D, "x");
+  MTA_CHECK_F32(rstd);
+  TORCH_CHECK(rstd.numel() >= M, "rstd too small");
+  if (!rms) TORCH_CHECK(has(mean) && mean->numel() >= M, "LayerNorm needs mean");
+  if (bwd) TORCH_CHECK(has(dy), "norm backward needs dy");
+  for (const OptT* o : {&y_bf16, &y_f32, &dy, &pre, &dx_bf16}) {
+    if (has(*o)) check_span(**o, M, D, D, "row tensor");
+  }
+  for (const OptT* o : {&dres, &dx_f32}) {
+    if (has(*o)) check_span(**o, M, ldx, D, "residual-stride tensor");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int rc = mta_norm(bwd ? 1 : 0, x.data_ptr<float>(), (int)ldx, (int)M, (int)D, rms ? 1 : 0, (float)eps,
+                          opt_typed<float>(gamma, at::kFloat, "gamma"), opt_typed<float>(beta, at::kFloat, "beta"),
+                          opt_typed<void>(y_bf16, at::kBFloat16, "y_bf16"), opt_typed<float>(y_f32, at::kFloat, "y_f32"),
+                          opt_typed<float>(mean, at::kFloat, "mean"), rstd.data_ptr<float>(),
+                          reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
+                          (float)drop_p, opt_typed<float>(dy, at::kFloat, "dy"),
+                          opt_typed<float>(dres, at::kFloat, "dres"), opt_typed<void>(pre, at::kBFloat16, "pre"),
+                          opt_typed<void>(dx_bf16, at::kBFloat16, "dx_bf16"),
+                          opt_typed<float>(dx_f32, at::kFloat, "dx_f32"), opt_typed<float>(dgamma, at::kFloat, "dgamma"),
+                          opt_typed<float>(dbeta, at::kFloat, "dbeta"), cur_stream());
+  TORCH_CHECK(rc == 0, "norm: unsupported arguments (D=", D, ")");
+}
+
+void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
+               int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base) {
+  MTA_CHECK_GPU(qkv, at::kBFloat16);
+  MTA_CHECK_GPU(out, at::kBFloat16);
+  MTA_CHECK_F32(lse);
+  TORCH_CHECK(qkv.numel() >= nseq * T * 3 * D && out.numel() >= nseq * T * D, "attention: qkv/out too small");
+  TORCH_CHECK(lse.numel() >= nseq * heads * 64, "attention: lse must hold nseq*heads*64");
+  if (bwd) {
+    TORCH_CHECK(has(dout) && has(dqkv), "attention backward needs dout and dqkv");
+    TORCH_CHECK(dout->numel() >= nseq * T * D && dqkv->numel() >= nseq * T * 3 * D, "attention: grads too small");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  const int rc = mta_attention(bwd ? 1 : 0, qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
+                               opt_typed<void>(dout, at::kBFloat16, "dout"), opt_typed<void>(dqkv, at::kBFloat16, "dqkv"),
+                               (int)nseq, (int)T, (int)D, (int)heads, (float)rope_base, cur_stream());
+  TORCH_CHECK(rc == 0, "attention: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc, ")");
+}
+
 // Native pinned-ring prefetcher (residency=stream).  Holds references to the host dataset and
 // staging tensors so their storage outlives the worker threads.
 class HostPrefetcher {
@@ -360,6 +502,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stop", &HostPrefetcher::stop)
       .def("close", &HostPrefetcher::close);
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
+  m.def("gemm_bf16", &gemm_bf16);
+  m.def("cast_pad", &cast_pad);
+  m.def("norm", &norm);
+  m.def("attention", &attention);
   m.def("lstm_fwd_layer", &lstm_fwd_layer);
   m.def("lstm_bwd_layer", &lstm_bwd_layer);
   m.def("lstm_wgrad", &lstm_wgrad);

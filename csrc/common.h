@@ -70,3 +70,40 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // s_waitcnt vmcnt(0) as a builtin (the compiler's waitcnt pass sees it, unlike inline asm).
 // gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]=0  ->  0x0F70
 __device__ __forceinline__ void mta_wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// GELU (erf form, torch.nn.GELU() default) and its derivative.
+__device__ __forceinline__ float mta_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float mta_gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// Counter-based dropout: keep(seed, row, col) from a stateless 32-bit hash (murmur3-style finaliser of
+// two rounds), so forward and backward regenerate the same mask without storing it and a captured
+// graph only needs the device-resident seed advanced once per step.
+__device__ __forceinline__ uint32_t mta_hash3(uint64_t seed, uint32_t a, uint32_t b) {
+  uint32_t h = (uint32_t)seed ^ 0x9E3779B9u;
+  uint32_t k[3] = {(uint32_t)(seed >> 32), a, b};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    uint32_t x = k[i] * 0xCC9E2D51u;
+    x = (x << 15) | (x >> 17);
+    x *= 0x1B873593u;
+    h ^= x;
+    h = (h << 13) | (h >> 19);
+    h = h * 5u + 0xE6546B64u;
+  }
+  h ^= 12u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+// 0 or 1/(1-p)
+__device__ __forceinline__ float mta_dropout_scale(uint64_t seed, uint32_t row, uint32_t col, float p) {
+  const float u = (float)(mta_hash3(seed, row, col) >> 8) * (1.0f / 16777216.0f);
+  return u >= p ? 1.0f / (1.0f - p) : 0.0f;
+}

@@ -1,0 +1,317 @@
+// bf16 MFMA GEMM for the MLP / transformer encoders (BASELINE.json north-star extras).
+//
+//   C[M,N] = alpha * sum_k A(m,k) * B(n,k)   (+ bias[n]) (GELU) (+ residual[m,n])
+//
+// A is stored row-major [M][K] (AT = false) or [K][M] (AT = true); B is stored [N][K] (BT = false,
+// nn.Linear's weight layout) or [K][N] (BT = true).  The three products of a Linear layer map to:
+//   forward   Y  = X  . W^T   A = X  [M][K],     B = W [N][K]          (AT=0, BT=0)
+//   input grad dX = dY . W   A = dY [M][N],     B = W stored [N][K] = [k][n]  (AT=0, BT=1)
+//   weight grad dW = dY^T . X A = dY stored [M][N] = [k][m], B = X stored [k][n] (AT=1, BT=1)
+// so no transposed copies of weights or activations are ever materialised: the staging pass
+// transposes 8x8 bf16 blocks in registers while writing the k-contiguous LDS images that make every
+// MFMA fragment a single ds_read_b128.
+//
+// Tiles: BM x BN per 256-thread workgroup (4 waves in 2 x 2), BK = 32 (= one v_mfma_f32_16x16x32_bf16),
+// register-staged prefetch of the next k-slice during the current slice's MFMAs, single LDS image with
+// 80-byte rows (conflict-free b128 writes and reads).  Split-K (grid.z) accumulates with f32 atomics
+// into an fp32 output (weight gradients straight into the flat gradient buffer); the weight-gradient
+// form also produces the bias gradient (row sums of A over K) from the A fragments it already holds.
+// Requirements (checked by the launcher): M, N, K multiples of 8, 16-byte aligned rows.
+#include "common.h"
+
+namespace {
+
+constexpr int GT = 256;  // threads per workgroup
+constexpr int BK = 32;
+constexpr int RS = 40;   // LDS row stride (bf16 elements): 32 + 8 pad = 80 B
+
+// epilogue flags (applied in this order): BIAS, [aux_pre store], GELU, DROPOUT, DGELU, RESID
+//   DGELU: v *= gelu'(aux_in[m][n]) (input-gradient GEMM of a GELU layer: dPre = dAct * gelu'(pre));
+//   DROPOUT: v *= keep(seed, m, n) / (1 - p), the same hash the backward regenerates.
+enum { EPI_BIAS = 1, EPI_GELU = 2, EPI_RESID = 4, EPI_ACCUM = 8, EPI_DROPOUT = 16, EPI_DGELU = 32 };
+
+struct GemmArgs {
+  const __bf16* A;
+  const __bf16* B;
+  int M, N, K, lda, ldb;
+  float alpha;
+  int flags;
+  const float* bias;        // [N]
+  const float* resid;       // [M][ldc] fp32 residual stream
+  const __bf16* aux_in;     // [M][ldc] pre-activation for DGELU
+  const uint64_t* seed;     // dropout seed (device scalar, advanced by the caller per step)
+  float drop_p;
+  __bf16* out_bf16;         // [M][ldc]
+  float* out_f32;           // [M][ldc]  (EPI_ACCUM: +=, atomics when split-K)
+  __bf16* aux_pre;          // [M][ldc]  pre-activation (GELU input) for the backward pass
+  int ldc, n_store;        // columns [0, n_store) of C are written (N may include zero padding)
+  int k_per_split;          // multiple of BK
+  float* bias_grad;         // AT mode: += row sums of A over K  ([M])
+};
+
+
+__device__ __forceinline__ uint4 and_mask(uint4 v, bool keep) {
+  const uint32_t m = keep ? 0xFFFFFFFFu : 0u;  // bitwise AND: no select of aggregates (which goes via scratch)
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+
+union Bf8 {
+  bf16x8 v;
+  uint4 u;
+  __bf16 e[8];
+};
+
+template <int BM, int BN, bool AT, bool BT>
+__global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
+  // staging work items: non-transposed = 16-B chunks (row, 8 k); transposed = 8x8 blocks (8 k-rows x 8 cols)
+  constexpr int A_ITEMS = AT ? (BK / 8) * (BM / 8) : BM * (BK / 8);
+  constexpr int B_ITEMS = BT ? (BK / 8) * (BN / 8) : BN * (BK / 8);
+  constexpr int A_PER = (A_ITEMS + GT - 1) / GT;
+  constexpr int B_PER = (B_ITEMS + GT - 1) / GT;
+  constexpr int A_REGS = AT ? 8 : 1;  // 16-B loads per item
+  constexpr int B_REGS = BT ? 8 : 1;
+
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * RS];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * RS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
+  const int kbeg = blockIdx.z * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  if (kbeg >= kend) return;
+
+  uint4 ra[A_PER][A_REGS];
+  uint4 rb[B_PER][B_REGS];
+  uint32_t ma[A_PER], mb[B_PER];  // validity bits (one per 16-B load)
+
+  // ---- global -> registers (raw values + masks; masks applied at LDS-store time) ----
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < A_PER; ++p) {
+      const int it = tid + p * GT;
+      uint32_t msk = 0;
+      if constexpr (!AT) {
+        const int r = it / (BK / 8), c = it % (BK / 8);
+        const int m = m0 + r, k = k0 + 8 * c;
+        const bool ok = (it < A_ITEMS) & (m < g.M) & (k < kend);
+        ra[p][0] = *reinterpret_cast<const uint4*>(g.A + (size_t)(ok ? m : 0) * g.lda + (ok ? k : 0));
+        msk = ok ? 1u : 0u;
+      } else {
+        const int kb = it % (BK / 8), mb8 = it / (BK / 8);
+        const int m = m0 + 8 * mb8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + 8 * kb + i;
+          const bool ok = (it < A_ITEMS) & (m < g.M) & (k < kend);
+          ra[p][i] = *reinterpret_cast<const uint4*>(g.A + (size_t)(ok ? k : 0) * g.lda + (ok ? m : 0));
+          msk |= ok ? 1u << i : 0u;
+        }
+      }
+      ma[p] = msk;
+    }
+#pragma unroll
+    for (int p = 0; p < B_PER; ++p) {
+      const int it = tid + p * GT;
+      uint32_t msk = 0;
+      if constexpr (!BT) {
+        const int r = it / (BK / 8), c = it % (BK / 8);
+        const int n = n0 + r, k = k0 + 8 * c;
+        const bool ok = (it < B_ITEMS) & (n < g.N) & (k < kend);
+        rb[p][0] = *reinterpret_cast<const uint4*>(g.B + (size_t)(ok ? n : 0) * g.ldb + (ok ? k : 0));
+        msk = ok ? 1u : 0u;
+      } else {
+        const int kb = it % (BK / 8), nb8 = it / (BK / 8);
+        const int n = n0 + 8 * nb8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int k = k0 + 8 * kb + i;
+          const bool ok = (it < B_ITEMS) & (n < g.N) & (k < kend);
+          rb[p][i] = *reinterpret_cast<const uint4*>(g.B + (size_t)(ok ? k : 0) * g.ldb + (ok ? n : 0));
+          msk |= ok ? 1u << i : 0u;
+        }
+      }
+      mb[p] = msk;
+    }
+  };
+
+  // ---- registers -> LDS k-contiguous images (transposing 8x8 blocks for AT/BT) ----
+  auto store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < A_PER; ++p) {
+      const int it = tid + p * GT;
+      if (it >= A_ITEMS) continue;
+      if constexpr (!AT) {
+        const int r = it / (BK / 8), c = it % (BK / 8);
+        *reinterpret_cast<uint4*>(&As[r * RS + 8 * c]) = and_mask(ra[p][0], ma[p] & 1u);
+      } else {
+        const int kb = it % (BK / 8), mb8 = it / (BK / 8);
+        Bf8 in[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) in[i].u = and_mask(ra[p][i], (ma[p] >> i) & 1u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          Bf8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o.e[i] = in[i].e[j];
+          *reinterpret_cast<uint4*>(&As[(8 * mb8 + j) * RS + 8 * kb]) = o.u;
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < B_PER; ++p) {
+      const int it = tid + p * GT;
+      if (it >= B_ITEMS) continue;
+      if constexpr (!BT) {
+        const int r = it / (BK / 8), c = it % (BK / 8);
+        *reinterpret_cast<uint4*>(&Bs[r * RS + 8 * c]) = and_mask(rb[p][0], mb[p] & 1u);
+      } else {
+        const int kb = it % (BK / 8), nb8 = it / (BK / 8);
+        Bf8 in[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) in[i].u = and_mask(rb[p][i], (mb[p] >> i) & 1u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          Bf8 o;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o.e[i] = in[i].e[j];
+          *reinterpret_cast<uint4*>(&Bs[(8 * nb8 + j) * RS + 8 * kb]) = o.u;
+        }
+      }
+    }
+  };
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rowsum[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) rowsum[i] = 0.f;
+  const bool want_rowsum = g.bias_grad != nullptr && blockIdx.x == 0 && wn == 0;
+
+  load(kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (k0 + BK < kend) load(k0 + BK);
+    bf16x8 af[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      af[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WM + 16 * i + (lane & 15)) * RS + 8 * (lane >> 4)]);
+      if (want_rowsum) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) rowsum[i] += (float)af[i][j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&Bs[(wn * WN + 16 * j + (lane & 15)) * RS + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) acc[i][j] = mfma16x16x32(af[i], bfr, acc[i][j]);
+    }
+  }
+
+  // ---- epilogue ----
+  const bool split = gridDim.z > 1;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = n0 + wn * WN + 16 * j + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+        if (m >= g.M || n >= g.n_store) continue;
+        float v = g.alpha * acc[i][j][r];
+        const size_t o = (size_t)m * g.ldc + n;
+        if (g.flags & EPI_ACCUM) {
+          if (split) atomicAdd(g.out_f32 + o, v);
+          else g.out_f32[o] += v;
+          continue;
+        }
+        if (g.flags & EPI_BIAS) v += g.bias[n];
+        if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
+        if (g.flags & EPI_GELU) v = mta_gelu(v);
+        if (g.flags & EPI_DROPOUT) v *= mta_dropout_scale(*g.seed, (uint32_t)m, (uint32_t)n, g.drop_p);
+        if (g.flags & EPI_DGELU) v *= mta_gelu_grad((float)g.aux_in[o]);
+        if (g.flags & EPI_RESID) v += g.resid[o];
+        if (g.out_f32) g.out_f32[o] = v;
+        if (g.out_bf16) g.out_bf16[o] = (__bf16)v;
+      }
+    }
+  }
+  if (want_rowsum) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float s = rowsum[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const int m = m0 + wm * WM + 16 * i + (lane & 15);
+      if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
+    }
+  }
+}
+
+template <int BM, int BN, bool AT, bool BT>
+void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ksplit);
+  gemm_bf16_kernel<BM, BN, AT, BT><<<grid, GT, 0, st>>>(g);
+}
+
+template <bool AT, bool BT>
+void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
+  // 128x128 tiles once they already fill the chip; 64x64 otherwise (these encoders' GEMMs are small)
+  const long tiles128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * ksplit;
+  if (tiles128 >= 256) launch<128, 128, AT, BT>(g, ksplit, st);
+  else launch<64, 64, AT, BT>(g, ksplit, st);
+}
+
+}  // namespace
+
+// mode: 0 = NN-linear forward (AT=0,BT=0), 1 = input grad (AT=0,BT=1), 2 = weight grad (AT=1,BT=1)
+extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb,
+                             float alpha, int flags, const float* bias, const float* resid, const void* aux_in,
+                             const uint64_t* seed, float drop_p, void* out_bf16, float* out_f32, void* aux_pre,
+                             int ldc, int n_store, int ksplit, float* bias_grad, hipStream_t st) {
+  if (n_store <= 0 || n_store > N) n_store = N;
+  if (M % 8 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc < n_store) return 1;
+  if ((flags & EPI_ACCUM) == 0 && ksplit > 1) return 2;
+  if (bias_grad && mode != 2) return 3;
+  GemmArgs g;
+  g.A = static_cast<const __bf16*>(A);
+  g.B = static_cast<const __bf16*>(B);
+  g.M = M;
+  g.N = N;
+  g.K = K;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.alpha = alpha;
+  g.flags = flags;
+  g.bias = bias;
+  g.resid = resid;
+  g.aux_in = static_cast<const __bf16*>(aux_in);
+  g.seed = seed;
+  g.drop_p = drop_p;
+  if ((flags & EPI_DROPOUT) && !seed) return 5;
+  if ((flags & EPI_DGELU) && !aux_in) return 6;
+  g.out_bf16 = static_cast<__bf16*>(out_bf16);
+  g.out_f32 = out_f32;
+  g.aux_pre = static_cast<__bf16*>(aux_pre);
+  g.ldc = ldc;
+  g.n_store = n_store;
+  if (ksplit < 1) ksplit = 1;
+  int kps = (K + ksplit - 1) / ksplit;
+  kps = (kps + BK - 1) / BK * BK;
+  ksplit = (K + kps - 1) / kps;
+  g.k_per_split = kps;
+  g.bias_grad = bias_grad;
+  if (mode == 0) dispatch<false, false>(g, ksplit, st);
+  else if (mode == 1) dispatch<false, true>(g, ksplit, st);
+  else if (mode == 2) dispatch<true, true>(g, ksplit, st);
+  else return 4;
+  return 0;
+}

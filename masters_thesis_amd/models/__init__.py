@@ -48,6 +48,8 @@ def model_params_from_config(cfg) -> Dict[str, Any]:
     for k in ("num_heads", "mlp_ratio", "norm"):
         if k in m:
             params[k] = m[k]
+    if m.get("arch", "lstm") == "mlp":
+        params["lookback"] = int(cfg.datamodule.lookback_window)
     if cfg.loss.name == "combined":
         params["mse_weight"] = cfg.loss.mse_weight
     if "nll_mode" in cfg.loss:

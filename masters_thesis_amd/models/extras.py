@@ -1,0 +1,177 @@
+"""North-star extra encoder families (``BASELINE.json`` configs 1-4; not in the reference).
+
+``model.arch=mlp`` / ``model.arch=transformer`` swap the reference's LSTM encoder
+(`src/model.py:88-94`) for an MLP over the flattened lookback window or a pre-norm
+transformer encoder over its T tokens.  Everything else is the reference model: the two
+``Linear(H, 1)`` alpha/beta heads, the MSE / Woodbury-NLL / combined losses and their logging
+(`src/model.py:176-331`), Adam/AdamW + ReduceLROnPlateau.  Module classes are
+``FinancialMlp{Mse,Nll,Combined}`` and ``FinancialTransformer{Mse,Nll,Combined}``, selected by
+``get_model_class(loss.module_class, arch)``.
+
+On the GPU the encoders run as bf16-mixed HIP kernels (``ops.extras``); on the CPU as fp32 PyTorch.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+
+from ..ops import extras as xops
+from . import register_model_class
+from .lstm import FinancialLstmCombined, FinancialLstmMse, FinancialLstmNll
+
+ARCH_PREFIX = {"mlp": "FinancialMlp", "transformer": "FinancialTransformer"}
+
+
+def _linear_init(w: Tensor, b: Tensor) -> None:
+    # nn.Linear's default init
+    torch.nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+    bound = 1.0 / math.sqrt(w.shape[1])
+    torch.nn.init.uniform_(b, -bound, bound)
+
+
+class _Linear(torch.nn.Module):
+    def __init__(self, fin: int, fout: int):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.empty(fout, fin))
+        self.bias = torch.nn.Parameter(torch.empty(fout))
+        _linear_init(self.weight, self.bias)
+
+
+class _Norm(torch.nn.Module):
+    def __init__(self, d: int, bias: bool):
+        super().__init__()
+        self.weight = torch.nn.Parameter(torch.ones(d))
+        if bias:
+            self.bias = torch.nn.Parameter(torch.zeros(d))
+
+
+class MLPEncoder(torch.nn.Module):
+    """``z = flatten(x)``; per layer ``z = Dropout(Norm(GELU(Linear(z))))`` (no dropout after the last)."""
+
+    def __init__(self, input_size: int, lookback: int, hidden_size: int, num_layers: int, dropout: float,
+                 norm: str = "layernorm"):
+        super().__init__()
+        if norm not in ("layernorm", "rmsnorm"):
+            raise ValueError(f"norm must be layernorm or rmsnorm, got {norm}")
+        self.num_layers, self.dropout, self.norm = num_layers, float(dropout), norm
+        self.layers = torch.nn.ModuleList(
+            [_Linear(input_size * lookback if i == 0 else hidden_size, hidden_size) for i in range(num_layers)])
+        self.norms = torch.nn.ModuleList([_Norm(hidden_size, norm == "layernorm") for _ in range(num_layers)])
+        self.register_buffer("seeds", torch.randint(0, 2 ** 62, (max(num_layers, 1),), dtype=torch.int64),
+                             persistent=False)
+
+    def flat_params(self):
+        out = []
+        for lin, nrm in zip(self.layers, self.norms):
+            out += [lin.weight, lin.bias, nrm.weight] + ([nrm.bias] if self.norm == "layernorm" else [])
+        return out
+
+    def forward(self, x: Tensor) -> Tensor:
+        return xops.mlp_encode(x, self.flat_params(), self.seeds, self.num_layers, self.norm, self.dropout,
+                               self.training)
+
+
+class _Block(torch.nn.Module):
+    def __init__(self, d: int, mlp_ratio: int):
+        super().__init__()
+        self.norm1 = _Norm(d, False)
+        self.qkv = _Linear(d, 3 * d)
+        self.proj = _Linear(d, d)
+        self.norm2 = _Norm(d, False)
+        self.fc1 = _Linear(d, mlp_ratio * d)
+        self.fc2 = _Linear(mlp_ratio * d, d)
+
+    def flat_params(self):
+        return [self.norm1.weight, self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
+                self.norm2.weight, self.fc1.weight, self.fc1.bias, self.fc2.weight, self.fc2.bias]
+
+
+class TransformerEncoder(torch.nn.Module):
+    """Pre-norm encoder: Linear embed -> [x + Attn(RoPE)(RMSNorm x); x + MLP(RMSNorm x)] x L -> RMSNorm(last token)."""
+
+    def __init__(self, input_size: int, hidden_size: int, num_layers: int, num_heads: int, mlp_ratio: int = 4,
+                 dropout: float = 0.0):
+        super().__init__()
+        if hidden_size % num_heads or (hidden_size // num_heads) not in (32, 64):
+            raise ValueError("transformer: head dim (hidden_size / num_heads) must be 32 or 64")
+        self.num_layers, self.num_heads, self.dropout = num_layers, num_heads, float(dropout)
+        self.embed = _Linear(input_size, hidden_size)
+        self.blocks = torch.nn.ModuleList([_Block(hidden_size, mlp_ratio) for _ in range(num_layers)])
+        self.final_norm = _Norm(hidden_size, False)
+        self.register_buffer("seeds", torch.randint(0, 2 ** 62, (max(num_layers, 1),), dtype=torch.int64),
+                             persistent=False)
+
+    def flat_params(self):
+        out = [self.embed.weight, self.embed.bias]
+        for b in self.blocks:
+            out += b.flat_params()
+        return out + [self.final_norm.weight]
+
+    def forward(self, x: Tensor) -> Tensor:
+        if x.shape[1] > 64:
+            raise ValueError("transformer encoder supports lookback windows of up to 64 tokens")
+        return xops.transformer_encode(x, self.flat_params(), self.seeds, self.num_layers, self.num_heads,
+                                       self.dropout, self.training)
+
+
+def _make(base, arch: str):
+    prefix = ARCH_PREFIX[arch]
+    name = base.__name__.replace("FinancialLstm", prefix)
+
+    if arch == "mlp":
+        def __init__(self, input_size: int = 3, hidden_size: int = 256, num_layers: int = 2, dropout: float = 0.1,
+                     learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,
+                     lookback: int = 60, norm: str = "layernorm", backend: str = "auto", nll_mode: str = "reference",
+                     optimizer: str = "adamw"):
+            kw = dict(backend=backend, nll_mode=nll_mode, optimizer=optimizer)
+            if base is FinancialLstmCombined:
+                base.__init__(self, input_size, 8, 1, 0.0, learning_rate, weight_decay, mse_weight, **kw)
+            else:
+                base.__init__(self, input_size, 8, 1, 0.0, learning_rate, weight_decay, **kw)
+            del self.lstm
+            self.encoder = MLPEncoder(input_size, lookback, hidden_size, num_layers, dropout, norm)
+            self.alpha_head = torch.nn.Linear(hidden_size, 1)
+            self.beta_head = torch.nn.Linear(hidden_size, 1)
+            self._hparams.clear()
+            self.save_hyperparameters()
+    else:
+        def __init__(self, input_size: int = 3, hidden_size: int = 128, num_layers: int = 4, dropout: float = 0.1,
+                     learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,
+                     num_heads: int = 4, mlp_ratio: int = 4, backend: str = "auto", nll_mode: str = "reference",
+                     optimizer: str = "adamw"):
+            kw = dict(backend=backend, nll_mode=nll_mode, optimizer=optimizer)
+            if base is FinancialLstmCombined:
+                base.__init__(self, input_size, 8, 1, 0.0, learning_rate, weight_decay, mse_weight, **kw)
+            else:
+                base.__init__(self, input_size, 8, 1, 0.0, learning_rate, weight_decay, **kw)
+            del self.lstm
+            self.encoder = TransformerEncoder(input_size, hidden_size, num_layers, num_heads, mlp_ratio, dropout)
+            self.alpha_head = torch.nn.Linear(hidden_size, 1)
+            self.beta_head = torch.nn.Linear(hidden_size, 1)
+            self._hparams.clear()
+            self.save_hyperparameters()
+
+    def encode(self, x: Tensor) -> Tensor:
+        return self.encoder(x)
+
+    cls = type(name, (base,), {"__init__": __init__, "encode": encode, "__doc__": f"{base.__name__} with the {arch} "
+                                                                                   f"encoder (north-star extra)."})
+    return cls
+
+
+FinancialMlpMse = _make(FinancialLstmMse, "mlp")
+FinancialMlpNll = _make(FinancialLstmNll, "mlp")
+FinancialMlpCombined = _make(FinancialLstmCombined, "mlp")
+FinancialTransformerMse = _make(FinancialLstmMse, "transformer")
+FinancialTransformerNll = _make(FinancialLstmNll, "transformer")
+FinancialTransformerCombined = _make(FinancialLstmCombined, "transformer")
+
+for _c in (FinancialMlpMse, FinancialMlpNll, FinancialMlpCombined, FinancialTransformerMse, FinancialTransformerNll,
+           FinancialTransformerCombined):
+    register_model_class(_c.__name__, _c)
+
+__all__ = ["ARCH_PREFIX", "MLPEncoder", "TransformerEncoder", "FinancialMlpMse", "FinancialMlpNll",
+           "FinancialMlpCombined", "FinancialTransformerMse", "FinancialTransformerNll",
+           "FinancialTransformerCombined"]

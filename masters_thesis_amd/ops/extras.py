@@ -1,0 +1,396 @@
+"""MLP and transformer encoder ops for the ``BASELINE.json`` north-star extras (bf16-mixed on MI355X).
+
+Not in the reference (it only has the LSTM, `src/model.py:88-94`); the north star asks for the
+``src/model.py`` forward path as Linear/GEMM+bias, GELU and LayerNorm/RMSNorm HIP kernels and a
+transformer-encoder config with attention + RMSNorm + RoPE kernels.
+
+GPU path = one autograd Function per encoder, built from four hand-written HIP kernels:
+
+* ``gemm_bf16`` (``csrc/gemm.hip``) -- MFMA GEMM whose three layouts cover forward ``X W^T``,
+  input gradient ``dY W`` and weight gradient ``dY^T X`` with no transposed copies; epilogues fuse
+  bias, GELU (saving its input), dropout, GELU', the fp32 residual add, the fp32 weight-gradient
+  accumulation straight into the flat gradient buffer and the bias gradient;
+* ``norm`` (``csrc/norm.hip``) -- LayerNorm / RMSNorm forward and backward (dropout, GELU' and the
+  residual-stream gradient fused into the backward, dgamma/dbeta accumulated);
+* ``attention`` (``csrc/attention.hip``) -- RoPE attention, one wave per (sequence, head);
+* ``cast_pad`` -- fp32 master weights -> zero-padded bf16 operands, once per step.
+
+Precision: fp32 master weights (FlatParameters) and fp32 residual stream / gradients, bf16 GEMM
+operands with fp32 accumulation ("bf16-mixed").  Like the LSTM op, the weights' gradients are
+accumulated inside the op and ``None`` is returned for them.
+
+CPU path: the same architectures in plain fp32 PyTorch (``mlp_reference`` / ``transformer_reference``),
+which also serve as the numerics oracle of the GPU tests.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn.functional as Fn
+from torch import Tensor
+
+from ._lib import lib, use_hip
+
+EPI_BIAS, EPI_GELU, EPI_RESID, EPI_ACCUM, EPI_DROPOUT, EPI_DGELU = 1, 2, 4, 8, 16, 32
+ROPE_BASE = 10000.0
+LN_EPS = 1e-5
+RMS_EPS = 1e-6
+
+
+def _r8(n: int) -> int:
+    return (n + 7) // 8 * 8
+
+
+def _r16(n: int) -> int:
+    return (n + 15) // 16 * 16
+
+
+# --------------------------------------------------------------------------------------------------
+# thin launchers
+# --------------------------------------------------------------------------------------------------
+def gemm(mode: int, A: Tensor, B: Tensor, M: int, N: int, K: int, lda: int, ldb: int, *, flags: int = 0,
+         alpha: float = 1.0, bias=None, resid=None, aux_in=None, seed=None, drop_p: float = 0.0, out_bf16=None,
+         out_f32=None, aux_pre=None, ldc: Optional[int] = None, n_store: int = 0, ksplit: int = 1,
+         bias_grad=None) -> None:
+    lib().gemm_bf16(mode, A, B, M, N, K, lda, ldb, alpha, flags, bias, resid, aux_in, seed, drop_p, out_bf16,
+                    out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad)
+
+
+def wgrad_split(M: int, N: int, K: int) -> int:
+    """Split-K count for a weight-gradient GEMM: ~256 workgroups, >= 4 k-slices of 32 each."""
+    tiles = -(-M // 64) * -(-N // 64)
+    return max(1, min(256 // max(tiles, 1), K // 128))
+
+
+def cast_pad(srcs: Sequence[Tensor], dsts: Sequence[Tensor]) -> None:
+    C = lib()
+    for i in range(0, len(srcs), 16):
+        C.cast_pad(list(srcs[i:i + 16]), list(dsts[i:i + 16]))
+
+
+def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
+    return torch.empty((w.shape[0], cols_p), device=w.device, dtype=torch.bfloat16)
+
+
+def advance_seeds(seeds: Tensor) -> None:
+    # per-step, in-graph: every dropout site gets a fresh counter-hash seed
+    seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))
+
+
+def _grad_view(p: Tensor) -> Tensor:
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+# --------------------------------------------------------------------------------------------------
+# MLP encoder:  z_0 = flatten(x);  z_{i+1} = dropout_i(Norm_i(GELU(z_i W_i^T + b_i)))   (no dropout last)
+# --------------------------------------------------------------------------------------------------
+def mlp_reference(x: Tensor, params: Sequence[Tensor], num_layers: int, norm: str, dropout: float,
+                  training: bool) -> Tensor:
+    z = x.flatten(1)
+    per = 4 if norm == "layernorm" else 3
+    for i in range(num_layers):
+        w, b = params[per * i], params[per * i + 1]
+        z = Fn.gelu(Fn.linear(z, w, b))
+        if norm == "layernorm":
+            z = Fn.layer_norm(z, (z.shape[-1],), params[per * i + 2], params[per * i + 3], LN_EPS)
+        else:
+            z = Fn.rms_norm(z, (z.shape[-1],), params[per * i + 2], RMS_EPS)
+        if i < num_layers - 1 and dropout > 0 and training:
+            z = Fn.dropout(z, dropout, True)
+    return z
+
+
+class _MlpEncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, seeds, num_layers, norm, dropout, training, need_grad, *params):
+        dev = x.device
+        N = x.shape[0]
+        Mp = _r16(N)
+        L = num_layers
+        per = 4 if norm == "layernorm" else 3
+        rms = norm != "layernorm"
+        drop = dropout > 0 and training
+        if drop:
+            advance_seeds(seeds)
+        K0 = x[0].numel()
+        dims = [K0] + [params[per * i].shape[0] for i in range(L)]
+        kp = [_r8(d) for d in dims]
+        X0 = torch.empty((Mp, kp[0]), device=dev, dtype=torch.bfloat16)
+        wb = [_padded_bf16(params[per * i], kp[i]) for i in range(L)]
+        cast_pad([x.reshape(N, K0)] + [params[per * i] for i in range(L)], [X0] + wb)
+        Xs, pres, acts, means, rstds = [X0], [], [], [], []
+        h = None
+        for i in range(L):
+            D = dims[i + 1]
+            assert D % 8 == 0, "MLP hidden size must be a multiple of 8"
+            pre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
+            act = torch.empty((Mp, D), device=dev, dtype=torch.float32)
+            gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU, bias=params[per * i + 1],
+                 aux_pre=pre, out_f32=act)
+            mean = None if rms else torch.empty(Mp, device=dev, dtype=torch.float32)
+            rstd = torch.empty(Mp, device=dev, dtype=torch.float32)
+            last = i == L - 1
+            y = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16) if not last else None
+            if last:
+                h = torch.empty((Mp, D), device=dev, dtype=torch.float32)
+            lib().norm(False, act, D, Mp, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
+                       None if rms else params[per * i + 3], y, h if last else None, mean, rstd,
+                       seeds[i:i + 1] if (drop and not last) else None, float(dropout), None, None, None, None, None,
+                       None, None)
+            pres.append(pre)
+            acts.append(act)
+            means.append(mean)
+            rstds.append(rstd)
+            if not last:
+                Xs.append(y)
+        ctx.meta = (N, Mp, L, per, rms, drop, float(dropout), dims, kp)
+        ctx.params = params
+        ctx.wb = wb
+        ctx.seeds = seeds
+        if need_grad:
+            ctx.save_for_backward(*Xs, *pres, *acts)
+            ctx.stats = (means, rstds)
+        return h[:N]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh):
+        N, Mp, L, per, rms, drop, p, dims, kp = ctx.meta
+        params, wb = ctx.params, ctx.wb
+        saved = ctx.saved_tensors
+        Xs, pres, acts = saved[:L], saved[L:2 * L], saved[2 * L:]
+        means, rstds = ctx.stats
+        dev = dh.device
+        dy = torch.zeros((Mp, dims[-1]), device=dev, dtype=torch.float32)
+        dy[:N].copy_(dh)
+        for i in range(L - 1, -1, -1):
+            D, Din = dims[i + 1], dims[i]
+            dpre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
+            dropped = drop and i < L - 1
+            lib().norm(True, acts[i], D, Mp, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
+                       None if rms else params[per * i + 3], None, None, means[i], rstds[i],
+                       ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], dpre, None,
+                       _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]))
+            # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre)
+            gemm(2, dpre, Xs[i], D, kp[i], Mp, D, kp[i], flags=EPI_ACCUM, out_f32=_grad_view(params[per * i]),
+                 ldc=Din, n_store=Din, ksplit=wgrad_split(D, kp[i], Mp), bias_grad=_grad_view(params[per * i + 1]))
+            if i > 0:
+                dy = torch.empty((Mp, Din), device=dev, dtype=torch.float32)
+                gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], out_f32=dy)
+        return (None,) * (7 + len(params))
+
+
+def mlp_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, norm: str,
+               dropout: float, training: bool) -> Tensor:
+    if use_hip(x):
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        return _MlpEncoderFn.apply(x.contiguous(), seeds, num_layers, norm, float(dropout), bool(training),
+                                   need_grad, *params)
+    return mlp_reference(x, params, num_layers, norm, dropout, training)
+
+
+# --------------------------------------------------------------------------------------------------
+# transformer encoder (pre-norm, RMSNorm, RoPE attention, GELU MLP, last-token pooling)
+# --------------------------------------------------------------------------------------------------
+def rope_reference(x: Tensor, base: float = ROPE_BASE) -> Tensor:
+    """Interleaved-pair rotary embedding over (..., T, hd)."""
+    T, hd = x.shape[-2], x.shape[-1]
+    inv = base ** (-torch.arange(0, hd, 2, device=x.device, dtype=torch.float32) / hd)
+    ang = torch.arange(T, device=x.device, dtype=torch.float32)[:, None] * inv[None, :]
+    c, s = ang.cos().to(x.dtype), ang.sin().to(x.dtype)
+    x0, x1 = x[..., 0::2], x[..., 1::2]
+    out = torch.stack([x0 * c - x1 * s, x0 * s + x1 * c], dim=-1)
+    return out.flatten(-2)
+
+
+def attention_reference(qkv: Tensor, heads: int) -> Tensor:
+    """qkv (N, T, 3d) -> (N, T, d); RoPE on q, k; bidirectional softmax attention."""
+    N, T, d3 = qkv.shape
+    d = d3 // 3
+    hd = d // heads
+    q, k, v = qkv.split(d, dim=-1)
+    q = rope_reference(q.view(N, T, heads, hd).transpose(1, 2))
+    k = rope_reference(k.view(N, T, heads, hd).transpose(1, 2))
+    v = v.view(N, T, heads, hd).transpose(1, 2)
+    att = torch.softmax((q @ k.transpose(-1, -2)) / math.sqrt(hd), dim=-1)
+    return (att @ v).transpose(1, 2).reshape(N, T, d)
+
+
+PER_BLOCK = 8  # norm1.w, qkv.w, qkv.b, proj.w, proj.b, norm2.w, fc1.w, fc1.b, fc2.w, fc2.b -> see names below
+BLOCK_NAMES = ("norm1.weight", "qkv.weight", "qkv.bias", "proj.weight", "proj.bias", "norm2.weight", "fc1.weight",
+               "fc1.bias", "fc2.weight", "fc2.bias")
+
+
+def transformer_reference(x: Tensor, params: Sequence[Tensor], num_layers: int, heads: int, dropout: float,
+                          training: bool) -> Tensor:
+    we, be = params[0], params[1]
+    h = Fn.linear(x, we, be)
+    nb = len(BLOCK_NAMES)
+    for l in range(num_layers):
+        g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[2 + nb * l: 2 + nb * (l + 1)]
+        a = attention_reference(Fn.linear(Fn.rms_norm(h, (h.shape[-1],), g1, RMS_EPS), wqkv, bqkv), heads)
+        h = h + Fn.linear(a, wo, bo)
+        u = Fn.gelu(Fn.linear(Fn.rms_norm(h, (h.shape[-1],), g2, RMS_EPS), w1, b1))
+        if dropout > 0 and training:
+            u = Fn.dropout(u, dropout, True)
+        h = h + Fn.linear(u, w2, b2)
+    gf = params[2 + nb * num_layers]
+    return Fn.rms_norm(h[:, -1], (h.shape[-1],), gf, RMS_EPS)
+
+
+class _TransformerEncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, seeds, num_layers, heads, dropout, training, need_grad, *params):
+        dev = x.device
+        N, T, F = x.shape
+        Np = _r8(N)
+        M = Np * T
+        L = num_layers
+        nb = len(BLOCK_NAMES)
+        d = params[0].shape[0]
+        drop = dropout > 0 and training
+        if drop:
+            advance_seeds(seeds)
+        Fp = _r8(F)
+        C = lib()
+        # bf16 operands: input tokens + every matrix (padded along K only where needed)
+        Xin = torch.empty((M, Fp), device=dev, dtype=torch.bfloat16)
+        mats = [params[0]]
+        for l in range(L):
+            base = 2 + nb * l
+            mats += [params[base + 1], params[base + 3], params[base + 6], params[base + 8]]
+        mats_b = [_padded_bf16(w, _r8(w.shape[1])) for w in mats]
+        xin_src = x.reshape(N * T, F)
+        if Np != N:
+            xin_src = torch.cat([xin_src, xin_src.new_zeros(((Np - N) * T, F))])
+        cast_pad([xin_src] + mats, [Xin] + mats_b)
+        xs = torch.empty((M, d), device=dev, dtype=torch.float32)
+        gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
+        saved: List[Tensor] = [Xin]
+        stats: List[Tensor] = []
+        for l in range(L):
+            base = 2 + nb * l
+            g1, bqkv, bo, g2, b1, b2 = (params[base], params[base + 2], params[base + 4], params[base + 5],
+                                        params[base + 7], params[base + 9])
+            wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
+            dff = w1_b.shape[0]
+            xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            r1 = torch.empty(M, device=dev, dtype=torch.float32)
+            C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
+                   None, None, None, None)
+            qkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
+            gemm(0, xn, wqkv_b, M, 3 * d, d, d, d, flags=EPI_BIAS, bias=bqkv, out_bf16=qkv)
+            o = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
+            C.attention(False, qkv, o, lse, None, None, Np, T, d, heads, ROPE_BASE)
+            x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
+            gemm(0, o, wo_b, M, d, d, d, d, flags=EPI_BIAS | EPI_RESID, bias=bo, resid=xs, out_f32=x1)
+            xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            r2 = torch.empty(M, device=dev, dtype=torch.float32)
+            C.norm(False, x1, d, M, d, True, RMS_EPS, g2, None, xn2, None, None, r2, None, 0.0, None, None, None,
+                   None, None, None, None)
+            pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+            u = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+            fl = EPI_BIAS | EPI_GELU | (EPI_DROPOUT if drop else 0)
+            gemm(0, xn2, w1_b, M, dff, d, d, d, flags=fl, bias=b1, seed=seeds[l:l + 1] if drop else None,
+                 drop_p=float(dropout), aux_pre=pre1, out_bf16=u)
+            x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
+            gemm(0, u, w2_b, M, d, dff, dff, dff, flags=EPI_BIAS | EPI_RESID, bias=b2, resid=x1, out_f32=x2)
+            saved += [xs, xn, qkv, o, x1, xn2, pre1, u]
+            stats += [r1, lse, r2]
+            xs = x2
+        gf = params[2 + nb * L]
+        h = torch.empty((Np, d), device=dev, dtype=torch.float32)
+        rf = torch.empty(Np, device=dev, dtype=torch.float32)
+        C.norm(False, xs.view(-1)[(T - 1) * d:], T * d, Np, d, True, RMS_EPS, gf, None, None, h, None, rf, None, 0.0,
+               None, None, None, None, None, None, None)
+        saved.append(xs)
+        stats.append(rf)
+        ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout))
+        ctx.params, ctx.mats_b, ctx.seeds = params, mats_b, seeds
+        if need_grad:
+            ctx.save_for_backward(*saved)
+            ctx.stats = stats
+        return h[:N]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh):
+        N, Np, T, F, Fp, d, L, heads, drop, p = ctx.meta
+        params, mats_b = ctx.params, ctx.mats_b
+        saved = ctx.saved_tensors
+        stats = ctx.stats
+        C = lib()
+        dev = dh.device
+        M = Np * T
+        nb = len(BLOCK_NAMES)
+        Xin = saved[0]
+        x_final = saved[-1]
+        # final RMSNorm over the last-token rows -> residual-stream gradient (zero elsewhere)
+        dX = torch.zeros((M, d), device=dev, dtype=torch.float32)
+        dhp = torch.zeros((Np, d), device=dev, dtype=torch.float32)
+        dhp[:N].copy_(dh)
+        gf = params[2 + nb * L]
+        C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, Np, d, True, RMS_EPS, gf, None, None, None, None,
+               stats[-1], None, 0.0, dhp, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
+        dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+        cast_pad([dX], [dXb])
+        for l in range(L - 1, -1, -1):
+            base = 2 + nb * l
+            g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
+            wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
+            dff = w1_b.shape[0]
+            xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
+            r1, lse, r2 = stats[3 * l: 3 * l + 3]
+            # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
+            gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                 ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2))
+            dpre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+            fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
+            gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1, seed=ctx.seeds[l:l + 1] if drop else None,
+                 drop_p=p, out_bf16=dpre1)
+            # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
+            gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                 ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+            dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
+            gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
+            # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
+            dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
+            dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None, dX1b,
+                   dX1, _grad_view(g2), None)
+            # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
+            gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
+                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo))
+            do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
+            # attention backward (RoPE inverse fused) -> dqkv
+            dqkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
+            C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
+            # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
+            gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
+                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv))
+            dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
+            gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
+            # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
+            dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
+            C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None, dXb,
+                   dXn, _grad_view(g1), None)
+            dX = dXn
+        # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
+        gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,
+             ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]))
+        return (None,) * (7 + len(params))
+
+
+def transformer_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, heads: int,
+                       dropout: float, training: bool) -> Tensor:
+    if use_hip(x):
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        return _TransformerEncoderFn.apply(x.contiguous(), seeds, num_layers, heads, float(dropout), bool(training),
+                                           need_grad, *params)
+    return transformer_reference(x, params, num_layers, heads, dropout, training)

@@ -1,0 +1,193 @@
+"""Numerics of the north-star extra kernels (GEMM / norms / RoPE attention) and encoders vs fp32 PyTorch."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from masters_thesis_amd.ops import _lib
+
+    assert _lib.lib(required=True) is not None
+
+
+def _bf(x):
+    return x.to(DEV, torch.bfloat16)
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(112, 256, 184), (6000, 384, 128), (64, 64, 32), (200, 136, 520)])
+def test_gemm_forward_epilogues(M, N, K):
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(0)
+    A, W = torch.randn(M, K) * 0.5, torch.randn(N, K) * 0.1
+    bias, res = torch.randn(N), torch.randn(M, N)
+    Ab, Wb = _bf(A), _bf(W)
+    ref_pre = Ab.float() @ Wb.float().t() + bias.to(DEV)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    out = torch.empty(M, N, device=DEV)
+    X.gemm(0, Ab, Wb, M, N, K, K, K, flags=X.EPI_BIAS | X.EPI_GELU | X.EPI_RESID, bias=bias.to(DEV),
+           resid=res.to(DEV), aux_pre=pre, out_f32=out)
+    assert _rel(pre.float(), ref_pre) < 5e-3
+    assert _rel(out, Fn.gelu(ref_pre) + res.to(DEV)) < 2e-3
+
+
+def test_gemm_input_grad_dgelu_and_weight_grad_split():
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(1)
+    M, D, Din = 6000, 128, 96
+    dY, W, Xa, pre = torch.randn(M, D), torch.randn(D, Din) * 0.1, torch.randn(M, Din), torch.randn(M, D)
+    dYb, Wb, Xb, preb = _bf(dY), _bf(W), _bf(Xa), _bf(pre)
+    # input grad: dX = dY W
+    dX = torch.empty(M, Din, device=DEV)
+    X.gemm(1, dYb, Wb, M, Din, D, D, Din, out_f32=dX)
+    assert _rel(dX, dYb.float() @ Wb.float()) < 2e-3
+    # input grad with GELU' epilogue (through W^T of a square layer)
+    W2b = _bf(torch.randn(Din, D) * 0.1)  # a D -> Din layer: weight [out=Din][in=D]
+    dpre = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    dAct = torch.randn(M, Din)
+    X.gemm(1, _bf(dAct), W2b, M, D, Din, Din, D, flags=X.EPI_DGELU, aux_in=preb, out_bf16=dpre)
+    p = preb.float().requires_grad_(True)
+    (g,) = torch.autograd.grad(Fn.gelu(p), p, _bf(dAct).float() @ W2b.float())
+    assert _rel(dpre.float(), g) < 8e-3
+    # weight grad with split-K, bias grad and an n_store narrower than the padded width
+    gW = torch.ones(D, Din - 3, device=DEV)  # accumulates on top of existing grads
+    gb = torch.ones(D, device=DEV)
+    X.gemm(2, dYb, Xb, D, Din, M, D, Din, flags=X.EPI_ACCUM, out_f32=gW, ldc=Din - 3, n_store=Din - 3,
+           ksplit=X.wgrad_split(D, Din, M), bias_grad=gb)
+    ref = dYb.float().t() @ Xb.float()
+    assert _rel(gW - 1, ref[:, :Din - 3]) < 2e-3
+    assert _rel(gb - 1, dYb.float().sum(0)) < 2e-3
+
+
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("D", [128, 256, 2048])
+def test_norm_forward_backward(rms, D):
+    from masters_thesis_amd.ops import _lib
+    from masters_thesis_amd.ops.extras import LN_EPS, RMS_EPS
+
+    C = _lib.lib()
+    torch.manual_seed(2)
+    M = 300
+    x = (torch.randn(M, D) * 2 + 0.5).to(DEV)
+    g, b = (torch.rand(D) + 0.5).to(DEV), torch.randn(D).to(DEV)
+    dy = torch.randn(M, D).to(DEV)
+    pre = _bf(torch.randn(M, D))
+    dres = torch.randn(M, D).to(DEV)
+    eps = RMS_EPS if rms else LN_EPS
+    yb = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    yf = torch.empty(M, D, device=DEV)
+    mean = None if rms else torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    C.norm(False, x, D, M, D, rms, eps, g, None if rms else b, yb, yf, mean, rstd, None, 0.0, None, None, None, None,
+           None, None, None)
+    xr, gr, br = x.clone().requires_grad_(True), g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = Fn.rms_norm(xr, (D,), gr, eps) if rms else Fn.layer_norm(xr, (D,), gr, br, eps)
+    assert _rel(yf, ref) < 1e-5 and _rel(yb.float(), ref) < 5e-3
+    dxf = torch.empty(M, D, device=DEV)
+    dgam = torch.zeros(D, device=DEV)
+    dbet = torch.zeros(D, device=DEV)
+    C.norm(True, x, D, M, D, rms, eps, g, None if rms else b, None, None, mean, rstd, None, 0.0, dy, dres, None, None,
+           dxf, dgam, None if rms else dbet)
+    gx, gg, gb = torch.autograd.grad(ref, (xr, gr, br), dy, allow_unused=True)
+    assert _rel(dxf - dres, gx) < 1e-4
+    assert _rel(dgam, gg) < 1e-4
+    if not rms:
+        assert _rel(dbet, gb) < 1e-4
+    # GELU' fusion
+    dxb = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    C.norm(True, x, D, M, D, rms, eps, g, None if rms else b, None, None, mean, rstd, None, 0.0, dy, None, pre, dxb,
+           None, None, None)
+    p = pre.float().requires_grad_(True)
+    (gp,) = torch.autograd.grad(Fn.gelu(p), p, gx)
+    assert _rel(dxb.float(), gp) < 8e-3
+
+
+@pytest.mark.parametrize("T,heads,hd", [(60, 4, 32), (64, 2, 64), (17, 3, 32)])
+def test_attention_forward_backward(T, heads, hd):
+    from masters_thesis_amd.ops import _lib
+    from masters_thesis_amd.ops.extras import ROPE_BASE, attention_reference
+
+    C = _lib.lib()
+    torch.manual_seed(3)
+    N, d = 24, heads * hd
+    qkv = _bf(torch.randn(N * T, 3 * d))
+    out = torch.empty(N * T, d, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(N * heads * 64, device=DEV)
+    C.attention(False, qkv, out, lse, None, None, N, T, d, heads, ROPE_BASE)
+    q = qkv.float().view(N, T, 3 * d).requires_grad_(True)
+    ref = attention_reference(q, heads)
+    assert _rel(out.float().view(N, T, d), ref) < 1e-2
+    dout = _bf(torch.randn(N * T, d))
+    dqkv = torch.empty(N * T, 3 * d, device=DEV, dtype=torch.bfloat16)
+    C.attention(True, qkv, out, lse, dout, dqkv, N, T, d, heads, ROPE_BASE)
+    (gq,) = torch.autograd.grad(ref, q, dout.float().view(N, T, d))
+    gq = gq.view(N * T, 3 * d)
+    for part in range(3):
+        sl = slice(part * d, (part + 1) * d)
+        assert _rel(dqkv.float()[:, sl], gq[:, sl]) < 2.5e-2, part
+
+
+def _encoder_parity(model_cls, kw, tol_h, tol_g):
+    torch.manual_seed(5)
+    cpu = model_cls(**kw)
+    gpu = model_cls(**kw)
+    gpu.load_state_dict(cpu.state_dict())
+    gpu = gpu.to(DEV)
+    x = torch.randn(100, 60, 3) * 0.8
+    cpu.train()
+    gpu.train()
+    h_ref = cpu.encode(x)
+    h = gpu.encode(x.to(DEV))
+    w = torch.randn_like(h_ref)
+    (h_ref * w).sum().backward()
+    (h * w.to(DEV)).sum().backward()
+    assert _rel(h.cpu(), h_ref.detach()) < tol_h
+    for (n, p_ref), (_, p) in zip(cpu.encoder.named_parameters(), gpu.encoder.named_parameters()):
+        assert p.grad is not None, n
+        e = _rel(p.grad.cpu(), p_ref.grad)
+        assert e < tol_g, (n, e)
+
+
+@pytest.mark.parametrize("norm", ["layernorm", "rmsnorm"])
+def test_mlp_encoder_matches_fp32_reference(norm):
+    from masters_thesis_amd.models.extras import FinancialMlpMse
+
+    _encoder_parity(FinancialMlpMse, dict(hidden_size=256, num_layers=3, dropout=0.0, norm=norm), 2e-2, 5e-2)
+
+
+def test_transformer_encoder_matches_fp32_reference():
+    from masters_thesis_amd.models.extras import FinancialTransformerMse
+
+    _encoder_parity(FinancialTransformerMse, dict(hidden_size=128, num_layers=2, num_heads=4, dropout=0.0), 3e-2, 8e-2)
+
+
+def test_extras_dropout_train_vs_eval_and_finite_grads():
+    from masters_thesis_amd.models.extras import FinancialMlpCombined, FinancialTransformerCombined
+
+    batch = (torch.randn(1, 100, 60, 3, device=DEV), torch.randn(1, 100, 30, 4, device=DEV),
+             torch.tensor([[0.05, 0.4]], device=DEV), torch.rand(1, 100, device=DEV) + 1)
+    for cls, kw in ((FinancialMlpCombined, dict(hidden_size=128, num_layers=3, dropout=0.3)),
+                    (FinancialTransformerCombined, dict(hidden_size=64, num_layers=2, num_heads=2, dropout=0.3))):
+        torch.manual_seed(0)
+        m = cls(**kw).to(DEV)
+        m.eval()
+        with torch.no_grad():
+            h_eval = m.encode(batch[0][0])
+        m.train()
+        h1 = m.encode(batch[0][0])
+        h2 = m.encode(batch[0][0])
+        assert not torch.allclose(h1, h_eval) and not torch.allclose(h1, h2)  # fresh mask per call
+        loss = m.training_step(batch, 0)
+        loss.backward()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
