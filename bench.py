@@ -32,6 +32,10 @@ REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
 REFERENCE_SAMPLES_PER_S = 59.0  # reference-equivalent replica, model=small, loss=mse, B=1
+# BASELINE.md yardstick rows (model, loss, per-GPU batch) -> samples/s; other configs have no yardstick
+YARDSTICK = {("small", "mse", 1): 59.0, ("small", "nll", 1): 58.0, ("small", "combined", 1): 59.0,
+             ("medium", "mse", 1): 21.0, ("large", "mse", 1): 14.0, ("small", "mse", 8): 65.0,
+             ("small", "mse", 64): 68.0}
 
 
 def log(*a):
@@ -138,8 +142,10 @@ def main(argv=None):
             "p50_step_ms": round(p50, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / REFERENCE_SAMPLES_PER_S, 3),
-            "dtype": "fp32" if cfg.trainer.precision == "32-true" else "bf16",
+            "vs_baseline": (round(value / YARDSTICK[(args.model, args.loss, args.batch)], 3)
+                            if (args.model, args.loss, args.batch) in YARDSTICK else None),
+            "dtype": ("bf16" if (cfg.model.get("arch", "lstm") != "lstm" and dev.type == "cuda")
+                      or cfg.trainer.precision != "32-true" else "fp32"),
             "data": "synthetic (reference DGP, generated on device), random-init weights",
             "config": {
                 "model": f"{type(model).__name__} model={args.model} "

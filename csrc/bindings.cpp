@@ -257,10 +257,12 @@ void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total,
     if (has(dh)) TORCH_CHECK(dh->numel() == N * H, "dh must be (N, H)");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(gmse.device());
+  // the grid-parallel path of wide heads stages d(alpha, beta) in global memory
+  at::Tensor dab_buf = has(dab) ? *dab : at::empty({2 * N}, gmse.options());
   mta_heads_losses_bwd(opt_ptr(g_mse), opt_ptr(g_nll), opt_ptr(g_total), (float)c_nll, (float)c_mse, gmse.data_ptr<float>(),
                        gnll.data_ptr<float>(), has_nll ? 1 : 0, opt_ptr(h), (int)N, (int)H, opt_ptr(wa), opt_ptr(wb),
-                       opt_mut(dh), opt_mut(dab), opt_mut(g_wa), opt_mut(g_ba), opt_mut(g_wb), opt_mut(g_bb),
-                       cur_stream());
+                       opt_mut(dh), dab_buf.data_ptr<float>(), opt_mut(g_wa), opt_mut(g_ba), opt_mut(g_wb),
+                       opt_mut(g_bb), cur_stream());
 }
 
 // ------------------------------------------------------------------------------------------- optimizer

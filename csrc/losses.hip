@@ -259,6 +259,92 @@ __global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
   }
 }
 
+// ---- large N*H (wide encoders, big batches): grid-parallel heads and head backward ----
+// heads: one wave per sequence, ab_out = [h.wa + ba, h.wb + bb]
+__global__ __launch_bounds__(TPB) void heads_kernel(const float* __restrict__ h, int N, int H,
+                                                    const float* __restrict__ wa, const float* __restrict__ ba,
+                                                    const float* __restrict__ wb, const float* __restrict__ bb,
+                                                    float* __restrict__ ab_out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * NWAVES + (threadIdx.x >> 6);
+  if (i >= N) return;
+  float sa = 0.f, sb = 0.f;
+  for (int k = 4 * lane; k < H; k += 256) {  // H % 4 == 0 on this path
+    const float4 hv = *reinterpret_cast<const float4*>(h + (size_t)i * H + k);
+    const float4 av = *reinterpret_cast<const float4*>(wa + k);
+    const float4 bv = *reinterpret_cast<const float4*>(wb + k);
+    sa += hv.x * av.x + hv.y * av.y + hv.z * av.z + hv.w * av.w;
+    sb += hv.x * bv.x + hv.y * bv.y + hv.z * bv.z + hv.w * bv.w;
+  }
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  if (lane == 0) {
+    ab_out[2 * i] = sa + ba[0];
+    ab_out[2 * i + 1] = sb + bb[0];
+  }
+}
+
+// d(alpha, beta) per sequence from the saved loss gradients
+__global__ void heads_dab_kernel(const float* __restrict__ g_mse, const float* __restrict__ g_nll,
+                                 const float* __restrict__ g_total, float c_nll, float c_mse,
+                                 const float* __restrict__ gmse, const float* __restrict__ gnll, int has_nll, int N,
+                                 float* __restrict__ dab) {
+  const float gt = g_total ? g_total[0] : 0.f;
+  const float gm = (g_mse ? g_mse[0] : 0.f) + gt * c_mse;
+  const float gn = has_nll ? (g_nll ? g_nll[0] : 0.f) + gt * c_nll : 0.f;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 2 * N; k += gridDim.x * blockDim.x) {
+    float v = gm * gmse[k];
+    if (has_nll) v = fmaf(gn, gnll[k], v);
+    dab[k] = v;
+  }
+}
+
+// dh = d_a wa + d_b wb (row-wise), head weight / bias gradients: per-block column partials over
+// HB_ROWS rows, one atomic per column per block (contiguous, full-rate no-return atomics)
+constexpr int HB_ROWS = 32;
+__global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __restrict__ dab,
+                                                             const float* __restrict__ h, int N, int H,
+                                                             const float* __restrict__ wa,
+                                                             const float* __restrict__ wb, float* __restrict__ dh,
+                                                             float* __restrict__ g_wa, float* __restrict__ g_ba,
+                                                             float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  const int r0 = blockIdx.x * HB_ROWS;
+  const int r1 = min(r0 + HB_ROWS, N);
+  for (int k = threadIdx.x; k < H; k += TPB) {
+    const float a = wa[k], b = wb[k];
+    float sa = 0.f, sb = 0.f;
+    for (int i = r0; i < r1; ++i) {
+      const float da = dab[2 * i], db = dab[2 * i + 1];
+      if (dh) dh[(size_t)i * H + k] = da * a + db * b;
+      if (g_wa) {
+        const float hv = h[(size_t)i * H + k];
+        sa = fmaf(da, hv, sa);
+        sb = fmaf(db, hv, sb);
+      }
+    }
+    if (g_wa) {
+      atomicAdd(g_wa + k, sa);
+      atomicAdd(g_wb + k, sb);
+    }
+  }
+  if (g_ba && threadIdx.x < 64) {
+    float da = 0.f, db = 0.f;
+    for (int i = r0 + threadIdx.x; i < r1; i += 64) {
+      da += dab[2 * i];
+      db += dab[2 * i + 1];
+    }
+    da = wave_sum(da);
+    db = wave_sum(db);
+    if (threadIdx.x == 0) {
+      atomicAdd(g_ba, da);
+      atomicAdd(g_bb, db);
+    }
+  }
+}
+
+// small problems (the reference config: N = 100, H = 64) stay in the single fused workgroup
+inline bool heads_big(int N, int H) { return (long)N * H > 32768 && H % 4 == 0; }
+
 }  // namespace
 
 extern "C" void mta_decoder_losses(const float* ab, const float* y, const float* factor, const float* inv_psi, int N,
@@ -277,6 +363,11 @@ extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const f
                                  float* gnll, double* acc, hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, gmse, gnll, acc};
+  if (heads_big(N, H)) {
+    heads_kernel<<<(N + NWAVES - 1) / NWAVES, TPB, 0, st>>>(h, N, H, wa, ba, wb, bb, ab_out);
+    decoder_losses_kernel<<<1, TPB, (size_t)((n + 3) & ~3) * sizeof(float), st>>>(ab_out, A);
+    return;
+  }
   const size_t lds = (size_t)(2 * ((N + 1) & ~1) + 4 + ((n + 3) & ~3)) * sizeof(float);
   heads_losses_kernel<<<1, TPB, lds, st>>>(h, H, wa, ba, wb, bb, ab_out, A);
 }
@@ -285,6 +376,13 @@ extern "C" void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, con
                                      const float* gnll, int has_nll, const float* h, int N, int H, const float* wa,
                                      const float* wb, float* dh, float* dab, float* g_wa, float* g_ba, float* g_wb,
                                      float* g_bb, hipStream_t st) {
+  if (heads_big(N, H) && dab) {
+    heads_dab_kernel<<<(2 * N + 255) / 256, 256, 0, st>>>(g_mse, g_nll, g_total, c_nll, c_mse, gmse, gnll, has_nll,
+                                                          N, dab);
+    heads_bwd_grid_kernel<<<(N + HB_ROWS - 1) / HB_ROWS, TPB, 0, st>>>(dab, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb,
+                                                                       g_bb);
+    return;
+  }
   heads_losses_bwd_kernel<<<1, TPB, (size_t)(2 * N) * sizeof(float), st>>>(g_mse, g_nll, g_total, c_nll, c_mse, gmse, gnll, has_nll, h,
                                                                            N, H, wa, wb, dh, dab, g_wa, g_ba, g_wb,
                                                                            g_bb);

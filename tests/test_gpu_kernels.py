@@ -248,3 +248,30 @@ def test_train_step_graph_matches_eager():
     p_graph, acc_graph = run(True)
     torch.testing.assert_close(p_graph, p_eager, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(acc_graph, acc_eager, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,H", [(64, 2048), (8, 512)])
+def test_wide_heads_losses_grid_path(B, H):
+    """N*H above the fused single-workgroup limit: grid-parallel heads forward / backward."""
+    from masters_thesis_amd.ops.losses import heads_losses
+
+    torch.manual_seed(9)
+    N, n = 100 * B, 30
+    h = torch.randn(N, H, dtype=torch.float64) * 0.1
+    wa, ba = torch.randn(1, H, dtype=torch.float64) * 0.05, torch.randn(1, dtype=torch.float64) * 0.1
+    wb, bb = torch.randn(1, H, dtype=torch.float64) * 0.05, torch.ones(1, dtype=torch.float64)
+    y = torch.randn(N, n, 4, dtype=torch.float64)
+    factor = torch.stack([torch.randn(B) * 0.1, torch.rand(B) * 0.5 + 0.2], -1).double()
+    inv_psi = torch.rand(N, dtype=torch.float64) * 3 + 1
+    ref_in = [t.clone().requires_grad_(True) for t in (h, wa, ba, wb, bb)]
+    _, _, _, _, tot_r = heads_losses(*ref_in, y, factor, inv_psi, batch_windows=B, nll_mode="per_window",
+                                     c_nll=1.0, c_mse=100.0)
+    tot_r.backward()
+    gin = [t.float().to(DEV).requires_grad_(True) for t in (h, wa, ba, wb, bb)]
+    _, _, _, _, tot = heads_losses(*gin, y.float().to(DEV), factor.float().to(DEV), inv_psi.float().to(DEV),
+                                   batch_windows=B, nll_mode="per_window", c_nll=1.0, c_mse=100.0)
+    tot.backward()
+    assert abs(tot.item() - tot_r.item()) <= 1e-4 * abs(tot_r.item())
+    for a, b in zip(gin, ref_in):
+        err = (a.grad.double().cpu() - b.grad).abs().max().item()
+        assert err <= 1e-3 * b.grad.abs().max().item() + 1e-6, err
