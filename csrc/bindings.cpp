@@ -48,6 +48,15 @@ int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps,
              float* dgamma, float* dbeta, hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
                   int D, int heads, float rope_base, hipStream_t st);
+// lstm_stack.hip (layer-pipelined multi-layer LSTM)
+int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
+                       const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                       float* const* hseq, float* const* xdrop, float* const* stash, const uint64_t* seeds,
+                       float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
+int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* stash, const float* const* w_hh,
+                       const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
+                       const uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
+                       hipStream_t st);
 // host/prefetch.cpp
 void* mta_prefetch_create(int ntensors, const void* const* host, const long* row_bytes, void* const* staging, int B,
                           int R, int nthreads);
@@ -435,6 +444,84 @@ void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const O
   TORCH_CHECK(rc == 0, "attention: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc, ")");
 }
 
+
+// ------------------------------------------------------------------------------- pipelined LSTM stack
+// list entries with numel() == 0 stand for "no tensor"
+std::vector<float*> ptrs_f32(const std::vector<at::Tensor>& v, const char* name) {
+  std::vector<float*> out;
+  for (const auto& t : v) {
+    if (!t.defined() || t.numel() == 0) {
+      out.push_back(nullptr);
+      continue;
+    }
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), name, ": fp32 contiguous GPU");
+    out.push_back(t.data_ptr<float>());
+  }
+  return out;
+}
+
+int64_t lstm_stack_flag_words(int64_t Np) { return 8 * (((Np / 16) + 7) / 8 * 8) + 4; }
+
+void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
+                    std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
+                    std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> stash,
+                    at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
+  const int64_t L = (int64_t)w_hh.size();
+  MTA_CHECK_F32(x);
+  TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
+  TORCH_CHECK(w_ih.size() == (size_t)L && b_ih.size() == (size_t)L && b_hh.size() == (size_t)L &&
+              hseq.size() == (size_t)L && xdrop.size() == (size_t)L && stash.size() == (size_t)L, "per-layer lists");
+  for (int64_t l = 0; l < L; ++l) {
+    TORCH_CHECK(w_hh[l].numel() == 4 * H * H && w_ih[l].numel() == 4 * H * (l == 0 ? fin : H), "weight shapes");
+    TORCH_CHECK(hseq[l].numel() == T * Np * H, "hseq shape");
+    if (xdrop[l].numel()) TORCH_CHECK(l > 0 && xdrop[l].numel() == T * Np * H, "xdrop shape");
+    if (stash[l].numel()) TORCH_CHECK(stash[l].numel() == T * Np * 5 * H, "stash shape");
+  }
+  TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= L, "seeds: int64[L]");
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.numel() >= lstm_stack_flag_words(Np),
+              "flags: int32 scratch of lstm_stack_flag_words(Np)");
+  auto wi = ptrs_f32(w_ih, "w_ih"), wh = ptrs_f32(w_hh, "w_hh"), bi = ptrs_f32(b_ih, "b_ih"),
+       bh = ptrs_f32(b_hh, "b_hh"), hs = ptrs_f32(hseq, "hseq"), xd = ptrs_f32(xdrop, "xdrop"),
+       sh = ptrs_f32(stash, "stash");
+  std::vector<const float*> cwi(wi.begin(), wi.end()), cwh(wh.begin(), wh.end()), cbi(bi.begin(), bi.end()),
+      cbh(bh.begin(), bh.end());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int rc = mta_lstm_stack_fwd((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(), cwh.data(),
+                                    cbi.data(), cbh.data(), hs.data(), xd.data(), sh.data(),
+                                    reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
+                                    reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
+                                    cur_stream());
+  TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
+}
+
+void lstm_stack_bwd(int64_t H, int64_t prec, std::vector<at::Tensor> stash, std::vector<at::Tensor> w_hh,
+                    std::vector<at::Tensor> w_ih, at::Tensor dh_last, std::vector<at::Tensor> dG,
+                    std::vector<at::Tensor> dX, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
+                    int64_t N, int64_t Np, int64_t T) {
+  const int64_t L = (int64_t)w_hh.size();
+  MTA_CHECK_F32(dh_last);
+  TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
+  TORCH_CHECK(stash.size() == (size_t)L && w_ih.size() == (size_t)L && dG.size() == (size_t)L &&
+              dX.size() == (size_t)L, "per-layer lists");
+  for (int64_t l = 0; l < L; ++l) {
+    TORCH_CHECK(stash[l].numel() == T * Np * 5 * H && dG[l].numel() == T * Np * 4 * H, "stash/dG shapes");
+    TORCH_CHECK(l == L - 1 || dX[l].numel() == T * Np * H, "dX shape");
+  }
+  TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= L, "seeds: int64[L]");
+  TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.numel() >= lstm_stack_flag_words(Np),
+              "flags scratch too small");
+  auto st = ptrs_f32(stash, "stash"), wh = ptrs_f32(w_hh, "w_hh"), wi = ptrs_f32(w_ih, "w_ih"),
+       dg = ptrs_f32(dG, "dG"), dx = ptrs_f32(dX, "dX");
+  std::vector<const float*> cst(st.begin(), st.end()), cwh(wh.begin(), wh.end()), cwi(wi.begin(), wi.end());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dh_last.device());
+  const int rc = mta_lstm_stack_bwd((int)H, (int)prec, (int)L, cst.data(), cwh.data(), cwi.data(),
+                                    dh_last.data_ptr<float>(), dg.data(), dx.data(),
+                                    reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
+                                    dropout ? 1 : 0, reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N,
+                                    (int)Np, (int)T, cur_stream());
+  TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
+}
+
 // Native pinned-ring prefetcher (residency=stream).  Holds references to the host dataset and
 // staging tensors so their storage outlives the worker threads.
 class HostPrefetcher {
@@ -504,6 +591,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stop", &HostPrefetcher::stop)
       .def("close", &HostPrefetcher::close);
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
+  m.def("lstm_stack_fwd", &lstm_stack_fwd);
+  m.def("lstm_stack_bwd", &lstm_stack_bwd);
+  m.def("lstm_stack_flag_words", &lstm_stack_flag_words);
   m.def("gemm_bf16", &gemm_bf16);
   m.def("cast_pad", &cast_pad);
   m.def("norm", &norm);

@@ -1,0 +1,702 @@
+// Layer-pipelined (wavefront) multi-layer LSTM for MI355X (gfx950): ALL layers in one launch.
+//
+// The per-layer kernels in lstm.hip run L x T dependent timesteps (L launches of T steps).  Here one
+// workgroup runs layer l for one 16-sequence tile, and layer l starts step t as soon as layer l-1 has
+// published h^{(l-1)}_t: the critical path becomes ~T + small lag steps instead of L x T
+// (reference: the cuDNN multi-layer LSTM of `src/model.py:88-94`; SURVEY.md K1/K2/K3 "diagonal
+// (layer, t) wavefront").
+//
+//   forward : layer 0 fuses its F-wide input projection (as lstm.hip); layers >= 1 compute
+//             W_ih x_t with MFMA inside the recurrence (W_ih and W_hh both resident in VGPRs), reading
+//             x_t = dropout(h^{(l-1)}_t) that the producer layer stored write-through (sc1) together with
+//             the dropout-masked copy (counter-hash mask, common.h), then publishes a per-(layer, tile)
+//             progress word.
+//   backward: layer l >= 1 also computes dx_t = dG_t W_ih (second MFMA product on the same LDS dG image),
+//             applies its input-dropout mask and hands dH^{(l-1)}_t to layer l-1 the same way.
+//
+// Hand-off protocol (cdna_hip_programming.md Guideline 16, R1 form, placement independent): payload
+// stores are sc1 (write-through); every storing wave drains them (s_waitcnt vmcnt(0)) before the
+// workgroup barrier after which ONE lane stores the progress word with an agent-scope atomic; the consumer
+// polls that word relaxed with s_sleep back-off (bounded: a timeout word is set instead of hanging) and
+// reads the payload with sc1 loads only.  Stores stay delayed by one step (lstm.hip), so progress is
+// published two steps behind; the consumer keeps a one-step-stale copy of the word so a poll is only
+// paid when it actually waits.  All workgroups (L x tiles <= 8 x 16) are co-resident.
+#include "common.h"
+
+namespace {
+
+constexpr int S = 16;
+constexpr int STASH = 5;
+constexpr int MAXL = 8;
+constexpr unsigned SPIN_LIMIT = 1u << 21;
+
+__device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
+  return ((((size_t)t * ntiles + tile) * nw + w) * 64 + lane) * STASH;
+}
+
+__device__ __forceinline__ void store_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// wait until *flag >= need (relaxed agent-scope polls); returns the value seen
+__device__ __forceinline__ unsigned wait_progress(unsigned* flag, unsigned need, unsigned seen, unsigned* tmo) {
+  unsigned spins = 0;
+  while (seen < need) {
+    __builtin_amdgcn_s_sleep(1);
+    seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (++spins > SPIN_LIMIT) {
+      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      seen = 0xFFFFFFFFu;  // give up waiting (results are garbage, the host sees the timeout word)
+    }
+  }
+  // every payload load after this point is sc1 (L1 bypass): only keep the compiler from hoisting them
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return seen;
+}
+
+// 16 bytes of handed-off data as two 8-byte agent-scope atomic loads (global_load_dwordx2 ... sc1:
+// L1-bypassing, the consumer form of the sc1 hand-off)
+__device__ __forceinline__ float4 load_sc1(const float* base, size_t elem) {
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(const_cast<float*>(base) + elem);
+  const unsigned long long a = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  float4 o;
+  o.x = __builtin_bit_cast(float, (unsigned)a);
+  o.y = __builtin_bit_cast(float, (unsigned)(a >> 32));
+  o.z = __builtin_bit_cast(float, (unsigned)b);
+  o.w = __builtin_bit_cast(float, (unsigned)(b >> 32));
+  return o;
+}
+
+struct StackFwdArgs {
+  const float* x;  // layer-0 input (N, T, FIN0), batch-first
+  const float* w_ih[MAXL];
+  const float* w_hh[MAXL];
+  const float* b_ih[MAXL];
+  const float* b_hh[MAXL];
+  float* hseq[MAXL];    // (T, Np, H) outputs of every layer
+  float* xdrop[MAXL];   // xdrop[l] (l >= 1): dropout(h^{(l-1)}), the input of layer l (null: no dropout)
+  float* stash[MAXL];   // BPTT stash per layer (null: inference)
+  const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
+  float drop_p;
+  unsigned* flags;      // [MAXL][tr8] progress words (zeroed per call)
+  unsigned* timeout;
+  int N, Np, T, L, ntiles, tr8;
+};
+
+template <int H, int PREC, int FIN0>
+__global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdArgs a) {
+  constexpr int NW = H / 16;
+  constexpr int KB = H / 32;
+  constexpr int KF = H / 4;
+  constexpr int XR = H / 16;   // float4 of a layer input row per lane (bf16: 2 per k-block; f32: KF/4)
+  constexpr int ROWB = H + 8;
+  constexpr int ROWF = H + 4;
+
+  // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
+  const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+  if (tile >= a.ntiles) return;
+  const bool first = layer == 0, last = layer == a.L - 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  const int u = 16 * w + j;
+  const int n0 = tile * S;
+  const int N = a.N, Np = a.Np, T = a.T;
+  const float* w_hh = a.w_hh[layer];
+  const float* w_ih = a.w_ih[layer];
+  float* hseq = a.hseq[layer];
+  float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
+  const float* xin = first ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
+  float* xout = last ? nullptr : a.xdrop[layer + 1];
+  const uint64_t seed_next = xout ? a.seeds[layer + 1] : 0;
+  unsigned* my_flag = a.flags + layer * a.tr8 + tile;
+  unsigned* in_flag = first ? my_flag : a.flags + (layer - 1) * a.tr8 + tile;
+
+  __shared__ __attribute__((aligned(16))) __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __shared__ __attribute__((aligned(16))) __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  __shared__ __attribute__((aligned(16))) float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+
+  // ---- weights -> registers: W_hh (recurrent) and, for layers >= 1, W_ih as MFMA B fragments ----
+  bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
+  bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : KB], Xlo[4][PREC == PREC_BF16X3 ? KB : 1];
+  float Bf[4][PREC == PREC_F32 ? KF : 1], Xf[4][PREC == PREC_F32 ? KF : 1];
+  if constexpr (PREC == PREC_F32) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk) {
+        Bf[g][kk] = w_hh[(size_t)(g * H + u) * H + 4 * kk + q];
+        // input product: lane (j, q) holds k = (H/4) q + kk (contiguous row quarter, see load_x)
+        Xf[g][kk] = first ? 0.f : w_ih[(size_t)(g * H + u) * H + KF * q + kk];
+      }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          __bf16 hi, lo;
+          split_bf16(w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
+          Bhi[g][kb][e] = hi;
+          if constexpr (PREC == PREC_BF16X3) Blo[g][kb][e] = lo;
+          split_bf16(first ? 0.f : w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
+          Xhi[g][kb][e] = hi;
+          if constexpr (PREC == PREC_BF16X3) Xlo[g][kb][e] = lo;
+        }
+  }
+  float wi[4][FIN0], bias[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
+#pragma unroll
+    for (int f = 0; f < FIN0; ++f) wi[g][f] = first ? w_ih[(g * H + u) * FIN0 + f] : 0.f;
+  }
+
+  if constexpr (PREC == PREC_F32) {
+    for (int idx = threadIdx.x; idx < S * ROWF; idx += blockDim.x) (&h_f[0][0][0])[idx] = 0.f;
+  } else {
+    for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_hi[0][0][0])[idx] = (__bf16)0.f;
+    if constexpr (PREC == PREC_BF16X3)
+      for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
+  }
+  __syncthreads();
+
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  int nrow[4];
+  float nmask[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 4 * q + i;
+    nrow[i] = n < N ? n : N - 1;
+    nmask[i] = n < N ? 1.f : 0.f;
+  }
+
+  // layer 0: fused F-wide projection (bias included); layers >= 1: raw input row quarter of sequence j
+  float nxt[4][4];
+  float4 xr_nxt[XR];
+  auto load_in0 = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float* xs = a.x + ((size_t)nrow[i] * T + t) * FIN0;
+      float xv[FIN0];
+#pragma unroll
+      for (int f = 0; f < FIN0; ++f) xv[f] = xs[f] * nmask[i];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float s = bias[g];
+#pragma unroll
+        for (int f = 0; f < FIN0; ++f) s = fmaf(xv[f], wi[g][f], s);
+        nxt[g][i] = s;
+      }
+    }
+  };
+  auto load_x = [&](int t) {
+    const size_t row = (size_t)t * Np + n0 + j;
+#pragma unroll
+    for (int v = 0; v < XR; ++v) {
+      // bf16: float4 v covers k = 32 (v/2) + 8 q + 4 (v&1) .. +4;  f32: k = KF q + 4 v .. +4
+      const int k = PREC == PREC_F32 ? KF * q + 4 * v : 32 * (v >> 1) + 8 * q + 4 * (v & 1);
+      xr_nxt[v] = load_sc1(xin, row * H + k);
+    }
+  };
+
+  unsigned seen = 0, pend = 0;
+  if (first) {
+    load_in0(0);
+  } else {
+    seen = wait_progress(in_flag, 1, 0, a.timeout);
+    load_x(0);
+  }
+
+  f32x4 pgi, pgf, pgg, pgo, pcc;
+  float ph[4];
+  auto store_step = [&](int t) {
+    if (stash) {
+      float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
+      st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
+      st[1] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      st[2] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      st[3] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      st[4] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
+      store_sc1(hseq + o, ph[i]);
+      if (xout) {
+        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+        store_sc1(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p));
+      }
+    }
+  };
+
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1;
+    f32x4 acc[4];
+    float4 xr[XR];
+    if (first) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{nxt[g][0], nxt[g][1], nxt[g][2], nxt[g][3]};
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
+#pragma unroll
+      for (int v = 0; v < XR; ++v) xr[v] = xr_nxt[v];
+    }
+    mta_wait_vmem();  // this step's prefetch, last step's stores, the pending progress load
+    if (!first) seen = seen > pend ? seen : pend;
+    // progress: every wave drained the stores of step t-3 before the barrier that ended step t-1
+    if (!last && t >= 3 && threadIdx.x == 0)
+      __hip_atomic_store(my_flag, (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t > 0) store_step(t - 1);
+    if (t + 1 < T) {
+      if (first) {
+        load_in0(t + 1);
+      } else {
+        seen = wait_progress(in_flag, (unsigned)(t + 2), seen, a.timeout);
+        load_x(t + 1);
+        pend = __hip_atomic_load(in_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- input product (layers >= 1): acc[g] += x_t (16 x H) . W_ih[g]^T ----------------------
+    if (!first) {
+      if constexpr (PREC == PREC_F32) {
+#pragma unroll
+        for (int kk = 0; kk < KF; ++kk) {
+          const float4 v4 = xr[kk >> 2];
+          const float av = (kk & 3) == 0 ? v4.x : (kk & 3) == 1 ? v4.y : (kk & 3) == 2 ? v4.z : v4.w;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb) {
+          const float4 v0 = xr[2 * kb], v1 = xr[2 * kb + 1];
+          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          bf16x8 ahi, alo;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            __bf16 hi, lo;
+            split_bf16(xv[e], hi, lo);
+            ahi[e] = hi;
+            alo[e] = lo;
+          }
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if constexpr (PREC == PREC_BF16X3) {
+              acc[g] = mfma16x16x32(alo, Xhi[g][kb], acc[g]);
+              acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
+            }
+            acc[g] = mfma16x16x32(ahi, Xhi[g][kb], acc[g]);
+          }
+        }
+      }
+    }
+
+    // ---- recurrent product: acc[g] += h_{t-1} (16 x H) . W_hh[g]^T ------------------------------
+    if constexpr (PREC == PREC_F32) {
+      const float* hrow = &h_f[cur][j][q * KF];
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk) {
+        const float av = hrow[kk];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Bf[g][kk], acc[g]);
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
+        if constexpr (PREC == PREC_BF16X3) {
+          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            acc[g] = mfma16x16x32(alo, Bhi[g][kb], acc[g]);
+            acc[g] = mfma16x16x32(ahi, Blo[g][kb], acc[g]);
+          }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
+      }
+    }
+
+    // ---- gates + cell update -------------------------------------------------------------------
+    const int nb = (t + 1) & 1;
+    float h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pgi[i] = mta_sigmoid(acc[0][i]);
+      pgf[i] = mta_sigmoid(acc[1][i]);
+      pgg[i] = mta_tanh(acc[2][i]);
+      pgo[i] = mta_sigmoid(acc[3][i]);
+      c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
+      pcc[i] = c[i];
+      h[i] = pgo[i] * mta_tanh(c[i]);
+      ph[i] = h[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = 4 * q + i;
+      if constexpr (PREC == PREC_F32) {
+        h_f[nb][s][(u & 3) * KF + (u >> 2)] = h[i];
+      } else {
+        __bf16 hi, lo;
+        split_bf16(h[i], hi, lo);
+        h_hi[nb][s][u] = hi;
+        if constexpr (PREC == PREC_BF16X3) h_lo[nb][s][u] = lo;
+      }
+    }
+    __syncthreads();
+  }
+  store_step(T - 1);
+  mta_wait_vmem();
+  __syncthreads();
+  if (!last && threadIdx.x == 0)
+    __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------------------
+template <int H>
+__device__ __forceinline__ int rperm_to_r(int rp) {
+  const int e = rp & 7, p = rp >> 3;
+  const int uu = 2 * p + (e >> 2), g = e & 3;
+  return g * H + uu;
+}
+
+struct StackBwdArgs {
+  const float* stash[MAXL];
+  const float* w_hh[MAXL];
+  const float* w_ih[MAXL];
+  const float* dh_last;   // (N, H): gradient wrt h_{T-1} of the top layer
+  float* dG[MAXL];        // (T, Np, 4H) per layer, unit-major columns
+  float* dX[MAXL];        // dX[l] (l < L-1): gradient wrt layer l's output sequence, written by layer l+1
+  const uint64_t* seeds;  // [MAXL]: dropout seed of layer l's input
+  float drop_p;
+  int dropout;
+  unsigned* flags;        // [MAXL][tr8]: reverse steps of dX[l-1] published by layer l
+  unsigned* timeout;
+  int N, Np, T, L, ntiles, tr8;
+};
+
+template <int H, int PREC>
+__global__ __launch_bounds__((H / 16) * 64) void lstm_stack_bwd_kernel(StackBwdArgs a) {
+  constexpr int G4 = 4 * H;
+  constexpr int NW = H / 16;
+  constexpr int KB = G4 / 32;
+  constexpr int KF = G4 / 4;
+  constexpr int ROWB = G4 + 8;
+  constexpr int ROWF = G4 + 4;
+
+  // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
+  // so every workgroup a spinning one waits for is already resident): top layer first here
+  const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+  if (tile >= a.ntiles) return;
+  const bool top = layer == a.L - 1, bottom = layer == 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int q = lane >> 4, j = lane & 15;
+  const int u = 16 * w + j;
+  const int n0 = tile * S;
+  const int N = a.N, Np = a.Np, T = a.T;
+  const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
+  const float* w_hh = a.w_hh[layer];
+  const float* w_ih = a.w_ih[layer];
+  float* dG = a.dG[layer];
+  const float* dH = top ? nullptr : a.dX[layer];
+  float* dXout = bottom ? nullptr : a.dX[layer - 1];
+  const uint64_t seed_in = (!bottom && a.dropout) ? a.seeds[layer] : 0;
+  unsigned* my_flag = a.flags + layer * a.tr8 + tile;
+  unsigned* in_flag = top ? my_flag : a.flags + (layer + 1) * a.tr8 + tile;
+
+  __shared__ __attribute__((aligned(16))) __bf16 g_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __shared__ __attribute__((aligned(16))) __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  __shared__ __attribute__((aligned(16))) float g_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+
+  // B fragments: recurrent B[r'][k] = W_hh[r(r')][u]; input-gradient B[r'][k] = W_ih[r(r')][u]
+  bf16x8 Bhi[PREC == PREC_F32 ? 1 : KB], Blo[PREC == PREC_BF16X3 ? KB : 1];
+  bf16x8 Xhi[PREC == PREC_F32 ? 1 : KB], Xlo[PREC == PREC_BF16X3 ? KB : 1];
+  float Bf[PREC == PREC_F32 ? KF : 1], Xf[PREC == PREC_F32 ? KF : 1];
+  if constexpr (PREC == PREC_F32) {
+#pragma unroll
+    for (int kk = 0; kk < KF; ++kk) {
+      Bf[kk] = w_hh[(size_t)(4 * kk + q) * H + u];
+      Xf[kk] = bottom ? 0.f : w_ih[(size_t)(4 * kk + q) * H + u];
+    }
+  } else {
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = rperm_to_r<H>(32 * kb + 8 * q + e);
+        __bf16 hi, lo;
+        split_bf16(w_hh[(size_t)r * H + u], hi, lo);
+        Bhi[kb][e] = hi;
+        if constexpr (PREC == PREC_BF16X3) Blo[kb][e] = lo;
+        split_bf16(bottom ? 0.f : w_ih[(size_t)r * H + u], hi, lo);
+        Xhi[kb][e] = hi;
+        if constexpr (PREC == PREC_BF16X3) Xlo[kb][e] = lo;
+      }
+  }
+
+  float dc[4] = {0.f, 0.f, 0.f, 0.f};
+  float dhr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + 4 * q + i;
+    if (top) {
+      const float v = a.dh_last[(size_t)(n < N ? n : N - 1) * H + u];
+      dhr[i] = n < N ? v : 0.f;
+    } else {
+      dhr[i] = 0.f;
+    }
+  }
+
+  float4 st_nxt[STASH], cp_nxt;
+  float dh_nxt[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_step = [&](int t) {
+    const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
+#pragma unroll
+    for (int k = 0; k < STASH; ++k) st_nxt[k] = src[k];
+    cp_nxt = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 4];
+    if (!top) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        // sc1 scalar loads of the hand-off
+        dh_nxt[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  };
+  float pdG[4][4], pdx[4];
+  auto store_step = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      *reinterpret_cast<float4*>(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u) =
+          make_float4(pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]);
+      if (dXout) {
+        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+        float v = pdx[i];
+        if (seed_in) v *= mta_dropout_scale(seed_in, row, (uint32_t)u, a.drop_p);
+        store_sc1(dXout + (size_t)row * H + u, v);
+      }
+    }
+  };
+
+  unsigned seen = 0, pend = 0;
+  if (!top) seen = wait_progress(in_flag, 1, 0, a.timeout);
+  load_step(T - 1);
+
+  for (int t = T - 1; t >= 0; --t) {
+    float4 st[STASH];
+    float dho[4];
+#pragma unroll
+    for (int k = 0; k < STASH; ++k) st[k] = st_nxt[k];
+    const float cpm = t > 0 ? 1.f : 0.f;
+    const float cp4[4] = {cp_nxt.x * cpm, cp_nxt.y * cpm, cp_nxt.z * cpm, cp_nxt.w * cpm};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dho[i] = dh_nxt[i];
+    mta_wait_vmem();
+    if (!top) seen = seen > pend ? seen : pend;
+    // progress: reverse steps T-1 .. t+3 (stored at the top of t+2.., drained before the last barrier)
+    if (!bottom && t <= T - 4 && threadIdx.x == 0)
+      __hip_atomic_store(my_flag, (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < T - 1) store_step(t + 1);
+    if (t > 0) {
+      if (!top) {
+        seen = wait_progress(in_flag, (unsigned)(T - t + 1), seen, a.timeout);
+        load_step(t - 1);
+        pend = __hip_atomic_load(in_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        load_step(t - 1);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const float ig4[4] = {st[0].x, st[0].y, st[0].z, st[0].w};
+    const float fg4[4] = {st[1].x, st[1].y, st[1].z, st[1].w};
+    const float gg4[4] = {st[2].x, st[2].y, st[2].z, st[2].w};
+    const float og4[4] = {st[3].x, st[3].y, st[3].z, st[3].w};
+    const float ct4[4] = {st[4].x, st[4].y, st[4].z, st[4].w};
+
+    const int buf = t & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float ig = ig4[i], fg = fg4[i], gg = gg4[i], og = og4[i];
+      const float dh = dho[i] + dhr[i];
+      const float tc = mta_tanh(ct4[i]);
+      const float d_o = dh * tc * og * (1.f - og);
+      const float dcc = fmaf(dh * og, 1.f - tc * tc, dc[i]);
+      pdG[0][i] = dcc * gg * ig * (1.f - ig);
+      pdG[1][i] = dcc * cp4[i] * fg * (1.f - fg);
+      pdG[2][i] = dcc * ig * (1.f - gg * gg);
+      pdG[3][i] = d_o;
+      dc[i] = dcc * fg;
+      const int s = 4 * q + i;
+      if constexpr (PREC == PREC_F32) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int r = g * H + u;
+          g_f[buf][s][(r & 3) * KF + (r >> 2)] = pdG[g][i];
+        }
+      } else {
+        bf16x4 hi4, lo4;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          __bf16 hi, lo;
+          split_bf16(pdG[g][i], hi, lo);
+          hi4[g] = hi;
+          lo4[g] = lo;
+        }
+        const int rp = 8 * (u >> 1) + 4 * (u & 1);
+        *reinterpret_cast<bf16x4*>(&g_hi[buf][s][rp]) = hi4;
+        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s][rp]) = lo4;
+      }
+    }
+    if (t == 0 && bottom) {
+      store_step(0);
+      break;
+    }
+    __syncthreads();
+
+    // ---- dh_{t-1} = dG_t . W_hh (t > 0) and dx_t = dG_t . W_ih (layers >= 1) ---------------------
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    f32x4 ax0 = {0.f, 0.f, 0.f, 0.f}, ax1 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (PREC == PREC_F32) {
+      const float* arow = &g_f[buf][j][q * KF];
+#pragma unroll
+      for (int kk = 0; kk < KF; kk += 2) {
+        acc0 = mfma16x16x4f32(arow[kk], Bf[kk], acc0);
+        acc1 = mfma16x16x4f32(arow[kk + 1], Bf[kk + 1], acc1);
+        if (!bottom) {
+          ax0 = mfma16x16x4f32(arow[kk], Xf[kk], ax0);
+          ax1 = mfma16x16x4f32(arow[kk + 1], Xf[kk + 1], ax1);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
+        bf16x8 alo;
+        if constexpr (PREC == PREC_BF16X3) {
+          alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
+          acc1 = mfma16x16x32(alo, Bhi[kb], acc1);
+          acc1 = mfma16x16x32(ahi, Blo[kb], acc1);
+        }
+        acc0 = mfma16x16x32(ahi, Bhi[kb], acc0);
+        if (!bottom) {
+          if constexpr (PREC == PREC_BF16X3) {
+            ax1 = mfma16x16x32(alo, Xhi[kb], ax1);
+            ax1 = mfma16x16x32(ahi, Xlo[kb], ax1);
+          }
+          ax0 = mfma16x16x32(ahi, Xhi[kb], ax0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      dhr[i] = acc0[i] + acc1[i];
+      pdx[i] = ax0[i] + ax1[i];
+    }
+    if (t == 0) {
+      store_step(0);
+      break;
+    }
+  }
+  if (!bottom) {
+    mta_wait_vmem();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int H, int PREC>
+int launch_fwd(int fin, const StackFwdArgs& a, hipStream_t st) {
+  const dim3 grid(a.L * a.tr8), block((H / 16) * 64);
+  if (fin == 3) lstm_stack_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(a);
+  else if (fin == 5) lstm_stack_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(a);
+  else return -1;
+  return 0;
+}
+
+template <int H>
+int dispatch_fwd(int prec, int fin, const StackFwdArgs& a, hipStream_t st) {
+  if (prec == PREC_F32) return launch_fwd<H, PREC_F32>(fin, a, st);
+  if (prec == PREC_BF16X3) return launch_fwd<H, PREC_BF16X3>(fin, a, st);
+  return launch_fwd<H, PREC_BF16>(fin, a, st);
+}
+
+template <int H>
+int dispatch_bwd(int prec, const StackBwdArgs& a, hipStream_t st) {
+  const dim3 grid(a.L * a.tr8), block((H / 16) * 64);
+  if (prec == PREC_F32) lstm_stack_bwd_kernel<H, PREC_F32><<<grid, block, 0, st>>>(a);
+  else if (prec == PREC_BF16X3) lstm_stack_bwd_kernel<H, PREC_BF16X3><<<grid, block, 0, st>>>(a);
+  else lstm_stack_bwd_kernel<H, PREC_BF16><<<grid, block, 0, st>>>(a);
+  return 0;
+}
+
+}  // namespace
+
+// flags: [2][MAXL][tr8] unsigned progress words + timeout word, zeroed here (memset node) every call.
+extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
+                                  const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                                  float* const* hseq, float* const* xdrop, float* const* stash,
+                                  const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
+                                  hipStream_t st) {
+  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
+  StackFwdArgs a{};
+  a.x = x;
+  for (int l = 0; l < L; ++l) {
+    a.w_ih[l] = w_ih[l];
+    a.w_hh[l] = w_hh[l];
+    a.b_ih[l] = b_ih[l];
+    a.b_hh[l] = b_hh[l];
+    a.hseq[l] = hseq[l];
+    a.xdrop[l] = xdrop ? xdrop[l] : nullptr;
+    a.stash[l] = stash ? stash[l] : nullptr;
+  }
+  a.seeds = seeds;
+  a.drop_p = drop_p;
+  a.N = N;
+  a.Np = Np;
+  a.T = T;
+  a.L = L;
+  a.ntiles = Np / S;
+  a.tr8 = (a.ntiles + 7) / 8 * 8;  // tile i of every layer gets the same block id modulo 8
+  a.flags = flags;
+  a.timeout = flags + MAXL * a.tr8;
+  if (hipMemsetAsync(flags, 0, (size_t)(MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess) return -2;
+  if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
+  return dispatch_fwd<64>(prec, fin, a, st);
+}
+
+extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* stash, const float* const* w_hh,
+                                  const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
+                                  const uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np,
+                                  int T, hipStream_t st) {
+  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
+  StackBwdArgs a{};
+  for (int l = 0; l < L; ++l) {
+    a.stash[l] = stash[l];
+    a.w_hh[l] = w_hh[l];
+    a.w_ih[l] = w_ih[l];
+    a.dG[l] = dG[l];
+    a.dX[l] = dX ? dX[l] : nullptr;
+  }
+  a.dh_last = dh_last;
+  a.seeds = seeds;
+  a.drop_p = drop_p;
+  a.dropout = dropout;
+  a.N = N;
+  a.Np = Np;
+  a.T = T;
+  a.L = L;
+  a.ntiles = Np / S;
+  a.tr8 = (a.ntiles + 7) / 8 * 8;
+  a.flags = flags;
+  a.timeout = flags + MAXL * a.tr8;
+  if (hipMemsetAsync(flags, 0, (size_t)(MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess) return -2;
+  if (H == 32) return dispatch_bwd<32>(prec, a, st);
+  return dispatch_bwd<64>(prec, a, st);
+}

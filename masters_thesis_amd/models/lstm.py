@@ -44,6 +44,8 @@ class LSTMStack(torch.nn.Module):
                                 (f"bias_ih_l{l}", (4 * hidden_size,)), (f"bias_hh_l{l}", (4 * hidden_size,))):
                 self.register_parameter(name, torch.nn.Parameter(torch.empty(shape)))
                 self._flat_names.append(name)
+        # counter-hash dropout seeds of the pipelined HIP path (one per layer input), advanced in-graph
+        self.register_buffer("seeds", torch.randint(0, 2 ** 62, (8,), dtype=torch.int64), persistent=False)
         self.reset_parameters()
 
     def reset_parameters(self) -> None:
@@ -68,7 +70,8 @@ class LSTMStack(torch.nn.Module):
                                        self.training, False, True)
             return out[:, -1, :]
         return lstm_op.lstm_last_hidden(x, self.flat_weights, self.num_layers,
-                                        self.dropout if self.num_layers > 1 else 0.0, self.training, precision)
+                                        self.dropout if self.num_layers > 1 else 0.0, self.training, precision,
+                                        self.seeds)
 
 
 class FinancialLstm(LightningModule):

@@ -126,6 +126,96 @@ class _LSTMStackFn(torch.autograd.Function):
         return (dx, None, None, None, None, *([None] * (4 * L)))
 
 
+_E = {}
+
+
+def _empty(dev) -> Tensor:
+    key = str(dev)
+    if key not in _E:
+        _E[key] = torch.empty(0, device=dev)
+    return _E[key]
+
+
+def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) -> bool:
+    """Layer-pipelined single-launch path (csrc/lstm_stack.hip) applicability."""
+    import os
+
+    if os.environ.get("MTA_LSTM_PIPELINE", "1") == "0" or x.requires_grad:
+        return False
+    H = weights[1].shape[1]
+    N, T, F = x.shape
+    tr8 = -(-(padded_rows(N) // 16) // 8) * 8
+    # all L x tiles workgroups must be co-resident (<= 2 per CU at 256 VGPRs)
+    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= 448
+
+
+class _LSTMPipelinedFn(torch.autograd.Function):
+    """All layers in one forward launch and one backward launch (wavefront over (layer, t))."""
+
+    @staticmethod
+    def forward(ctx, x: Tensor, seeds: Tensor, prec: int, dropout: float, training: bool, need_grad: bool,
+                *flat: Tensor) -> Tensor:
+        L = len(flat) // 4
+        N, T, F = x.shape
+        H = flat[1].shape[1]
+        Np = padded_rows(N)
+        C = lib()
+        dev = x.device
+        E = _empty(dev)
+        drop = dropout > 0.0 and training
+        if drop:
+            seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))  # fresh counter-hash masks every step (in-graph)
+        hseq = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L)]
+        xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E
+                       for _ in range(1, L)]
+        stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E
+                 for _ in range(L)]
+        flags = torch.empty(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
+        C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
+                         hseq, xdrop, stash, seeds, float(dropout), flags, N, Np, T)
+        ctx.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
+        ctx.params = flat
+        ctx.seeds = seeds
+        ctx.fwd_flags = flags
+        if need_grad:
+            ctx.save_for_backward(x, *stash, *hseq, *[t for t in xdrop[1:] if drop])
+        return hseq[L - 1][T - 1, :N]
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh_last: Tensor):
+        L, H, N, Np, T, F, prec, p, drop = ctx.meta
+        C = lib()
+        dev = dh_last.device
+        saved = ctx.saved_tensors
+        x = saved[0]
+        stash = list(saved[1:1 + L])
+        hseq = list(saved[1 + L:1 + 2 * L])
+        xdrop = list(saved[1 + 2 * L:]) if drop else []
+        flat = ctx.params
+        dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
+        dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
+        flags = torch.empty(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
+        C.lstm_stack_bwd(H, prec, stash, list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
+                         ctx.seeds, p, drop, flags, N, Np, T)
+        ctx.bwd_flags = flags
+        for l in range(L):
+            w_ih, w_hh, b_ih, b_hh = flat[4 * l: 4 * l + 4]
+            if l == 0:
+                inp = x
+            else:
+                inp = (xdrop[l - 1] if drop else hseq[l - 1]).view(T * Np, H)
+            C.lstm_wgrad(prec, dG[l], hseq[l], inp, l == 0, N, Np, T, H, _grad_buffer(w_ih), _grad_buffer(w_hh),
+                         _grad_buffer(b_ih), _grad_buffer(b_hh))
+        return (None,) * (6 + len(flat))
+
+
+def stack_timed_out(flags: Tensor) -> bool:
+    """True if a pipelined launch gave up waiting on a producer (diagnostic; host sync)."""
+    Np_tiles8 = (flags.numel() - 4) // 8
+    return bool(flags[8 * Np_tiles8].item() != 0)
+
+
 _PERM_CACHE = {}
 
 
@@ -139,11 +229,19 @@ def _unit_major_rows(H: int, device) -> Tensor:
 
 
 def lstm_last_hidden(x: Tensor, weights: Sequence[Tensor], num_layers: int, dropout: float, training: bool,
-                     precision=None) -> Tensor:
+                     precision=None, seeds: Tensor = None) -> Tensor:
     """Run the stacked LSTM over batch-first ``x (N, T, F)`` and return ``h_T`` of the top layer (N, H).
 
     ``weights`` is nn.LSTM's flat list ``[w_ih_l0, w_hh_l0, b_ih_l0, b_hh_l0, w_ih_l1, ...]``.
+    ``seeds`` (int64[>= L] on the device) drives the pipelined path's counter-hash dropout masks.
     """
+    if use_hip(x) and pipeline_supported(x, weights, num_layers) and (
+            seeds is not None or not (dropout > 0 and training)):
+        if seeds is None:
+            seeds = torch.zeros(8, dtype=torch.int64, device=x.device)
+        need_grad = torch.is_grad_enabled() and any(t.requires_grad for t in weights)
+        return _LSTMPipelinedFn.apply(x.contiguous(), seeds, precision_code(precision), float(dropout),
+                                      bool(training), need_grad, *weights)
     if use_hip(x):
         # grad mode is off inside Function.forward: decide here whether to keep the stash
         need_grad = torch.is_grad_enabled() and any(t.requires_grad for t in (x, *weights))

@@ -1,0 +1,130 @@
+"""Layer-pipelined LSTM (csrc/lstm_stack.hip): one launch for all layers, vs fp64 references."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+TOLS = {"highest": 2e-5, "high": 3e-4, "medium": 3e-2}
+
+
+def _weights(F, H, L, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    k = 1.0 / math.sqrt(H)
+    ws = []
+    for l in range(L):
+        fin = F if l == 0 else H
+        for shape in ((4 * H, fin), (4 * H, H), (4 * H,), (4 * H,)):
+            ws.append((torch.rand(shape, generator=g) * 2 - 1) * k)
+    return ws
+
+
+def _hash3(seed: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Python mirror of mta_hash3 (csrc/common.h)."""
+    M = np.uint64(0xFFFFFFFF)
+
+    def u32(v):
+        return np.asarray(v, dtype=np.uint64) & M
+
+    def rotl(x, r):
+        return ((x << np.uint64(r)) | (x >> np.uint64(32 - r))) & M
+
+    h = u32(np.full(a.shape, (seed & 0xFFFFFFFF) ^ 0x9E3779B9, dtype=np.uint64))
+    for k in (u32(np.full(a.shape, seed >> 32, dtype=np.uint64)), u32(a), u32(b)):
+        x = (k * np.uint64(0xCC9E2D51)) & M
+        x = rotl(x, 15)
+        x = (x * np.uint64(0x1B873593)) & M
+        h = h ^ x
+        h = rotl(h, 13)
+        h = (h * np.uint64(5) + np.uint64(0xE6546B64)) & M
+    h = h ^ np.uint64(12)
+    h = h ^ (h >> np.uint64(16))
+    h = (h * np.uint64(0x85EBCA6B)) & M
+    h = h ^ (h >> np.uint64(13))
+    h = (h * np.uint64(0xC2B2AE35)) & M
+    h = h ^ (h >> np.uint64(16))
+    return h
+
+
+def _mask(seed: int, T: int, Np: int, N: int, H: int, p: float) -> torch.Tensor:
+    """(N, T, H) dropout scale of the kernel's row = t*Np + n, col = unit."""
+    t = np.arange(T)[:, None, None]
+    n = np.arange(N)[None, :, None]
+    u = np.arange(H)[None, None, :]
+    rows = np.broadcast_to(t * Np + n, (T, N, H))
+    cols = np.broadcast_to(u, (T, N, H))
+    hv = _hash3(seed, rows, cols)
+    uni = (hv >> np.uint64(8)).astype(np.float64) / 16777216.0
+    keep = (uni >= p).astype(np.float64) / (1.0 - p)
+    return torch.from_numpy(keep).permute(1, 0, 2).contiguous()
+
+
+def _ref(x, ws, L, masks=None):
+    """fp64 per-layer reference (masks[l]: dropout scale of layer l's input, l >= 1)."""
+    inp = x.double()
+    ws64 = [w.double().requires_grad_(True) for w in ws]
+    N, H = x.shape[0], ws[1].shape[1]
+    for l in range(L):
+        if masks is not None and l > 0:
+            inp = inp * masks[l]
+        h0 = torch.zeros(1, N, H, dtype=torch.float64)
+        out, _, _ = torch._VF.lstm(inp, (h0, h0), ws64[4 * l: 4 * l + 4], True, 1, 0.0, False, False, True)
+        inp = out
+    return inp[:, -1], ws64
+
+
+@pytest.mark.parametrize("prec", ["highest", "high", "medium"])
+@pytest.mark.parametrize("N,T,F,H,L", [(100, 60, 3, 64, 2), (37, 20, 5, 64, 3), (40, 15, 3, 32, 8),
+                                       (300, 60, 3, 64, 4)])
+def test_pipelined_matches_fp64(prec, N, T, F, H, L):
+    from masters_thesis_amd.ops import lstm as op
+
+    torch.manual_seed(1)
+    x = torch.randn(N, T, F)
+    ws = _weights(F, H, L)
+    R = torch.randn(N, H)
+    ref, w64 = _ref(x, ws, L)
+    (ref * R.double()).sum().backward()
+    xg = x.to(DEV)
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    assert op.pipeline_supported(xg, wg, L)
+    out = op.lstm_last_hidden(xg, wg, L, 0.0, True, prec)
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    tol = TOLS[prec]
+    scale = ref.abs().max().item()
+    err = (out.double().cpu() - ref.detach()).abs().max().item()
+    assert err <= tol * max(scale, 1.0), f"forward err {err}"
+    for i, (a, b) in enumerate(zip(wg, w64)):
+        sc = b.grad.abs().max().item()
+        e = (a.grad.double().cpu() - b.grad).abs().max().item()
+        assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad w{i}: err {e} (scale {sc})"
+
+
+def test_pipelined_dropout_masks_match_counter_hash():
+    from masters_thesis_amd.ops import lstm as op
+
+    torch.manual_seed(2)
+    N, T, F, H, L, p = 50, 24, 3, 64, 3, 0.3
+    Np = op.padded_rows(N)
+    x = torch.randn(N, T, F)
+    ws = _weights(F, H, L, seed=3)
+    seeds = torch.randint(0, 2 ** 62, (8,), dtype=torch.int64, device=DEV)
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    out = op.lstm_last_hidden(x.to(DEV), wg, L, p, True, "highest", seeds)
+    R = torch.randn(N, H)
+    (out * R.to(DEV)).sum().backward()
+    used = seeds.cpu().tolist()  # advanced in-op before the launch
+    masks = [None] + [_mask(used[l] & ((1 << 64) - 1), T, Np, N, H, p).double() for l in range(1, L)]
+    ref, w64 = _ref(x, ws, L, masks)
+    (ref * R.double()).sum().backward()
+    assert (out.double().cpu() - ref.detach()).abs().max().item() < 1e-4
+    for a, b in zip(wg, w64):
+        assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-4 * max(b.grad.abs().max().item(), 1e-3)
+    # eval mode: no dropout, no seed advance
+    before = seeds.clone()
+    with torch.no_grad():
+        ev = op.lstm_last_hidden(x.to(DEV), wg, L, p, False, "highest", seeds)
+    assert torch.equal(before, seeds) and not torch.allclose(ev, out)
