@@ -460,7 +460,7 @@ std::vector<float*> ptrs_f32(const std::vector<at::Tensor>& v, const char* name)
   return out;
 }
 
-int64_t lstm_stack_flag_words(int64_t Np) { return 8 * (((Np / 16) + 7) / 8 * 8) + 4; }
+int64_t lstm_stack_flag_words(int64_t Np) { return 32 * 8 * (((Np / 16) + 7) / 8 * 8) + 4; }
 
 void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
                     std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,

@@ -21,6 +21,8 @@
 // reads the payload with sc1 loads only.  Stores stay delayed by one step (lstm.hip), so progress is
 // published two steps behind; the consumer keeps a one-step-stale copy of the word so a poll is only
 // paid when it actually waits.  All workgroups (L x tiles <= 8 x 16) are co-resident.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -29,6 +31,7 @@ constexpr int S = 16;
 constexpr int STASH = 5;
 constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;
+constexpr int FLAG_STRIDE = 32;  // one 128-byte line per progress word (polled words never share a line)
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
   return ((((size_t)t * ntiles + tile) * nw + w) * 64 + lane) * STASH;
@@ -36,6 +39,11 @@ __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w
 
 __device__ __forceinline__ void store_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// timing probe only (MTA_STACK_PLAIN_STORES=1): plain stores are NOT a valid cross-XCD hand-off
+__device__ __forceinline__ void store_handoff(float* p, float v, int plain) {
+  if (plain) *p = v;
+  else store_sc1(p, v);
 }
 
 // wait until *flag >= need (relaxed agent-scope polls); returns the value seen
@@ -81,54 +89,196 @@ struct StackFwdArgs {
   float drop_p;
   unsigned* flags;      // [MAXL][tr8] progress words (zeroed per call)
   unsigned* timeout;
-  int N, Np, T, L, ntiles, tr8;
+  int N, Np, T, L, ntiles, tr8, plain_probe;
 };
 
-template <int H, int PREC, int FIN0>
-__global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdArgs a) {
+// Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
+// (W_hh in VGPRs, h through LDS, one barrier per step); waves [H/16, 2 H/16) are INPUT waves: one step
+// ahead they wait for / load the layer input and compute the gate pre-activations
+// gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products for layer 0, MFMA for layers >= 1) into a
+// double-buffered LDS slot, so the recurrent critical path never sees the hand-off latency, the progress
+// polls or the input product.  Both roles execute the same barriers (pre-loop, one per step, final).
+template <int H, int PREC>
+struct FwdSmem {
+  static constexpr int ROWB = H + 8, ROWF = H + 4;
+  float4 gxs[2][S][H];  // gate pre-activations (i, f, g, o) per (sequence, unit)
+  __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+};
+
+template <int H, int PREC, int FIN0, bool FIRST>
+__device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
+                                               FwdSmem<H, PREC>& sm) {
   constexpr int NW = H / 16;
   constexpr int KB = H / 32;
   constexpr int KF = H / 4;
-  constexpr int XR = H / 16;   // float4 of a layer input row per lane (bf16: 2 per k-block; f32: KF/4)
+  constexpr int XR = H / 16;  // float4 of a layer input row per lane (bf16: 2 per k-block; f32: KF/4)
   constexpr int ROWB = H + 8;
   constexpr int ROWF = H + 4;
 
-  // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
-  const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
-  if (tile >= a.ntiles) return;
-  const bool first = layer == 0, last = layer == a.L - 1;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool last = layer == a.L - 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool input_wave = wave >= NW;
+  const int w = input_wave ? wave - NW : wave;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
   const int n0 = tile * S;
   const int N = a.N, Np = a.Np, T = a.T;
+
+  auto& gxs = sm.gxs;
+  auto& h_hi = sm.h_hi;
+  auto& h_lo = sm.h_lo;
+  auto& h_f = sm.h_f;
+
+  float bias[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
+
+  if (input_wave) {
+    // =========================== input waves ===========================
+    const float* w_ih = a.w_ih[layer];
+    const float* xin = FIRST ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
+    unsigned* in_flag = a.flags + FLAG_STRIDE * (FIRST ? 0 : (layer - 1) * a.tr8 + tile);
+    constexpr int XKB = FIRST ? 1 : KB, XKF = FIRST ? 1 : KF;
+    bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][PREC == PREC_BF16X3 ? XKB : 1];
+    float Xf[4][PREC == PREC_F32 ? XKF : 1];
+    float wi[4][FIRST ? FIN0 : 1];
+    if constexpr (FIRST) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int f = 0; f < FIN0; ++f) wi[g][f] = w_ih[(g * H + u) * FIN0 + f];
+    } else if constexpr (PREC == PREC_F32) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int kk = 0; kk < KF; ++kk) Xf[g][kk] = w_ih[(size_t)(g * H + u) * H + KF * q + kk];
+    } else {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            __bf16 hi, lo;
+            split_bf16(w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
+            Xhi[g][kb][e] = hi;
+            if constexpr (PREC == PREC_BF16X3) Xlo[g][kb][e] = lo;
+          }
+    }
+    int nrow[4];
+    float nmask[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + 4 * q + i;
+      nrow[i] = n < N ? n : N - 1;
+      nmask[i] = n < N ? 1.f : 0.f;
+    }
+    float xin0[4][FIRST ? FIN0 : 1];
+    float4 xr[FIRST ? 1 : XR];
+    unsigned seen = 0;
+    auto load_input = [&](int t) {
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float* xs = a.x + ((size_t)nrow[i] * T + t) * FIN0;
+#pragma unroll
+          for (int f = 0; f < FIN0; ++f) xin0[i][f] = xs[f];
+        }
+      } else {
+        // poll only when the last value seen does not cover step t (polling every step from every
+        // consumer wave measured slower: the progress words share cache lines across tiles)
+        seen = wait_progress(in_flag, (unsigned)(t + 1), seen, a.timeout);
+        const size_t row = (size_t)t * Np + n0 + j;
+#pragma unroll
+        for (int v = 0; v < XR; ++v) {
+          // bf16: float4 v covers k = 32 (v/2) + 8 q + 4 (v&1) .. +4;  f32: k = KF q + 4 v .. +4
+          const int k = PREC == PREC_F32 ? KF * q + 4 * v : 32 * (v >> 1) + 8 * q + 4 * (v & 1);
+          xr[v] = load_sc1(xin, row * H + k);
+        }
+      }
+    };
+    auto compute_gx = [&](int slot) {
+      f32x4 acc[4];
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float sacc = bias[g];
+#pragma unroll
+            for (int f = 0; f < FIN0; ++f) sacc = fmaf(xin0[i][f] * nmask[i], wi[g][f], sacc);
+            acc[g][i] = sacc;
+          }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
+        if constexpr (PREC == PREC_F32) {
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) {
+            const float4 v4 = xr[kk >> 2];
+            const float av = (kk & 3) == 0 ? v4.x : (kk & 3) == 1 ? v4.y : (kk & 3) == 2 ? v4.z : v4.w;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
+          }
+        } else {
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            const float4 v0 = xr[2 * kb], v1 = xr[2 * kb + 1];
+            const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            bf16x8 ahi, alo;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              __bf16 hi, lo;
+              split_bf16(xv[e], hi, lo);
+              ahi[e] = hi;
+              alo[e] = lo;
+            }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if constexpr (PREC == PREC_BF16X3) {
+                acc[g] = mfma16x16x32(alo, Xhi[g][kb], acc[g]);
+                acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
+              }
+              acc[g] = mfma16x16x32(ahi, Xhi[g][kb], acc[g]);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+    };
+    load_input(0);
+    compute_gx(0);
+    if (T > 1) load_input(1);
+    __syncthreads();  // pre-loop barrier: gx_0 ready
+    for (int t = 0; t < T; ++t) {
+      if (t + 1 < T) {
+        compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
+        if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
+      }
+      __syncthreads();
+    }
+    __syncthreads();  // final barrier (the recurrent waves publish after it)
+    return;
+  }
+
+  // =========================== recurrent waves ===========================
   const float* w_hh = a.w_hh[layer];
-  const float* w_ih = a.w_ih[layer];
   float* hseq = a.hseq[layer];
   float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
-  const float* xin = first ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
   float* xout = last ? nullptr : a.xdrop[layer + 1];
   const uint64_t seed_next = xout ? a.seeds[layer + 1] : 0;
-  unsigned* my_flag = a.flags + layer * a.tr8 + tile;
-  unsigned* in_flag = first ? my_flag : a.flags + (layer - 1) * a.tr8 + tile;
+  unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
 
-  __shared__ __attribute__((aligned(16))) __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
-  __shared__ __attribute__((aligned(16))) __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
-  __shared__ __attribute__((aligned(16))) float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
-
-  // ---- weights -> registers: W_hh (recurrent) and, for layers >= 1, W_ih as MFMA B fragments ----
   bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
-  bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : KB], Xlo[4][PREC == PREC_BF16X3 ? KB : 1];
-  float Bf[4][PREC == PREC_F32 ? KF : 1], Xf[4][PREC == PREC_F32 ? KF : 1];
+  float Bf[4][PREC == PREC_F32 ? KF : 1];
   if constexpr (PREC == PREC_F32) {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int kk = 0; kk < KF; ++kk) {
-        Bf[g][kk] = w_hh[(size_t)(g * H + u) * H + 4 * kk + q];
-        // input product: lane (j, q) holds k = (H/4) q + kk (contiguous row quarter, see load_x)
-        Xf[g][kk] = first ? 0.f : w_ih[(size_t)(g * H + u) * H + KF * q + kk];
-      }
+      for (int kk = 0; kk < KF; ++kk) Bf[g][kk] = w_hh[(size_t)(g * H + u) * H + 4 * kk + q];
   } else {
 #pragma unroll
     for (int g = 0; g < 4; ++g)
@@ -140,75 +290,18 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdA
           split_bf16(w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
           Bhi[g][kb][e] = hi;
           if constexpr (PREC == PREC_BF16X3) Blo[g][kb][e] = lo;
-          split_bf16(first ? 0.f : w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
-          Xhi[g][kb][e] = hi;
-          if constexpr (PREC == PREC_BF16X3) Xlo[g][kb][e] = lo;
         }
   }
-  float wi[4][FIN0], bias[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
-#pragma unroll
-    for (int f = 0; f < FIN0; ++f) wi[g][f] = first ? w_ih[(g * H + u) * FIN0 + f] : 0.f;
-  }
-
   if constexpr (PREC == PREC_F32) {
-    for (int idx = threadIdx.x; idx < S * ROWF; idx += blockDim.x) (&h_f[0][0][0])[idx] = 0.f;
+    for (int idx = threadIdx.x; idx < S * ROWF; idx += NW * 64) (&h_f[0][0][0])[idx] = 0.f;
   } else {
-    for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_hi[0][0][0])[idx] = (__bf16)0.f;
+    for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_hi[0][0][0])[idx] = (__bf16)0.f;
     if constexpr (PREC == PREC_BF16X3)
-      for (int idx = threadIdx.x; idx < S * ROWB; idx += blockDim.x) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
+      for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
   }
-  __syncthreads();
+  __syncthreads();  // pre-loop barrier
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  int nrow[4];
-  float nmask[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + 4 * q + i;
-    nrow[i] = n < N ? n : N - 1;
-    nmask[i] = n < N ? 1.f : 0.f;
-  }
-
-  // layer 0: fused F-wide projection (bias included); layers >= 1: raw input row quarter of sequence j
-  float nxt[4][4];
-  float4 xr_nxt[XR];
-  auto load_in0 = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float* xs = a.x + ((size_t)nrow[i] * T + t) * FIN0;
-      float xv[FIN0];
-#pragma unroll
-      for (int f = 0; f < FIN0; ++f) xv[f] = xs[f] * nmask[i];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float s = bias[g];
-#pragma unroll
-        for (int f = 0; f < FIN0; ++f) s = fmaf(xv[f], wi[g][f], s);
-        nxt[g][i] = s;
-      }
-    }
-  };
-  auto load_x = [&](int t) {
-    const size_t row = (size_t)t * Np + n0 + j;
-#pragma unroll
-    for (int v = 0; v < XR; ++v) {
-      // bf16: float4 v covers k = 32 (v/2) + 8 q + 4 (v&1) .. +4;  f32: k = KF q + 4 v .. +4
-      const int k = PREC == PREC_F32 ? KF * q + 4 * v : 32 * (v >> 1) + 8 * q + 4 * (v & 1);
-      xr_nxt[v] = load_sc1(xin, row * H + k);
-    }
-  };
-
-  unsigned seen = 0, pend = 0;
-  if (first) {
-    load_in0(0);
-  } else {
-    seen = wait_progress(in_flag, 1, 0, a.timeout);
-    load_x(0);
-  }
-
   f32x4 pgi, pgf, pgg, pgo, pcc;
   float ph[4];
   auto store_step = [&](int t) {
@@ -220,83 +313,37 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdA
       st[3] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
       st[4] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
     }
+    if (xout) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
-      store_sc1(hseq + o, ph[i]);
-      if (xout) {
+      for (int i = 0; i < 4; ++i) {
+        const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
         const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-        store_sc1(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p));
+        store_handoff(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p), a.plain_probe);
       }
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) store_handoff(hseq + ((size_t)t * Np + n0 + 4 * q + i) * H + u, ph[i], a.plain_probe);
   };
 
   for (int t = 0; t < T; ++t) {
     const int cur = t & 1;
     f32x4 acc[4];
-    float4 xr[XR];
-    if (first) {
 #pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{nxt[g][0], nxt[g][1], nxt[g][2], nxt[g][3]};
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
-#pragma unroll
-      for (int v = 0; v < XR; ++v) xr[v] = xr_nxt[v];
+    for (int i = 0; i < 4; ++i) {
+      const float4 v = gxs[cur][4 * q + i][u];
+      acc[0][i] = v.x;
+      acc[1][i] = v.y;
+      acc[2][i] = v.z;
+      acc[3][i] = v.w;
     }
-    mta_wait_vmem();  // this step's prefetch, last step's stores, the pending progress load
-    if (!first) seen = seen > pend ? seen : pend;
-    // progress: every wave drained the stores of step t-3 before the barrier that ended step t-1
+    mta_wait_vmem();  // the stores issued at the previous top (a whole step ago)
+    // progress: stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
+    // the barrier that ended step t-1
     if (!last && t >= 3 && threadIdx.x == 0)
       __hip_atomic_store(my_flag, (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t > 0) store_step(t - 1);
-    if (t + 1 < T) {
-      if (first) {
-        load_in0(t + 1);
-      } else {
-        seen = wait_progress(in_flag, (unsigned)(t + 2), seen, a.timeout);
-        load_x(t + 1);
-        pend = __hip_atomic_load(in_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     __builtin_amdgcn_sched_barrier(0);
 
-    // ---- input product (layers >= 1): acc[g] += x_t (16 x H) . W_ih[g]^T ----------------------
-    if (!first) {
-      if constexpr (PREC == PREC_F32) {
-#pragma unroll
-        for (int kk = 0; kk < KF; ++kk) {
-          const float4 v4 = xr[kk >> 2];
-          const float av = (kk & 3) == 0 ? v4.x : (kk & 3) == 1 ? v4.y : (kk & 3) == 2 ? v4.z : v4.w;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
-        }
-      } else {
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          const float4 v0 = xr[2 * kb], v1 = xr[2 * kb + 1];
-          const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-          bf16x8 ahi, alo;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            __bf16 hi, lo;
-            split_bf16(xv[e], hi, lo);
-            ahi[e] = hi;
-            alo[e] = lo;
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            if constexpr (PREC == PREC_BF16X3) {
-              acc[g] = mfma16x16x32(alo, Xhi[g][kb], acc[g]);
-              acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
-            }
-            acc[g] = mfma16x16x32(ahi, Xhi[g][kb], acc[g]);
-          }
-        }
-      }
-    }
-
-    // ---- recurrent product: acc[g] += h_{t-1} (16 x H) . W_hh[g]^T ------------------------------
     if constexpr (PREC == PREC_F32) {
       const float* hrow = &h_f[cur][j][q * KF];
 #pragma unroll
@@ -322,7 +369,6 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdA
       }
     }
 
-    // ---- gates + cell update -------------------------------------------------------------------
     const int nb = (t + 1) & 1;
     float h[4];
 #pragma unroll
@@ -338,23 +384,33 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_fwd_kernel(StackFwdA
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int s = 4 * q + i;
+      const int s4 = 4 * q + i;
       if constexpr (PREC == PREC_F32) {
-        h_f[nb][s][(u & 3) * KF + (u >> 2)] = h[i];
+        h_f[nb][s4][(u & 3) * KF + (u >> 2)] = h[i];
       } else {
         __bf16 hi, lo;
         split_bf16(h[i], hi, lo);
-        h_hi[nb][s][u] = hi;
-        if constexpr (PREC == PREC_BF16X3) h_lo[nb][s][u] = lo;
+        h_hi[nb][s4][u] = hi;
+        if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
       }
     }
     __syncthreads();
   }
   store_step(T - 1);
   mta_wait_vmem();
-  __syncthreads();
+  __syncthreads();  // final barrier
   if (!last && threadIdx.x == 0)
     __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int H, int PREC, int FIN0>
+__global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
+  // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
+  const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+  if (tile >= a.ntiles) return;
+  __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
+  if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm);
+  else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -379,147 +435,216 @@ struct StackBwdArgs {
   int dropout;
   unsigned* flags;        // [MAXL][tr8]: reverse steps of dX[l-1] published by layer l
   unsigned* timeout;
-  int N, Np, T, L, ntiles, tr8;
+  int N, Np, T, L, ntiles, tr8, plain_probe;
 };
 
 template <int H, int PREC>
-__global__ __launch_bounds__((H / 16) * 64) void lstm_stack_bwd_kernel(StackBwdArgs a) {
+struct BwdSmem {
+  static constexpr int ROWB = 4 * H + 8, ROWF = 4 * H + 4;
+  __bf16 g_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  float g_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+  float dhs[2][S][H];  // dH_t of the layer above, staged by the gradient waves
+};
+
+// Backward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run BPTT exactly like lstm.hip (dG_t from the
+// stash, dh_{t-1} = dG_t W_hh through the LDS dG image, one barrier per step); waves [H/16, 2 H/16) are
+// GRADIENT waves: they stage dH_t of the layer above into LDS two steps ahead (progress polls and hand-off
+// latency off the recurrent path) and compute dx_t = dG_t W_ih from the same LDS image one step behind,
+// apply this layer's input-dropout mask and hand dH^{(l-1)} to the layer below.
+// Intervals: I(t) = between barriers A(t+1) and A(t); the recurrent waves read dhs[t&1] and write the
+// dG image (t&1) in I(t); the gradient waves write dhs[(t-1)&1] and read image ((t+1)&1) in I(t).
+template <int H, int PREC, bool TOP, bool BOTTOM>
+__device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int layer, const int tile,
+                                               BwdSmem<H, PREC>& sm) {
   constexpr int G4 = 4 * H;
   constexpr int NW = H / 16;
   constexpr int KB = G4 / 32;
   constexpr int KF = G4 / 4;
-  constexpr int ROWB = G4 + 8;
-  constexpr int ROWF = G4 + 4;
 
-  // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
-  // so every workgroup a spinning one waits for is already resident): top layer first here
-  const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
-  if (tile >= a.ntiles) return;
-  const bool top = layer == a.L - 1, bottom = layer == 0;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool grad_wave = wave >= NW;
+  const int w = grad_wave ? wave - NW : wave;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
   const int n0 = tile * S;
   const int N = a.N, Np = a.Np, T = a.T;
+  auto& g_hi = sm.g_hi;
+  auto& g_lo = sm.g_lo;
+  auto& g_f = sm.g_f;
+  auto& dhs = sm.dhs;
+
+  if (grad_wave) {
+    // =========================== gradient waves ===========================
+    const float* dH = TOP ? nullptr : a.dX[layer];
+    float* dXout = BOTTOM ? nullptr : a.dX[layer - 1];
+    const uint64_t seed_in = (!BOTTOM && a.dropout) ? a.seeds[layer] : 0;
+    unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+    unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
+    const float* w_ih = a.w_ih[layer];
+    constexpr int XKB = BOTTOM ? 1 : KB, XKF = BOTTOM ? 1 : KF;
+    bf16x8 Xhi[PREC == PREC_F32 ? 1 : XKB], Xlo[PREC == PREC_BF16X3 ? XKB : 1];
+    float Xf[PREC == PREC_F32 ? XKF : 1];
+    if constexpr (!BOTTOM) {
+      if constexpr (PREC == PREC_F32) {
+#pragma unroll
+        for (int kk = 0; kk < KF; ++kk) Xf[kk] = w_ih[(size_t)(4 * kk + q) * H + u];
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            __bf16 hi, lo;
+            split_bf16(w_ih[(size_t)rperm_to_r<H>(32 * kb + 8 * q + e) * H + u], hi, lo);
+            Xhi[kb][e] = hi;
+            if constexpr (PREC == PREC_BF16X3) Xlo[kb][e] = lo;
+          }
+      }
+    }
+    float dreg[4] = {0.f, 0.f, 0.f, 0.f};
+    unsigned seen = 0;
+    auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
+      if constexpr (!TOP) {
+        seen = wait_progress(in_flag, (unsigned)(T - t), seen, a.timeout);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    auto stage_dh = [&](int t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = dreg[i];
+    };
+    auto dx_step = [&](int t) {  // dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
+      if constexpr (!BOTTOM) {
+        const int buf = t & 1;
+        f32x4 ax0 = {0.f, 0.f, 0.f, 0.f}, ax1 = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (PREC == PREC_F32) {
+          const float* arow = &g_f[buf][j][q * KF];
+#pragma unroll
+          for (int kk = 0; kk < KF; kk += 2) {
+            ax0 = mfma16x16x4f32(arow[kk], Xf[kk], ax0);
+            ax1 = mfma16x16x4f32(arow[kk + 1], Xf[kk + 1], ax1);
+          }
+        } else {
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
+            if constexpr (PREC == PREC_BF16X3) {
+              const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
+              ax1 = mfma16x16x32(alo, Xhi[kb], ax1);
+              ax1 = mfma16x16x32(ahi, Xlo[kb], ax1);
+            }
+            ax0 = mfma16x16x32(ahi, Xhi[kb], ax0);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+          float v = ax0[i] + ax1[i];
+          if (seed_in) v *= mta_dropout_scale(seed_in, row, (uint32_t)u, a.drop_p);
+          store_handoff(dXout + (size_t)row * H + u, v, a.plain_probe);
+        }
+      }
+    };
+    if constexpr (!TOP) {
+      load_dh(T - 1);
+      stage_dh(T - 1);
+      if (T > 1) load_dh(T - 2);
+    }
+    __syncthreads();  // B0
+    for (int t = T - 1; t >= 0; --t) {
+      // ---- interval I(t) ----
+      mta_wait_vmem();  // this wave's dH loads and its dx stores of the previous interval
+      // progress: dx of steps >= t+3 (stored in I(t+2)) was drained by every gradient wave's wait in
+      // I(t+1), before barrier A(t+1)
+      if (!BOTTOM && t + 3 <= T - 1 && wave == NW && lane == 0)
+        __hip_atomic_store(my_flag, (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 <= T - 1) dx_step(t + 1);
+      if constexpr (!TOP) {
+        if (t >= 1) {
+          stage_dh(t - 1);
+          if (t >= 2) load_dh(t - 2);
+        }
+      }
+      __syncthreads();  // A(t)
+    }
+    dx_step(0);
+    mta_wait_vmem();
+    __syncthreads();  // F
+    if (!BOTTOM && wave == NW && lane == 0)
+      __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+
+  // =========================== recurrent waves ===========================
   const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
   const float* w_hh = a.w_hh[layer];
-  const float* w_ih = a.w_ih[layer];
   float* dG = a.dG[layer];
-  const float* dH = top ? nullptr : a.dX[layer];
-  float* dXout = bottom ? nullptr : a.dX[layer - 1];
-  const uint64_t seed_in = (!bottom && a.dropout) ? a.seeds[layer] : 0;
-  unsigned* my_flag = a.flags + layer * a.tr8 + tile;
-  unsigned* in_flag = top ? my_flag : a.flags + (layer + 1) * a.tr8 + tile;
-
-  __shared__ __attribute__((aligned(16))) __bf16 g_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
-  __shared__ __attribute__((aligned(16))) __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
-  __shared__ __attribute__((aligned(16))) float g_f[2][S][PREC == PREC_F32 ? ROWF : 4];
-
-  // B fragments: recurrent B[r'][k] = W_hh[r(r')][u]; input-gradient B[r'][k] = W_ih[r(r')][u]
   bf16x8 Bhi[PREC == PREC_F32 ? 1 : KB], Blo[PREC == PREC_BF16X3 ? KB : 1];
-  bf16x8 Xhi[PREC == PREC_F32 ? 1 : KB], Xlo[PREC == PREC_BF16X3 ? KB : 1];
-  float Bf[PREC == PREC_F32 ? KF : 1], Xf[PREC == PREC_F32 ? KF : 1];
+  float Bf[PREC == PREC_F32 ? KF : 1];
   if constexpr (PREC == PREC_F32) {
 #pragma unroll
-    for (int kk = 0; kk < KF; ++kk) {
-      Bf[kk] = w_hh[(size_t)(4 * kk + q) * H + u];
-      Xf[kk] = bottom ? 0.f : w_ih[(size_t)(4 * kk + q) * H + u];
-    }
+    for (int kk = 0; kk < KF; ++kk) Bf[kk] = w_hh[(size_t)(4 * kk + q) * H + u];
   } else {
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int r = rperm_to_r<H>(32 * kb + 8 * q + e);
         __bf16 hi, lo;
-        split_bf16(w_hh[(size_t)r * H + u], hi, lo);
+        split_bf16(w_hh[(size_t)rperm_to_r<H>(32 * kb + 8 * q + e) * H + u], hi, lo);
         Bhi[kb][e] = hi;
         if constexpr (PREC == PREC_BF16X3) Blo[kb][e] = lo;
-        split_bf16(bottom ? 0.f : w_ih[(size_t)r * H + u], hi, lo);
-        Xhi[kb][e] = hi;
-        if constexpr (PREC == PREC_BF16X3) Xlo[kb][e] = lo;
       }
   }
-
   float dc[4] = {0.f, 0.f, 0.f, 0.f};
   float dhr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n = n0 + 4 * q + i;
-    if (top) {
+    if constexpr (TOP) {
       const float v = a.dh_last[(size_t)(n < N ? n : N - 1) * H + u];
       dhr[i] = n < N ? v : 0.f;
     } else {
       dhr[i] = 0.f;
     }
   }
-
   float4 st_nxt[STASH], cp_nxt;
-  float dh_nxt[4] = {0.f, 0.f, 0.f, 0.f};
   auto load_step = [&](int t) {
     const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
 #pragma unroll
     for (int k = 0; k < STASH; ++k) st_nxt[k] = src[k];
     cp_nxt = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 4];
-    if (!top) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        // sc1 scalar loads of the hand-off
-        dh_nxt[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   };
-  float pdG[4][4], pdx[4];
+  float pdG[4][4];
   auto store_step = [&](int t) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i)
       *reinterpret_cast<float4*>(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u) =
           make_float4(pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]);
-      if (dXout) {
-        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-        float v = pdx[i];
-        if (seed_in) v *= mta_dropout_scale(seed_in, row, (uint32_t)u, a.drop_p);
-        store_sc1(dXout + (size_t)row * H + u, v);
-      }
-    }
   };
-
-  unsigned seen = 0, pend = 0;
-  if (!top) seen = wait_progress(in_flag, 1, 0, a.timeout);
   load_step(T - 1);
+  __syncthreads();  // B0 (dhs[(T-1)&1] staged)
 
   for (int t = T - 1; t >= 0; --t) {
     float4 st[STASH];
-    float dho[4];
 #pragma unroll
     for (int k = 0; k < STASH; ++k) st[k] = st_nxt[k];
     const float cpm = t > 0 ? 1.f : 0.f;
     const float cp4[4] = {cp_nxt.x * cpm, cp_nxt.y * cpm, cp_nxt.z * cpm, cp_nxt.w * cpm};
+    float dho[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dho[i] = dh_nxt[i];
+    for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[t & 1][4 * q + i][u];
     mta_wait_vmem();
-    if (!top) seen = seen > pend ? seen : pend;
-    // progress: reverse steps T-1 .. t+3 (stored at the top of t+2.., drained before the last barrier)
-    if (!bottom && t <= T - 4 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t < T - 1) store_step(t + 1);
-    if (t > 0) {
-      if (!top) {
-        seen = wait_progress(in_flag, (unsigned)(T - t + 1), seen, a.timeout);
-        load_step(t - 1);
-        pend = __hip_atomic_load(in_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        load_step(t - 1);
-      }
-    }
+    if (t > 0) load_step(t - 1);
     __builtin_amdgcn_sched_barrier(0);
     const float ig4[4] = {st[0].x, st[0].y, st[0].z, st[0].w};
     const float fg4[4] = {st[1].x, st[1].y, st[1].z, st[1].w};
     const float gg4[4] = {st[2].x, st[2].y, st[2].z, st[2].w};
     const float og4[4] = {st[3].x, st[3].y, st[3].z, st[3].w};
     const float ct4[4] = {st[4].x, st[4].y, st[4].z, st[4].w};
-
     const int buf = t & 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -533,12 +658,12 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_bwd_kernel(StackBwdA
       pdG[2][i] = dcc * ig * (1.f - gg * gg);
       pdG[3][i] = d_o;
       dc[i] = dcc * fg;
-      const int s = 4 * q + i;
+      const int s4 = 4 * q + i;
       if constexpr (PREC == PREC_F32) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int r = g * H + u;
-          g_f[buf][s][(r & 3) * KF + (r >> 2)] = pdG[g][i];
+          g_f[buf][s4][(r & 3) * KF + (r >> 2)] = pdG[g][i];
         }
       } else {
         bf16x4 hi4, lo4;
@@ -550,70 +675,57 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_stack_bwd_kernel(StackBwdA
           lo4[g] = lo;
         }
         const int rp = 8 * (u >> 1) + 4 * (u & 1);
-        *reinterpret_cast<bf16x4*>(&g_hi[buf][s][rp]) = hi4;
-        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s][rp]) = lo4;
+        *reinterpret_cast<bf16x4*>(&g_hi[buf][s4][rp]) = hi4;
+        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s4][rp]) = lo4;
       }
     }
-    if (t == 0 && bottom) {
-      store_step(0);
-      break;
-    }
-    __syncthreads();
-
-    // ---- dh_{t-1} = dG_t . W_hh (t > 0) and dx_t = dG_t . W_ih (layers >= 1) ---------------------
+    __syncthreads();  // A(t): dG_t image visible to the gradient waves and to this step's dh product
+    if (t == 0) break;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    f32x4 ax0 = {0.f, 0.f, 0.f, 0.f}, ax1 = {0.f, 0.f, 0.f, 0.f};
     if constexpr (PREC == PREC_F32) {
       const float* arow = &g_f[buf][j][q * KF];
 #pragma unroll
       for (int kk = 0; kk < KF; kk += 2) {
         acc0 = mfma16x16x4f32(arow[kk], Bf[kk], acc0);
         acc1 = mfma16x16x4f32(arow[kk + 1], Bf[kk + 1], acc1);
-        if (!bottom) {
-          ax0 = mfma16x16x4f32(arow[kk], Xf[kk], ax0);
-          ax1 = mfma16x16x4f32(arow[kk + 1], Xf[kk + 1], ax1);
-        }
       }
     } else {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
-        bf16x8 alo;
         if constexpr (PREC == PREC_BF16X3) {
-          alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
+          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
           acc1 = mfma16x16x32(alo, Bhi[kb], acc1);
           acc1 = mfma16x16x32(ahi, Blo[kb], acc1);
         }
         acc0 = mfma16x16x32(ahi, Bhi[kb], acc0);
-        if (!bottom) {
-          if constexpr (PREC == PREC_BF16X3) {
-            ax1 = mfma16x16x32(alo, Xhi[kb], ax1);
-            ax1 = mfma16x16x32(ahi, Xlo[kb], ax1);
-          }
-          ax0 = mfma16x16x32(ahi, Xhi[kb], ax0);
-        }
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dhr[i] = acc0[i] + acc1[i];
-      pdx[i] = ax0[i] + ax1[i];
-    }
-    if (t == 0) {
-      store_step(0);
-      break;
-    }
+    for (int i = 0; i < 4; ++i) dhr[i] = acc0[i] + acc1[i];
   }
-  if (!bottom) {
-    mta_wait_vmem();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  store_step(0);
+  mta_wait_vmem();
+  __syncthreads();  // F
+}
+
+template <int H, int PREC>
+__global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwdArgs a) {
+  // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
+  // so every workgroup a spinning one waits for is already resident): top layer first here
+  const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+  if (tile >= a.ntiles) return;
+  const bool top = layer == a.L - 1, bottom = layer == 0;
+  __shared__ __attribute__((aligned(16))) BwdSmem<H, PREC> sm;  // one image shared by the role bodies
+  if (top && bottom) stack_bwd_body<H, PREC, true, true>(a, layer, tile, sm);
+  else if (top) stack_bwd_body<H, PREC, true, false>(a, layer, tile, sm);
+  else if (bottom) stack_bwd_body<H, PREC, false, true>(a, layer, tile, sm);
+  else stack_bwd_body<H, PREC, false, false>(a, layer, tile, sm);
 }
 
 template <int H, int PREC>
 int launch_fwd(int fin, const StackFwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.L * a.tr8), block((H / 16) * 64);
+  const dim3 grid(a.L * a.tr8), block((H / 16) * 128);  // recurrent + input waves
   if (fin == 3) lstm_stack_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(a);
   else if (fin == 5) lstm_stack_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(a);
   else return -1;
@@ -629,7 +741,7 @@ int dispatch_fwd(int prec, int fin, const StackFwdArgs& a, hipStream_t st) {
 
 template <int H>
 int dispatch_bwd(int prec, const StackBwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.L * a.tr8), block((H / 16) * 64);
+  const dim3 grid(a.L * a.tr8), block((H / 16) * 128);  // recurrent + gradient waves
   if (prec == PREC_F32) lstm_stack_bwd_kernel<H, PREC_F32><<<grid, block, 0, st>>>(a);
   else if (prec == PREC_BF16X3) lstm_stack_bwd_kernel<H, PREC_BF16X3><<<grid, block, 0, st>>>(a);
   else lstm_stack_bwd_kernel<H, PREC_BF16><<<grid, block, 0, st>>>(a);
@@ -665,8 +777,10 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;  // tile i of every layer gets the same block id modulo 8
   a.flags = flags;
-  a.timeout = flags + MAXL * a.tr8;
-  if (hipMemsetAsync(flags, 0, (size_t)(MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess) return -2;
+  a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
+  a.plain_probe = getenv("MTA_STACK_PLAIN_STORES") != nullptr;
+  if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
+    return -2;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
 }
@@ -695,8 +809,10 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* st
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;
   a.flags = flags;
-  a.timeout = flags + MAXL * a.tr8;
-  if (hipMemsetAsync(flags, 0, (size_t)(MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess) return -2;
+  a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
+  a.plain_probe = getenv("MTA_STACK_PLAIN_STORES") != nullptr;
+  if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
+    return -2;
   if (H == 32) return dispatch_bwd<32>(prec, a, st);
   return dispatch_bwd<64>(prec, a, st);
 }

@@ -212,8 +212,7 @@ class _LSTMPipelinedFn(torch.autograd.Function):
 
 def stack_timed_out(flags: Tensor) -> bool:
     """True if a pipelined launch gave up waiting on a producer (diagnostic; host sync)."""
-    Np_tiles8 = (flags.numel() - 4) // 8
-    return bool(flags[8 * Np_tiles8].item() != 0)
+    return bool(flags[flags.numel() - 4].item() != 0)
 
 
 _PERM_CACHE = {}

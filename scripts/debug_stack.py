@@ -53,7 +53,7 @@ def main():
                          seeds, 0.0, flags, N, Np, T)
         torch.cuda.synchronize()
         fl = flags.cpu()
-        print(f"[{mode}] prec={prec} H={H} L={L} flags={fl[:8].tolist()} ... timeout={fl[-4:].tolist()}", flush=True)
+        print(f"[{mode}] prec={prec} H={H} L={L} flags={fl[:256:32].tolist()} ... timeout={fl[-4:].tolist()}", flush=True)
         for l in range(L):
             got = hseq[l].cpu()[:, :N].permute(1, 0, 2).double()
             err = (got - refs[l]).abs().amax(dim=(0, 2))
