@@ -57,6 +57,12 @@ int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* stash, const 
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
                        hipStream_t st);
+// data.hip (dataset build)
+int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
+            float idio_loc, float idio_scale, float a_loc, float a_scale, float b_loc, float b_scale, float* r_market,
+            float* r_stocks, float* alphas, float* betas, hipStream_t st);
+void mta_ols_features(const float* target, int W, int K, int n, int C, float* alphas, float* betas, float* factor,
+                      float* inv_psi, hipStream_t st);
 // host/prefetch.cpp
 void* mta_prefetch_create(int ntensors, const void* const* host, const long* row_bytes, void* const* staging, int B,
                           int R, int nthreads);
@@ -522,6 +528,42 @@ void lstm_stack_bwd(int64_t H, int64_t prec, std::vector<at::Tensor> stash, std:
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
 }
 
+
+// ------------------------------------------------------------------------------- dataset build
+void dgp(int64_t seed, int64_t mkt_df, double mkt_loc, double mkt_scale, int64_t idio_df, double idio_loc,
+         double idio_scale, double a_loc, double a_scale, double b_loc, double b_scale, at::Tensor r_market,
+         at::Tensor r_stocks, at::Tensor alphas, at::Tensor betas) {
+  MTA_CHECK_F32(r_market);
+  MTA_CHECK_F32(r_stocks);
+  MTA_CHECK_F32(alphas);
+  MTA_CHECK_F32(betas);
+  const int64_t K = r_stocks.size(0), S = r_market.numel();
+  TORCH_CHECK(r_stocks.dim() == 2 && r_stocks.size(1) == S && alphas.numel() == K && betas.numel() == K,
+              "dgp: shapes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(r_market.device());
+  const int rc = mta_dgp((uint64_t)seed, (int)K, (long)S, (int)mkt_df, (float)mkt_loc, (float)mkt_scale,
+                         (int)idio_df, (float)idio_loc, (float)idio_scale, (float)a_loc, (float)a_scale,
+                         (float)b_loc, (float)b_scale, r_market.data_ptr<float>(), r_stocks.data_ptr<float>(),
+                         alphas.data_ptr<float>(), betas.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "dgp: unsupported degrees of freedom or sample count");
+}
+
+void ols_features(at::Tensor target, at::Tensor alphas, at::Tensor betas, at::Tensor factor, at::Tensor inv_psi) {
+  MTA_CHECK_F32(target);
+  TORCH_CHECK(target.dim() == 4 && target.size(3) >= 2 && target.size(2) >= 2, "target must be (W, K, n, C>=2)");
+  const int64_t W = target.size(0), K = target.size(1);
+  for (auto* t : {&alphas, &betas, &inv_psi}) {
+    MTA_CHECK_F32(*t);
+    TORCH_CHECK(t->numel() == W * K, "per-(window, stock) output shape");
+  }
+  MTA_CHECK_F32(factor);
+  TORCH_CHECK(factor.numel() == W * 2, "factor must be (W, 2)");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(target.device());
+  mta_ols_features(target.data_ptr<float>(), (int)W, (int)K, (int)target.size(2), (int)target.size(3),
+                   alphas.data_ptr<float>(), betas.data_ptr<float>(), factor.data_ptr<float>(),
+                   inv_psi.data_ptr<float>(), cur_stream());
+}
+
 // Native pinned-ring prefetcher (residency=stream).  Holds references to the host dataset and
 // staging tensors so their storage outlives the worker threads.
 class HostPrefetcher {
@@ -591,6 +633,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("stop", &HostPrefetcher::stop)
       .def("close", &HostPrefetcher::close);
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
+  m.def("dgp", &dgp);
+  m.def("ols_features", &ols_features);
   m.def("lstm_stack_fwd", &lstm_stack_fwd);
   m.def("lstm_stack_bwd", &lstm_stack_bwd);
   m.def("lstm_stack_flag_words", &lstm_stack_flag_words);

@@ -53,13 +53,15 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = device != "cpu" and torch.cuda.is_available()
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # ranks beyond the visible devices share them (gloo rehearsal of N ranks on a 1-GPU box)
+        idx = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
     be = None
     if world > 1:
-        be = backend or ("nccl" if use_gpu else "gloo")
+        be = backend or os.environ.get("MTA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
             kw = {}
