@@ -51,7 +51,8 @@ constexpr int S = 16;       // sequences per workgroup (MFMA M tile)
 constexpr int STASH = 5;    // float4 per lane per step: i, f, g, o (4 seqs each), c (4 seqs)
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
-  return ((((size_t)t * ntiles + tile) * nw + w) * 64 + lane) * STASH;
+  // component k of a lane at + 64 k: every stash store / load instruction covers 1 KB contiguous
+  return (((size_t)t * ntiles + tile) * nw + w) * (64 * STASH) + lane;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -176,10 +177,10 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_fwd_kernel(
     if constexpr (WSTASH) {
       float4* st = stash + stash_index(t, tile, ntiles, w, NW, lane);
       st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
-      st[1] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
-      st[2] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
-      st[3] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
-      st[4] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+      st[64] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      st[128] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      st[192] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      st[256] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) hseq[((size_t)t * Np + n0 + 4 * q + i) * H + u] = ph[i];
@@ -340,8 +341,8 @@ __global__ __launch_bounds__((H / 16) * 64) void lstm_bwd_kernel(
   auto load_step = [&](int t, float4 (&sdst)[STASH], float4& cdst, float (&ddst)[4]) {
     const float4* src = stash + stash_index(t, tile, ntiles, w, NW, lane);
 #pragma unroll
-    for (int k = 0; k < STASH; ++k) sdst[k] = src[k];
-    cdst = stash[stash_index(t > 0 ? t - 1 : 0, tile, ntiles, w, NW, lane) + 4];
+    for (int k = 0; k < STASH; ++k) sdst[k] = src[64 * k];
+    cdst = stash[stash_index(t > 0 ? t - 1 : 0, tile, ntiles, w, NW, lane) + 64 * 4];
     if constexpr (HAS_DH) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) ddst[i] = dH[((size_t)t * Np + n0 + 4 * q + i) * H + u];

@@ -34,13 +34,20 @@ constexpr unsigned SPIN_LIMIT = 1u << 21;
 constexpr int FLAG_STRIDE = 32;  // one 128-byte line per progress word (polled words never share a line)
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
-  return ((((size_t)t * ntiles + tile) * nw + w) * 64 + lane) * STASH;
+  // component k of a lane at + 64 k: every stash store / load instruction covers 1 KB contiguous
+  return (((size_t)t * ntiles + tile) * nw + w) * (64 * STASH) + lane;
 }
 
 __device__ __forceinline__ void store_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// timing probe only (MTA_STACK_PLAIN_STORES=1): plain stores are NOT a valid cross-XCD hand-off
+// timing probes (MTA_STACK_PLAIN_STORES=n, results invalid): 1 plain hand-off stores (NOT a valid
+// cross-XCD hand-off), 2 also no stash / dG stores, 3 also no stash loads in the backward
+inline int stack_probe() {
+  const char* e = getenv("MTA_STACK_PLAIN_STORES");
+  return e ? atoi(e) : 0;
+}
+
 __device__ __forceinline__ void store_handoff(float* p, float v, int plain) {
   if (plain) *p = v;
   else store_sc1(p, v);
@@ -305,13 +312,13 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   f32x4 pgi, pgf, pgg, pgo, pcc;
   float ph[4];
   auto store_step = [&](int t) {
-    if (stash) {
+    if (stash && a.plain_probe < 2) {
       float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
       st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
-      st[1] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
-      st[2] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
-      st[3] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
-      st[4] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+      st[64] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      st[128] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      st[192] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      st[256] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
     }
     if (xout) {
 #pragma unroll
@@ -610,15 +617,19 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       dhr[i] = 0.f;
     }
   }
-  float4 st_nxt[STASH], cp_nxt;
+  float4 st_nxt[STASH], cp_nxt = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < STASH; ++k) st_nxt[k] = cp_nxt;
   auto load_step = [&](int t) {
+    if (a.plain_probe >= 3) return;
     const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
 #pragma unroll
-    for (int k = 0; k < STASH; ++k) st_nxt[k] = src[k];
-    cp_nxt = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 4];
+    for (int k = 0; k < STASH; ++k) st_nxt[k] = src[64 * k];
+    cp_nxt = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 64 * 4];
   };
   float pdG[4][4];
   auto store_step = [&](int t) {
+    if (a.plain_probe >= 2) return;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       *reinterpret_cast<float4*>(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u) =
@@ -778,7 +789,7 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.tr8 = (a.ntiles + 7) / 8 * 8;  // tile i of every layer gets the same block id modulo 8
   a.flags = flags;
   a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
-  a.plain_probe = getenv("MTA_STACK_PLAIN_STORES") != nullptr;
+  a.plain_probe = stack_probe();
   if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
     return -2;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
@@ -810,7 +821,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* st
   a.tr8 = (a.ntiles + 7) / 8 * 8;
   a.flags = flags;
   a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
-  a.plain_probe = getenv("MTA_STACK_PLAIN_STORES") != nullptr;
+  a.plain_probe = stack_probe();
   if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
     return -2;
   if (H == 32) return dispatch_bwd<32>(prec, a, st);

@@ -1,7 +1,7 @@
 """Timing of the pipelined LSTM stack kernels vs the per-layer kernels (fwd / bwd, L = 1..8).
 
-MTA_STACK_PLAIN_STORES=1 rows use plain (not write-through) hand-off stores: a timing probe of the
-store-drain cost only, not a valid cross-XCD protocol.
+plain=1 rows use plain (not write-through) hand-off stores, plain=2 also drop the stash / dG stores,
+plain=3 also the backward's stash loads: timing probes of the memory-traffic cost only (invalid results).
 """
 import math
 import os
@@ -18,7 +18,7 @@ def run(C, L, prec, plain):
     from masters_thesis_amd.ops.lstm import padded_rows
 
     if plain:
-        os.environ["MTA_STACK_PLAIN_STORES"] = "1"
+        os.environ["MTA_STACK_PLAIN_STORES"] = str(int(plain))
     else:
         os.environ.pop("MTA_STACK_PLAIN_STORES", None)
     dev = "cuda"
@@ -66,7 +66,7 @@ def main():
 
     C = _lib.lib()
     for L in (1, 2, 4, 8):
-        for plain in (False, True):
+        for plain in (0, 1, 2, 3):
             run(C, L, 1, plain)
     os.environ.pop("MTA_STACK_PLAIN_STORES", None)
 
