@@ -53,10 +53,12 @@ int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const fl
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, float* const* stash, const uint64_t* seeds,
                        float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
-int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* stash, const float* const* w_hh,
+int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
-                       const uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
-                       hipStream_t st);
+                       const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
+                       float* const* g_bih, float* const* g_bhh, uint64_t* seeds, float drop_p, int dropout,
+                       unsigned* flags, int N, int Np, int T, hipStream_t st);
+long mta_lstm_stack_flag_words(int Np);
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
             float idio_loc, float idio_scale, float a_loc, float a_scale, float b_loc, float b_scale, float* r_market,
@@ -466,7 +468,7 @@ std::vector<float*> ptrs_f32(const std::vector<at::Tensor>& v, const char* name)
   return out;
 }
 
-int64_t lstm_stack_flag_words(int64_t Np) { return 32 * 8 * (((Np / 16) + 7) / 8 * 8) + 4; }
+int64_t lstm_stack_flag_words(int64_t Np) { return mta_lstm_stack_flag_words((int)Np); }
 
 void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
                     std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
@@ -500,10 +502,13 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
 }
 
-void lstm_stack_bwd(int64_t H, int64_t prec, std::vector<at::Tensor> stash, std::vector<at::Tensor> w_hh,
+// grads: [] (weight gradients by the caller) or 4 lists g_wih, g_whh, g_bih, g_bhh of per-layer gradient
+// views the fused weight-gradient workgroups accumulate into; inp[0] = x (N, T, fin), inp[l] = layer input.
+void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor> stash, std::vector<at::Tensor> w_hh,
                     std::vector<at::Tensor> w_ih, at::Tensor dh_last, std::vector<at::Tensor> dG,
-                    std::vector<at::Tensor> dX, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
-                    int64_t N, int64_t Np, int64_t T) {
+                    std::vector<at::Tensor> dX, std::vector<at::Tensor> hseq, std::vector<at::Tensor> inp,
+                    std::vector<std::vector<at::Tensor>> grads, at::Tensor seeds, double drop_p, bool dropout,
+                    at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
@@ -513,18 +518,41 @@ void lstm_stack_bwd(int64_t H, int64_t prec, std::vector<at::Tensor> stash, std:
     TORCH_CHECK(stash[l].numel() == T * Np * 5 * H && dG[l].numel() == T * Np * 4 * H, "stash/dG shapes");
     TORCH_CHECK(l == L - 1 || dX[l].numel() == T * Np * H, "dX shape");
   }
+  const bool fused = !grads.empty();
+  if (fused) {
+    TORCH_CHECK(grads.size() == 4 && hseq.size() == (size_t)L && inp.size() == (size_t)L, "fused wgrad lists");
+    for (int64_t l = 0; l < L; ++l) {
+      const int64_t F = l == 0 ? fin : H;
+      TORCH_CHECK(hseq[l].numel() == T * Np * H, "hseq shape");
+      TORCH_CHECK(inp[l].numel() == (l == 0 ? N * T * fin : T * Np * H), "layer input shape");
+      TORCH_CHECK(grads[0][l].numel() == 4 * H * F && grads[1][l].numel() == 4 * H * H &&
+                      grads[2][l].numel() == 4 * H && grads[3][l].numel() == 4 * H,
+                  "gradient view shapes");
+    }
+  }
   TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= L, "seeds: int64[L]");
   TORCH_CHECK(flags.is_cuda() && flags.scalar_type() == at::kInt && flags.numel() >= lstm_stack_flag_words(Np),
               "flags scratch too small");
   auto st = ptrs_f32(stash, "stash"), wh = ptrs_f32(w_hh, "w_hh"), wi = ptrs_f32(w_ih, "w_ih"),
        dg = ptrs_f32(dG, "dG"), dx = ptrs_f32(dX, "dX");
-  std::vector<const float*> cst(st.begin(), st.end()), cwh(wh.begin(), wh.end()), cwi(wi.begin(), wi.end());
+  std::vector<float*> hs, in, g0, g1, g2, g3;
+  if (fused) {
+    hs = ptrs_f32(hseq, "hseq");
+    in = ptrs_f32(inp, "inp");
+    g0 = ptrs_f32(grads[0], "g_wih");
+    g1 = ptrs_f32(grads[1], "g_whh");
+    g2 = ptrs_f32(grads[2], "g_bih");
+    g3 = ptrs_f32(grads[3], "g_bhh");
+  }
+  std::vector<const float*> cst(st.begin(), st.end()), cwh(wh.begin(), wh.end()), cwi(wi.begin(), wi.end()),
+      chs(hs.begin(), hs.end()), cin(in.begin(), in.end());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dh_last.device());
-  const int rc = mta_lstm_stack_bwd((int)H, (int)prec, (int)L, cst.data(), cwh.data(), cwi.data(),
-                                    dh_last.data_ptr<float>(), dg.data(), dx.data(),
-                                    reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
-                                    dropout ? 1 : 0, reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N,
-                                    (int)Np, (int)T, cur_stream());
+  const int rc = mta_lstm_stack_bwd(
+      (int)H, (int)prec, (int)L, (int)fin, cst.data(), cwh.data(), cwi.data(), dh_last.data_ptr<float>(), dg.data(),
+      dx.data(), fused ? chs.data() : nullptr, fused ? cin.data() : nullptr, fused ? g0.data() : nullptr,
+      fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr,
+      reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p, dropout ? 1 : 0,
+      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
 }
 

@@ -70,6 +70,13 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
 // s_waitcnt vmcnt(0) as a builtin (the compiler's waitcnt pass sees it, unlike inline asm).
 // gfx9 encoding: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt[5:4]=0  ->  0x0F70
 __device__ __forceinline__ void mta_wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// s_waitcnt vmcnt(N): all but the N most recently issued vector-memory ops have completed (gfx9 returns
+// them in issue order); expcnt / lgkmcnt not waited on
+template <int N>
+__device__ __forceinline__ void mta_wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N & 15) | ((N >> 4) << 14));
+}
 
 // GELU (erf form, torch.nn.GELU() default) and its derivative.
 __device__ __forceinline__ float mta_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }

@@ -24,6 +24,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "lstm_wgrad.h"
 
 namespace {
 
@@ -31,7 +32,8 @@ constexpr int S = 16;
 constexpr int STASH = 5;
 constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;
-constexpr int FLAG_STRIDE = 32;  // one 128-byte line per progress word (polled words never share a line)
+constexpr int FLAG_STRIDE = 32;
+constexpr int EPOCH_SHIFT = 12;  // one 128-byte line per progress word (polled words never share a line)
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
   // component k of a lane at + 64 k: every stash store / load instruction covers 1 KB contiguous
@@ -41,27 +43,46 @@ __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w
 __device__ __forceinline__ void store_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// timing probes (MTA_STACK_PLAIN_STORES=n, results invalid): 1 plain hand-off stores (NOT a valid
-// cross-XCD hand-off), 2 also no stash / dG stores, 3 also no stash loads in the backward
-inline int stack_probe() {
-  const char* e = getenv("MTA_STACK_PLAIN_STORES");
-  return e ? atoi(e) : 0;
+// 16-byte write-through store (the dG rows the fused weight-gradient workgroups read); one vector-memory op.
+// The s_nop covers the >8-byte store-data hazard (the hazard recognizer does not see into inline asm: a
+// VALU write to the data VGPRs right after the store would corrupt what it stores).
+__device__ __forceinline__ void store_sc1_x4(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" : : "v"(p), "v"(v) : "memory");
 }
 
-__device__ __forceinline__ void store_handoff(float* p, float v, int plain) {
-  if (plain) *p = v;
-  else store_sc1(p, v);
+// Control words (one 128-byte line each) after the three progress regions.
+constexpr int CTL_TIMEOUT = 0, CTL_FWD_EPOCH = 32, CTL_FWD_DONE = 64, CTL_BWD_EPOCH = 96, CTL_BWD_DONE = 128;
+constexpr int CTL_WORDS = 160;
+
+__device__ __forceinline__ unsigned read_epoch_base(unsigned* ctl, int which) {
+  return __hip_atomic_load(ctl + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << EPOCH_SHIFT;
+}
+// every workgroup arrives once after its work; the last one re-arms the counter and advances the epoch
+// (every workgroup read the epoch before arriving, so no launch sees a torn value)
+__device__ __forceinline__ bool finish_launch(unsigned* ctl, int epoch_word, int done_word, unsigned base) {
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  const unsigned prev = __hip_atomic_fetch_add(ctl + done_word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != gridDim.x - 1) return false;
+  __hip_atomic_store(ctl + done_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(ctl + epoch_word, (base >> EPOCH_SHIFT) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
 }
 
-// wait until *flag >= need (relaxed agent-scope polls); returns the value seen
+// Progress words are never reset: a launch reads its epoch E (control word, advanced by the launch's last
+// workgroup) and publishes E * 4096 + steps, so a stale word of an earlier launch always compares below
+// (wrap-safe signed difference, T < 4096).  No memset node per launch.
+__device__ __forceinline__ bool reached(unsigned seen, unsigned need) { return (int)(seen - need) >= 0; }
+
+// wait until *flag reaches need (relaxed agent-scope polls); returns the value seen
 __device__ __forceinline__ unsigned wait_progress(unsigned* flag, unsigned need, unsigned seen, unsigned* tmo) {
   unsigned spins = 0;
-  while (seen < need) {
+  while (!reached(seen, need)) {
     __builtin_amdgcn_s_sleep(1);
     seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (++spins > SPIN_LIMIT) {
       __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      seen = 0xFFFFFFFFu;  // give up waiting (results are garbage, the host sees the timeout word)
+      seen = need;  // give up waiting (results are garbage, the host sees the timeout word)
     }
   }
   // every payload load after this point is sc1 (L1 bypass): only keep the compiler from hoisting them
@@ -94,9 +115,10 @@ struct StackFwdArgs {
   float* stash[MAXL];   // BPTT stash per layer (null: inference)
   const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
   float drop_p;
-  unsigned* flags;      // [MAXL][tr8] progress words (zeroed per call)
+  unsigned* flags;      // [MAXL][tr8] progress words (epoch-stamped, never reset)
   unsigned* timeout;
-  int N, Np, T, L, ntiles, tr8, plain_probe;
+  unsigned* ctl;
+  int N, Np, T, L, ntiles, tr8;
 };
 
 // Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
@@ -116,7 +138,7 @@ struct FwdSmem {
 
 template <int H, int PREC, int FIN0, bool FIRST>
 __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
-                                               FwdSmem<H, PREC>& sm) {
+                                               FwdSmem<H, PREC>& sm, const unsigned base) {
   constexpr int NW = H / 16;
   constexpr int KB = H / 32;
   constexpr int KF = H / 4;
@@ -184,7 +206,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     }
     float xin0[4][FIRST ? FIN0 : 1];
     float4 xr[FIRST ? 1 : XR];
-    unsigned seen = 0;
+    unsigned seen = base;
     auto load_input = [&](int t) {
       if constexpr (FIRST) {
 #pragma unroll
@@ -196,7 +218,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       } else {
         // poll only when the last value seen does not cover step t (polling every step from every
         // consumer wave measured slower: the progress words share cache lines across tiles)
-        seen = wait_progress(in_flag, (unsigned)(t + 1), seen, a.timeout);
+        seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout);
         const size_t row = (size_t)t * Np + n0 + j;
 #pragma unroll
         for (int v = 0; v < XR; ++v) {
@@ -311,8 +333,25 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 pgi, pgf, pgg, pgo, pcc;
   float ph[4];
+  // issue order per step: hand-off stores, then the 5 stash stores; the loop-head vmcnt(STASH) then drains
+  // the previous step's hand-offs (in-order completion) and leaves its stash stores another step
   auto store_step = [&](int t) {
-    if (stash && a.plain_probe < 2) {
+    if (xout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
+        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+        store_sc1(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p));
+      }
+    }
+    if (last) {  // consumed after the kernel (heads, weight gradients): plain stores
+#pragma unroll
+      for (int i = 0; i < 4; ++i) hseq[((size_t)t * Np + n0 + 4 * q + i) * H + u] = ph[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) store_sc1(hseq + ((size_t)t * Np + n0 + 4 * q + i) * H + u, ph[i]);
+    }
+    if (stash) {
       float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
       st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
       st[64] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
@@ -320,16 +359,6 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       st[192] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
       st[256] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
     }
-    if (xout) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
-        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-        store_handoff(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p), a.plain_probe);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) store_handoff(hseq + ((size_t)t * Np + n0 + 4 * q + i) * H + u, ph[i], a.plain_probe);
   };
 
   for (int t = 0; t < T; ++t) {
@@ -343,11 +372,13 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[2][i] = v.z;
       acc[3][i] = v.w;
     }
-    mta_wait_vmem();  // the stores issued at the previous top (a whole step ago)
-    // progress: stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
+    // the hand-off stores issued at the previous top (a whole step ago)
+    if (stash && t >= 2) mta_wait_vmcnt<STASH>();
+    else mta_wait_vmem();
+    // progress: hand-off stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
     // the barrier that ended step t-1
     if (!last && t >= 3 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t > 0) store_step(t - 1);
     __builtin_amdgcn_sched_barrier(0);
 
@@ -407,17 +438,20 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   mta_wait_vmem();
   __syncthreads();  // final barrier
   if (!last && threadIdx.x == 0)
-    __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int H, int PREC, int FIN0>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
   const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
-  if (tile >= a.ntiles) return;
+  const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH);
   __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
-  if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm);
-  else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm);
+  if (tile < a.ntiles) {
+    if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
+    else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
+  }
+  finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -437,12 +471,17 @@ struct StackBwdArgs {
   const float* dh_last;   // (N, H): gradient wrt h_{T-1} of the top layer
   float* dG[MAXL];        // (T, Np, 4H) per layer, unit-major columns
   float* dX[MAXL];        // dX[l] (l < L-1): gradient wrt layer l's output sequence, written by layer l+1
-  const uint64_t* seeds;  // [MAXL]: dropout seed of layer l's input
+  uint64_t* seeds;        // [MAXL]: dropout seed of layer l's input (advanced by the launch's last workgroup)
   float drop_p;
   int dropout;
   unsigned* flags;        // [MAXL][tr8]: reverse steps of dX[l-1] published by layer l
+  unsigned* dg_flags;     // [MAXL][tr8]: reverse steps of dG[l] drained (write-through) by layer l
   unsigned* timeout;
-  int N, Np, T, L, ntiles, tr8, plain_probe;
+  unsigned* ctl;
+  int N, Np, T, L, ntiles, tr8;
+  // fused weight gradients: wg_per_layer workgroups per layer follow the L x tr8 recurrence workgroups
+  mta_wgrad::WgArgs wg[MAXL];
+  int wg_nq, wg_per_layer;
 };
 
 template <int H, int PREC>
@@ -463,7 +502,7 @@ struct BwdSmem {
 // dG image (t&1) in I(t); the gradient waves write dhs[(t-1)&1] and read image ((t+1)&1) in I(t).
 template <int H, int PREC, bool TOP, bool BOTTOM>
 __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int layer, const int tile,
-                                               BwdSmem<H, PREC>& sm) {
+                                               BwdSmem<H, PREC>& sm, const unsigned base) {
   constexpr int G4 = 4 * H;
   constexpr int NW = H / 16;
   constexpr int KB = G4 / 32;
@@ -488,6 +527,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     const uint64_t seed_in = (!BOTTOM && a.dropout) ? a.seeds[layer] : 0;
     unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
+    unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     const float* w_ih = a.w_ih[layer];
     constexpr int XKB = BOTTOM ? 1 : KB, XKF = BOTTOM ? 1 : KF;
     bf16x8 Xhi[PREC == PREC_F32 ? 1 : XKB], Xlo[PREC == PREC_BF16X3 ? XKB : 1];
@@ -509,10 +549,10 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       }
     }
     float dreg[4] = {0.f, 0.f, 0.f, 0.f};
-    unsigned seen = 0;
+    unsigned seen = base;
     auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
       if constexpr (!TOP) {
-        seen = wait_progress(in_flag, (unsigned)(T - t), seen, a.timeout);
+        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
@@ -551,7 +591,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
           const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
           float v = ax0[i] + ax1[i];
           if (seed_in) v *= mta_dropout_scale(seed_in, row, (uint32_t)u, a.drop_p);
-          store_handoff(dXout + (size_t)row * H + u, v, a.plain_probe);
+          store_sc1(dXout + (size_t)row * H + u, v);
         }
       }
     };
@@ -567,7 +607,11 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       // progress: dx of steps >= t+3 (stored in I(t+2)) was drained by every gradient wave's wait in
       // I(t+1), before barrier A(t+1)
       if (!BOTTOM && t + 3 <= T - 1 && wave == NW && lane == 0)
-        __hip_atomic_store(my_flag, (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // dG progress: every recurrent wave passed its top-of-(t+1) vmcnt wait before A(t+1), which drains
+      // its dG stores of steps >= t+4
+      if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
+        __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t + 1 <= T - 1) dx_step(t + 1);
       if constexpr (!TOP) {
         if (t >= 1) {
@@ -581,7 +625,9 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     mta_wait_vmem();
     __syncthreads();  // F
     if (!BOTTOM && wave == NW && lane == 0)
-      __hip_atomic_store(my_flag, (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == NW + 1 && lane == 0)
+      __hip_atomic_store(dg_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
 
@@ -617,40 +663,40 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       dhr[i] = 0.f;
     }
   }
-  float4 st_nxt[STASH], cp_nxt = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int k = 0; k < STASH; ++k) st_nxt[k] = cp_nxt;
-  auto load_step = [&](int t) {
-    if (a.plain_probe >= 3) return;
-    const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
-#pragma unroll
-    for (int k = 0; k < STASH; ++k) st_nxt[k] = src[64 * k];
-    cp_nxt = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 64 * 4];
-  };
-  float pdG[4][4];
-  auto store_step = [&](int t) {
-    if (a.plain_probe >= 2) return;
+  float pdG[4][4] = {};
+  auto store_step = [&](int t) {  // write-through: the fused weight-gradient workgroups read these rows
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      *reinterpret_cast<float4*>(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u) =
-          make_float4(pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]);
+      store_sc1_x4(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u,
+                   f32x4{pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]});
   };
-  load_step(T - 1);
+  // stash of step t (i, f, g, o, c) plus c_{t-1}, prefetched ~two steps ahead into one of two register
+  // sets (even / odd steps); per step the issue order is [4 dG stores of t+1, 6 stash loads of t-2], so at
+  // the top of step t <= T-2 the loads it needs are followed by exactly 10 newer ops: vmcnt(10)
+  auto load_into = [&](int t, float4 (&sb)[STASH], float4& cb) {
+    const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
+#pragma unroll
+    for (int k = 0; k < STASH; ++k) sb[k] = src[64 * k];
+    cb = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 64 * 4];
+  };
+  float4 sA[STASH], cA, sB[STASH], cB;
+  load_into(T - 1, sA, cA);
+  if (T > 1) load_into(T - 2, sB, cB);
   __syncthreads();  // B0 (dhs[(T-1)&1] staged)
 
-  for (int t = T - 1; t >= 0; --t) {
-    float4 st[STASH];
-#pragma unroll
-    for (int k = 0; k < STASH; ++k) st[k] = st_nxt[k];
-    const float cpm = t > 0 ? 1.f : 0.f;
-    const float cp4[4] = {cp_nxt.x * cpm, cp_nxt.y * cpm, cp_nxt.z * cpm, cp_nxt.w * cpm};
+  // one reverse step; returns false after step 0
+  auto step = [&](int t, float4 (&sb)[STASH], float4& cb) {
     float dho[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[t & 1][4 * q + i][u];
-    mta_wait_vmem();
-    if (t < T - 1) store_step(t + 1);
-    if (t > 0) load_step(t - 1);
+    if (t <= T - 2) mta_wait_vmcnt<10>();
+    else mta_wait_vmcnt<6>();
+    store_step(t < T - 1 ? t + 1 : t);  // unconditional (step T-1 stores its zero pdG to row T-1, which
+                                        // step T-2 then overwrites in order): keeps the count exact
     __builtin_amdgcn_sched_barrier(0);
+    const float4* st = sb;
+    const float cpm = t > 0 ? 1.f : 0.f;
+    const float cp4[4] = {cb.x * cpm, cb.y * cpm, cb.z * cpm, cb.w * cpm};
     const float ig4[4] = {st[0].x, st[0].y, st[0].z, st[0].w};
     const float fg4[4] = {st[1].x, st[1].y, st[1].z, st[1].w};
     const float gg4[4] = {st[2].x, st[2].y, st[2].z, st[2].w};
@@ -690,8 +736,11 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s4][rp]) = lo4;
       }
     }
+    // prefetch step t-2 into this set (its values are dead now); unconditional, so the set needs no copy
+    __builtin_amdgcn_sched_barrier(0);
+    load_into(t >= 2 ? t - 2 : 0, sb, cb);
     __syncthreads();  // A(t): dG_t image visible to the gradient waves and to this step's dh product
-    if (t == 0) break;
+    if (t == 0) return;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if constexpr (PREC == PREC_F32) {
       const float* arow = &g_f[buf][j][q * KF];
@@ -714,7 +763,15 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) dhr[i] = acc0[i] + acc1[i];
+  };
+  // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip (no
+  // conditional step inside, so the sets keep their registers across the back-edge), odd T peels step 0
+  int t = T - 1;
+  for (; t >= 1; t -= 2) {
+    step(t, sA, cA);
+    step(t - 1, sB, cB);
   }
+  if (t == 0) step(0, sA, cA);
   store_step(0);
   mta_wait_vmem();
   __syncthreads();  // F
@@ -722,16 +779,40 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 
 template <int H, int PREC>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwdArgs a) {
-  // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
-  // so every workgroup a spinning one waits for is already resident): top layer first here
-  const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
-  if (tile >= a.ntiles) return;
-  const bool top = layer == a.L - 1, bottom = layer == 0;
-  __shared__ __attribute__((aligned(16))) BwdSmem<H, PREC> sm;  // one image shared by the role bodies
-  if (top && bottom) stack_bwd_body<H, PREC, true, true>(a, layer, tile, sm);
-  else if (top) stack_bwd_body<H, PREC, true, false>(a, layer, tile, sm);
-  else if (bottom) stack_bwd_body<H, PREC, false, true>(a, layer, tile, sm);
-  else stack_bwd_body<H, PREC, false, false>(a, layer, tile, sm);
+  // one dynamic LDS block: the recurrence image (BwdSmem) or a weight-gradient staging image
+  extern __shared__ __attribute__((aligned(16))) char dyn_lds[];
+  const unsigned base = read_epoch_base(a.ctl, CTL_BWD_EPOCH);
+  const int nrec = a.L * a.tr8;
+  if ((int)blockIdx.x < nrec) {
+    // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
+    // so every workgroup a spinning one waits for is already resident): top layer first here
+    const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+    if (tile < a.ntiles) {
+      const bool top = layer == a.L - 1, bottom = layer == 0;
+      auto& sm = *reinterpret_cast<BwdSmem<H, PREC>*>(dyn_lds);
+      if (top && bottom) stack_bwd_body<H, PREC, true, true>(a, layer, tile, sm, base);
+      else if (top) stack_bwd_body<H, PREC, true, false>(a, layer, tile, sm, base);
+      else if (bottom) stack_bwd_body<H, PREC, false, true>(a, layer, tile, sm, base);
+      else stack_bwd_body<H, PREC, false, false>(a, layer, tile, sm, base);
+    }
+  } else {
+    // fused weight gradient of (layer, time chunk, c' block), top layer and late chunks first (the order
+    // in which the recurrence drains dG); waits until every tile of the layer has drained the chunk's steps
+    const int idx = blockIdx.x - nrec;
+    const int layer = a.L - 1 - idx / a.wg_per_layer, rem = idx % a.wg_per_layer;
+    const mta_wgrad::WgArgs& w = a.wg[layer];
+    const int chunk = w.nchunks - 1 - rem / a.wg_nq, quarter = rem % a.wg_nq;
+    const int t_lo = chunk * (w.rows_per_chunk / a.Np);
+    if (threadIdx.x < a.ntiles)
+      wait_progress(a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + threadIdx.x), base + (unsigned)(a.T - t_lo), base,
+                    a.timeout);
+    __syncthreads();
+    mta_wgrad::wgrad_body<PREC, H / 8, true>(w, chunk, quarter, dyn_lds);
+  }
+  if (finish_launch(a.ctl, CTL_BWD_EPOCH, CTL_BWD_DONE, base) && a.dropout) {
+    // fresh counter-hash masks for the next step (the graph needs no seed-update node)
+    for (int l = 0; l < a.L; ++l) a.seeds[l] += 0x9E3779B97F4A7C15ull;
+  }
 }
 
 template <int H, int PREC>
@@ -750,18 +831,33 @@ int dispatch_fwd(int prec, int fin, const StackFwdArgs& a, hipStream_t st) {
   return launch_fwd<H, PREC_BF16>(fin, a, st);
 }
 
-template <int H>
-int dispatch_bwd(int prec, const StackBwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.L * a.tr8), block((H / 16) * 128);  // recurrent + gradient waves
-  if (prec == PREC_F32) lstm_stack_bwd_kernel<H, PREC_F32><<<grid, block, 0, st>>>(a);
-  else if (prec == PREC_BF16X3) lstm_stack_bwd_kernel<H, PREC_BF16X3><<<grid, block, 0, st>>>(a);
-  else lstm_stack_bwd_kernel<H, PREC_BF16><<<grid, block, 0, st>>>(a);
+template <int H, int PREC>
+int launch_bwd(const StackBwdArgs& a, size_t lds, hipStream_t st) {
+  const dim3 grid(a.L * a.tr8 + a.L * a.wg_per_layer), block((H / 16) * 128);  // recurrent + gradient waves
+  lds = lds > sizeof(BwdSmem<H, PREC>) ? lds : sizeof(BwdSmem<H, PREC>);
+  if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_stack_bwd_kernel<H, PREC>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    return -3;
+  lstm_stack_bwd_kernel<H, PREC><<<grid, block, lds, st>>>(a);
   return 0;
+}
+
+template <int H>
+int dispatch_bwd(int prec, const StackBwdArgs& a, size_t wg_lds, hipStream_t st) {
+  if (prec == PREC_F32) return launch_bwd<H, PREC_F32>(a, wg_lds, st);
+  if (prec == PREC_BF16X3) return launch_bwd<H, PREC_BF16X3>(a, wg_lds, st);
+  return launch_bwd<H, PREC_BF16>(a, wg_lds, st);
 }
 
 }  // namespace
 
-// flags: [2][MAXL][tr8] unsigned progress words + timeout word, zeroed here (memset node) every call.
+// flags (zero-initialised once, then never reset): [3][MAXL][tr8] progress words (forward, backward dX,
+// backward dG; FLAG_STRIDE apart) + CTL_WORDS control words (timeout, per-direction epoch + arrival counter).
+extern "C" long mta_lstm_stack_flag_words(int Np) {
+  const int tr8 = (Np / S + 7) / 8 * 8;
+  return 3L * FLAG_STRIDE * MAXL * tr8 + CTL_WORDS;
+}
+
 extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                                   const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                   float* const* hseq, float* const* xdrop, float* const* stash,
@@ -787,20 +883,22 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.L = L;
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;  // tile i of every layer gets the same block id modulo 8
+  if (T >= (1 << EPOCH_SHIFT)) return -1;
   a.flags = flags;
-  a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
-  a.plain_probe = stack_probe();
-  if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
-    return -2;
+  a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
+  a.timeout = a.ctl + CTL_TIMEOUT;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
 }
 
-extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* stash, const float* const* w_hh,
+// Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's
+// (dropped-out) input sequence (T, Np, H); the gradients accumulate into g_* (the flat gradient buffer).
+extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
-                                  const uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np,
-                                  int T, hipStream_t st) {
-  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
+                                  const float* const* hseq, const float* const* inp, float* const* g_wih,
+                                  float* const* g_whh, float* const* g_bih, float* const* g_bhh, uint64_t* seeds,
+                                  float drop_p, int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
+  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T >= (1 << EPOCH_SHIFT)) return -1;
   StackBwdArgs a{};
   for (int l = 0; l < L; ++l) {
     a.stash[l] = stash[l];
@@ -819,11 +917,49 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, const float* const* st
   a.L = L;
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;
-  a.flags = flags;
-  a.timeout = flags + FLAG_STRIDE * MAXL * a.tr8;
-  a.plain_probe = stack_probe();
-  if (hipMemsetAsync(flags, 0, (size_t)(FLAG_STRIDE * MAXL * a.tr8 + 4) * sizeof(unsigned), st) != hipSuccess)
-    return -2;
-  if (H == 32) return dispatch_bwd<32>(prec, a, st);
-  return dispatch_bwd<64>(prec, a, st);
+  a.flags = flags + FLAG_STRIDE * MAXL * a.tr8;
+  a.dg_flags = flags + 2 * FLAG_STRIDE * MAXL * a.tr8;
+  a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
+  a.timeout = a.ctl + CTL_TIMEOUT;
+  size_t wg_lds = 0;
+  if (g_whh) {
+    // NWAVES = 2 H / 16 waves per workgroup -> CQ = 16 NWAVES gate columns, 4H / CQ = 2 blocks per chunk
+    const int nwaves = H / 8, cq = 16 * nwaves;
+    int tc = (T + 59) / 60;  // time steps per chunk: short chunks keep the tail after the last layer small
+    if (const char* e = getenv("MTA_WGRAD_TC")) tc = atoi(e) > 0 ? atoi(e) : tc;
+    a.wg_nq = 4 * H / cq;
+    for (int l = 0; l < L; ++l) {
+      mta_wgrad::WgArgs& w = a.wg[l];
+      w.dG = dG[l];
+      w.hseq = hseq[l];
+      w.inp = inp[l];
+      w.inp_batch_first = l == 0;
+      w.N = N;
+      w.Np = Np;
+      w.T = T;
+      w.H = H;
+      w.F = l == 0 ? fin : H;
+      w.FP = (w.F + 15) / 16 * 16;
+      w.rows_per_chunk = tc * Np;
+      w.nchunks = (T + tc - 1) / tc;
+      w.g_wih = g_wih[l];
+      w.g_whh = g_whh[l];
+      w.g_bih = g_bih[l];
+      w.g_bhh = g_bhh[l];
+      const int NB = H + w.FP;
+      if (NB / 16 > 16 || cq + NB > mta_wgrad::WG_MAX_UNITS_PER_THREAD * 64 * nwaves) return -1;
+      size_t bytes;
+      if (prec == PREC_F32) {
+        w.lo_off = 0;
+        bytes = (size_t)(cq + NB) * mta_wgrad::WgImg<PREC_F32>::RS * 4;
+      } else {
+        w.lo_off = (cq + NB) * mta_wgrad::WgImg<PREC_BF16>::RS;
+        bytes = (size_t)w.lo_off * 2 * (prec == PREC_BF16X3 ? 2 : 1);
+      }
+      wg_lds = bytes > wg_lds ? bytes : wg_lds;
+    }
+    a.wg_per_layer = a.wg[0].nchunks * a.wg_nq;
+  }
+  if (H == 32) return dispatch_bwd<32>(prec, a, wg_lds, st);
+  return dispatch_bwd<64>(prec, a, wg_lds, st);
 }

@@ -149,6 +149,19 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
     return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= 448
 
 
+_FLAGS = {}
+_CTL_WORDS = 160  # control words at the end of the flag buffer (csrc/lstm_stack.hip CTL_*): [0] = timeout
+
+
+def _stack_flags(C, Np: int, device) -> Tensor:
+    """Persistent, zero-initialised progress/epoch words of the pipelined kernels (never reset per launch:
+    progress is epoch-stamped in-kernel, so a captured graph has no memset nodes)."""
+    key = (C.lstm_stack_flag_words(Np), str(device))
+    if key not in _FLAGS:
+        _FLAGS[key] = torch.zeros(key[0], dtype=torch.int32, device=device)
+    return _FLAGS[key]
+
+
 class _LSTMPipelinedFn(torch.autograd.Function):
     """All layers in one forward launch and one backward launch (wavefront over (layer, t))."""
 
@@ -163,14 +176,15 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         dev = x.device
         E = _empty(dev)
         drop = dropout > 0.0 and training
-        if drop:
-            seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))  # fresh counter-hash masks every step (in-graph)
+        if drop and not need_grad:
+            # the backward launch advances the seeds after use; without one, advance them here
+            seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))
         hseq = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L)]
         xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E
                        for _ in range(1, L)]
         stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E
                  for _ in range(L)]
-        flags = torch.empty(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
+        flags = _stack_flags(C, Np, dev)
         C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
                          hseq, xdrop, stash, seeds, float(dropout), flags, N, Np, T)
         ctx.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
@@ -195,24 +209,20 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         flat = ctx.params
         dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
         dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
-        flags = torch.empty(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
-        C.lstm_stack_bwd(H, prec, stash, list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
-                         ctx.seeds, p, drop, flags, N, Np, T)
+        flags = _stack_flags(C, Np, dev)
+        inp = [x] + [xdrop[l - 1] if drop else hseq[l - 1] for l in range(1, L)]
+        # weight gradients are computed by the same launch (fused workgroups consume dG as it drains) and
+        # accumulated straight into the parameters' gradient views
+        grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
+        C.lstm_stack_bwd(H, prec, F, stash, list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
+                         hseq, inp, grads, ctx.seeds, p, drop, flags, N, Np, T)
         ctx.bwd_flags = flags
-        for l in range(L):
-            w_ih, w_hh, b_ih, b_hh = flat[4 * l: 4 * l + 4]
-            if l == 0:
-                inp = x
-            else:
-                inp = (xdrop[l - 1] if drop else hseq[l - 1]).view(T * Np, H)
-            C.lstm_wgrad(prec, dG[l], hseq[l], inp, l == 0, N, Np, T, H, _grad_buffer(w_ih), _grad_buffer(w_hh),
-                         _grad_buffer(b_ih), _grad_buffer(b_hh))
         return (None,) * (6 + len(flat))
 
 
 def stack_timed_out(flags: Tensor) -> bool:
     """True if a pipelined launch gave up waiting on a producer (diagnostic; host sync)."""
-    return bool(flags[flags.numel() - 4].item() != 0)
+    return bool(flags[flags.numel() - _CTL_WORDS].item() != 0)
 
 
 _PERM_CACHE = {}

@@ -1,10 +1,9 @@
 """Timing of the pipelined LSTM stack kernels vs the per-layer kernels (fwd / bwd, L = 1..8).
 
-plain=1 rows use plain (not write-through) hand-off stores, plain=2 also drop the stash / dG stores,
-plain=3 also the backward's stash loads: timing probes of the memory-traffic cost only (invalid results).
+(The MTA_STACK_PLAIN_STORES probes of round 1 showed the stash traffic costing ~25% of the forward:
+fixed by the lane-contiguous stash layout and vmcnt-counted waits.)
 """
 import math
-import os
 import sys
 from pathlib import Path
 
@@ -14,13 +13,9 @@ sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 from scripts.microbench import timeit  # noqa: E402
 
 
-def run(C, L, prec, plain):
+def run(C, L, prec):
     from masters_thesis_amd.ops.lstm import padded_rows
 
-    if plain:
-        os.environ["MTA_STACK_PLAIN_STORES"] = str(int(plain))
-    else:
-        os.environ.pop("MTA_STACK_PLAIN_STORES", None)
     dev = "cuda"
     N, T, F, H = 100, 60, 3, 64
     Np = padded_rows(N)
@@ -34,7 +29,7 @@ def run(C, L, prec, plain):
     E = torch.empty(0, device=dev)
     hseq = [torch.empty((T, Np, H), device=dev) for _ in range(L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev) for _ in range(L)]
-    flags = torch.empty(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
+    flags = torch.zeros(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
     seeds = torch.zeros(8, dtype=torch.int64, device=dev)
 
     def fwd():
@@ -45,10 +40,25 @@ def run(C, L, prec, plain):
     dX = [torch.empty((T, Np, H), device=dev) for _ in range(L - 1)] + [E]
     dh = torch.randn(N, H, device=dev)
 
+    inp = [x] + hseq[:-1]
+    grads = [[torch.zeros_like(ws[4 * l + k]) for l in range(L)] for k in range(4)]
+
     def bwd():
-        C.lstm_stack_bwd(H, prec, stash, ws[1::4], ws[0::4], dh, dG, dX, seeds, 0.0, False, flags, N, Np, T)
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], seeds, 0.0, False, flags,
+                         N, Np, T)
+
+    def bwd_fused():
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, seeds, 0.0, False,
+                         flags, N, Np, T)
+
+    def bwd_wgrad():
+        bwd()
+        for l in range(L):
+            C.lstm_wgrad(prec, dG[l], hseq[l], inp[l] if l else x, l == 0, N, Np, T, H, grads[0][l], grads[1][l],
+                         grads[2][l], grads[3][l])
 
     tf, tb = timeit(fwd), timeit(bwd)
+    tbf, tbw = timeit(bwd_fused), timeit(bwd_wgrad)
     gx = torch.randn(T, Np, 4 * H, device=dev)
 
     def old_fwd():
@@ -57,8 +67,8 @@ def run(C, L, prec, plain):
             C.lstm_fwd_layer(H, prec, None, None, None, None, gx, stash[l], ws[4 * l + 1], hseq[l], N, Np, T)
 
     to = timeit(old_fwd)
-    print(f"L={L} plain={int(plain)} prec={prec}: stack fwd {tf:7.1f} us  bwd {tb:7.1f} us | per-layer fwd {to:7.1f} us",
-          flush=True)
+    print(f"L={L} prec={prec}: stack fwd {tf:7.1f} us  bwd {tb:7.1f} us  bwd+fused wgrad {tbf:7.1f} us  "
+          f"bwd then {L} wgrad kernels {tbw:7.1f} us | per-layer fwd {to:7.1f} us", flush=True)
 
 
 def main():
@@ -66,9 +76,7 @@ def main():
 
     C = _lib.lib()
     for L in (1, 2, 4, 8):
-        for plain in (0, 1, 2, 3):
-            run(C, L, 1, plain)
-    os.environ.pop("MTA_STACK_PLAIN_STORES", None)
+        run(C, L, 1)
 
 
 if __name__ == "__main__":

@@ -113,10 +113,13 @@ def test_pipelined_dropout_masks_match_counter_hash():
     ws = _weights(F, H, L, seed=3)
     seeds = torch.randint(0, 2 ** 62, (8,), dtype=torch.int64, device=DEV)
     wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    used = seeds.cpu().tolist()  # the backward launch advances them after use
     out = op.lstm_last_hidden(x.to(DEV), wg, L, p, True, "highest", seeds)
     R = torch.randn(N, H)
     (out * R.to(DEV)).sum().backward()
-    used = seeds.cpu().tolist()  # advanced in-op before the launch
+    golden = 0x9E3779B97F4A7C15
+    assert seeds.cpu().tolist()[:L] == [((u + golden) % (1 << 64)) - ((1 << 64) if (u + golden) % (1 << 64) >= (1 << 63) else 0)
+                                        for u in used[:L]]
     masks = [None] + [_mask(used[l] & ((1 << 64) - 1), T, Np, N, H, p).double() for l in range(1, L)]
     ref, w64 = _ref(x, ws, L, masks)
     (ref * R.double()).sum().backward()
