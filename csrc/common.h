@@ -55,6 +55,42 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// Wave sums on the DPP path (no LDS round trip per step, unlike __shfl_xor -> ds_bpermute): two quad_perm
+// and two row_shr steps reduce each 16-lane row (the row total lands in its lane 15), the four row totals
+// are read as scalars.  Every lane of the wave must be active (all call sites run whole waves).
+template <int CTRL>
+__device__ __forceinline__ int mta_dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);  // invalid source lane -> 0
+}
+template <int CTRL>
+__device__ __forceinline__ float mta_dpp(float v) {
+  return __builtin_bit_cast(float, mta_dpp_i<CTRL>(__builtin_bit_cast(int, v)));
+}
+template <int CTRL>
+__device__ __forceinline__ double mta_dpp(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const unsigned lo = (unsigned)mta_dpp_i<CTRL>((int)(b & 0xffffffffll));
+  const unsigned hi = (unsigned)mta_dpp_i<CTRL>((int)(b >> 32));
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float mta_readlane(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+__device__ __forceinline__ double mta_readlane(double v, int lane) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)hi << 32) | lo));
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum_dpp(T v) {
+  v += mta_dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += mta_dpp<0x4E>(v);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
+  v += mta_dpp<0x114>(v);  // row_shr:4
+  v += mta_dpp<0x118>(v);  // row_shr:8: lane 15 of each row holds the row's sum
+  return (mta_readlane(v, 15) + mta_readlane(v, 31)) + (mta_readlane(v, 47) + mta_readlane(v, 63));
+}
+
 // Block-level sum for blockDim.x <= 1024; `scratch` needs blockDim.x/64 floats.
 __device__ __forceinline__ float block_sum(float v, float* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;

@@ -57,10 +57,10 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
       ss = fmaf(e, e, ss);
       sa += fabsf(e);
     }
-    se = wave_sum(se);
-    serm = wave_sum(serm);
-    sse += (double)wave_sum(ss);
-    sae += (double)wave_sum(sa);
+    se = wave_sum_dpp(se);
+    serm = wave_sum_dpp(serm);
+    sse += (double)wave_sum_dpp(ss);
+    sae += (double)wave_sum_dpp(sa);
     if (lane == 0) {
       A.gmse[2 * i] = 2.f * se * inv_cnt;
       A.gmse[2 * i + 1] = 2.f * serm * inv_cnt;
@@ -94,7 +94,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
           sdd = fmaf(D, D, sdd);
           atomicAdd(&ut[t], wb * D);
         }
-        sdd = wave_sum(sdd);
+        sdd = wave_sum_dpp(sdd);
         if (lane == 0) {
           s_wbb += (double)wb * b;
           s_logw += log((double)w);
@@ -106,7 +106,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
       for (int t = tid; t < n; t += TPB) { s_u1 += ut[t]; s_u2 += (double)ut[t] * ut[t]; }
       double v[5] = {s_wbb, s_logw, s_wdd, s_u1, s_u2};
 #pragma unroll
-      for (int m = 0; m < 5; ++m) v[m] = wave_sum_d(v[m]);
+      for (int m = 0; m < 5; ++m) v[m] = wave_sum_dpp(v[m]);
       if (lane == 0)
         for (int m = 0; m < 5; ++m) red[wid][m] = v[m];
       __syncthreads();
@@ -135,8 +135,8 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
           sd += D;
           ud = fmaf(ut[t], D, ud);
         }
-        sd = wave_sum(sd);
-        ud = wave_sum(ud);
+        sd = wave_sum_dpp(sd);
+        ud = wave_sum_dpp(ud);
         if (lane == 0) {
           const float wb = w * b;
           A.gnll[2 * i] = -w * sd + wb * fU1 / fden;
@@ -187,8 +187,8 @@ __global__ __launch_bounds__(TPB) void heads_losses_kernel(const float* __restri
       sa = fmaf(hv, wa[k], sa);
       sb = fmaf(hv, wb[k], sb);
     }
-    sa = wave_sum(sa) + ba[0];
-    sb = wave_sum(sb) + bb[0];
+    sa = wave_sum_dpp(sa) + ba[0];
+    sb = wave_sum_dpp(sb) + bb[0];
     if (lane == 0) {
       ab[2 * i] = sa;
       ab[2 * i + 1] = sb;
@@ -276,8 +276,8 @@ __global__ __launch_bounds__(TPB) void heads_kernel(const float* __restrict__ h,
     sa += hv.x * av.x + hv.y * av.y + hv.z * av.z + hv.w * av.w;
     sb += hv.x * bv.x + hv.y * bv.y + hv.z * bv.z + hv.w * bv.w;
   }
-  sa = wave_sum(sa);
-  sb = wave_sum(sb);
+  sa = wave_sum_dpp(sa);
+  sb = wave_sum_dpp(sb);
   if (lane == 0) {
     ab_out[2 * i] = sa + ba[0];
     ab_out[2 * i + 1] = sb + bb[0];
@@ -333,8 +333,8 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
       da += dab[2 * i];
       db += dab[2 * i + 1];
     }
-    da = wave_sum(da);
-    db = wave_sum(db);
+    da = wave_sum_dpp(da);
+    db = wave_sum_dpp(db);
     if (threadIdx.x == 0) {
       atomicAdd(g_ba, da);
       atomicAdd(g_bb, db);

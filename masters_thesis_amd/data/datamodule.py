@@ -117,7 +117,7 @@ class FinancialLstmDataModule:
     def _compute_hparams_hash(self) -> str:
         h = {k: self.hparams[k] for k in ("lookback_window", "target_window", "stride", "prediction_task",
                                           "interaction_only")}
-        h["source"] = self._stored_source() or self.source_signature()
+        h["source"] = self.source_signature()
         return hashlib.sha256(json.dumps(h, sort_keys=True).encode()).hexdigest()
 
     @property
@@ -185,7 +185,6 @@ class FinancialLstmDataModule:
                 return
             ds = self._build(persist=True)
             self.datasets_dir.mkdir(parents=True, exist_ok=True)
-            path = self.dataset_path()  # the source may have been (re)generated just now
             atomic_torch_save({k: ds[k].detach().cpu().contiguous() for k in self.KEYS}, path)
             atomic_write_text(self.datasets_dir / "hparams_hash.txt", self._compute_hparams_hash())
 
