@@ -125,9 +125,11 @@ def main(argv=None):
     elapsed = pdist.all_reduce_max(elapsed, dev)
     step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs else [elapsed * 1e3 / args.steps]
     p50 = pdist.all_reduce_max(step_ms[len(step_ms) // 2], dev)
+    p90 = pdist.all_reduce_max(step_ms[min(len(step_ms) - 1, (len(step_ms) * 9) // 10)], dev)
     ms_per_step = elapsed * 1e3 / args.steps
     value = args.batch * world * args.steps / elapsed
     nonfinite = float(trainer.optimizer.nonfinite.item())
+    trainer._check_device_health()  # raises if a pipelined hand-off gave up (garbage steps)
     if denv.rank == 0:
         log(f"[bench] p50 step {p50:.3f} ms, mean {ms_per_step:.3f} ms, graphs={'on' if trainer._graphs else 'off'}, "
             f"nonfinite={nonfinite}, static_batches={trainer._static_ok(loader)}")
@@ -140,6 +142,7 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "p50_step_ms": round(p50, 4),
+            "p90_step_ms": round(p90, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / YARDSTICK[(args.model, args.loss, args.batch)], 3)

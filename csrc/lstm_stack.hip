@@ -31,7 +31,7 @@ namespace {
 constexpr int S = 16;
 constexpr int STASH = 5;
 constexpr int MAXL = 8;
-constexpr unsigned SPIN_LIMIT = 1u << 21;
+constexpr unsigned SPIN_LIMIT = 1u << 21;  // default poll bound (env MTA_LSTM_SPIN_LIMIT overrides: fault tests)
 constexpr int FLAG_STRIDE = 32;
 constexpr int EPOCH_SHIFT = 12;  // one 128-byte line per progress word (polled words never share a line)
 
@@ -74,15 +74,18 @@ __device__ __forceinline__ bool finish_launch(unsigned* ctl, int epoch_word, int
 // (wrap-safe signed difference, T < 4096).  No memset node per launch.
 __device__ __forceinline__ bool reached(unsigned seen, unsigned need) { return (int)(seen - need) >= 0; }
 
-// wait until *flag reaches need (relaxed agent-scope polls); returns the value seen
-__device__ __forceinline__ unsigned wait_progress(unsigned* flag, unsigned need, unsigned seen, unsigned* tmo) {
+// wait until *flag reaches need (relaxed agent-scope polls); returns the value seen.  A wait that exceeds
+// `limit` polls gives up (so the grid always drains) and counts itself in the timeout word, which the host
+// checks (ops.lstm.check_pipeline_health: the trainer raises at epoch end, bench.py at the end of the run).
+__device__ __forceinline__ unsigned wait_progress(unsigned* flag, unsigned need, unsigned seen, unsigned* tmo,
+                                                  unsigned limit) {
   unsigned spins = 0;
   while (!reached(seen, need)) {
     __builtin_amdgcn_s_sleep(1);
     seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (++spins > SPIN_LIMIT) {
-      __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      seen = need;  // give up waiting (results are garbage, the host sees the timeout word)
+    if (++spins > limit) {
+      __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      seen = need;  // give up waiting (results are garbage: the host raises on the non-zero timeout count)
     }
   }
   // every payload load after this point is sc1 (L1 bypass): only keep the compiler from hoisting them
@@ -118,6 +121,7 @@ struct StackFwdArgs {
   unsigned* flags;      // [MAXL][tr8] progress words (epoch-stamped, never reset)
   unsigned* timeout;
   unsigned* ctl;
+  unsigned spin_limit;
   int N, Np, T, L, ntiles, tr8;
 };
 
@@ -218,7 +222,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       } else {
         // poll only when the last value seen does not cover step t (polling every step from every
         // consumer wave measured slower: the progress words share cache lines across tiles)
-        seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout);
+        seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
         const size_t row = (size_t)t * Np + n0 + j;
 #pragma unroll
         for (int v = 0; v < XR; ++v) {
@@ -478,6 +482,7 @@ struct StackBwdArgs {
   unsigned* dg_flags;     // [MAXL][tr8]: reverse steps of dG[l] drained (write-through) by layer l
   unsigned* timeout;
   unsigned* ctl;
+  unsigned spin_limit;
   int N, Np, T, L, ntiles, tr8;
   // fused weight gradients: wg_per_layer workgroups per layer follow the L x tr8 recurrence workgroups
   mta_wgrad::WgArgs wg[MAXL];
@@ -552,7 +557,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     unsigned seen = base;
     auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
       if constexpr (!TOP) {
-        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout);
+        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
@@ -805,7 +810,7 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     const int t_lo = chunk * (w.rows_per_chunk / a.Np);
     if (threadIdx.x < a.ntiles)
       wait_progress(a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + threadIdx.x), base + (unsigned)(a.T - t_lo), base,
-                    a.timeout);
+                    a.timeout, a.spin_limit);
     __syncthreads();
     mta_wgrad::wgrad_body<PREC, H / 8, true>(w, chunk, quarter, dyn_lds);
   }
@@ -849,6 +854,14 @@ int dispatch_bwd(int prec, const StackBwdArgs& a, size_t wg_lds, hipStream_t st)
   return launch_bwd<H, PREC_BF16>(a, wg_lds, st);
 }
 
+unsigned spin_limit() {
+  static const unsigned v = [] {
+    const char* e = getenv("MTA_LSTM_SPIN_LIMIT");
+    return e && atol(e) > 0 ? (unsigned)atol(e) : SPIN_LIMIT;
+  }();
+  return v;
+}
+
 }  // namespace
 
 // flags (zero-initialised once, then never reset): [3][MAXL][tr8] progress words (forward, backward dX,
@@ -887,6 +900,7 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.flags = flags;
   a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
+  a.spin_limit = spin_limit();
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
 }
@@ -921,6 +935,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
   a.dg_flags = flags + 2 * FLAG_STRIDE * MAXL * a.tr8;
   a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
+  a.spin_limit = spin_limit();
   size_t wg_lds = 0;
   if (g_whh) {
     // NWAVES = 2 H / 16 waves per workgroup -> CQ = 16 NWAVES gate columns, 4H / CQ = 2 blocks per chunk

@@ -35,8 +35,11 @@ def load_checkpoint(path: os.PathLike, map_location=None) -> Dict[str, Any]:
 
 
 def capture_rng_states() -> Dict[str, Any]:
-    st = {"torch": torch.random.get_rng_state(), "python_state": list(random.getstate()[1]),
-          "numpy_state": np.random.get_state()[1].tolist()}
+    py = random.getstate()
+    npk, npst, nppos, nphas, npg = np.random.get_state()
+    st = {"torch": torch.random.get_rng_state(), "python_state": list(py[1]),
+          "numpy_state": npst.tolist(), "numpy_pos": int(nppos), "numpy_has_gauss": int(nphas),
+          "numpy_gauss": float(npg)}
     if torch.cuda.is_available() and torch.cuda.is_initialized():
         st["cuda"] = torch.cuda.get_rng_state()
     return st
@@ -50,4 +53,6 @@ def restore_rng_states(st: Dict[str, Any]) -> None:
     if "python_state" in st:
         random.setstate((3, tuple(st["python_state"]), None))
     if "numpy_state" in st:
-        np.random.set_state(("MT19937", np.array(st["numpy_state"], dtype=np.uint32), 624, 0, 0.0))
+        # the whole generator state (key, position, cached Gaussian): the stream continues exactly
+        np.random.set_state(("MT19937", np.array(st["numpy_state"], dtype=np.uint32), int(st.get("numpy_pos", 624)),
+                             int(st.get("numpy_has_gauss", 0)), float(st.get("numpy_gauss", 0.0))))

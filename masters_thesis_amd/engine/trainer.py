@@ -149,6 +149,11 @@ class Trainer:
                 c.dirpath = str(Path(self.logger.log_dir) / "checkpoints")
 
     def _setup_model(self, model) -> None:
+        if self.model is not None and self.model is not model:
+            # captured graphs hold the previous model's parameter / metric buffers: never replay them
+            self._graphs.clear()
+            self._eager_counts.clear()
+            self._graph_loaders.clear()
         model.trainer = self
         model.to(self.device)
         model.matmul_precision = self._effective_matmul_precision()
@@ -391,12 +396,20 @@ class Trainer:
                 break
             self._eval_step(stage, loader, i, False, batch)
 
+    def _check_device_health(self) -> None:
+        """Raise if a pipelined LSTM launch gave up on a hand-off (its results were garbage)."""
+        if self.device.type == "cuda":
+            from ..ops.lstm import check_pipeline_health
+
+            check_pipeline_health()
+
     def _run_eval(self, stage: str, loader, limit=None) -> Dict[str, torch.Tensor]:
         model = self.model
         model.eval()
         model._stage = "val" if stage == "sanity" else stage
         with torch.no_grad():
             self._eval_loop(model._stage, loader, limit)
+        self._check_device_health()
         res = self._compute_stage_metrics(model._stage)
         self._reset_stage_metrics(model._stage)
         model.train()
@@ -509,6 +522,7 @@ class Trainer:
             if nonfinite > 0:
                 self._print(f"WARNING: {int(nonfinite)} step(s) with a non-finite gradient norm")
                 self.optimizer.nonfinite.zero_()
+            self._check_device_health()
 
             train_metrics = self._compute_stage_metrics("train")
             self._reset_stage_metrics("train")
@@ -577,6 +591,7 @@ class Trainer:
         model.on_test_start()
         with torch.no_grad():
             self._eval_loop("test", loader, self.limit_test_batches)
+        self._check_device_health()
         # sync every test-time Metric (logged or attribute) across ranks before on_test_end
         test_metrics = list(self._metrics_of("test").values())
         test_metrics += [m for name, m in model.named_children() if isinstance(m, Metric) and name.startswith("test")]
@@ -607,7 +622,10 @@ class Trainer:
             "hyper_parameters": dict(model.hparams),
             "rng_states": capture_rng_states(),
             "mta": {"world_size": self.world_size, "precision": self.precision,
-                    "matmul_precision": self._effective_matmul_precision()},
+                    "matmul_precision": self._effective_matmul_precision(),
+                    # non-persistent device RNG state (LSTM counter-hash dropout seeds): exact resume
+                    "buffers": {k: v.detach().cpu().clone() for k, v in model.named_buffers()
+                                if k.endswith("seeds")}},
         }
         model.on_save_checkpoint(ck)
         return ck
@@ -631,6 +649,10 @@ class Trainer:
                 c.load_state_dict(cbs[c.state_key])
         if "rng_states" in ck:
             restore_rng_states(ck["rng_states"])
+        bufs = dict(self.model.named_buffers())
+        for k, v in ck.get("mta", {}).get("buffers", {}).items():
+            if k in bufs and bufs[k].shape == v.shape:
+                bufs[k].copy_(v)
         self.global_step = int(ck.get("global_step", 0))
         self._print(f"Restored training state from {path} (epoch {ck['epoch']}, step {self.global_step})")
         return int(ck["epoch"]) + 1

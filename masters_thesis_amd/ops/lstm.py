@@ -150,16 +150,45 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
 
 
 _FLAGS = {}
-_CTL_WORDS = 160  # control words at the end of the flag buffer (csrc/lstm_stack.hip CTL_*): [0] = timeout
+_CTL_WORDS = 160  # control words at the end of the flag buffer (csrc/lstm_stack.hip CTL_*): [0] = timeout count
 
 
-def _stack_flags(C, Np: int, device) -> Tensor:
+def _stack_flags(C, Np: int, L: int, device) -> Tensor:
     """Persistent, zero-initialised progress/epoch words of the pipelined kernels (never reset per launch:
-    progress is epoch-stamped in-kernel, so a captured graph has no memset nodes)."""
-    key = (C.lstm_stack_flag_words(Np), str(device))
+    progress is epoch-stamped in-kernel, so a captured graph has no memset nodes).
+
+    One buffer per (Np, L, device): every progress word a launch polls is then rewritten by every launch
+    that shares the buffer, so a stale word is always exactly one epoch behind and compares below the
+    awaited value under the kernel's wrap-safe signed difference.  (A buffer shared between stack depths
+    would leave the deeper layers' words at 0 while the epoch advances; once the epoch passes 2^19 such a
+    never-written word would read as 'reached'.)"""
+    key = (C.lstm_stack_flag_words(Np), int(L), str(device))
     if key not in _FLAGS:
         _FLAGS[key] = torch.zeros(key[0], dtype=torch.int32, device=device)
     return _FLAGS[key]
+
+
+def stack_timeouts(flags: Tensor) -> int:
+    """Number of hand-off waits that gave up since the last check (host sync)."""
+    return int(flags[flags.numel() - _CTL_WORDS].item())
+
+
+def check_pipeline_health(clear: bool = True) -> None:
+    """Raise if any pipelined LSTM launch gave up waiting on a producer (its outputs were garbage).
+
+    The kernels bound every spin (the grid always drains) and count give-ups in a device word; the
+    trainer calls this at every epoch end and ``bench.py`` after its timed loop."""
+    bad = []
+    for (words, L, dev), f in _FLAGS.items():
+        n = stack_timeouts(f)
+        if n:
+            bad.append(f"L={L} on {dev}: {n} wait(s)")
+            if clear:
+                f[f.numel() - _CTL_WORDS].zero_()
+    if bad:
+        raise RuntimeError("pipelined LSTM hand-off timed out (results of the affected steps are invalid): "
+                           + "; ".join(bad) + ". Another process time-slicing the GPU, or MTA_LSTM_SPIN_LIMIT "
+                           "set too low, can cause this; MTA_LSTM_PIPELINE=0 selects the per-layer kernels.")
 
 
 class _LSTMPipelinedFn(torch.autograd.Function):
@@ -184,7 +213,7 @@ class _LSTMPipelinedFn(torch.autograd.Function):
                        for _ in range(1, L)]
         stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E
                  for _ in range(L)]
-        flags = _stack_flags(C, Np, dev)
+        flags = _stack_flags(C, Np, L, dev)
         C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
                          hseq, xdrop, stash, seeds, float(dropout), flags, N, Np, T)
         ctx.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
@@ -209,7 +238,7 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         flat = ctx.params
         dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
         dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
-        flags = _stack_flags(C, Np, dev)
+        flags = _stack_flags(C, Np, L, dev)
         inp = [x] + [xdrop[l - 1] if drop else hseq[l - 1] for l in range(1, L)]
         # weight gradients are computed by the same launch (fused workgroups consume dG as it drains) and
         # accumulated straight into the parameters' gradient views
@@ -218,11 +247,6 @@ class _LSTMPipelinedFn(torch.autograd.Function):
                          hseq, inp, grads, ctx.seeds, p, drop, flags, N, Np, T)
         ctx.bwd_flags = flags
         return (None,) * (6 + len(flat))
-
-
-def stack_timed_out(flags: Tensor) -> bool:
-    """True if a pipelined launch gave up waiting on a producer (diagnostic; host sync)."""
-    return bool(flags[flags.numel() - _CTL_WORDS].item() != 0)
 
 
 _PERM_CACHE = {}

@@ -1,0 +1,112 @@
+"""The product end to end on an MI355X: ``train.py`` (fit with sanity-val, graph-captured train/eval steps,
+ModelCheckpoint, plateau LR, test) -> checkpoint -> ``test.py`` figures, for the HIP path and for the
+reference-equivalent PyTorch path (MIOpen LSTM, ``+model.backend=torch``) on the same seed and data.
+
+Reference: `train.py:187-211` (fit, best/last checkpoint, test, hparams) and `test.py:199-210`."""
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+REPO = Path(__file__).resolve().parents[1]
+# 2,222 windows -> 1,555 / 444 / 223 train / val / test batches of one window
+DATA = ["datamodule.n_samples=200000", "seed=0"]
+COMMON = [*DATA, "loss=combined", "model.dropout=0", "+trainer.matmul_precision=highest", "trainer.max_epochs=3",
+          "trainer.enable_progress_bar=false"]
+
+
+def _run(args, cwd, timeout=300):
+    e = dict(os.environ)
+    e.pop("MTA_FAIL_AT_STEP", None)
+    r = subprocess.run([sys.executable, *args], cwd=cwd, env=e, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise AssertionError(f"{args} failed ({r.returncode}):\n{r.stdout[-4000:]}\n{r.stderr[-4000:]}")
+    return r.stdout
+
+
+def _scalars(vdir):
+    from masters_thesis_amd.utils.tfevents import read_scalars
+
+    ev = sorted(vdir.glob("events.out.tfevents.*"))
+    assert ev, vdir
+    return read_scalars(ev[0])
+
+
+def _final(out, what):
+    m = re.search(rf"Test {what}: ([0-9.eE+-]+)", out)
+    assert m, out[-2000:]
+    return float(m.group(1))
+
+
+@pytest.fixture(scope="module")
+def runs(tmp_path_factory):
+    d = tmp_path_factory.mktemp("gpu_e2e")
+    out = {}
+    for name, extra in (("hip", []), ("torch", ["+model.backend=torch"])):
+        out[name] = _run([str(REPO / "train.py"), *COMMON, *extra, f"logger.version={name}"], d)
+    return d, out
+
+
+def test_gpu_train_writes_reference_layout_and_tags(runs):
+    d, out = runs
+    vdir = d / "logs/FinancialLstm/synthetic/hip"
+    names = sorted(p.name for p in (vdir / "checkpoints").glob("*.ckpt"))
+    assert "last.ckpt" in names and any(n.startswith("best_epoch=") and "_val=" in n for n in names), names
+    ck = torch.load(vdir / "checkpoints/last.ckpt", weights_only=True, map_location="cpu")
+    assert ck["epoch"] == 2 and ck["global_step"] == 3 * 1555, (ck["epoch"], ck["global_step"])
+    assert all(torch.isfinite(v).all() for v in ck["state_dict"].values())
+    sc = _scalars(vdir)
+    for tag in ("loss/mse/train", "loss/nll/train", "loss/total/train", "loss/mse/val", "loss/nll/val",
+                "loss/total/val", "lr-Adam", "perf/step_ms_p50"):
+        assert tag in sc, (tag, sorted(sc))
+    assert len(sc["loss/total/train"]) == 3 and len(sc["loss/total/val"]) == 3
+    # training makes progress on the GPU
+    tr = [v for _, v in sc["loss/total/train"]]
+    assert tr[-1] < tr[0], tr
+    assert "cuda" in out["hip"] or "Test MAE" in out["hip"]
+
+
+def test_gpu_hip_matches_miopen_reference_path(runs):
+    """Same seed, same data order, dropout off, fp32 ("highest"): per-epoch losses of the HIP LSTM and of
+    the MIOpen LSTM (autograd) agree, as do the final test metrics."""
+    d, out = runs
+    a = _scalars(d / "logs/FinancialLstm/synthetic/hip")
+    b = _scalars(d / "logs/FinancialLstm/synthetic/torch")
+    for tag in ("loss/total/train", "loss/total/val", "loss/mse/val", "loss/nll/val"):
+        va = [v for _, v in a[tag]]
+        vb = [v for _, v in b[tag]]
+        assert len(va) == len(vb) == 3, tag
+        for x, y in zip(va, vb):
+            assert abs(x - y) <= 1e-3 * max(abs(y), 1e-6), (tag, va, vb)
+    for what in ("MAE", "NLL"):
+        x, y = _final(out["hip"], what), _final(out["torch"], what)
+        assert abs(x - y) <= 1e-3 * max(abs(y), 1e-6), (what, x, y)
+
+
+def test_gpu_plateau_halves_device_lr(tmp_path):
+    """ReduceLROnPlateau(patience=2, factor=0.5) on the GPU: a learning rate too small to move the val loss
+    past the threshold is halved after the third non-improving epoch and the device LR follows."""
+    _run([str(REPO / "train.py"), *DATA, "model.learning_rate=1e-7", "trainer.max_epochs=5",
+          "+trainer.limit_train_batches=5", "+trainer.limit_val_batches=50", "trainer.enable_progress_bar=false",
+          "logger.version=plateau"], tmp_path)
+    lrs = [v for _, v in _scalars(tmp_path / "logs/FinancialLstm/synthetic/plateau")["lr-Adam"]]
+    assert lrs[0] == pytest.approx(1e-7) and lrs[-1] == pytest.approx(5e-8), lrs
+
+
+def test_gpu_test_py_on_gpu_checkpoint(runs):
+    from masters_thesis_amd.utils.tfevents import read_tags
+
+    d, _ = runs
+    ck = "logs/FinancialLstm/synthetic/hip/checkpoints/last.ckpt"
+    _run([str(REPO / "test.py"), *DATA, "loss=combined", f"checkpoint={ck}", "+device=cuda"], d)
+    tags = set()
+    for ev in (d / "logs/FinancialLstm/synthetic/hip").rglob("events.out.tfevents.*"):
+        tags |= set(read_tags(ev))
+    for t in ("scatter/recon_residuals", "scatter/alphas", "scatter/betas", "hist/recon_residuals", "hist/alphas",
+              "hist/betas", "estimation/alpha", "estimation/beta"):
+        assert t in tags, (t, sorted(tags))

@@ -131,3 +131,73 @@ def test_pipelined_dropout_masks_match_counter_hash():
     with torch.no_grad():
         ev = op.lstm_last_hidden(x.to(DEV), wg, L, p, False, "highest", seeds)
     assert torch.equal(before, seeds) and not torch.allclose(ev, out)
+
+
+def _run_and_check(x, ws, L, prec="highest"):
+    from masters_thesis_amd.ops import lstm as op
+
+    N, H = x.shape[0], ws[1].shape[1]
+    R = torch.randn(N, H)
+    ref, w64 = _ref(x, ws, L)
+    (ref * R.double()).sum().backward()
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    out = op.lstm_last_hidden(x.to(DEV), wg, L, 0.0, True, prec)
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert (out.double().cpu() - ref.detach()).abs().max().item() < 1e-4
+    for a, b in zip(wg, w64):
+        assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-4 * max(b.grad.abs().max().item(), 1e-3)
+
+
+def test_flag_buffers_isolated_per_depth_across_epoch_window():
+    """a 4-layer stack must not poll progress words a 2-layer stack never wrote, even when
+    the shared epoch has advanced into [2^19, 2^20) (where a never-written 0 would read as 'reached')."""
+    from masters_thesis_amd.ops import lstm as op
+
+    torch.manual_seed(5)
+    N, T, F, H = 100, 20, 3, 64
+    x = torch.randn(N, T, F)
+    _run_and_check(x, _weights(F, H, 2, seed=1), 2)
+    Np = op.padded_rows(N)
+    keys = [k for k in op._FLAGS if k[1] == 2 and k[0] == op.lib().lstm_stack_flag_words(Np)]
+    assert keys
+    f = op._FLAGS[keys[0]]
+    ctl = f.numel() - op._CTL_WORDS
+    f[ctl + 32] = (1 << 19) + 1  # CTL_FWD_EPOCH
+    f[ctl + 96] = (1 << 19) + 1  # CTL_BWD_EPOCH
+    _run_and_check(x, _weights(F, H, 4, seed=2), 4)
+    op.check_pipeline_health()
+
+
+_TIMEOUT_SCRIPT = r"""
+import torch, sys
+sys.path.insert(0, {root!r})
+from masters_thesis_amd.ops import lstm as op
+x = torch.randn(100, 60, 3, device="cuda")
+ws = [torch.randn(s, device="cuda") * 0.1 for l in range(3)
+      for s in ((256, 3 if l == 0 else 64), (256, 64), (256,), (256,))]
+with torch.no_grad():
+    op.lstm_last_hidden(x, ws, 3, 0.0, False, "high")
+torch.cuda.synchronize()
+try:
+    op.check_pipeline_health()
+except RuntimeError as e:
+    print("RAISED", e)
+    op.check_pipeline_health()  # cleared by the first check
+    print("CLEARED")
+"""
+
+
+def test_handoff_timeout_is_reported_not_silent():
+    """A hand-off wait that gives up (spin bound forced to 1 poll) is counted and raised on the host."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = str(Path(__file__).resolve().parents[1])
+    env = dict(os.environ, MTA_LSTM_SPIN_LIMIT="1")
+    r = subprocess.run([sys.executable, "-c", _TIMEOUT_SCRIPT.format(root=root)], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "RAISED pipelined LSTM hand-off timed out" in r.stdout and "CLEARED" in r.stdout, r.stdout
