@@ -26,6 +26,38 @@
 #include "common.h"
 #include "lstm_wgrad.h"
 
+#ifndef MTA_STACK_STAMPS
+#define MTA_STACK_STAMPS 0
+#endif
+// Steps between issuing a hand-off store and draining it on the recurrent path (forward recurrent waves,
+// backward gradient waves).  1: drained at the top of the next step; 2: one step later (progress is then
+// published one step later too, the consumer layer lags one more step).
+#ifndef MTA_STACK_DRAIN_LAG
+#define MTA_STACK_DRAIN_LAG 1
+#endif
+#if MTA_STACK_STAMPS
+// Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
+// wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
+__device__ unsigned long long mta_stack_stamp_acc[2][2][8];
+#define SSTAMP_DECL unsigned long long _ts_prev = 0, _ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SSTAMP(k)                                                                  \
+  {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    const unsigned long long _n = __builtin_amdgcn_s_memtime();                    \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
+    if ((k) > 0) _ts_acc[(k)] += _n - _ts_prev;                                    \
+    _ts_prev = _n;                                                                 \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+  }
+#define SSTAMP_FLUSH(dir, role, first_wave)                                        \
+  if (blockIdx.x == 0 && (first_wave) && (threadIdx.x & 63) == 0)                  \
+    for (int _k = 0; _k < 8; ++_k) mta_stack_stamp_acc[(dir)][(role)][_k] = _ts_acc[_k];
+#else
+#define SSTAMP_DECL
+#define SSTAMP(k)
+#define SSTAMP_FLUSH(dir, role, first_wave)
+#endif
+
 namespace {
 
 constexpr int S = 16;
@@ -286,13 +318,19 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     compute_gx(0);
     if (T > 1) load_input(1);
     __syncthreads();  // pre-loop barrier: gx_0 ready
+    SSTAMP_DECL
     for (int t = 0; t < T; ++t) {
+      SSTAMP(0)
       if (t + 1 < T) {
         compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
+        SSTAMP(1)
         if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
+        SSTAMP(2)
       }
       __syncthreads();
+      SSTAMP(3)
     }
+    SSTAMP_FLUSH(0, 1, w == 0)
     __syncthreads();  // final barrier (the recurrent waves publish after it)
     return;
   }
@@ -365,7 +403,9 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     }
   };
 
+  SSTAMP_DECL
   for (int t = 0; t < T; ++t) {
+    SSTAMP(0)
     const int cur = t & 1;
     f32x4 acc[4];
 #pragma unroll
@@ -376,6 +416,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[2][i] = v.z;
       acc[3][i] = v.w;
     }
+    SSTAMP(1)
+#if MTA_STACK_DRAIN_LAG == 1
     // the hand-off stores issued at the previous top (a whole step ago)
     if (stash && t >= 2) mta_wait_vmcnt<STASH>();
     else mta_wait_vmem();
@@ -383,8 +425,26 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     // the barrier that ended step t-1
     if (!last && t >= 3 && threadIdx.x == 0)
       __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    // the hand-off stores issued two tops ago: the newer ones are the previous top's full step (hand-offs +
+    // stash) plus this older top's stash stores; the counts are immediates, so branch on the (uniform) layout
+    if (t >= 3) {
+      if (stash) {
+        if (xout) mta_wait_vmcnt<8 + 2 * STASH>();
+        else mta_wait_vmcnt<4 + 2 * STASH>();
+      } else {
+        if (xout) mta_wait_vmcnt<8>();
+        else mta_wait_vmcnt<4>();
+      }
+    }
+    // progress: hand-off stores of step t-4 were drained by every recurrent wave's wait at the top of t-1
+    if (!last && t >= 4 && threadIdx.x == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)(t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+    SSTAMP(2)
     if (t > 0) store_step(t - 1);
     __builtin_amdgcn_sched_barrier(0);
+    SSTAMP(3)
 
     if constexpr (PREC == PREC_F32) {
       const float* hrow = &h_f[cur][j][q * KF];
@@ -410,6 +470,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
       }
     }
+    SSTAMP(4)
 
     const int nb = (t + 1) & 1;
     float h[4];
@@ -436,8 +497,11 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
       }
     }
+    SSTAMP(5)
     __syncthreads();
+    SSTAMP(6)
   }
+  SSTAMP_FLUSH(0, 0, wave == 0)
   store_step(T - 1);
   mta_wait_vmem();
   __syncthreads();  // final barrier
@@ -606,26 +670,49 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       if (T > 1) load_dh(T - 2);
     }
     __syncthreads();  // B0
+    SSTAMP_DECL
     for (int t = T - 1; t >= 0; --t) {
       // ---- interval I(t) ----
+      SSTAMP(0)
+#if MTA_STACK_DRAIN_LAG == 1
       mta_wait_vmem();  // this wave's dH loads and its dx stores of the previous interval
+#else
+      // this wave's dH loads of the previous interval; they were issued before that interval's (at most 1)
+      // flag store and its 4 dx stores, so vmcnt(4) also drains every dx store of the interval before it
+      mta_wait_vmcnt<4>();
+#endif
+      SSTAMP(1)
+#if MTA_STACK_DRAIN_LAG == 1
       // progress: dx of steps >= t+3 (stored in I(t+2)) was drained by every gradient wave's wait in
       // I(t+1), before barrier A(t+1)
       if (!BOTTOM && t + 3 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
       // dG progress: every recurrent wave passed its top-of-(t+1) vmcnt wait before A(t+1), which drains
       // its dG stores of steps >= t+4
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if MTA_STACK_DRAIN_LAG == 1
       if (t + 1 <= T - 1) dx_step(t + 1);
+#endif
+      SSTAMP(2)
       if constexpr (!TOP) {
         if (t >= 1) {
           stage_dh(t - 1);
           if (t >= 2) load_dh(t - 2);
         }
       }
+#if MTA_STACK_DRAIN_LAG != 1
+      // progress: dx of steps >= t+4 (stored in I(t+3)) was drained by every gradient wave's wait in I(t+1)
+      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
+        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 <= T - 1) dx_step(t + 1);
+#endif
+      SSTAMP(3)
       __syncthreads();  // A(t)
+      SSTAMP(4)
     }
+    SSTAMP_FLUSH(1, 1, w == 0)
     dx_step(0);
     mta_wait_vmem();
     __syncthreads();  // F
@@ -690,15 +777,20 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   __syncthreads();  // B0 (dhs[(T-1)&1] staged)
 
   // one reverse step; returns false after step 0
+  SSTAMP_DECL
   auto step = [&](int t, float4 (&sb)[STASH], float4& cb) {
+    SSTAMP(0)
     float dho[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[t & 1][4 * q + i][u];
+    SSTAMP(1)
     if (t <= T - 2) mta_wait_vmcnt<10>();
     else mta_wait_vmcnt<6>();
+    SSTAMP(2)
     store_step(t < T - 1 ? t + 1 : t);  // unconditional (step T-1 stores its zero pdG to row T-1, which
                                         // step T-2 then overwrites in order): keeps the count exact
     __builtin_amdgcn_sched_barrier(0);
+    SSTAMP(3)
     const float4* st = sb;
     const float cpm = t > 0 ? 1.f : 0.f;
     const float cp4[4] = {cb.x * cpm, cb.y * cpm, cb.z * cpm, cb.w * cpm};
@@ -741,10 +833,13 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s4][rp]) = lo4;
       }
     }
+    SSTAMP(4)
     // prefetch step t-2 into this set (its values are dead now); unconditional, so the set needs no copy
     __builtin_amdgcn_sched_barrier(0);
     load_into(t >= 2 ? t - 2 : 0, sb, cb);
+    SSTAMP(5)
     __syncthreads();  // A(t): dG_t image visible to the gradient waves and to this step's dh product
+    SSTAMP(6)
     if (t == 0) return;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     if constexpr (PREC == PREC_F32) {
@@ -768,6 +863,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) dhr[i] = acc0[i] + acc1[i];
+    SSTAMP(7)
   };
   // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip (no
   // conditional step inside, so the sets keep their registers across the back-edge), odd T peels step 0
@@ -777,6 +873,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     step(t - 1, sB, cB);
   }
   if (t == 0) step(0, sA, cA);
+  SSTAMP_FLUSH(1, 0, wave == 0)
   store_step(0);
   mta_wait_vmem();
   __syncthreads();  // F

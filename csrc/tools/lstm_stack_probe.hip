@@ -1,0 +1,141 @@
+// Diagnostic probe (not part of the extension): times the layer-pipelined LSTM kernels of lstm_stack.hip
+// (forward, and backward with the fused weight gradients) on random data at the headline shape, and in a
+// -DMTA_STACK_STAMPS=1 build prints per-segment s_memtime cycles per step of block 0 for each wave role.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STACK_STAMPS=1] [-DMTA_STACK_DRAIN_LAG=2] \
+//         csrc/tools/lstm_stack_probe.hip -o build/lstm_stack_probe
+//   ./build/lstm_stack_probe [N=100] [L=2] [prec=1] [T=60]
+// Stamp builds are slower than the real kernel (each stamp waits lgkmcnt): read the SHARES there and the
+// absolute times from the stamp-free build.
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../lstm_stack.hip"
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);            \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+static float* dev_rand(size_t n, float scale) {
+  std::vector<float> h(n);
+  for (auto& v : h) v = scale * (2.f * rand() / RAND_MAX - 1.f);
+  float* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+static float* dev_zero(size_t n) {
+  float* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemset(d, 0, n * 4));
+  return d;
+}
+
+int main(int argc, char** argv) {
+  const int H = 64, FIN = 3;
+  const int N = argc > 1 ? atoi(argv[1]) : 100;
+  const int L = argc > 2 ? atoi(argv[2]) : 2;
+  const int prec = argc > 3 ? atoi(argv[3]) : PREC_BF16X3;
+  const int T = argc > 4 ? atoi(argv[4]) : 60;
+  const int Np = (N + 15) / 16 * 16;
+  if (L < 2 || L > 8 || N < 1 || T < 4 || T > 1000) {
+    printf("bad arguments\n");
+    return 1;
+  }
+  const float k = 0.125f;
+  float* x = dev_rand((size_t)N * T * FIN, 1.f);
+  std::vector<float*> wih(L), whh(L), bih(L), bhh(L), hseq(L), xdrop(L, nullptr), stash(L), dG(L), dX(L, nullptr),
+      inp(L), gwih(L), gwhh(L), gbih(L), gbhh(L);
+  for (int l = 0; l < L; ++l) {
+    const int fin = l == 0 ? FIN : H;
+    wih[l] = dev_rand((size_t)4 * H * fin, k);
+    whh[l] = dev_rand((size_t)4 * H * H, k);
+    bih[l] = dev_rand(4 * H, k);
+    bhh[l] = dev_rand(4 * H, k);
+    hseq[l] = dev_zero((size_t)T * Np * H);
+    if (l >= 1) xdrop[l] = dev_zero((size_t)T * Np * H);
+    if (l < L - 1) dX[l] = dev_zero((size_t)T * Np * H);
+    stash[l] = dev_zero((size_t)T * Np * 5 * H);
+    dG[l] = dev_zero((size_t)T * Np * 4 * H);
+    gwih[l] = dev_zero((size_t)4 * H * fin);
+    gwhh[l] = dev_zero((size_t)4 * H * H);
+    gbih[l] = dev_zero(4 * H);
+    gbhh[l] = dev_zero(4 * H);
+    inp[l] = l == 0 ? x : xdrop[l];
+  }
+  float* dh_last = dev_rand((size_t)N * H, 1.f);
+  uint64_t* seeds;
+  CK(hipMalloc(&seeds, 8 * sizeof(uint64_t)));
+  std::vector<uint64_t> hs(8);
+  for (int i = 0; i < 8; ++i) hs[i] = 0x1234567ull * (i + 1);
+  CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  unsigned* flags;
+  const long nflags = mta_lstm_stack_flag_words(Np);
+  CK(hipMalloc(&flags, nflags * 4));
+  CK(hipMemset(flags, 0, nflags * 4));
+
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const int reps = 200, skip = 20;
+  double ms_f = 0, ms_b = 0;
+  for (int rep = 0; rep < reps; ++rep) {
+    float m;
+    CK(hipEventRecord(a));
+    int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
+                                xdrop.data(), stash.data(), seeds, 0.2f, flags, N, Np, T, 0);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    if (rc) {
+      printf("fwd rc=%d\n", rc);
+      return 1;
+    }
+    CK(hipEventElapsedTime(&m, a, b));
+    if (rep >= skip) ms_f += m / (reps - skip);
+    CK(hipEventRecord(a));
+    rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
+                            hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(), seeds, 0.2f,
+                            1, flags, N, Np, T, 0);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    if (rc) {
+      printf("bwd rc=%d\n", rc);
+      return 1;
+    }
+    CK(hipEventElapsedTime(&m, a, b));
+    if (rep >= skip) ms_b += m / (reps - skip);
+  }
+  unsigned tmo = 0;
+  CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
+  printf("N=%d L=%d T=%d prec=%d drain_lag=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
+         "timeouts=%u\n",
+         N, L, T, prec, MTA_STACK_DRAIN_LAG, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         tmo);
+#if MTA_STACK_STAMPS
+  unsigned long long acc[2][2][8];
+  CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
+  const char* seg[2][2][8] = {
+      {{"", "gx_lds_read", "vmcnt_drain", "store_issue", "mfma_chain", "act+lds_write", "barrier", ""},
+       {"", "compute_gx", "load_input(poll)", "barrier", "", "", "", ""}},
+      {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
+        "mfma_dh"},
+       {"", "vmem_wait", "flags+dx(lag1)", "stage+load_dh(+dx lag2)", "barrier", "", "", ""}}};
+  const char* dir[2] = {"fwd", "bwd"};
+  const char* role[2][2] = {{"recurrent", "input"}, {"recurrent", "gradient"}};
+  for (int d = 0; d < 2; ++d)
+    for (int r = 0; r < 2; ++r) {
+      unsigned long long tot = 0;
+      for (int s = 1; s < 8; ++s) tot += acc[d][r][s];
+      printf("  %s %-9s cycles/step total=%6.0f :", dir[d], role[d][r], (double)tot / T);
+      for (int s = 1; s < 8; ++s)
+        if (seg[d][r][s][0]) printf(" %s=%.0f", seg[d][r][s], (double)acc[d][r][s] / T);
+      printf("\n");
+    }
+#endif
+  return 0;
+}

@@ -1,7 +1,7 @@
 """Training engine (Lightning-compatible loops, callbacks, checkpoints, HIP-graph step capture)."""
-from .callbacks import Callback, EarlyStopping, LearningRateMonitor, ModelCheckpoint, StepTimer
+from .callbacks import Callback, DeltaLossReporter, EarlyStopping, LearningRateMonitor, ModelCheckpoint, StepTimer
 from .module import LightningModule
 from .trainer import Trainer
 
-__all__ = ["Callback", "EarlyStopping", "LearningRateMonitor", "ModelCheckpoint", "StepTimer", "LightningModule",
+__all__ = ["Callback", "DeltaLossReporter", "EarlyStopping", "LearningRateMonitor", "ModelCheckpoint", "StepTimer", "LightningModule",
            "Trainer"]

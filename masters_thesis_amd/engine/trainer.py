@@ -310,6 +310,20 @@ class Trainer:
     def _eval_step(self, stage: str, loader, batch_idx: int, static: bool, batch=None):
         model = self.model
         fn = model.validation_step if stage == "val" else model.test_step
+        if not getattr(model, "eval_graph_capturable", True):
+            # MIOpen's inference LSTM initialises hipBLASLt state on first use, which is illegal while a
+            # stream is capturing: the reference-equivalent path evaluates eagerly
+            if static:
+                model._current_batch_size = loader.batch_size
+                pre, post = self._static_hooks(loader)
+                if pre is not None:
+                    pre()
+                out = fn(loader.gather_static(), batch_idx)
+                if post is not None:
+                    post()
+                return out
+            model._current_batch_size = _batch_size(batch)
+            return fn(batch, batch_idx)
         if static:
             B = loader.batch_size
             model._current_batch_size = B
@@ -597,6 +611,8 @@ class Trainer:
         test_metrics += [m for name, m in model.named_children() if isinstance(m, Metric) and name.startswith("test")]
         sync_metrics(test_metrics)
         model.on_test_end()
+        for c in self.callbacks:
+            c.on_test_end(self, model)
         res = {k: float(v) for k, v in self._compute_stage_metrics("test").items()}
         self._reset_stage_metrics("test")
         model._stage = "train"

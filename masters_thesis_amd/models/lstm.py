@@ -100,6 +100,10 @@ class FinancialLstm(LightningModule):
         self._hparams.update(dict(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers,
                                   dropout=dropout, learning_rate=learning_rate, weight_decay=weight_decay))
 
+    @property
+    def eval_graph_capturable(self) -> bool:
+        return self.backend != "torch"
+
     # ---- forward ---------------------------------------------------------------------
     def encode(self, x: Tensor) -> Tensor:
         return self.lstm.last_hidden(x, self.matmul_precision, self.backend)

@@ -105,3 +105,24 @@ def test_multirun_expands_and_runs_each_job(tmp_path):
     assert len(runs) == 2, runs
     for v in ("mse_small_lr0.001_fast", "mse_small_lr0.0001_fast"):
         assert (tmp_path / "logs/FinancialLstm/synthetic" / v / "checkpoints/last.ckpt").exists()
+
+
+def test_report_delta_and_best_ckpt(tmp_path):
+    """SURVEY Q10 (ΔL vs the OLS-on-future-window baseline, `tex/diplomski_rad.tex:1061-1084`) and Q9
+    (``test_ckpt=best`` tests the best-validation weights, `train.py:198` tests the last ones)."""
+    from masters_thesis_amd.utils.tfevents import read_scalars
+
+    r = _run([str(REPO / "train.py"), *TINY, "trainer.max_epochs=2", "loss=combined", "report_delta=true",
+              "test_ckpt=best", "logger.version=delta"], tmp_path)
+    assert "Testing best weights" in r.stdout and "Test ΔNLL" in r.stdout
+    vdir = tmp_path / "logs/FinancialLstm/synthetic/delta"
+    sc = read_scalars(sorted(vdir.glob("events.out.tfevents.*"))[0])
+    for tag in ("delta/total/train", "delta/mse/val", "delta/nll/val", "delta/total/val", "test/delta_mse",
+                "test/delta_nll"):
+        assert tag in sc, (tag, sorted(sc))
+    # ΔL = L(model) - L(OLS baseline): the implied baseline is non-negative and the same every epoch
+    base = [lv - dv for (_, lv), (_, dv) in zip(sc["loss/mse/val"], sc["delta/mse/val"])]
+    assert len(base) == 2 and base[0] >= 0 and abs(base[0] - base[1]) <= 1e-5 * max(base[0], 1e-12), base
+    bad = _run([str(REPO / "train.py"), *TINY, "trainer.max_epochs=1", "test_ckpt=worst", "logger.version=bad"],
+               tmp_path, ok=False)
+    assert bad.returncode != 0 and "test_ckpt" in (bad.stdout + bad.stderr)

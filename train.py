@@ -11,7 +11,9 @@
 MI355X additions (all optional): ``resume=<ckpt>`` (full state), ``init_from=<ckpt>``
 (weights only: the thesis' synthetic->real warm-up), ``seed=<int>``,
 ``+trainer.use_hip_graphs=false``, ``+trainer.matmul_precision=highest|high|medium``,
-``trainer.precision=bf16-mixed``, ``hydra/launcher=gpu_pool`` (one trial per GPU).
+``trainer.precision=bf16-mixed``, ``hydra/launcher=gpu_pool`` (one trial per GPU),
+``test_ckpt=best`` (test the best-validation weights instead of the last ones),
+``report_delta=true`` (log ΔL = model loss minus the OLS-on-future-window loss).
 """
 from __future__ import annotations
 
@@ -22,7 +24,7 @@ import torch
 
 from masters_thesis_amd.config import OmegaConf, main as config_main, register_default_resolvers
 from masters_thesis_amd.data import FinancialLstmDataModule
-from masters_thesis_amd.engine import LearningRateMonitor, ModelCheckpoint, Trainer, EarlyStopping
+from masters_thesis_amd.engine import DeltaLossReporter, EarlyStopping, LearningRateMonitor, ModelCheckpoint, Trainer
 from masters_thesis_amd.engine.checkpoint import load_checkpoint
 from masters_thesis_amd.models import get_model_class, model_params_from_config
 from masters_thesis_amd.utils.logger import TensorBoardLogger
@@ -94,6 +96,10 @@ def main(cfg):
                         monitor="loss/total/val", mode="min", save_last=True, auto_insert_metric_name=False),
         LearningRateMonitor(logging_interval="epoch", log_momentum=False),
     ]
+    delta = None
+    if cfg.get("report_delta"):
+        delta = DeltaLossReporter()
+        callbacks.append(delta)
     if cfg.trainer.get("early_stopping_patience"):
         callbacks.append(EarlyStopping(monitor="loss/total/val", patience=int(cfg.trainer.early_stopping_patience)))
 
@@ -113,7 +119,13 @@ def main(cfg):
     print(f"Best validation loss: {float(best) if best is not None else float('nan'):.6f}")
     print("=" * 50 + "\n")
 
-    # ==================== Test (current weights, like the reference: SURVEY Q9) ====================
+    # ==================== Test (last weights like the reference, or the best ones: SURVEY Q9) ==========
+    test_ckpt = str(cfg.get("test_ckpt") or "last")
+    if test_ckpt not in ("best", "last"):
+        raise ValueError(f"test_ckpt must be 'best' or 'last', got {test_ckpt!r}")
+    if test_ckpt == "best" and ckpt_cb.best_model_path:
+        model.load_state_dict(load_checkpoint(ckpt_cb.best_model_path, map_location="cpu")["state_dict"])
+        print(f"Testing best weights: {ckpt_cb.best_model_path}")
     trainer.test(model, datamodule=dm)
 
     config_dict = OmegaConf.to_container(cfg, resolve=True)
@@ -124,6 +136,7 @@ def main(cfg):
             "test/mae": model.test_results["test_loss"]["mae"],
             "test/nll": model.test_results["test_loss"]["nll"],
             "test/best_val_loss": float(best) if best is not None else float("nan"),
+            **({k: v for k, v in delta.last.items() if k.startswith("test/")} if delta is not None else {}),
         },
     )
     tb_logger.close()
@@ -133,6 +146,9 @@ def main(cfg):
     print("=" * 50)
     print(f"Test MAE: {model.test_results['test_loss']['mae']:.6f}")
     print(f"Test NLL: {model.test_results['test_loss']['nll']:.6f}")
+    if delta is not None:
+        print(f"Test ΔMSE: {delta.last.get('test/delta_mse', float('nan')):.6f}")
+        print(f"Test ΔNLL: {delta.last.get('test/delta_nll', float('nan')):.6f}")
     print("=" * 50 + "\n")
     return float(best) if best is not None else None
 
