@@ -31,8 +31,12 @@ import torch
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-REFERENCE_SAMPLES_PER_S = 59.0  # reference-equivalent replica, model=small, loss=mse, B=1
-# BASELINE.md yardstick rows (model, loss, per-GPU batch) -> samples/s; other configs have no yardstick
+# vs_baseline: the same-node reference-equivalent PyTorch path (``--backend torch --no-graphs``: nn.LSTM on
+# MIOpen + autograd, eager, 1 MI355X), measured by this bench (profiles/r2_bench_same_node_torch_vs_hip.jsonl);
+# samples/s per GPU keyed (model, loss, per-GPU batch).  Weak scaling: the baseline of N GPUs is N x this.
+SAME_NODE_TORCH_EAGER = {("small", "mse", 1): 169.863, ("medium", "mse", 1): 85.333, ("large", "mse", 1): 44.098,
+                         ("small", "mse", 8): 2047.487, ("small", "mse", 64): 4144.375}
+# the 8-vCPU CPU replica of the reference step (BASELINE.md yardstick rows); reported as vs_cpu_yardstick
 YARDSTICK = {("small", "mse", 1): 59.0, ("small", "nll", 1): 58.0, ("small", "combined", 1): 59.0,
              ("medium", "mse", 1): 21.0, ("large", "mse", 1): 14.0, ("small", "mse", 8): 65.0,
              ("small", "mse", 64): 68.0}
@@ -88,6 +92,8 @@ def main(argv=None):
 
     ModelClass = get_model_class(cfg.loss.module_class, cfg.model.get("arch", "lstm"))
     model = ModelClass(**model_params_from_config(cfg))
+    if args.backend == "torch":
+        model.allow_torch_capture = not args.no_graphs  # eager warm-up first: measured capture-safe here
     trainer = Trainer(max_epochs=1, gradient_clip_val=cfg.trainer.gradient_clip_val, precision=cfg.trainer.precision,
                       enable_progress_bar=False, enable_model_summary=False, logger=None, callbacks=[],
                       use_hip_graphs=not args.no_graphs, matmul_precision=args.matmul_precision)
@@ -130,6 +136,7 @@ def main(argv=None):
     value = args.batch * world * args.steps / elapsed
     nonfinite = float(trainer.optimizer.nonfinite.item())
     trainer._check_device_health()  # raises if a pipelined hand-off gave up (garbage steps)
+    key = (args.model, args.loss, args.batch)
     if denv.rank == 0:
         log(f"[bench] p50 step {p50:.3f} ms, mean {ms_per_step:.3f} ms, graphs={'on' if trainer._graphs else 'off'}, "
             f"nonfinite={nonfinite}, static_batches={trainer._static_ok(loader)}")
@@ -145,8 +152,10 @@ def main(argv=None):
             "p90_step_ms": round(p90, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(value / YARDSTICK[(args.model, args.loss, args.batch)], 3)
-                            if (args.model, args.loss, args.batch) in YARDSTICK else None),
+            "vs_baseline": (round(value / (world * SAME_NODE_TORCH_EAGER[key]), 3)
+                            if key in SAME_NODE_TORCH_EAGER and args.backend == "auto" else None),
+            "baseline": "same-node PyTorch-ROCm reference path (MIOpen nn.LSTM, autograd, eager), x n_gpus",
+            "vs_cpu_yardstick": (round(value / YARDSTICK[key], 3) if key in YARDSTICK else None),
             "dtype": ("bf16" if (cfg.model.get("arch", "lstm") != "lstm" and dev.type == "cuda")
                       or cfg.trainer.precision != "32-true" else "fp32"),
             "data": "synthetic (reference DGP, generated on device), random-init weights",
@@ -162,7 +171,7 @@ def main(argv=None):
                 "trainer": args.trainer,
                 "precision": cfg.trainer.precision,
                 "matmul_precision": args.matmul_precision,
-                "backend": "hip" if args.backend == "auto" else "torch-eager",
+                "backend": "hip" if args.backend == "auto" else "torch-miopen",
                 "hip_graphs": not args.no_graphs,
             },
         }

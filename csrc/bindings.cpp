@@ -31,6 +31,10 @@ void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g
                           float* dab, float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st);
 int mta_optim_num_partials(long n);
 void mta_grad_sqnorm(const float* g, long n, float scale, float* partials, float* step, hipStream_t st);
+int mta_adam_fused_partials();
+void mta_adam_fused(float* p, float* g, float* m, float* v, long n, float* partials, unsigned long long* ticket,
+                    const float* lr, float* step, float beta1, float beta2, float eps, float wd, float max_norm,
+                    float scale, int adamw, int zero_grad, float* norm_out, float* nonfinite, hipStream_t st);
 void mta_adam(float* p, float* g, float* m, float* v, long n, const float* partials, const float* lr,
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
               float* norm_out, float* nonfinite, hipStream_t st);
@@ -51,13 +55,13 @@ int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* d
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
-                       float* const* hseq, float* const* xdrop, float* const* stash, const uint64_t* seeds,
-                       float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
+                       float* const* hseq, float* const* xdrop, uint8_t* const* mask, float* const* stash,
+                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
-                       float* const* g_bih, float* const* g_bhh, uint64_t* seeds, float drop_p, int dropout,
-                       unsigned* flags, int N, int Np, int T, hipStream_t st);
+                       float* const* g_bih, float* const* g_bhh, const uint8_t* const* mask, uint64_t* seeds,
+                       float drop_p, int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
@@ -314,6 +318,32 @@ void adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor par
            cur_stream());
 }
 
+int64_t adam_fused_partials() { return mta_adam_fused_partials(); }
+
+// one launch: grad norm + clip + Adam/AdamW (+ grad zeroing); ticket is an int64[1] zero-initialised once
+void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor partials, at::Tensor ticket,
+                at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd, double max_norm,
+                double scale, bool adamw, bool zero_grad, const OptT& norm_out, const OptT& nonfinite) {
+  MTA_CHECK_F32(p);
+  MTA_CHECK_F32(g);
+  MTA_CHECK_F32(m);
+  MTA_CHECK_F32(v);
+  MTA_CHECK_F32(partials);
+  MTA_CHECK_F32(lr);
+  MTA_CHECK_F32(step);
+  TORCH_CHECK(ticket.is_cuda() && ticket.scalar_type() == at::kLong && ticket.numel() >= 1, "ticket: int64[1]");
+  TORCH_CHECK(partials.numel() >= mta_adam_fused_partials(), "partials too small");
+  TORCH_CHECK(!has(nonfinite) || nonfinite->numel() >= 2, "nonfinite needs 2 floats");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "flat buffer size mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  mta_adam_fused(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (long)n,
+                 partials.data_ptr<float>(), reinterpret_cast<unsigned long long*>(ticket.data_ptr<int64_t>()),
+                 lr.data_ptr<float>(), step.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps, (float)wd,
+                 (float)max_norm, (float)scale, adamw ? 1 : 0, zero_grad ? 1 : 0, opt_mut(norm_out),
+                 opt_mut(nonfinite), cur_stream());
+}
+
 void scale_(at::Tensor x, double s) {
   MTA_CHECK_F32(x);
   TORCH_CHECK(x.numel() % 4 == 0, "flat buffers must be padded to a multiple of 4");
@@ -472,8 +502,9 @@ int64_t lstm_stack_flag_words(int64_t Np) { return mta_lstm_stack_flag_words((in
 
 void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
                     std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
-                    std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> stash,
-                    at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
+                    std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
+                    std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N,
+                    int64_t Np, int64_t T) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(x);
   TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
@@ -483,6 +514,10 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
     TORCH_CHECK(w_hh[l].numel() == 4 * H * H && w_ih[l].numel() == 4 * H * (l == 0 ? fin : H), "weight shapes");
     TORCH_CHECK(hseq[l].numel() == T * Np * H, "hseq shape");
     if (xdrop[l].numel()) TORCH_CHECK(l > 0 && xdrop[l].numel() == T * Np * H, "xdrop shape");
+    TORCH_CHECK(masks.size() == (size_t)L, "per-layer keep-byte list");
+    if (xdrop[l].numel())
+      TORCH_CHECK(masks[l].is_cuda() && masks[l].scalar_type() == at::kByte && masks[l].numel() == T * Np * H,
+                  "keep bytes: uint8 (T, Np, H) per dropout layer");
     if (stash[l].numel()) TORCH_CHECK(stash[l].numel() == T * Np * 5 * H, "stash shape");
   }
   TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= L, "seeds: int64[L]");
@@ -493,9 +528,12 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
        sh = ptrs_f32(stash, "stash");
   std::vector<const float*> cwi(wi.begin(), wi.end()), cwh(wh.begin(), wh.end()), cbi(bi.begin(), bi.end()),
       cbh(bh.begin(), bh.end());
+  std::vector<uint8_t*> mk(L, nullptr);
+  for (int64_t l = 0; l < L; ++l)
+    if (xdrop[l].numel()) mk[l] = masks[l].data_ptr<uint8_t>();
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int rc = mta_lstm_stack_fwd((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(), cwh.data(),
-                                    cbi.data(), cbh.data(), hs.data(), xd.data(), sh.data(),
+                                    cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
                                     reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
                                     reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
                                     cur_stream());
@@ -507,8 +545,8 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
 void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor> stash, std::vector<at::Tensor> w_hh,
                     std::vector<at::Tensor> w_ih, at::Tensor dh_last, std::vector<at::Tensor> dG,
                     std::vector<at::Tensor> dX, std::vector<at::Tensor> hseq, std::vector<at::Tensor> inp,
-                    std::vector<std::vector<at::Tensor>> grads, at::Tensor seeds, double drop_p, bool dropout,
-                    at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
+                    std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks, at::Tensor seeds,
+                    double drop_p, bool dropout, at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
@@ -546,11 +584,20 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
   }
   std::vector<const float*> cst(st.begin(), st.end()), cwh(wh.begin(), wh.end()), cwi(wi.begin(), wi.end()),
       chs(hs.begin(), hs.end()), cin(in.begin(), in.end());
+  std::vector<const uint8_t*> mk(L, nullptr);
+  if (dropout) {
+    TORCH_CHECK(masks.size() == (size_t)L, "per-layer keep-byte list");
+    for (int64_t l = 1; l < L; ++l) {
+      TORCH_CHECK(masks[l].is_cuda() && masks[l].scalar_type() == at::kByte && masks[l].numel() == T * Np * H,
+                  "keep bytes: uint8 (T, Np, H) per dropout layer");
+      mk[l] = masks[l].data_ptr<uint8_t>();
+    }
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dh_last.device());
   const int rc = mta_lstm_stack_bwd(
       (int)H, (int)prec, (int)L, (int)fin, cst.data(), cwh.data(), cwi.data(), dh_last.data_ptr<float>(), dg.data(),
       dx.data(), fused ? chs.data() : nullptr, fused ? cin.data() : nullptr, fused ? g0.data() : nullptr,
-      fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr,
+      fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr, mk.data(),
       reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p, dropout ? 1 : 0,
       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
@@ -681,6 +728,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_num_partials", &optim_num_partials);
   m.def("grad_sqnorm", &grad_sqnorm);
   m.def("adam", &adam);
+  m.def("adam_fused_partials", &adam_fused_partials);
+  m.def("adam_fused", &adam_fused);
   m.def("scale_", &scale_);
   m.attr("ARCH") = "gfx950";
 }

@@ -29,12 +29,6 @@
 #ifndef MTA_STACK_STAMPS
 #define MTA_STACK_STAMPS 0
 #endif
-// Steps between issuing a hand-off store and draining it on the recurrent path (forward recurrent waves,
-// backward gradient waves).  1: drained at the top of the next step; 2: one step later (progress is then
-// published one step later too, the consumer layer lags one more step).
-#ifndef MTA_STACK_DRAIN_LAG
-#define MTA_STACK_DRAIN_LAG 1
-#endif
 #if MTA_STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
@@ -147,6 +141,7 @@ struct StackFwdArgs {
   const float* b_hh[MAXL];
   float* hseq[MAXL];    // (T, Np, H) outputs of every layer
   float* xdrop[MAXL];   // xdrop[l] (l >= 1): dropout(h^{(l-1)}), the input of layer l (null: no dropout)
+  uint8_t* mask[MAXL];  // mask[l] (l >= 1, with xdrop): keep bytes of that dropout, (T, Np, H), for the backward
   float* stash[MAXL];   // BPTT stash per layer (null: inference)
   const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
   float drop_p;
@@ -157,20 +152,39 @@ struct StackFwdArgs {
   int N, Np, T, L, ntiles, tr8;
 };
 
-// Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
-// (W_hh in VGPRs, h through LDS, one barrier per step); waves [H/16, 2 H/16) are INPUT waves: one step
-// ahead they wait for / load the layer input and compute the gate pre-activations
-// gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products for layer 0, MFMA for layers >= 1) into a
-// double-buffered LDS slot, so the recurrent critical path never sees the hand-off latency, the progress
-// polls or the input product.  Both roles execute the same barriers (pre-loop, one per step, final).
+// Forward workgroup = 2 x (H/16) waves.
+//  * RECURRENT waves [0, H/16): the recurrence (W_hh in VGPRs, h through LDS, one barrier per step) and
+//    NOTHING else: no vector-memory instruction in the loop.  Step t's outputs (f32 h_t and the BPTT stash
+//    fragments) go to a double-buffered LDS slot.
+//  * INPUT waves [H/16, 2 H/16), one step ahead / one step behind the recurrence in the same interval:
+//    wait for / load the layer input and compute gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products
+//    for layer 0, MFMA for layers >= 1) into a double-buffered LDS slot; then drain step t-1's outputs from
+//    LDS to global memory: hseq and the dropout-masked hand-off (16-byte write-through stores of one
+//    sequence row per lane), the dropout keep bytes, the stash (the recurrent lanes' fragment order) and
+//    the progress word.  The counter-hash dropout masks are computed here, off the recurrent path
+//    (measured: the hash's 32-bit multiplies plus the stores were ~40 % of a recurrent step, r2 probe).
+//  Both roles execute the same barriers (pre-loop, one per step, final).
 template <int H, int PREC>
 struct FwdSmem {
-  static constexpr int ROWB = H + 8, ROWF = H + 4;
+  static constexpr int ROWB = H + 8, ROWF = H + 4, NW = H / 16;
   float4 gxs[2][S][H];  // gate pre-activations (i, f, g, o) per (sequence, unit)
   __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+  float hout[2][S][ROWF];       // f32 h_t, row-major (sequence, unit): the input waves' store image
+  float4 sto[2][NW][STASH][64]; // stash fragments of step t per recurrent wave / lane
 };
+
+// vmcnt(n) for a runtime-uniform n from a small set (the count must be an immediate)
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  if (n >= 8) mta_wait_vmcnt<8>();
+  else if (n >= 7) mta_wait_vmcnt<7>();
+  else if (n >= 6) mta_wait_vmcnt<6>();
+  else if (n >= 3) mta_wait_vmcnt<3>();
+  else if (n >= 2) mta_wait_vmcnt<2>();
+  else if (n >= 1) mta_wait_vmcnt<1>();
+  else mta_wait_vmem();
+}
 
 template <int H, int PREC, int FIN0, bool FIRST>
 __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
@@ -205,6 +219,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     const float* w_ih = a.w_ih[layer];
     const float* xin = FIRST ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
     unsigned* in_flag = a.flags + FLAG_STRIDE * (FIRST ? 0 : (layer - 1) * a.tr8 + tile);
+    unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     constexpr int XKB = FIRST ? 1 : KB, XKF = FIRST ? 1 : KF;
     bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][PREC == PREC_BF16X3 ? XKB : 1];
     float Xf[4][PREC == PREC_F32 ? XKF : 1];
@@ -252,8 +267,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           for (int f = 0; f < FIN0; ++f) xin0[i][f] = xs[f];
         }
       } else {
-        // poll only when the last value seen does not cover step t (polling every step from every
-        // consumer wave measured slower: the progress words share cache lines across tiles)
+        // poll only when the last value seen does not cover step t
         seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
         const size_t row = (size_t)t * Np + n0 + j;
 #pragma unroll
@@ -314,6 +328,44 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 #pragma unroll
       for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
     };
+
+    // ---- output drain: step t's outputs from the LDS slot (t & 1) to global memory ----
+    float* hseq = a.hseq[layer];
+    float* xout = last ? nullptr : a.xdrop[layer + 1];
+    uint8_t* mout = last ? nullptr : a.mask[layer + 1];
+    const uint64_t seed_next = xout ? a.seeds[layer + 1] : 0;
+    float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
+    const float keep_scale = 1.0f / (1.0f - a.drop_p);
+    // one sequence row chunk per lane: 4 H float4 per step = NW x 64 lanes
+    const int gl = w * 64 + lane, srow = gl / (H / 4), scol = 4 * (gl % (H / 4));
+    // vector-memory ops each drain issues (counted waits below)
+    const int nst = 1 + (xout ? 1 : 0) + (mout ? 1 : 0) + (stash ? STASH : 0);
+    auto store_outputs = [&](int t) {
+      const int p = t & 1;
+      const float4 hv = *reinterpret_cast<const float4*>(&sm.hout[p][srow][scol]);
+      const size_t row = (size_t)t * Np + n0 + srow;
+      if (last) *reinterpret_cast<float4*>(hseq + row * H + scol) = hv;  // read after the kernel
+      else store_sc1_x4(hseq + row * H + scol, f32x4{hv.x, hv.y, hv.z, hv.w});
+      if (xout) {
+        float sc[4];
+        uint32_t kb = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float m = mta_dropout_scale(seed_next, (uint32_t)row, (uint32_t)(scol + e), a.drop_p);
+          sc[e] = m;
+          kb |= (m != 0.f ? 1u : 0u) << (8 * e);
+        }
+        store_sc1_x4(xout + row * H + scol, f32x4{hv.x * sc[0], hv.y * sc[1], hv.z * sc[2], hv.w * sc[3]});
+        if (mout) *reinterpret_cast<uint32_t*>(mout + row * H + scol) = kb;
+      }
+      if (stash) {
+        float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
+#pragma unroll
+        for (int k = 0; k < STASH; ++k) st[64 * k] = sm.sto[p][w][k][lane];
+      }
+    };
+    (void)keep_scale;
+
     load_input(0);
     compute_gx(0);
     if (T > 1) load_input(1);
@@ -321,27 +373,34 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     SSTAMP_DECL
     for (int t = 0; t < T; ++t) {
       SSTAMP(0)
-      if (t + 1 < T) {
-        compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
-        SSTAMP(1)
-        if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
-        SSTAMP(2)
-      }
-      __syncthreads();
+      // interval t: the recurrence runs step t.  Per interval the issue order is [progress word, input loads,
+      // output stores]; waiting for the previous interval's input loads (vmcnt = its store count) therefore
+      // also drains every store of the interval before it: step t-3's outputs, drained by every input wave
+      // here, before barrier t, are published at the top of interval t+1 (as steps <= t-3 at the top of t).
+      if (t >= 1) wait_vmcnt_le(nst);
+      if (!last && t >= 3 && w == 0 && lane == 0)
+        __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t + 1 < T) compute_gx((t + 1) & 1);  // x_{t+1} arrived during interval t-1
+      SSTAMP(1)
+      if (t + 2 < T) load_input(t + 2);         // (waits for the producer here, off the recurrent path)
+      SSTAMP(2)
+      if (t >= 1) store_outputs(t - 1);         // slot (t-1)&1 was filled by the recurrence before barrier t-1
       SSTAMP(3)
+      __syncthreads();
+      SSTAMP(4)
     }
     SSTAMP_FLUSH(0, 1, w == 0)
-    __syncthreads();  // final barrier (the recurrent waves publish after it)
+    store_outputs(T - 1);
+    mta_wait_vmem();
+    __syncthreads();  // final barrier
+    if (!last && w == 0 && lane == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
 
   // =========================== recurrent waves ===========================
   const float* w_hh = a.w_hh[layer];
-  float* hseq = a.hseq[layer];
-  float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
-  float* xout = last ? nullptr : a.xdrop[layer + 1];
-  const uint64_t seed_next = xout ? a.seeds[layer + 1] : 0;
-  unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+  const bool keep_stash = a.stash[layer] != nullptr;
 
   bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
   float Bf[4][PREC == PREC_F32 ? KF : 1];
@@ -373,36 +432,6 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   __syncthreads();  // pre-loop barrier
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
-  f32x4 pgi, pgf, pgg, pgo, pcc;
-  float ph[4];
-  // issue order per step: hand-off stores, then the 5 stash stores; the loop-head vmcnt(STASH) then drains
-  // the previous step's hand-offs (in-order completion) and leaves its stash stores another step
-  auto store_step = [&](int t) {
-    if (xout) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const size_t o = ((size_t)t * Np + n0 + 4 * q + i) * H + u;
-        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-        store_sc1(xout + o, ph[i] * mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p));
-      }
-    }
-    if (last) {  // consumed after the kernel (heads, weight gradients): plain stores
-#pragma unroll
-      for (int i = 0; i < 4; ++i) hseq[((size_t)t * Np + n0 + 4 * q + i) * H + u] = ph[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) store_sc1(hseq + ((size_t)t * Np + n0 + 4 * q + i) * H + u, ph[i]);
-    }
-    if (stash) {
-      float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
-      st[0] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
-      st[64] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
-      st[128] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
-      st[192] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
-      st[256] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
-    }
-  };
-
   SSTAMP_DECL
   for (int t = 0; t < T; ++t) {
     SSTAMP(0)
@@ -417,34 +446,6 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[3][i] = v.w;
     }
     SSTAMP(1)
-#if MTA_STACK_DRAIN_LAG == 1
-    // the hand-off stores issued at the previous top (a whole step ago)
-    if (stash && t >= 2) mta_wait_vmcnt<STASH>();
-    else mta_wait_vmem();
-    // progress: hand-off stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
-    // the barrier that ended step t-1
-    if (!last && t >= 3 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    // the hand-off stores issued two tops ago: the newer ones are the previous top's full step (hand-offs +
-    // stash) plus this older top's stash stores; the counts are immediates, so branch on the (uniform) layout
-    if (t >= 3) {
-      if (stash) {
-        if (xout) mta_wait_vmcnt<8 + 2 * STASH>();
-        else mta_wait_vmcnt<4 + 2 * STASH>();
-      } else {
-        if (xout) mta_wait_vmcnt<8>();
-        else mta_wait_vmcnt<4>();
-      }
-    }
-    // progress: hand-off stores of step t-4 were drained by every recurrent wave's wait at the top of t-1
-    if (!last && t >= 4 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-    SSTAMP(2)
-    if (t > 0) store_step(t - 1);
-    __builtin_amdgcn_sched_barrier(0);
-    SSTAMP(3)
 
     if constexpr (PREC == PREC_F32) {
       const float* hrow = &h_f[cur][j][q * KF];
@@ -470,10 +471,11 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
       }
     }
-    SSTAMP(4)
+    SSTAMP(2)
 
     const int nb = (t + 1) & 1;
     float h[4];
+    f32x4 pgi, pgf, pgg, pgo, pcc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       pgi[i] = mta_sigmoid(acc[0][i]);
@@ -483,8 +485,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
       pcc[i] = c[i];
       h[i] = pgo[i] * mta_tanh(c[i]);
-      ph[i] = h[i];
     }
+    SSTAMP(3)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s4 = 4 * q + i;
@@ -496,17 +498,21 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         h_hi[nb][s4][u] = hi;
         if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
       }
+      sm.hout[cur][s4][u] = h[i];
     }
-    SSTAMP(5)
+    if (keep_stash) {
+      sm.sto[cur][w][0][lane] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
+      sm.sto[cur][w][1][lane] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      sm.sto[cur][w][2][lane] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      sm.sto[cur][w][3][lane] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      sm.sto[cur][w][4][lane] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+    }
+    SSTAMP(4)
     __syncthreads();
-    SSTAMP(6)
+    SSTAMP(5)
   }
   SSTAMP_FLUSH(0, 0, wave == 0)
-  store_step(T - 1);
-  mta_wait_vmem();
-  __syncthreads();  // final barrier
-  if (!last && threadIdx.x == 0)
-    __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();  // final barrier (the input waves drain step T-1 and publish after it)
 }
 
 template <int H, int PREC, int FIN0>
@@ -539,6 +545,7 @@ struct StackBwdArgs {
   const float* dh_last;   // (N, H): gradient wrt h_{T-1} of the top layer
   float* dG[MAXL];        // (T, Np, 4H) per layer, unit-major columns
   float* dX[MAXL];        // dX[l] (l < L-1): gradient wrt layer l's output sequence, written by layer l+1
+  const uint8_t* mask[MAXL];  // mask[l] (l >= 1, dropout): keep bytes of layer l's input dropout (forward)
   uint64_t* seeds;        // [MAXL]: dropout seed of layer l's input (advanced by the launch's last workgroup)
   float drop_p;
   int dropout;
@@ -593,7 +600,8 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     // =========================== gradient waves ===========================
     const float* dH = TOP ? nullptr : a.dX[layer];
     float* dXout = BOTTOM ? nullptr : a.dX[layer - 1];
-    const uint64_t seed_in = (!BOTTOM && a.dropout) ? a.seeds[layer] : 0;
+    const uint8_t* min = (!BOTTOM && a.dropout) ? a.mask[layer] : nullptr;
+    const float keep_scale = 1.0f / (1.0f - a.drop_p);
     unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
     unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
@@ -628,6 +636,15 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
+    uint32_t mreg[4] = {1u, 1u, 1u, 1u};
+    auto load_mask = [&](int t) {  // keep bytes of step t (rows 4q+i, unit u) for dx_step(t), one interval ahead
+      if constexpr (!BOTTOM) {
+        if (min) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mreg[i] = min[((size_t)t * Np + n0 + 4 * q + i) * H + u];
+        }
+      }
+    };
     auto stage_dh = [&](int t) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = dreg[i];
@@ -635,31 +652,29 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     auto dx_step = [&](int t) {  // dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
       if constexpr (!BOTTOM) {
         const int buf = t & 1;
-        f32x4 ax0 = {0.f, 0.f, 0.f, 0.f}, ax1 = {0.f, 0.f, 0.f, 0.f};
+        // four independent accumulation chains (even / odd k-blocks x hi / cross terms)
+        f32x4 ax[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
         if constexpr (PREC == PREC_F32) {
           const float* arow = &g_f[buf][j][q * KF];
 #pragma unroll
-          for (int kk = 0; kk < KF; kk += 2) {
-            ax0 = mfma16x16x4f32(arow[kk], Xf[kk], ax0);
-            ax1 = mfma16x16x4f32(arow[kk + 1], Xf[kk + 1], ax1);
-          }
+          for (int kk = 0; kk < KF; ++kk) ax[kk & 3] = mfma16x16x4f32(arow[kk], Xf[kk], ax[kk & 3]);
         } else {
 #pragma unroll
           for (int kb = 0; kb < KB; ++kb) {
             const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
             if constexpr (PREC == PREC_BF16X3) {
               const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
-              ax1 = mfma16x16x32(alo, Xhi[kb], ax1);
-              ax1 = mfma16x16x32(ahi, Xlo[kb], ax1);
+              ax[2 + (kb & 1)] = mfma16x16x32(alo, Xhi[kb], ax[2 + (kb & 1)]);
+              ax[2 + (kb & 1)] = mfma16x16x32(ahi, Xlo[kb], ax[2 + (kb & 1)]);
             }
-            ax0 = mfma16x16x32(ahi, Xhi[kb], ax0);
+            ax[kb & 1] = mfma16x16x32(ahi, Xhi[kb], ax[kb & 1]);
           }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-          float v = ax0[i] + ax1[i];
-          if (seed_in) v *= mta_dropout_scale(seed_in, row, (uint32_t)u, a.drop_p);
+          float v = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
+          if (min) v *= mreg[i] ? keep_scale : 0.f;
           store_sc1(dXout + (size_t)row * H + u, v);
         }
       }
@@ -669,32 +684,23 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       stage_dh(T - 1);
       if (T > 1) load_dh(T - 2);
     }
+    load_mask(T - 1);
     __syncthreads();  // B0
     SSTAMP_DECL
     for (int t = T - 1; t >= 0; --t) {
       // ---- interval I(t) ----
       SSTAMP(0)
-#if MTA_STACK_DRAIN_LAG == 1
-      mta_wait_vmem();  // this wave's dH loads and its dx stores of the previous interval
-#else
-      // this wave's dH loads of the previous interval; they were issued before that interval's (at most 1)
-      // flag store and its 4 dx stores, so vmcnt(4) also drains every dx store of the interval before it
-      mta_wait_vmcnt<4>();
-#endif
+      mta_wait_vmem();  // this wave's dH / keep-byte loads and its dx stores of the previous interval
       SSTAMP(1)
-#if MTA_STACK_DRAIN_LAG == 1
       // progress: dx of steps >= t+3 (stored in I(t+2)) was drained by every gradient wave's wait in
       // I(t+1), before barrier A(t+1)
       if (!BOTTOM && t + 3 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
       // dG progress: every recurrent wave passed its top-of-(t+1) vmcnt wait before A(t+1), which drains
       // its dG stores of steps >= t+4
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#if MTA_STACK_DRAIN_LAG == 1
       if (t + 1 <= T - 1) dx_step(t + 1);
-#endif
       SSTAMP(2)
       if constexpr (!TOP) {
         if (t >= 1) {
@@ -702,12 +708,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
           if (t >= 2) load_dh(t - 2);
         }
       }
-#if MTA_STACK_DRAIN_LAG != 1
-      // progress: dx of steps >= t+4 (stored in I(t+3)) was drained by every gradient wave's wait in I(t+1)
-      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
-        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1 <= T - 1) dx_step(t + 1);
-#endif
+      load_mask(t);  // for dx_step(t) in I(t-1)
       SSTAMP(3)
       __syncthreads();  // A(t)
       SSTAMP(4)
@@ -841,28 +842,27 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     __syncthreads();  // A(t): dG_t image visible to the gradient waves and to this step's dh product
     SSTAMP(6)
     if (t == 0) return;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // four independent accumulation chains (even / odd k-blocks x hi / cross terms): the dependent-MFMA
+    // latency, not issue, bounded the two-chain form (r2 stamp probe: 795 cycles for 24 MFMAs)
+    f32x4 ac[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     if constexpr (PREC == PREC_F32) {
       const float* arow = &g_f[buf][j][q * KF];
 #pragma unroll
-      for (int kk = 0; kk < KF; kk += 2) {
-        acc0 = mfma16x16x4f32(arow[kk], Bf[kk], acc0);
-        acc1 = mfma16x16x4f32(arow[kk + 1], Bf[kk + 1], acc1);
-      }
+      for (int kk = 0; kk < KF; ++kk) ac[kk & 3] = mfma16x16x4f32(arow[kk], Bf[kk], ac[kk & 3]);
     } else {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
         if constexpr (PREC == PREC_BF16X3) {
           const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
-          acc1 = mfma16x16x32(alo, Bhi[kb], acc1);
-          acc1 = mfma16x16x32(ahi, Blo[kb], acc1);
+          ac[2 + (kb & 1)] = mfma16x16x32(alo, Bhi[kb], ac[2 + (kb & 1)]);
+          ac[2 + (kb & 1)] = mfma16x16x32(ahi, Blo[kb], ac[2 + (kb & 1)]);
         }
-        acc0 = mfma16x16x32(ahi, Bhi[kb], acc0);
+        ac[kb & 1] = mfma16x16x32(ahi, Bhi[kb], ac[kb & 1]);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dhr[i] = acc0[i] + acc1[i];
+    for (int i = 0; i < 4; ++i) dhr[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
     SSTAMP(7)
   };
   // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip (no
@@ -970,9 +970,9 @@ extern "C" long mta_lstm_stack_flag_words(int Np) {
 
 extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                                   const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
-                                  float* const* hseq, float* const* xdrop, float* const* stash,
-                                  const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
-                                  hipStream_t st) {
+                                  float* const* hseq, float* const* xdrop, uint8_t* const* mask,
+                                  float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
+                                  int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
   StackFwdArgs a{};
   a.x = x;
@@ -983,6 +983,8 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
     a.b_hh[l] = b_hh[l];
     a.hseq[l] = hseq[l];
     a.xdrop[l] = xdrop ? xdrop[l] : nullptr;
+    a.mask[l] = mask ? mask[l] : nullptr;
+    if (a.xdrop[l] && !a.mask[l]) return -2;  // the backward reads the keep bytes
     a.stash[l] = stash ? stash[l] : nullptr;
   }
   a.seeds = seeds;
@@ -1007,8 +1009,9 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
 extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
-                                  float* const* g_whh, float* const* g_bih, float* const* g_bhh, uint64_t* seeds,
-                                  float drop_p, int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
+                                  float* const* g_whh, float* const* g_bih, float* const* g_bhh,
+                                  const uint8_t* const* mask, uint64_t* seeds, float drop_p, int dropout,
+                                  unsigned* flags, int N, int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T >= (1 << EPOCH_SHIFT)) return -1;
   StackBwdArgs a{};
   for (int l = 0; l < L; ++l) {
@@ -1017,6 +1020,8 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     a.w_ih[l] = w_ih[l];
     a.dG[l] = dG[l];
     a.dX[l] = dX ? dX[l] : nullptr;
+    a.mask[l] = mask ? mask[l] : nullptr;
+    if (dropout && l > 0 && !a.mask[l]) return -2;
   }
   a.dh_last = dh_last;
   a.seeds = seeds;

@@ -84,6 +84,107 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
   }
 }
 
+// ---- single-launch clip + Adam/AdamW (the captured training step's only optimizer node) ----
+// Phase 1: every workgroup reduces ||scale*g||^2 over its slice and publishes the partial (write-through
+// store, drained, then one agent-scope arrival add on a 64-bit monotonic ticket: the cdna_hip_programming.md
+// G16 R1 hand-off, no fences).  Phase 2: every workgroup polls the ticket until the whole grid arrived,
+// re-reads the partials in index order (deterministic norm), and updates its slice; with `zero_grad` it
+// writes g = 0 back instead of the clipped gradient, which replaces the per-step grad-zeroing fill.
+// The grid is capped at one workgroup per CU (256), so every workgroup is co-resident and the poll is
+// bounded only for safety (a give-up counts in nonfinite[1]).
+constexpr int FUSED_MAX_BLOCKS = 256;
+constexpr unsigned FUSED_SPIN_LIMIT = 1u << 22;
+
+__global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
+                                                         float4* __restrict__ m, float4* __restrict__ v, long n4,
+                                                         float* __restrict__ partials,
+                                                         unsigned long long* __restrict__ ticket,
+                                                         const float* __restrict__ lr_ptr, float* __restrict__ step_ptr,
+                                                         float beta1, float beta2, float eps, float wd,
+                                                         float max_norm, float scale, int adamw, int zero_grad,
+                                                         float* __restrict__ norm_out, float* __restrict__ nonfinite) {
+  __shared__ float scratch[TPB / 64];
+  __shared__ float s_norm;
+  const long stride = (long)gridDim.x * TPB;
+  float acc = 0.f;
+  for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
+    const float4 q = g[i];
+    acc = fmaf(q.x, q.x, acc);
+    acc = fmaf(q.y, q.y, acc);
+    acc = fmaf(q.z, q.z, acc);
+    acc = fmaf(q.w, q.w, acc);
+  }
+  acc = block_sum(acc, scratch) * (scale * scale);
+  // the step counter is read by every workgroup BEFORE it arrives; the last arriver advances it
+  const float t = step_ptr[0] + 1.0f;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partials + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long prev =
+        __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = (prev / gridDim.x + 1) * gridDim.x;
+    if (prev + 1 == target) step_ptr[0] = t;
+    unsigned long long seen = prev + 1;
+    unsigned spins = 0;
+    while (seen < target) {
+      __builtin_amdgcn_s_sleep(1);
+      seen = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > FUSED_SPIN_LIMIT) {
+        if (nonfinite) atomicAdd(nonfinite + 1, 1.0f);
+        break;
+      }
+    }
+    float sq = 0.f;
+    for (int b = 0; b < (int)gridDim.x; ++b)
+      sq += __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_norm = sqrtf(sq);
+  }
+  __syncthreads();
+  const float norm = s_norm;
+  float clip = 1.0f;
+  if (max_norm > 0.f) clip = fminf(1.0f, max_norm / (norm + 1e-6f));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (norm_out) norm_out[0] = norm;
+    if (nonfinite && !isfinite(norm)) nonfinite[0] += 1.0f;
+  }
+  const float gs = scale * clip;
+  const float lr = lr_ptr[0];
+  const float bc1 = 1.0f - powf(beta1, t);
+  const float bc2 = 1.0f - powf(beta2, t);
+  const float step_size = lr / bc1;
+  const float bc2_sqrt = sqrtf(bc2);
+  const float decay = adamw ? (1.0f - lr * wd) : 1.0f;
+  const float l2 = adamw ? 0.0f : wd;
+  for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
+    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    float* pf = reinterpret_cast<float*>(&pp);
+    float* gf = reinterpret_cast<float*>(&gg);
+    float* mf = reinterpret_cast<float*>(&mm);
+    float* vf = reinterpret_cast<float*>(&vv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = gf[k] * gs;
+      gf[k] = zero_grad ? 0.0f : gk;
+      gk = fmaf(l2, pf[k], gk);
+      mf[k] = fmaf(1.0f - beta1, gk - mf[k], mf[k]);
+      vf[k] = fmaf(beta2, vf[k], (1.0f - beta2) * gk * gk);
+      const float denom = sqrtf(vf[k]) / bc2_sqrt + eps;
+      pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
+    }
+    p[i] = pp;
+    g[i] = gg;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+inline int fused_grid(long n4) {
+  long blocks = (n4 + TPB * 4 - 1) / (TPB * 4);
+  if (blocks < 1) blocks = 1;
+  if (blocks > FUSED_MAX_BLOCKS) blocks = FUSED_MAX_BLOCKS;
+  return (int)blocks;
+}
+
 __global__ void scale_kernel(float4* __restrict__ x, long n4, float s) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     float4 a = x[i];
@@ -121,4 +222,19 @@ extern "C" void mta_adam(float* p, float* g, float* m, float* v, long n, const f
 extern "C" void mta_scale(float* x, long n, float s, hipStream_t st) {
   const long n4 = n / 4;
   scale_kernel<<<grid_for(n4), TPB, 0, st>>>(reinterpret_cast<float4*>(x), n4, s);
+}
+
+extern "C" int mta_adam_fused_partials() { return FUSED_MAX_BLOCKS; }
+
+// ticket: one zero-initialised uint64 per optimizer (monotonic across launches); nonfinite: 2 floats
+// ([0] steps with a non-finite norm, [1] arrival waits that gave up)
+extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, float* partials,
+                               unsigned long long* ticket, const float* lr, float* step, float beta1, float beta2,
+                               float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
+                               float* norm_out, float* nonfinite, hipStream_t st) {
+  const long n4 = n / 4;
+  adam_fused_kernel<<<fused_grid(n4), TPB, 0, st>>>(
+      reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
+      reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
+      zero_grad, norm_out, nonfinite);
 }

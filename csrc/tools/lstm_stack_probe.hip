@@ -1,9 +1,9 @@
 // Diagnostic probe (not part of the extension): times the layer-pipelined LSTM kernels of lstm_stack.hip
 // (forward, and backward with the fused weight gradients) on random data at the headline shape, and in a
 // -DMTA_STACK_STAMPS=1 build prints per-segment s_memtime cycles per step of block 0 for each wave role.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STACK_STAMPS=1] [-DMTA_STACK_DRAIN_LAG=2] \
-//         csrc/tools/lstm_stack_probe.hip -o build/lstm_stack_probe
-//   ./build/lstm_stack_probe [N=100] [L=2] [prec=1] [T=60]
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STACK_STAMPS=1] \
+//         csrc/tools/lstm_stack_probe.hip -o tools_bin/lstm_stack_probe
+//   ./tools_bin/lstm_stack_probe [N=100] [L=2] [prec=1] [T=60]
 // Stamp builds are slower than the real kernel (each stamp waits lgkmcnt): read the SHARES there and the
 // absolute times from the stamp-free build.
 #include <cstdio>
@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
   float* x = dev_rand((size_t)N * T * FIN, 1.f);
   std::vector<float*> wih(L), whh(L), bih(L), bhh(L), hseq(L), xdrop(L, nullptr), stash(L), dG(L), dX(L, nullptr),
       inp(L), gwih(L), gwhh(L), gbih(L), gbhh(L);
+  std::vector<uint8_t*> mask(L, nullptr);
   for (int l = 0; l < L; ++l) {
     const int fin = l == 0 ? FIN : H;
     wih[l] = dev_rand((size_t)4 * H * fin, k);
@@ -58,7 +59,10 @@ int main(int argc, char** argv) {
     bih[l] = dev_rand(4 * H, k);
     bhh[l] = dev_rand(4 * H, k);
     hseq[l] = dev_zero((size_t)T * Np * H);
-    if (l >= 1) xdrop[l] = dev_zero((size_t)T * Np * H);
+    if (l >= 1) {
+      xdrop[l] = dev_zero((size_t)T * Np * H);
+      CK(hipMalloc(&mask[l], (size_t)T * Np * H));
+    }
     if (l < L - 1) dX[l] = dev_zero((size_t)T * Np * H);
     stash[l] = dev_zero((size_t)T * Np * 5 * H);
     dG[l] = dev_zero((size_t)T * Np * 4 * H);
@@ -88,7 +92,7 @@ int main(int argc, char** argv) {
     float m;
     CK(hipEventRecord(a));
     int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                xdrop.data(), stash.data(), seeds, 0.2f, flags, N, Np, T, 0);
+                                xdrop.data(), mask.data(), stash.data(), seeds, 0.2f, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -99,7 +103,8 @@ int main(int argc, char** argv) {
     if (rep >= skip) ms_f += m / (reps - skip);
     CK(hipEventRecord(a));
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
-                            hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(), seeds, 0.2f,
+                            hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
+                            const_cast<const uint8_t* const*>(mask.data()), seeds, 0.2f,
                             1, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
@@ -112,19 +117,19 @@ int main(int argc, char** argv) {
   }
   unsigned tmo = 0;
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
-  printf("N=%d L=%d T=%d prec=%d drain_lag=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
+  printf("N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
          "timeouts=%u\n",
-         N, L, T, prec, MTA_STACK_DRAIN_LAG, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         N, L, T, prec, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
 #if MTA_STACK_STAMPS
   unsigned long long acc[2][2][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
   const char* seg[2][2][8] = {
-      {{"", "gx_lds_read", "vmcnt_drain", "store_issue", "mfma_chain", "act+lds_write", "barrier", ""},
-       {"", "compute_gx", "load_input(poll)", "barrier", "", "", "", ""}},
+      {{"", "gx_lds_read", "mfma_chain", "activations", "lds_writes", "barrier", "", ""},
+       {"", "wait+compute_gx", "load_input(poll)", "store_outputs", "barrier", "", "", ""}},
       {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
         "mfma_dh"},
-       {"", "vmem_wait", "flags+dx(lag1)", "stage+load_dh(+dx lag2)", "barrier", "", "", ""}}};
+       {"", "vmem_wait", "flags+dx", "stage+load_dh+mask", "barrier", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
   const char* role[2][2] = {{"recurrent", "input"}, {"recurrent", "gradient"}};
   for (int d = 0; d < 2; ++d)

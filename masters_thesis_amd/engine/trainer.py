@@ -113,6 +113,7 @@ class Trainer:
         self._graphs: Dict[Tuple, _Graph] = {}
         self._graph_loaders: Dict[int, Any] = {}  # keeps loaders alive while graphs key on id(loader)
         self._eager_counts: Dict[Tuple, int] = {}
+        self._ones: Dict[Tuple, torch.Tensor] = {}
         self.step_timer = StepTimer()
         self.perf: Dict[str, float] = {}
         self._in_graph = False
@@ -212,26 +213,38 @@ class Trainer:
 
     # ------------------------------------------------------------------ step machinery
     def _graphs_enabled(self) -> bool:
-        return self.use_hip_graphs and self.device.type == "cuda"
+        return (self.use_hip_graphs and self.device.type == "cuda"
+                and getattr(self.model, "graph_capturable", True))
 
     def _allreduce_in_graph(self) -> bool:
         return self.ddp.world == 1 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1"
 
+    def _seed_grad(self, loss: torch.Tensor) -> torch.Tensor:
+        # a persistent ones tensor: no fill node per step for autograd's implicit seed
+        one = self._ones.get((loss.shape, loss.device, loss.dtype))
+        if one is None:
+            one = torch.ones_like(loss)
+            self._ones[(loss.shape, loss.device, loss.dtype)] = one
+        return one
+
     def _train_body(self, batch, batch_idx: int):
-        """zero-grad, forward + fused loss, backward, [all-reduce], clip + Adam."""
-        self.flat.grad.zero_()
+        """zero-grad, forward + fused loss, backward, [all-reduce], clip + Adam.
+
+        The fused optimizer leaves the flat gradient zeroed, so a step that follows one needs no fill."""
+        if not getattr(self.optimizer, "grads_zeroed", False):
+            self.flat.grad.zero_()
         loss = self.model.training_step(batch, batch_idx)
-        loss.backward()
+        loss.backward(self._seed_grad(loss))
         if not self._in_graph or self._allreduce_in_graph():
             self.ddp.allreduce_grads()
-            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
         return loss
 
     def _after_graph(self) -> None:
         # world > 1: the RCCL all-reduce and the optimizer run outside the captured fwd/bwd graph
         if not self._allreduce_in_graph():
             self.ddp.allreduce_grads()
-            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale)
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
 
     def _run(self, key: Tuple, provider: Callable[[], Sequence[torch.Tensor]], body: Callable, static: bool,
              warmup: int):
@@ -310,7 +323,7 @@ class Trainer:
     def _eval_step(self, stage: str, loader, batch_idx: int, static: bool, batch=None):
         model = self.model
         fn = model.validation_step if stage == "val" else model.test_step
-        if not getattr(model, "eval_graph_capturable", True):
+        if not getattr(model, "graph_capturable", True):
             # MIOpen's inference LSTM initialises hipBLASLt state on first use, which is illegal while a
             # stream is capturing: the reference-equivalent path evaluates eagerly
             if static:

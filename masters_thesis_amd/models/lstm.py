@@ -100,9 +100,14 @@ class FinancialLstm(LightningModule):
         self._hparams.update(dict(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers,
                                   dropout=dropout, learning_rate=learning_rate, weight_decay=weight_decay))
 
+    # MIOpen's LSTM initialises hipBLASLt state lazily (per stream / precision), which is illegal while a
+    # stream is capturing: the reference-equivalent path runs eagerly in the trainer.  bench.py opts in
+    # after its eager warm-up (measured capture-safe there) via ``allow_torch_capture``.
+    allow_torch_capture = False
+
     @property
-    def eval_graph_capturable(self) -> bool:
-        return self.backend != "torch"
+    def graph_capturable(self) -> bool:
+        return self.backend != "torch" or self.allow_torch_capture
 
     # ---- forward ---------------------------------------------------------------------
     def encode(self, x: Tensor) -> Tensor:

@@ -129,10 +129,10 @@ class _LSTMStackFn(torch.autograd.Function):
 _E = {}
 
 
-def _empty(dev) -> Tensor:
-    key = str(dev)
+def _empty(dev, dtype=torch.float32) -> Tensor:
+    key = (str(dev), dtype)
     if key not in _E:
-        _E[key] = torch.empty(0, device=dev)
+        _E[key] = torch.empty(0, device=dev, dtype=dtype)
     return _E[key]
 
 
@@ -145,8 +145,10 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
     H = weights[1].shape[1]
     N, T, F = x.shape
     tr8 = -(-(padded_rows(N) // 16) // 8) * 8
-    # all L x tiles workgroups must be co-resident (<= 2 per CU at 256 VGPRs)
-    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= 448
+    # all L x tiles forward workgroups co-resident: H=64 takes ~90 KB of LDS (one workgroup per CU, 256 CUs),
+    # H=32 ~46 KB (several per CU)
+    cap = 256 if H == 64 else 448
+    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= cap
 
 
 _FLAGS = {}
@@ -211,17 +213,21 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         hseq = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L)]
         xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E
                        for _ in range(1, L)]
+        EB = _empty(dev, torch.uint8)
+        # keep bytes of every inter-layer dropout (written by the forward, read by the backward's dx masks)
+        masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB
+                        for _ in range(1, L)]
         stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E
                  for _ in range(L)]
         flags = _stack_flags(C, Np, L, dev)
         C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
-                         hseq, xdrop, stash, seeds, float(dropout), flags, N, Np, T)
+                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
         ctx.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
         ctx.params = flat
         ctx.seeds = seeds
         ctx.fwd_flags = flags
         if need_grad:
-            ctx.save_for_backward(x, *stash, *hseq, *[t for t in xdrop[1:] if drop])
+            ctx.save_for_backward(x, *stash, *hseq, *[t for t in xdrop[1:] if drop], *[m for m in masks[1:] if drop])
         return hseq[L - 1][T - 1, :N]
 
     @staticmethod
@@ -234,7 +240,8 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         x = saved[0]
         stash = list(saved[1:1 + L])
         hseq = list(saved[1 + L:1 + 2 * L])
-        xdrop = list(saved[1 + 2 * L:]) if drop else []
+        xdrop = list(saved[1 + 2 * L:1 + 3 * L - 1]) if drop else []
+        masks = ([_empty(dev, torch.uint8)] + list(saved[3 * L:4 * L - 1])) if drop else []
         flat = ctx.params
         dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
         dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
@@ -244,7 +251,7 @@ class _LSTMPipelinedFn(torch.autograd.Function):
         # accumulated straight into the parameters' gradient views
         grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
         C.lstm_stack_bwd(H, prec, F, stash, list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
-                         hseq, inp, grads, ctx.seeds, p, drop, flags, N, Np, T)
+                         hseq, inp, grads, masks, ctx.seeds, p, drop, flags, N, Np, T)
         ctx.bwd_flags = flags
         return (None,) * (6 + len(flat))
 

@@ -12,14 +12,18 @@ MI355X design:
   gradient buffer — which is then the single DDP all-reduce bucket (one RCCL call
   per step for the <= 1 MB gradients of this workload) and the single input of
   the fused optimizer.
-* ``FusedAdam.step`` is two HIP launches (``csrc/optim.hip``): partial grad norms,
-  then clip + Adam with ``lr`` and the step counter in device memory, i.e. it can
-  be captured once in a HIP graph and replayed forever; the plateau scheduler only
-  writes the lr scalar.
+* ``FusedAdam.step`` is ONE HIP launch (``csrc/optim.hip:adam_fused_kernel``): per-workgroup
+  partial grad norms, an in-launch arrival ticket (write-through partials, no fences), then
+  clip + Adam with ``lr`` and the step counter in device memory, i.e. it can be captured once
+  in a HIP graph and replayed forever; the plateau scheduler only writes the lr scalar.  With
+  ``zero_grad=True`` the kernel leaves the gradient zeroed, which replaces the per-step fill
+  (``grads_zeroed`` tells the trainer).  ``MTA_OPTIM_TWO_LAUNCH=1`` selects the older
+  norm + update pair.
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Iterable, List, Optional
 
 import torch
@@ -79,7 +83,11 @@ class FusedAdam:
         self.lr_t = torch.tensor([lr], device=dev, dtype=torch.float32)
         self.step_t = torch.zeros(1, device=dev, dtype=torch.float32)
         self.grad_norm = torch.zeros(1, device=dev, dtype=torch.float32)
-        self.nonfinite = torch.zeros(1, device=dev, dtype=torch.float32)  # steps with a NaN/Inf grad norm
+        # [0] steps with a NaN/Inf grad norm, [1] in-launch arrival waits that gave up (fused kernel)
+        self._health = torch.zeros(2, device=dev, dtype=torch.float32)
+        self.nonfinite = self._health[0:1]
+        self.sync_timeouts = self._health[1:2]
+        self.grads_zeroed = False  # True after a step that left the flat gradient zeroed
         self.betas = tuple(float(b) for b in betas)
         self.eps = float(eps)
         self.weight_decay = float(weight_decay)
@@ -87,7 +95,11 @@ class FusedAdam:
         self._lr = float(lr)
         self.hip = use_hip(flat.data)
         if self.hip:
-            self.partials = torch.zeros(lib().optim_num_partials(flat.padded), device=dev, dtype=torch.float32)
+            C = lib()
+            self.single_launch = os.environ.get("MTA_OPTIM_TWO_LAUNCH", "0") != "1"
+            n = C.adam_fused_partials() if self.single_launch else C.optim_num_partials(flat.padded)
+            self.partials = torch.zeros(n, device=dev, dtype=torch.float32)
+            self.ticket = torch.zeros(1, device=dev, dtype=torch.int64)
         # torch.optim-like surface for schedulers / LR monitors / checkpoints
         self.param_groups = [{
             "lr": lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay, "amsgrad": False,
@@ -110,11 +122,21 @@ class FusedAdam:
             self.set_lr(self.param_groups[0]["lr"])
 
     # ---- step -------------------------------------------------------------------
-    def step(self, max_norm: float = 0.0, grad_scale: float = 1.0) -> None:
-        """Clip (if max_norm > 0) the flat gradient scaled by ``grad_scale`` and apply one Adam step."""
+    def step(self, max_norm: float = 0.0, grad_scale: float = 1.0, zero_grad: bool = False) -> None:
+        """Clip (if max_norm > 0) the flat gradient scaled by ``grad_scale`` and apply one Adam step.
+
+        ``zero_grad``: leave the flat gradient zeroed (the fused kernel writes 0 instead of the clipped
+        gradient; ``grads_zeroed`` reports whether that happened)."""
         self.sync_lr_from_groups()
         f = self.flat
         b1, b2 = self.betas
+        self.grads_zeroed = False
+        if self.hip and self.single_launch:
+            lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
+                             self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
+                             float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health)
+            self.grads_zeroed = bool(zero_grad)
+            return
         if self.hip:
             C = lib()
             C.grad_sqnorm(f.grad, float(grad_scale), self.partials, self.step_t)

@@ -30,21 +30,21 @@ def main():
         stash = [torch.empty(T * Np * 5 * H, device=dev) for _ in range(L)]
         flags = torch.zeros(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
         seeds = torch.zeros(8, dtype=torch.int64, device=dev)
-        C.lstm_stack_fwd(H, 1, F, x, ws[0::4], ws[1::4], ws[2::4], ws[3::4], hseq, [E] * L, stash, seeds, 0.0,
+        C.lstm_stack_fwd(H, 1, F, x, ws[0::4], ws[1::4], ws[2::4], ws[3::4], hseq, [E] * L, [E] * L, stash, seeds, 0.0,
                          flags, N, Np, T)
         dG = [torch.empty((T, Np, 4 * H), device=dev) for _ in range(L)]
         dX = [torch.empty((T, Np, H), device=dev) for _ in range(L - 1)] + [E]
         dh = torch.randn(N, H, device=dev)
         inp = [x] + hseq[:-1]
         ref = [[torch.zeros_like(ws[4 * l + kk]) for l in range(L)] for kk in range(4)]
-        C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], seeds, 0.0, False, flags,
+        C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], seeds, 0.0, False, flags,
                          N, Np, T)
         for l in range(L):
             C.lstm_wgrad(1, dG[l], hseq[l], inp[l], l == 0, N, Np, T, H, ref[0][l], ref[1][l], ref[2][l], ref[3][l])
         dG_ref = [d.clone() for d in dG]
         for rep in range(3):
             got = [[torch.zeros_like(ws[4 * l + kk]) for l in range(L)] for kk in range(4)]
-            C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, got, seeds, 0.0, False,
+            C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, got, [], seeds, 0.0, False,
                              flags, N, Np, T)
             torch.cuda.synchronize()
             errs = []

@@ -33,7 +33,7 @@ def run(C, L, prec):
     seeds = torch.zeros(8, dtype=torch.int64, device=dev)
 
     def fwd():
-        C.lstm_stack_fwd(H, prec, F, x, ws[0::4], ws[1::4], ws[2::4], ws[3::4], hseq, [E] * L, stash, seeds, 0.0,
+        C.lstm_stack_fwd(H, prec, F, x, ws[0::4], ws[1::4], ws[2::4], ws[3::4], hseq, [E] * L, [E] * L, stash, seeds, 0.0,
                          flags, N, Np, T)
 
     dG = [torch.empty((T, Np, 4 * H), device=dev) for _ in range(L)]
@@ -44,11 +44,11 @@ def run(C, L, prec):
     grads = [[torch.zeros_like(ws[4 * l + k]) for l in range(L)] for k in range(4)]
 
     def bwd():
-        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], seeds, 0.0, False, flags,
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], seeds, 0.0, False, flags,
                          N, Np, T)
 
     def bwd_fused():
-        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, seeds, 0.0, False,
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, [], seeds, 0.0, False,
                          flags, N, Np, T)
 
     def bwd_wgrad():

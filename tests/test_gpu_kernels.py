@@ -156,6 +156,33 @@ def test_fused_adam_matches_torch_adam_with_clipping():
     assert float(opt.step_t.item()) == 5.0
 
 
+@pytest.mark.parametrize("n_params", [51_074, 3_000_000])
+def test_single_launch_adam_matches_two_launch_and_zeroes_grads(n_params, monkeypatch):
+    """csrc/optim.hip adam_fused_kernel (in-launch norm ticket, grid <= 256 workgroups) against the two-launch
+    norm + update pair, over several steps (the monotonic ticket spans launches), with grad zeroing."""
+    from masters_thesis_amd.ops.optim import FlatParameters, FusedAdam
+
+    torch.manual_seed(6)
+    opts = []
+    for two in ("1", "0"):
+        monkeypatch.setenv("MTA_OPTIM_TWO_LAUNCH", two)
+        ps = [torch.nn.Parameter(torch.full((n_params,), 0.5, device=DEV))]
+        flat = FlatParameters(ps)
+        opts.append((flat, FusedAdam(flat, lr=1e-3, weight_decay=1e-5)))
+    assert not opts[0][1].single_launch and opts[1][1].single_launch
+    for step in range(4):
+        g = torch.randn(opts[0][0].padded, device=DEV) * (3.0 if step % 2 else 0.01)
+        for flat, opt in opts:
+            flat.grad.copy_(g)
+            opt.step(max_norm=5.0, zero_grad=True)
+    (fa, oa), (fb, ob) = opts
+    torch.testing.assert_close(fb.data, fa.data, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(ob.grad_norm, oa.grad_norm, rtol=1e-5, atol=0)
+    assert ob.grads_zeroed and float(fb.grad.abs().max()) == 0.0
+    assert float(ob.step_t.item()) == 4.0 and int(ob.ticket.item()) > 0
+    assert float(ob.sync_timeouts.item()) == 0.0 and float(ob.nonfinite.item()) == 0.0
+
+
 def test_flat_grads_survive_backward():
     from masters_thesis_amd.ops.optim import FlatParameters
 
