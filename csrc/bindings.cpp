@@ -22,6 +22,11 @@ void mta_gather_batch(const float* const* src, float* const* dst, const long* ro
 void mta_decoder_losses(const float* ab, const float* y, const float* factor, const float* inv_psi, int N, int n,
                         int C, int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
                         float batch_weight, float* out, float* gmse, float* gnll, double* acc, hipStream_t st);
+int mta_heads_losses_train(const float* h, int H, const float* wa, const float* ba, const float* wb, const float* bb,
+                           const float* y, const float* factor, const float* inv_psi, int N, int n, int C, int windows,
+                           int kwin, int factor_stride, int want_nll, float c_nll, float c_mse, float batch_weight,
+                           float* out, double* acc, float* dh, float* g_wa, float* g_ba, float* g_wb, float* g_bb,
+                           hipStream_t st);
 void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb, const float* bb,
                       float* ab_out, const float* y, const float* factor, const float* inv_psi, int N, int n, int C,
                       int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
@@ -55,12 +60,12 @@ int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* d
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
-                       float* const* hseq, float* const* xdrop, uint8_t* const* mask, float* const* stash,
+                       float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
                        const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
-                       float* const* g_bih, float* const* g_bhh, const uint8_t* const* mask, uint64_t* seeds,
+                       float* const* g_bih, float* const* g_bhh, const uint32_t* const* mask, uint64_t* seeds,
                        float drop_p, int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 // data.hip (dataset build)
@@ -263,6 +268,42 @@ void heads_losses(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor wb, at:
                    (int)factor_stride, want_nll ? 1 : 0, (float)c_nll, (float)c_mse, (float)batch_weight,
                    out.data_ptr<float>(), gmse.data_ptr<float>(), gnll.data_ptr<float>(), opt_acc(acc),
                    cur_stream());
+}
+
+// the training step's decoder in one launch (upstream gradient 1 on the total loss): losses + metrics into
+// out / acc, dh (N, H) for the encoder, head gradients accumulated into g_*; false = too large (use the pair)
+bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor wb, at::Tensor bb, at::Tensor y,
+                        at::Tensor factor, at::Tensor inv_psi, int64_t windows, int64_t kwin, int64_t factor_stride,
+                        bool want_nll, double c_nll, double c_mse, double batch_weight, at::Tensor out,
+                        const OptT& acc, at::Tensor dh, at::Tensor g_wa, at::Tensor g_ba, at::Tensor g_wb,
+                        at::Tensor g_bb) {
+  MTA_CHECK_F32(h);
+  MTA_CHECK_F32(dh);
+  MTA_CHECK_F32(g_wa);
+  MTA_CHECK_F32(g_ba);
+  MTA_CHECK_F32(g_wb);
+  MTA_CHECK_F32(g_bb);
+  TORCH_CHECK(h.dim() == 2, "h must be (N, H)");
+  const int64_t N = h.size(0), H = h.size(1);
+  TORCH_CHECK(wa.numel() == H && wb.numel() == H && ba.numel() == 1 && bb.numel() == 1, "bad head shapes");
+  TORCH_CHECK(dh.numel() == N * H && g_wa.numel() == H && g_wb.numel() == H && g_ba.numel() == 1 &&
+                  g_bb.numel() == 1, "dh / head gradient shapes");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.is_contiguous() && y.dim() == 3 && y.size(0) == N &&
+                  y.size(2) >= 2, "y must be (N, n, C >= 2) fp32");
+  TORCH_CHECK(out.is_cuda() && out.numel() >= 4, "out: float[4]");
+  TORCH_CHECK(windows * kwin == N, "windows * kwin must equal N");
+  MTA_CHECK_F32(factor);
+  MTA_CHECK_F32(inv_psi);
+  TORCH_CHECK(inv_psi.numel() == N, "inv_psi must be (N,)");
+  TORCH_CHECK(factor.numel() >= 2 + (windows - 1) * factor_stride, "factor too small");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
+  const int rc = mta_heads_losses_train(
+      h.data_ptr<float>(), (int)H, wa.data_ptr<float>(), ba.data_ptr<float>(), wb.data_ptr<float>(),
+      bb.data_ptr<float>(), y.data_ptr<float>(), factor.data_ptr<float>(), inv_psi.data_ptr<float>(), (int)N,
+      (int)y.size(1), (int)y.size(2), (int)windows, (int)kwin, (int)factor_stride, want_nll ? 1 : 0, (float)c_nll,
+      (float)c_mse, (float)batch_weight, out.data_ptr<float>(), opt_acc(acc), dh.data_ptr<float>(),
+      g_wa.data_ptr<float>(), g_ba.data_ptr<float>(), g_wb.data_ptr<float>(), g_bb.data_ptr<float>(), cur_stream());
+  return rc == 0;
 }
 
 void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total, double c_nll, double c_mse,
@@ -517,7 +558,7 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
     TORCH_CHECK(masks.size() == (size_t)L, "per-layer keep-byte list");
     if (xdrop[l].numel())
       TORCH_CHECK(masks[l].is_cuda() && masks[l].scalar_type() == at::kByte && masks[l].numel() == T * Np * H,
-                  "keep bytes: uint8 (T, Np, H) per dropout layer");
+                  "keep bytes: uint8[T * Np * H] per dropout layer (u32 words (T, ntiles, 4, H))");
     if (stash[l].numel()) TORCH_CHECK(stash[l].numel() == T * Np * 5 * H, "stash shape");
   }
   TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() >= L, "seeds: int64[L]");
@@ -528,9 +569,9 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
        sh = ptrs_f32(stash, "stash");
   std::vector<const float*> cwi(wi.begin(), wi.end()), cwh(wh.begin(), wh.end()), cbi(bi.begin(), bi.end()),
       cbh(bh.begin(), bh.end());
-  std::vector<uint8_t*> mk(L, nullptr);
+  std::vector<uint32_t*> mk(L, nullptr);
   for (int64_t l = 0; l < L; ++l)
-    if (xdrop[l].numel()) mk[l] = masks[l].data_ptr<uint8_t>();
+    if (xdrop[l].numel()) mk[l] = reinterpret_cast<uint32_t*>(masks[l].data_ptr<uint8_t>());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   const int rc = mta_lstm_stack_fwd((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(), cwh.data(),
                                     cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
@@ -584,13 +625,13 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
   }
   std::vector<const float*> cst(st.begin(), st.end()), cwh(wh.begin(), wh.end()), cwi(wi.begin(), wi.end()),
       chs(hs.begin(), hs.end()), cin(in.begin(), in.end());
-  std::vector<const uint8_t*> mk(L, nullptr);
+  std::vector<const uint32_t*> mk(L, nullptr);
   if (dropout) {
     TORCH_CHECK(masks.size() == (size_t)L, "per-layer keep-byte list");
     for (int64_t l = 1; l < L; ++l) {
       TORCH_CHECK(masks[l].is_cuda() && masks[l].scalar_type() == at::kByte && masks[l].numel() == T * Np * H,
-                  "keep bytes: uint8 (T, Np, H) per dropout layer");
-      mk[l] = masks[l].data_ptr<uint8_t>();
+                  "keep bytes: uint8[T * Np * H] per dropout layer (u32 words (T, ntiles, 4, H))");
+      mk[l] = reinterpret_cast<const uint32_t*>(masks[l].data_ptr<uint8_t>());
     }
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dh_last.device());
@@ -728,6 +769,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_num_partials", &optim_num_partials);
   m.def("grad_sqnorm", &grad_sqnorm);
   m.def("adam", &adam);
+  m.def("heads_losses_train", &heads_losses_train);
   m.def("adam_fused_partials", &adam_fused_partials);
   m.def("adam_fused", &adam_fused);
   m.def("scale_", &scale_);

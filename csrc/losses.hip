@@ -36,7 +36,10 @@ struct LossArgs {
 // Work split: one wave per sequence, lanes over the n target days (looping when n > 64);
 // every per-sequence sum is a wave reduction, u_t accumulates with LDS atomics whose
 // addresses are distinct within a wave instruction.  `ab` may live in LDS or global memory.
-__device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
+// YL: the (r_target, r_mkt) pairs of every target day were staged in LDS as float2 (N, n) by the caller
+// (one coalesced burst instead of a dependent global load per sequence iteration).
+template <bool YL = false>
+__device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const float2* ys = nullptr) {
   __shared__ double red[NWAVES][6];
   __shared__ double bcast[6];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -50,7 +53,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
     const float* yi = A.y + (size_t)i * n * C;
     float se = 0.f, serm = 0.f, ss = 0.f, sa = 0.f;
     for (int t = lane; t < n; t += 64) {
-      const float r = yi[t * C], rm = yi[t * C + 1];
+      const float r = YL ? ys[i * n + t].x : yi[t * C], rm = YL ? ys[i * n + t].y : yi[t * C + 1];
       const float e = fmaf(b, rm, a) - r;
       se += e;
       serm = fmaf(e, rm, serm);
@@ -90,7 +93,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
         const float* yi = A.y + (size_t)i * n * C;
         float sdd = 0.f;
         for (int t = lane; t < n; t += 64) {
-          const float D = yi[t * C] - mu;
+          const float D = (YL ? ys[i * n + t].x : yi[t * C]) - mu;
           sdd = fmaf(D, D, sdd);
           atomicAdd(&ut[t], wb * D);
         }
@@ -131,7 +134,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut) {
         const float* yi = A.y + (size_t)i * n * C;
         float sd = 0.f, ud = 0.f;
         for (int t = lane; t < n; t += 64) {
-          const float D = yi[t * C] - mu;
+          const float D = (YL ? ys[i * n + t].x : yi[t * C]) - mu;
           sd += D;
           ud = fmaf(ut[t], D, ud);
         }
@@ -200,27 +203,14 @@ __global__ __launch_bounds__(TPB) void heads_losses_kernel(const float* __restri
   losses_body(ab, A, ut);
 }
 
-// backward: d(alpha, beta) from the saved per-sequence gradients, then dh_T and the head weight
-// gradients (accumulated into the parameters' gradient views)
-__global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
-    const float* __restrict__ g_mse, const float* __restrict__ g_nll, const float* __restrict__ g_total,  // nullable
-    float c_nll, float c_mse, const float* __restrict__ gmse, const float* __restrict__ gnll, int has_nll,
-    const float* __restrict__ h, int N, int H, const float* __restrict__ wa, const float* __restrict__ wb,
-    float* __restrict__ dh, float* __restrict__ dab, float* __restrict__ g_wa, float* __restrict__ g_ba,
-    float* __restrict__ g_wb, float* __restrict__ g_bb) {
-  extern __shared__ __attribute__((aligned(16))) float d[];  // 2N
+// dh_T = d_a wa + d_b wb and the head weight / bias gradients (accumulated) from per-sequence d(alpha, beta)
+// (`d`, 2N floats, LDS); single workgroup
+__device__ void heads_bwd_body(const float* d, const float* __restrict__ h, int N, int H,
+                               const float* __restrict__ wa, const float* __restrict__ wb, float* __restrict__ dh,
+                               float* __restrict__ g_wa, float* __restrict__ g_ba, float* __restrict__ g_wb,
+                               float* __restrict__ g_bb) {
   __shared__ float part[NWAVES][2][64 + 1];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float gt = g_total ? g_total[0] : 0.f;
-  const float gm = (g_mse ? g_mse[0] : 0.f) + gt * c_mse;
-  const float gn = has_nll ? (g_nll ? g_nll[0] : 0.f) + gt * c_nll : 0.f;
-  for (int k = tid; k < 2 * N; k += TPB) {
-    float v = gm * gmse[k];
-    if (has_nll) v = fmaf(gn, gnll[k], v);
-    d[k] = v;
-    if (dab) dab[k] = v;
-  }
-  __syncthreads();
   if (dh) {
     for (int e = tid; e < N * H; e += TPB) {
       const int i = e / H, k = e % H;
@@ -257,6 +247,80 @@ __global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
       __syncthreads();
     }
   }
+}
+
+// Training step's whole decoder in ONE launch (the trainer's fused step: the loss is the step's root, so its
+// upstream gradient is exactly 1): heads, every loss and metric, d(alpha, beta) = c_mse dMSE + c_nll dNLL,
+// dh_T for the encoder's backward and the head weight gradients.  Replaces heads_losses + autograd's seed fill
+// + heads_losses_bwd.  YL stages y in LDS (small N n).
+template <bool YL>
+__global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
+    const float* __restrict__ h, int H, const float* __restrict__ wa, const float* __restrict__ ba,
+    const float* __restrict__ wb, const float* __restrict__ bb, LossArgs A, float* __restrict__ dh,
+    float* __restrict__ g_wa, float* __restrict__ g_ba, float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int N = A.N, n = A.n;
+  const int N2 = 2 * ((N + 1) & ~1);
+  float* ab = smem;                      // 2N
+  float* gm = ab + N2;                   // 2N  d mse / d(alpha, beta)
+  float* gn = gm + N2;                   // 2N  d nll / d(alpha, beta)
+  float* ut = gn + N2;                   // n
+  float2* ys = reinterpret_cast<float2*>(ut + ((n + 3) & ~3));  // (N, n) when YL
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if constexpr (YL) {
+    for (int e = tid; e < N * n; e += TPB) {
+      const float* yp = A.y + (size_t)e * A.C;
+      ys[e] = make_float2(yp[0], yp[1]);
+    }
+  }
+  for (int i = wid; i < N; i += NWAVES) {
+    float sa = 0.f, sb = 0.f;
+    for (int k = lane; k < H; k += 64) {
+      const float hv = h[(size_t)i * H + k];
+      sa = fmaf(hv, wa[k], sa);
+      sb = fmaf(hv, wb[k], sb);
+    }
+    sa = wave_sum_dpp(sa) + ba[0];
+    sb = wave_sum_dpp(sb) + bb[0];
+    if (lane == 0) {
+      ab[2 * i] = sa;
+      ab[2 * i + 1] = sb;
+    }
+  }
+  __syncthreads();
+  LossArgs L = A;
+  L.gmse = gm;
+  L.gnll = gn;
+  losses_body<YL>(ab, L, ut, ys);
+  __syncthreads();
+  const float cm = A.c_mse, cn = A.want_nll ? A.c_nll : 0.f;
+  float* d = ab;  // alpha/beta are dead: reuse for d(alpha, beta)
+  for (int k = tid; k < 2 * N; k += TPB) d[k] = cn != 0.f ? fmaf(cn, gn[k], cm * gm[k]) : cm * gm[k];
+  __syncthreads();
+  heads_bwd_body(d, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb, g_bb);
+}
+
+// backward: d(alpha, beta) from the saved per-sequence gradients, then dh_T and the head weight
+// gradients (accumulated into the parameters' gradient views)
+__global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
+    const float* __restrict__ g_mse, const float* __restrict__ g_nll, const float* __restrict__ g_total,  // nullable
+    float c_nll, float c_mse, const float* __restrict__ gmse, const float* __restrict__ gnll, int has_nll,
+    const float* __restrict__ h, int N, int H, const float* __restrict__ wa, const float* __restrict__ wb,
+    float* __restrict__ dh, float* __restrict__ dab, float* __restrict__ g_wa, float* __restrict__ g_ba,
+    float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  extern __shared__ __attribute__((aligned(16))) float d[];  // 2N
+  const int tid = threadIdx.x;
+  const float gt = g_total ? g_total[0] : 0.f;
+  const float gm = (g_mse ? g_mse[0] : 0.f) + gt * c_mse;
+  const float gn = has_nll ? (g_nll ? g_nll[0] : 0.f) + gt * c_nll : 0.f;
+  for (int k = tid; k < 2 * N; k += TPB) {
+    float v = gm * gmse[k];
+    if (has_nll) v = fmaf(gn, gnll[k], v);
+    d[k] = v;
+    if (dab) dab[k] = v;
+  }
+  __syncthreads();
+  heads_bwd_body(d, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb, g_bb);
 }
 
 // ---- large N*H (wide encoders, big batches): grid-parallel heads and head backward ----
@@ -370,6 +434,27 @@ extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const f
   }
   const size_t lds = (size_t)(2 * ((N + 1) & ~1) + 4 + ((n + 3) & ~3)) * sizeof(float);
   heads_losses_kernel<<<1, TPB, lds, st>>>(h, H, wa, ba, wb, bb, ab_out, A);
+}
+
+// fused training decoder (see heads_losses_train_kernel); returns -1 when the problem is too large for one
+// workgroup's LDS (the caller keeps the forward / backward pair then)
+extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, const float* ba, const float* wb,
+                                      const float* bb, const float* y, const float* factor, const float* inv_psi,
+                                      int N, int n, int C, int windows, int kwin, int factor_stride, int want_nll,
+                                      float c_nll, float c_mse, float batch_weight, float* out, double* acc, float* dh,
+                                      float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st) {
+  LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
+             out, nullptr, nullptr, acc};
+  const size_t base = (size_t)(3 * 2 * ((N + 1) & ~1) + ((n + 3) & ~3)) * sizeof(float);
+  const size_t ybytes = (size_t)N * n * sizeof(float2);
+  if (base + ybytes <= 96 * 1024) {
+    heads_losses_train_kernel<true><<<1, TPB, base + ybytes, st>>>(h, H, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb,
+                                                                   g_bb);
+    return 0;
+  }
+  if (base > 60 * 1024) return -1;
+  heads_losses_train_kernel<false><<<1, TPB, base, st>>>(h, H, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb);
+  return 0;
 }
 
 extern "C" void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g_total, float c_nll, float c_mse, const float* gmse,

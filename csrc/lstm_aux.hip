@@ -49,19 +49,26 @@ __global__ void lstm_prep_kernel(const float* __restrict__ w_ih, const float* __
 }
 
 // ---------------------------------------------------------------------------------------------
-// batch gather: block (b, k) copies row perm[cursor*B + b] of tensor k into dst_k[b]; the last block
-// to finish advances the cursor (every block reads it before arriving, so the update is race-free)
+// batch gather: row perm[cursor*B + b] of tensor k -> dst_k[b].  Every (b, k) row is split over
+// GATHER_CHUNK-float4 blocks (grid.x = B * chunks of the longest row, grid.y = tensors), so all of a
+// step's loads are in flight at once (one 256-thread block per 16 KB: a 72 KB window row took 10 us as one
+// block's serial loop, r2 kernel trace).  Blocks past a shorter row's end only arrive.  The last block
+// to arrive advances the cursor (every block reads it before arriving, so the update is race-free).
 // ---------------------------------------------------------------------------------------------
+constexpr int GATHER_TPB = 256;
+constexpr int GATHER_CHUNK = GATHER_TPB * 4;  // float4 per block
+
 struct GatherArgs {
   const float* src[4];
   float* dst[4];
   long row_floats[4];
   int ntensors;
+  int chunks;  // blocks per row (of the longest row)
 };
 
-__global__ void gather_batch_kernel(GatherArgs a, const int* __restrict__ perm, int* cursor, int* arrive, int B,
-                                    int row_offset) {
-  const int b = blockIdx.x, k = blockIdx.y;
+__global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, const int* __restrict__ perm,
+                                                                  int* cursor, int* arrive, int B, int row_offset) {
+  const int b = blockIdx.x / a.chunks, chunk = blockIdx.x % a.chunks, k = blockIdx.y;
   const int idx = perm[cursor[0] * B + b] + row_offset;
   const long n = a.row_floats[k];
   const float* s = a.src[k] + (size_t)idx * n;
@@ -69,9 +76,21 @@ __global__ void gather_batch_kernel(GatherArgs a, const int* __restrict__ perm, 
   if ((n & 3) == 0 && ((((uintptr_t)s) | ((uintptr_t)d)) & 15) == 0) {
     const float4* s4 = reinterpret_cast<const float4*>(s);
     float4* d4 = reinterpret_cast<float4*>(d);
-    for (long i = threadIdx.x; i < n / 4; i += blockDim.x) d4[i] = s4[i];
+    const long lo = (long)chunk * GATHER_CHUNK, hi = lo + GATHER_CHUNK < n / 4 ? lo + GATHER_CHUNK : n / 4;
+    float4 v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long i = lo + r * GATHER_TPB + threadIdx.x;
+      if (i < hi) v[r] = s4[i];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long i = lo + r * GATHER_TPB + threadIdx.x;
+      if (i < hi) d4[i] = v[r];
+    }
   } else {
-    for (long i = threadIdx.x; i < n; i += blockDim.x) d[i] = s[i];
+    const long lo = (long)chunk * GATHER_CHUNK * 4, hi = lo + GATHER_CHUNK * 4 < n ? lo + GATHER_CHUNK * 4 : n;
+    for (long i = lo + threadIdx.x; i < hi; i += GATHER_TPB) d[i] = s[i];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -140,5 +159,8 @@ extern "C" void mta_gather_batch(const float* const* src, float* const* dst, con
     a.row_floats[k] = row_floats[k];
   }
   a.ntensors = ntensors;
-  gather_batch_kernel<<<dim3(B, ntensors), 256, 0, st>>>(a, perm, cursor, arrive, B, row_offset);
+  long longest = 1;
+  for (int k = 0; k < ntensors && k < 4; ++k) longest = row_floats[k] > longest ? row_floats[k] : longest;
+  a.chunks = (int)((longest + 4L * GATHER_CHUNK - 1) / (4L * GATHER_CHUNK));
+  gather_batch_kernel<<<dim3(B * a.chunks, ntensors), GATHER_TPB, 0, st>>>(a, perm, cursor, arrive, B, row_offset);
 }

@@ -59,6 +59,7 @@ constexpr int STASH = 5;
 constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;  // default poll bound (env MTA_LSTM_SPIN_LIMIT overrides: fault tests)
 constexpr int FLAG_STRIDE = 32;
+constexpr int TRS = 20;  // row stride (floats) of the per-wave 16 x 16 transpose scratch (conflict-free writes)
 constexpr int EPOCH_SHIFT = 12;  // one 128-byte line per progress word (polled words never share a line)
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
@@ -141,7 +142,8 @@ struct StackFwdArgs {
   const float* b_hh[MAXL];
   float* hseq[MAXL];    // (T, Np, H) outputs of every layer
   float* xdrop[MAXL];   // xdrop[l] (l >= 1): dropout(h^{(l-1)}), the input of layer l (null: no dropout)
-  uint8_t* mask[MAXL];  // mask[l] (l >= 1, with xdrop): keep bytes of that dropout, (T, Np, H), for the backward
+  uint32_t* mask[MAXL]; // mask[l] (with xdrop[l]): keep bytes of that dropout, (T, ntiles, 4, H) words of the
+                        // 4 sequences 4q..4q+3 of a lane (byte i = sequence 4q+i), read by the backward
   float* stash[MAXL];   // BPTT stash per layer (null: inference)
   const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
   float drop_p;
@@ -152,39 +154,25 @@ struct StackFwdArgs {
   int N, Np, T, L, ntiles, tr8;
 };
 
-// Forward workgroup = 2 x (H/16) waves.
-//  * RECURRENT waves [0, H/16): the recurrence (W_hh in VGPRs, h through LDS, one barrier per step) and
-//    NOTHING else: no vector-memory instruction in the loop.  Step t's outputs (f32 h_t and the BPTT stash
-//    fragments) go to a double-buffered LDS slot.
-//  * INPUT waves [H/16, 2 H/16), one step ahead / one step behind the recurrence in the same interval:
-//    wait for / load the layer input and compute gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products
-//    for layer 0, MFMA for layers >= 1) into a double-buffered LDS slot; then drain step t-1's outputs from
-//    LDS to global memory: hseq and the dropout-masked hand-off (16-byte write-through stores of one
-//    sequence row per lane), the dropout keep bytes, the stash (the recurrent lanes' fragment order) and
-//    the progress word.  The counter-hash dropout masks are computed here, off the recurrent path
-//    (measured: the hash's 32-bit multiplies plus the stores were ~40 % of a recurrent step, r2 probe).
-//  Both roles execute the same barriers (pre-loop, one per step, final).
+// Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
+// (W_hh in VGPRs, h through LDS, one barrier per step); waves [H/16, 2 H/16) are INPUT waves: one step
+// ahead they wait for / load the layer input and compute the gate pre-activations
+// gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products for layer 0, MFMA for layers >= 1) into a
+// double-buffered LDS slot, so the recurrent critical path never sees the hand-off latency, the progress
+// polls or the input product.  The input waves also draw the counter-hash dropout masks of the layer's
+// output (one step ahead, into LDS and the keep-byte words the backward reads): the hash's 32-bit multiplies
+// were ~30 % of a recurrent step when the recurrent waves drew them (r2 stamp probe).  Both roles execute
+// the same barriers (pre-loop, one per step, final).
 template <int H, int PREC>
 struct FwdSmem {
-  static constexpr int ROWB = H + 8, ROWF = H + 4, NW = H / 16;
+  static constexpr int ROWB = H + 8, ROWF = H + 4;
   float4 gxs[2][S][H];  // gate pre-activations (i, f, g, o) per (sequence, unit)
   __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
-  float hout[2][S][ROWF];       // f32 h_t, row-major (sequence, unit): the input waves' store image
-  float4 sto[2][NW][STASH][64]; // stash fragments of step t per recurrent wave / lane
+  uint32_t keep[2][H / 16][64];  // dropout keep bytes of step t (slot t & 1) per recurrent wave / lane
+  float tr[H / 16][2][S][TRS];   // per-wave transpose scratch of the h / masked-h store
 };
-
-// vmcnt(n) for a runtime-uniform n from a small set (the count must be an immediate)
-__device__ __forceinline__ void wait_vmcnt_le(int n) {
-  if (n >= 8) mta_wait_vmcnt<8>();
-  else if (n >= 7) mta_wait_vmcnt<7>();
-  else if (n >= 6) mta_wait_vmcnt<6>();
-  else if (n >= 3) mta_wait_vmcnt<3>();
-  else if (n >= 2) mta_wait_vmcnt<2>();
-  else if (n >= 1) mta_wait_vmcnt<1>();
-  else mta_wait_vmem();
-}
 
 template <int H, int PREC, int FIN0, bool FIRST>
 __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
@@ -219,7 +207,6 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     const float* w_ih = a.w_ih[layer];
     const float* xin = FIRST ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
     unsigned* in_flag = a.flags + FLAG_STRIDE * (FIRST ? 0 : (layer - 1) * a.tr8 + tile);
-    unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     constexpr int XKB = FIRST ? 1 : KB, XKF = FIRST ? 1 : KF;
     bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][PREC == PREC_BF16X3 ? XKB : 1];
     float Xf[4][PREC == PREC_F32 ? XKF : 1];
@@ -267,7 +254,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           for (int f = 0; f < FIN0; ++f) xin0[i][f] = xs[f];
         }
       } else {
-        // poll only when the last value seen does not cover step t
+        // poll only when the last value seen does not cover step t (polling every step from every
+        // consumer wave measured slower: the progress words share cache lines across tiles)
         seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
         const size_t row = (size_t)t * Np + n0 + j;
 #pragma unroll
@@ -328,44 +316,21 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 #pragma unroll
       for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
     };
-
-    // ---- output drain: step t's outputs from the LDS slot (t & 1) to global memory ----
-    float* hseq = a.hseq[layer];
-    float* xout = last ? nullptr : a.xdrop[layer + 1];
-    uint8_t* mout = last ? nullptr : a.mask[layer + 1];
-    const uint64_t seed_next = xout ? a.seeds[layer + 1] : 0;
-    float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
-    const float keep_scale = 1.0f / (1.0f - a.drop_p);
-    // one sequence row chunk per lane: 4 H float4 per step = NW x 64 lanes
-    const int gl = w * 64 + lane, srow = gl / (H / 4), scol = 4 * (gl % (H / 4));
-    // vector-memory ops each drain issues (counted waits below)
-    const int nst = 1 + (xout ? 1 : 0) + (mout ? 1 : 0) + (stash ? STASH : 0);
-    auto store_outputs = [&](int t) {
-      const int p = t & 1;
-      const float4 hv = *reinterpret_cast<const float4*>(&sm.hout[p][srow][scol]);
-      const size_t row = (size_t)t * Np + n0 + srow;
-      if (last) *reinterpret_cast<float4*>(hseq + row * H + scol) = hv;  // read after the kernel
-      else store_sc1_x4(hseq + row * H + scol, f32x4{hv.x, hv.y, hv.z, hv.w});
-      if (xout) {
-        float sc[4];
+    // dropout keep bytes of this layer's output (the next layer's input) for the lanes of recurrent wave w
+    uint32_t* mout = last ? nullptr : a.mask[layer + 1];
+    const uint64_t seed_next = mout ? a.seeds[layer + 1] : 0;
+    auto draw_mask = [&](int t) {
+      if (mout) {
         uint32_t kb = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float m = mta_dropout_scale(seed_next, (uint32_t)row, (uint32_t)(scol + e), a.drop_p);
-          sc[e] = m;
-          kb |= (m != 0.f ? 1u : 0u) << (8 * e);
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+          kb |= (mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p) != 0.f ? 1u : 0u) << (8 * i);
         }
-        store_sc1_x4(xout + row * H + scol, f32x4{hv.x * sc[0], hv.y * sc[1], hv.z * sc[2], hv.w * sc[3]});
-        if (mout) *reinterpret_cast<uint32_t*>(mout + row * H + scol) = kb;
-      }
-      if (stash) {
-        float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
-#pragma unroll
-        for (int k = 0; k < STASH; ++k) st[64 * k] = sm.sto[p][w][k][lane];
+        sm.keep[t & 1][w][lane] = kb;
+        mout[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u] = kb;  // before this interval's loads
       }
     };
-    (void)keep_scale;
-
     load_input(0);
     compute_gx(0);
     if (T > 1) load_input(1);
@@ -373,34 +338,29 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     SSTAMP_DECL
     for (int t = 0; t < T; ++t) {
       SSTAMP(0)
-      // interval t: the recurrence runs step t.  Per interval the issue order is [progress word, input loads,
-      // output stores]; waiting for the previous interval's input loads (vmcnt = its store count) therefore
-      // also drains every store of the interval before it: step t-3's outputs, drained by every input wave
-      // here, before barrier t, are published at the top of interval t+1 (as steps <= t-3 at the top of t).
-      if (t >= 1) wait_vmcnt_le(nst);
-      if (!last && t >= 3 && w == 0 && lane == 0)
-        __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1 < T) compute_gx((t + 1) & 1);  // x_{t+1} arrived during interval t-1
-      SSTAMP(1)
-      if (t + 2 < T) load_input(t + 2);         // (waits for the producer here, off the recurrent path)
-      SSTAMP(2)
-      if (t >= 1) store_outputs(t - 1);         // slot (t-1)&1 was filled by the recurrence before barrier t-1
-      SSTAMP(3)
+      // step t's keep bytes, into slot t & 1: read by the recurrent waves at the top of step t+1 (and after
+      // the loop for step T-1); the slot is rewritten in interval t+2, after barrier t+1
+      draw_mask(t);
+      if (t + 1 < T) {
+        compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
+        SSTAMP(1)
+        if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
+        SSTAMP(2)
+      }
       __syncthreads();
-      SSTAMP(4)
+      SSTAMP(3)
     }
     SSTAMP_FLUSH(0, 1, w == 0)
-    store_outputs(T - 1);
-    mta_wait_vmem();
-    __syncthreads();  // final barrier
-    if (!last && w == 0 && lane == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // final barrier (the recurrent waves publish after it)
     return;
   }
 
   // =========================== recurrent waves ===========================
   const float* w_hh = a.w_hh[layer];
-  const bool keep_stash = a.stash[layer] != nullptr;
+  float* hseq = a.hseq[layer];
+  float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
+  float* xout = last ? nullptr : a.xdrop[layer + 1];
+  unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
 
   bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
   float Bf[4][PREC == PREC_F32 ? KF : 1];
@@ -432,6 +392,47 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   __syncthreads();  // pre-loop barrier
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 pgi, pgf, pgg, pgo, pcc;
+  float ph[4];
+  // issue order per step: hand-off stores, then the 5 stash stores; the loop-head vmcnt(STASH) then drains
+  // the previous step's hand-offs (in-order completion) and leaves its stash stores another step
+  const float keep_scale = 1.0f / (1.0f - a.drop_p);
+  // h (and its dropout-masked copy) leave as ONE 16-byte store per lane: the wave's 16 x 16 (sequence, unit)
+  // block is transposed through its own LDS scratch (same-wave LDS ops are ordered: no barrier) so lane
+  // (s, c) holds units 4c..4c+3 of sequence s.  Four 4-byte write-through stores per value cost ~75 cycles
+  // each of recurrent-wave issue (r2 stamp probe), a 16-byte one about as much as a plain store.
+  float (*trh)[TRS] = sm.tr[w][0];
+  float (*trx)[TRS] = sm.tr[w][1];
+  const int ts = lane >> 2, tc = 4 * (lane & 3);
+  auto store_step = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) trh[4 * q + i][j] = ph[i];
+    if (xout) {
+      const uint32_t kb = sm.keep[t & 1][w][lane];  // drawn by the input waves during step t
+#pragma unroll
+      for (int i = 0; i < 4; ++i) trx[4 * q + i][j] = ph[i] * (((kb >> (8 * i)) & 0xFFu) ? keep_scale : 0.f);
+    }
+    const size_t o = ((size_t)t * Np + n0 + ts) * H + 16 * w + tc;
+    const float4 hv = *reinterpret_cast<const float4*>(&trh[ts][tc]);
+    if (xout) {
+      const float4 xv = *reinterpret_cast<const float4*>(&trx[ts][tc]);
+      store_sc1_x4(xout + o, f32x4{xv.x, xv.y, xv.z, xv.w});
+    }
+    if (last) *reinterpret_cast<float4*>(hseq + o) = hv;  // consumed after the kernel: plain store
+    else store_sc1_x4(hseq + o, f32x4{hv.x, hv.y, hv.z, hv.w});
+  };
+  // the 5 stash stores of step t-1 are spread over the MFMA chain of step t (one per gate group): issued
+  // together at the top they stalled the wave ~1000 cycles on the CU's store path (28 KB per step per
+  // workgroup, r2 stamp probe); between MFMAs the path drains in the background.  Issue order per step stays
+  // [hand-offs, 5 stash], so the loop-head vmcnt(STASH) is unchanged.
+  auto stash_store = [&](int t, int k) {
+    if (stash && t >= 0) {
+      float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane) + 64 * k;
+      const f32x4 v = k == 0 ? pgi : k == 1 ? pgf : k == 2 ? pgg : k == 3 ? pgo : pcc;
+      *st = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+
   SSTAMP_DECL
   for (int t = 0; t < T; ++t) {
     SSTAMP(0)
@@ -446,6 +447,17 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[3][i] = v.w;
     }
     SSTAMP(1)
+    // the hand-off stores issued at the previous top (a whole step ago)
+    if (stash && t >= 2) mta_wait_vmcnt<STASH>();
+    else mta_wait_vmem();
+    // progress: hand-off stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
+    // the barrier that ended step t-1
+    if (!last && t >= 3 && threadIdx.x == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    SSTAMP(2)
+    if (t > 0) store_step(t - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    SSTAMP(3)
 
     if constexpr (PREC == PREC_F32) {
       const float* hrow = &h_f[cur][j][q * KF];
@@ -454,28 +466,42 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         const float av = hrow[kk];
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Bf[g][kk], acc[g]);
+        if (kk < STASH) {
+          __builtin_amdgcn_sched_barrier(0);
+          stash_store(t - 1, kk);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     } else {
+      // stages of 4 independent MFMAs (one per gate chain): per k-block [lo x hi, hi x lo,] hi x hi; the
+      // stash stores go between stages
+      constexpr int NSTAGE = KB * (PREC == PREC_BF16X3 ? 3 : 1);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
-        if constexpr (PREC == PREC_BF16X3) {
-          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
+        bf16x8 alo;
+        if constexpr (PREC == PREC_BF16X3) alo = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
+#pragma unroll
+        for (int sg = 0; sg < (PREC == PREC_BF16X3 ? 3 : 1); ++sg) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            acc[g] = mfma16x16x32(alo, Bhi[g][kb], acc[g]);
-            acc[g] = mfma16x16x32(ahi, Blo[g][kb], acc[g]);
+            if (PREC == PREC_BF16X3 && sg == 0) acc[g] = mfma16x16x32(alo, Bhi[g][kb], acc[g]);
+            else if (PREC == PREC_BF16X3 && sg == 1) acc[g] = mfma16x16x32(ahi, Blo[g][kb], acc[g]);
+            else acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
           }
-        }
+          const int stage = kb * (PREC == PREC_BF16X3 ? 3 : 1) + sg;
+          __builtin_amdgcn_sched_barrier(0);
+          // spread the 5 stores over the stages (all of them by the last stage)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
+          for (int k = stage * STASH / NSTAGE; k < (stage + 1) * STASH / NSTAGE; ++k) stash_store(t - 1, k);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
-    SSTAMP(2)
+    SSTAMP(4)
 
     const int nb = (t + 1) & 1;
     float h[4];
-    f32x4 pgi, pgf, pgg, pgo, pcc;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       pgi[i] = mta_sigmoid(acc[0][i]);
@@ -485,8 +511,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
       pcc[i] = c[i];
       h[i] = pgo[i] * mta_tanh(c[i]);
+      ph[i] = h[i];
     }
-    SSTAMP(3)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s4 = 4 * q + i;
@@ -498,21 +524,19 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         h_hi[nb][s4][u] = hi;
         if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
       }
-      sm.hout[cur][s4][u] = h[i];
     }
-    if (keep_stash) {
-      sm.sto[cur][w][0][lane] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
-      sm.sto[cur][w][1][lane] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
-      sm.sto[cur][w][2][lane] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
-      sm.sto[cur][w][3][lane] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
-      sm.sto[cur][w][4][lane] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
-    }
-    SSTAMP(4)
-    __syncthreads();
     SSTAMP(5)
+    __syncthreads();
+    SSTAMP(6)
   }
   SSTAMP_FLUSH(0, 0, wave == 0)
-  __syncthreads();  // final barrier (the input waves drain step T-1 and publish after it)
+  store_step(T - 1);
+#pragma unroll
+  for (int k = 0; k < STASH; ++k) stash_store(T - 1, k);
+  mta_wait_vmem();
+  __syncthreads();  // final barrier
+  if (!last && threadIdx.x == 0)
+    __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int H, int PREC, int FIN0>
@@ -545,7 +569,7 @@ struct StackBwdArgs {
   const float* dh_last;   // (N, H): gradient wrt h_{T-1} of the top layer
   float* dG[MAXL];        // (T, Np, 4H) per layer, unit-major columns
   float* dX[MAXL];        // dX[l] (l < L-1): gradient wrt layer l's output sequence, written by layer l+1
-  const uint8_t* mask[MAXL];  // mask[l] (l >= 1, dropout): keep bytes of layer l's input dropout (forward)
+  const uint32_t* mask[MAXL];  // mask[l] (l >= 1, dropout): keep-byte words of layer l's input dropout (fwd)
   uint64_t* seeds;        // [MAXL]: dropout seed of layer l's input (advanced by the launch's last workgroup)
   float drop_p;
   int dropout;
@@ -567,6 +591,7 @@ struct BwdSmem {
   __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float g_f[2][S][PREC == PREC_F32 ? ROWF : 4];
   float dhs[2][S][H];  // dH_t of the layer above, staged by the gradient waves
+  float tr[H / 16][S][TRS];  // per-gradient-wave transpose scratch of the dx store
 };
 
 // Backward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run BPTT exactly like lstm.hip (dG_t from the
@@ -600,7 +625,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     // =========================== gradient waves ===========================
     const float* dH = TOP ? nullptr : a.dX[layer];
     float* dXout = BOTTOM ? nullptr : a.dX[layer - 1];
-    const uint8_t* min = (!BOTTOM && a.dropout) ? a.mask[layer] : nullptr;
+    const uint32_t* min = (!BOTTOM && a.dropout) ? a.mask[layer] : nullptr;
     const float keep_scale = 1.0f / (1.0f - a.drop_p);
     unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
@@ -636,13 +661,10 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
-    uint32_t mreg[4] = {1u, 1u, 1u, 1u};
+    uint32_t mreg = 0x01010101u;
     auto load_mask = [&](int t) {  // keep bytes of step t (rows 4q+i, unit u) for dx_step(t), one interval ahead
       if constexpr (!BOTTOM) {
-        if (min) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) mreg[i] = min[((size_t)t * Np + n0 + 4 * q + i) * H + u];
-        }
+        if (min) mreg = min[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u];
       }
     };
     auto stage_dh = [&](int t) {
@@ -670,13 +692,17 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
             ax[kb & 1] = mfma16x16x32(ahi, Xhi[kb], ax[kb & 1]);
           }
         }
+        // one 16-byte write-through store per lane (transpose through the wave's own LDS scratch)
+        float (*tr)[TRS] = sm.tr[w];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
           float v = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
-          if (min) v *= mreg[i] ? keep_scale : 0.f;
-          store_sc1(dXout + (size_t)row * H + u, v);
+          if (min) v *= ((mreg >> (8 * i)) & 0xFFu) ? keep_scale : 0.f;
+          tr[4 * q + i][j] = v;
         }
+        const int ts = lane >> 2, tc = 4 * (lane & 3);
+        const float4 dv = *reinterpret_cast<const float4*>(&tr[ts][tc]);
+        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, f32x4{dv.x, dv.y, dv.z, dv.w});
       }
     };
     if constexpr (!TOP) {
@@ -970,7 +996,7 @@ extern "C" long mta_lstm_stack_flag_words(int Np) {
 
 extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                                   const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
-                                  float* const* hseq, float* const* xdrop, uint8_t* const* mask,
+                                  float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                   float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
                                   int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
@@ -1010,7 +1036,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
                                   float* const* g_whh, float* const* g_bih, float* const* g_bhh,
-                                  const uint8_t* const* mask, uint64_t* seeds, float drop_p, int dropout,
+                                  const uint32_t* const* mask, uint64_t* seeds, float drop_p, int dropout,
                                   unsigned* flags, int N, int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T >= (1 << EPOCH_SHIFT)) return -1;
   StackBwdArgs a{};

@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
   float* x = dev_rand((size_t)N * T * FIN, 1.f);
   std::vector<float*> wih(L), whh(L), bih(L), bhh(L), hseq(L), xdrop(L, nullptr), stash(L), dG(L), dX(L, nullptr),
       inp(L), gwih(L), gwhh(L), gbih(L), gbhh(L);
-  std::vector<uint8_t*> mask(L, nullptr);
+  std::vector<uint32_t*> mask(L, nullptr);
   for (int l = 0; l < L; ++l) {
     const int fin = l == 0 ? FIN : H;
     wih[l] = dev_rand((size_t)4 * H * fin, k);
@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(a));
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
                             hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
-                            const_cast<const uint8_t* const*>(mask.data()), seeds, 0.2f,
+                            const_cast<const uint32_t* const*>(mask.data()), seeds, 0.2f,
                             1, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
@@ -125,8 +125,8 @@ int main(int argc, char** argv) {
   unsigned long long acc[2][2][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
   const char* seg[2][2][8] = {
-      {{"", "gx_lds_read", "mfma_chain", "activations", "lds_writes", "barrier", "", ""},
-       {"", "wait+compute_gx", "load_input(poll)", "store_outputs", "barrier", "", "", ""}},
+      {{"", "gx_lds_read", "vmcnt_drain", "store_issue", "mfma_chain", "act+lds_write", "barrier", ""},
+       {"", "mask+compute_gx", "load_input(poll)", "barrier", "", "", "", ""}},
       {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
         "mfma_dh"},
        {"", "vmem_wait", "flags+dx", "stage+load_dh+mask", "barrier", "", "", ""}}};

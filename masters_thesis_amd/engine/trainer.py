@@ -114,6 +114,8 @@ class Trainer:
         self._graph_loaders: Dict[int, Any] = {}  # keeps loaders alive while graphs key on id(loader)
         self._eager_counts: Dict[Tuple, int] = {}
         self._ones: Dict[Tuple, torch.Tensor] = {}
+        # models exposing fused_training_step run it instead of training_step + backward (MTA_FUSED_STEP=0: off)
+        self.fused_step = os.environ.get("MTA_FUSED_STEP", "1") != "0"
         self.step_timer = StepTimer()
         self.perf: Dict[str, float] = {}
         self._in_graph = False
@@ -233,8 +235,12 @@ class Trainer:
         The fused optimizer leaves the flat gradient zeroed, so a step that follows one needs no fill."""
         if not getattr(self.optimizer, "grads_zeroed", False):
             self.flat.grad.zero_()
-        loss = self.model.training_step(batch, batch_idx)
-        loss.backward(self._seed_grad(loss))
+        fused = getattr(self.model, "fused_training_step", None)
+        if fused is not None and self.fused_step and self.model.fused_step_supported(batch):
+            loss = fused(batch, batch_idx)  # forward + decoder + backward without autograd
+        else:
+            loss = self.model.training_step(batch, batch_idx)
+            loss.backward(self._seed_grad(loss))
         if not self._in_graph or self._allreduce_in_graph():
             self.ddp.allreduce_grads()
             self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)

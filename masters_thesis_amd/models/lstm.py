@@ -25,7 +25,8 @@ from ..engine.module import LightningModule
 from ..metrics import (LinkedMAE, LinkedMSE, LinkedNLL, LinkedTotal, MeanAbsoluteError, MetricAccumulator,
                        MultivariateGaussianNLLLoss)
 from ..ops import lstm as lstm_op
-from ..ops.losses import heads_losses
+from ..ops._lib import use_hip
+from ..ops.losses import heads_losses, heads_losses_train, train_decoder_fits
 
 
 class LSTMStack(torch.nn.Module):
@@ -143,6 +144,45 @@ class FinancialLstm(LightningModule):
             acc=acc.acc)
         return mse, nll, mae, total
 
+    # ---- fused training step (no autograd: 4 launches per step) ------------------------------------
+    # loss names logged by training_step (subclasses)
+    train_log_names: Tuple[str, ...] = ("mse",)
+
+    def fused_step_supported(self, batch) -> bool:
+        """The whole training step as [pipelined LSTM forward, one-launch decoder (losses, metrics, dh, head
+        grads), pipelined LSTM backward (+ weight grads)] without autograd: HIP path, pipelined kernel
+        applicable, decoder small enough for one workgroup."""
+        x, y = batch[0], batch[1]
+        if self.backend == "torch" or not use_hip(x) or not self.training:
+            return False
+        if any(p.grad is None for p in self.parameters()):
+            return False
+        ctx = x.flatten(0, 1)
+        drop = self.lstm.dropout if self.lstm.num_layers > 1 else 0.0
+        return (lstm_op.pipeline_supported(ctx, self.lstm.flat_weights, self.lstm.num_layers)
+                and (drop == 0.0 or self.lstm.seeds is not None)
+                and train_decoder_fits(ctx.shape[0], int(y.shape[2])))
+
+    def fused_training_step(self, batch, batch_idx):
+        """``training_step`` + ``loss.backward()`` in one go; gradients accumulate into the parameters' ``.grad``
+        (the flat buffer).  Same math and metric bookkeeping as the autograd path (tests/test_gpu_engine.py)."""
+        context, target, factor, inv_psi, B = self._unpack(batch)
+        lstm = self.lstm
+        drop = lstm.dropout if lstm.num_layers > 1 else 0.0
+        h, st = lstm_op.pipelined_forward(context.contiguous(), lstm.seeds,
+                                          lstm_op.precision_code(self.matmul_precision), float(drop), True, True,
+                                          lstm.flat_weights)
+        c_nll, c_mse = self.loss_coefficients
+        grads = (self.alpha_head.weight.grad, self.alpha_head.bias.grad, self.beta_head.weight.grad,
+                 self.beta_head.bias.grad)
+        out, dh = heads_losses_train(h, self.alpha_head.weight, self.alpha_head.bias, self.beta_head.weight,
+                                     self.beta_head.bias, target, factor, inv_psi, batch_windows=B,
+                                     want_nll=self.want_nll, nll_mode=self.nll_mode, c_nll=c_nll, c_mse=c_mse,
+                                     acc=self.train_acc.acc, grads=grads)
+        lstm_op.pipelined_backward(st, dh)
+        self._log_stage("train", self.train_acc, self.train_log_names)
+        return out[3]
+
     # ---- test hooks (`src/model.py:111-147`) ---------------------------------------------
     def on_test_start(self):
         self.test_results = {"test_loss": {"mae": None, "nll": None}}
@@ -215,6 +255,7 @@ class FinancialLstmMse(FinancialLstm):
 class FinancialLstmNll(FinancialLstm):
     loss_coefficients = (1.0, 0.0)
     want_nll = True
+    train_log_names = ("nll",)
 
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
@@ -237,6 +278,7 @@ class FinancialLstmNll(FinancialLstm):
 
 class FinancialLstmCombined(FinancialLstm):
     want_nll = True
+    train_log_names = ("mse", "nll")
 
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,

@@ -192,3 +192,31 @@ def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, ba
         res = _losses_torch(ab, y, factor, inv_psi, windows, kwin, fstride, want_nll, c_nll, c_mse,
                             float(batch_windows), acc)
     return res if with_total else res[:3]
+
+
+def train_decoder_fits(N: int, n: int) -> bool:
+    """Whether :func:`heads_losses_train`'s one-workgroup kernel takes (N sequences, n target days)."""
+    base = (3 * 2 * ((N + 1) & ~1) + ((n + 3) & ~3)) * 4
+    return base + N * n * 8 <= 96 * 1024 or base <= 60 * 1024
+
+
+def heads_losses_train(h: Tensor, wa: Tensor, ba: Tensor, wb: Tensor, bb: Tensor, y: Tensor, factor: Tensor,
+                       inv_psi: Tensor, *, batch_windows: int = 1, want_nll: bool = True, nll_mode: str = "reference",
+                       c_nll: float = 0.0, c_mse: float = 1.0, acc: Optional[Tensor] = None,
+                       grads: Tuple[Tensor, Tensor, Tensor, Tensor], out: Optional[Tensor] = None,
+                       dh: Optional[Tensor] = None):
+    """The training step's decoder without autograd, ONE HIP launch (``csrc/losses.hip``
+    ``heads_losses_train_kernel``): heads, losses + metrics into ``acc``, the encoder gradient ``dh`` = d total /
+    d h (the loss is the step's root: upstream gradient 1) and the head gradients accumulated into ``grads`` =
+    (g_wa, g_ba, g_wb, g_bb).  Returns ``(out, dh)`` with ``out = [mse, nll, mae, total]``, or None when the
+    problem is too large for the one-workgroup kernel (use :func:`heads_losses` + autograd then)."""
+    N, H = h.shape
+    windows, kwin, fstride = _windows(N, batch_windows, nll_mode)
+    if out is None:
+        out = torch.empty(4, device=h.device, dtype=torch.float32)
+    if dh is None:
+        dh = torch.empty((N, H), device=h.device, dtype=torch.float32)
+    ok = lib().heads_losses_train(h.contiguous(), wa, ba, wb, bb, y.contiguous(), factor.contiguous(),
+                                  inv_psi.contiguous(), windows, kwin, fstride, bool(want_nll), float(c_nll),
+                                  float(c_mse), float(batch_windows), out, acc, dh, *grads)
+    return (out, dh) if ok else None

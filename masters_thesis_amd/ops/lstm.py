@@ -145,10 +145,8 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
     H = weights[1].shape[1]
     N, T, F = x.shape
     tr8 = -(-(padded_rows(N) // 16) // 8) * 8
-    # all L x tiles forward workgroups co-resident: H=64 takes ~90 KB of LDS (one workgroup per CU, 256 CUs),
-    # H=32 ~46 KB (several per CU)
-    cap = 256 if H == 64 else 448
-    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= cap
+    # all L x tiles workgroups co-resident: one 8-wave workgroup per CU at 136-144 VGPRs, 256 CUs
+    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= 256
 
 
 _FLAGS = {}
@@ -193,67 +191,75 @@ def check_pipeline_health(clear: bool = True) -> None:
                            "set too low, can cause this; MTA_LSTM_PIPELINE=0 selects the per-layer kernels.")
 
 
+class PipelinedState:
+    """What the pipelined backward needs from its forward (the autograd Function's ctx, or held by the
+    trainer's fused step)."""
+    __slots__ = ("meta", "params", "seeds", "x", "stash", "hseq", "xdrop", "masks")
+
+
+def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, training: bool, need_grad: bool,
+                      flat: Sequence[Tensor]):
+    """One forward launch of every layer (csrc/lstm_stack.hip).  Returns (h_T of the top layer (N, H), state)."""
+    L = len(flat) // 4
+    N, T, F = x.shape
+    H = flat[1].shape[1]
+    Np = padded_rows(N)
+    C = lib()
+    dev = x.device
+    E = _empty(dev)
+    drop = dropout > 0.0 and training
+    if drop and not need_grad:
+        # the backward launch advances the seeds after use; without one, advance them here
+        seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))
+    hseq = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L)]
+    xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E for _ in range(1, L)]
+    EB = _empty(dev, torch.uint8)
+    # keep bytes of every inter-layer dropout, drawn by the forward's input waves and read by the backward's
+    # dx masks (u32 words (T, ntiles, 4, H): byte i of a word = sequence 4q+i of a lane)
+    masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
+    stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
+    flags = _stack_flags(C, Np, L, dev)
+    C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]), hseq,
+                     xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
+    st = PipelinedState()
+    st.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
+    st.params, st.seeds, st.x = tuple(flat), seeds, x
+    st.stash, st.hseq, st.xdrop, st.masks = stash, hseq, xdrop, masks
+    return hseq[L - 1][T - 1, :N], st
+
+
+def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
+    """One backward launch (BPTT of every layer + fused weight gradients accumulated into the parameters'
+    ``.grad`` views)."""
+    L, H, N, Np, T, F, prec, p, drop = st.meta
+    C = lib()
+    dev = dh_last.device
+    flat = st.params
+    dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
+    dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
+    flags = _stack_flags(C, Np, L, dev)
+    inp = [st.x] + [st.xdrop[l] if drop else st.hseq[l - 1] for l in range(1, L)]
+    grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
+    C.lstm_stack_bwd(H, prec, F, list(st.stash), list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
+                     list(st.hseq), inp, grads, list(st.masks) if drop else [], st.seeds, p, drop, flags, N, Np, T)
+
+
 class _LSTMPipelinedFn(torch.autograd.Function):
     """All layers in one forward launch and one backward launch (wavefront over (layer, t))."""
 
     @staticmethod
     def forward(ctx, x: Tensor, seeds: Tensor, prec: int, dropout: float, training: bool, need_grad: bool,
                 *flat: Tensor) -> Tensor:
-        L = len(flat) // 4
-        N, T, F = x.shape
-        H = flat[1].shape[1]
-        Np = padded_rows(N)
-        C = lib()
-        dev = x.device
-        E = _empty(dev)
-        drop = dropout > 0.0 and training
-        if drop and not need_grad:
-            # the backward launch advances the seeds after use; without one, advance them here
-            seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))
-        hseq = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L)]
-        xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E
-                       for _ in range(1, L)]
-        EB = _empty(dev, torch.uint8)
-        # keep bytes of every inter-layer dropout (written by the forward, read by the backward's dx masks)
-        masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB
-                        for _ in range(1, L)]
-        stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E
-                 for _ in range(L)]
-        flags = _stack_flags(C, Np, L, dev)
-        C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
-                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
-        ctx.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
-        ctx.params = flat
-        ctx.seeds = seeds
-        ctx.fwd_flags = flags
-        if need_grad:
-            ctx.save_for_backward(x, *stash, *hseq, *[t for t in xdrop[1:] if drop], *[m for m in masks[1:] if drop])
-        return hseq[L - 1][T - 1, :N]
+        out, st = pipelined_forward(x, seeds, prec, dropout, training, need_grad, flat)
+        ctx.st = st
+        return out
 
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, dh_last: Tensor):
-        L, H, N, Np, T, F, prec, p, drop = ctx.meta
-        C = lib()
-        dev = dh_last.device
-        saved = ctx.saved_tensors
-        x = saved[0]
-        stash = list(saved[1:1 + L])
-        hseq = list(saved[1 + L:1 + 2 * L])
-        xdrop = list(saved[1 + 2 * L:1 + 3 * L - 1]) if drop else []
-        masks = ([_empty(dev, torch.uint8)] + list(saved[3 * L:4 * L - 1])) if drop else []
-        flat = ctx.params
-        dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
-        dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
-        flags = _stack_flags(C, Np, L, dev)
-        inp = [x] + [xdrop[l - 1] if drop else hseq[l - 1] for l in range(1, L)]
-        # weight gradients are computed by the same launch (fused workgroups consume dG as it drains) and
-        # accumulated straight into the parameters' gradient views
-        grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
-        C.lstm_stack_bwd(H, prec, F, stash, list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
-                         hseq, inp, grads, masks, ctx.seeds, p, drop, flags, N, Np, T)
-        ctx.bwd_flags = flags
-        return (None,) * (6 + len(flat))
+        pipelined_backward(ctx.st, dh_last)
+        ctx.st = None
+        return (None,) * len(ctx.needs_input_grad)
 
 
 _PERM_CACHE = {}

@@ -65,3 +65,35 @@ def test_trainer_streaming_equals_resident():
 
     # float atomics in the weight-gradient kernel make runs differ in the last bits
     torch.testing.assert_close(run(True), run(False), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("cls_name", ["FinancialLstmMse", "FinancialLstmNll", "FinancialLstmCombined"])
+@pytest.mark.parametrize("B", [1, 2])
+def test_fused_training_step_matches_autograd(cls_name, B):
+    """models/lstm.py fused_training_step (pipelined fwd + one-launch decoder + pipelined bwd, no autograd)
+    against training_step + loss.backward(): same loss, gradients and epoch-metric sums, dropout on."""
+    import masters_thesis_amd.models as M
+    from masters_thesis_amd.ops.optim import FlatParameters
+
+    data = [t[:B].to(DEV) for t in _data(4)]
+    out = []
+    for fused in (False, True):
+        torch.manual_seed(11)
+        model = getattr(M, cls_name)(dropout=0.2).to(DEV)
+        model.lstm.seeds.copy_(torch.arange(8, device=DEV) * 977 + 5)
+        model.matmul_precision = "highest"
+        flat = FlatParameters(model.parameters())
+        model.train()
+        assert model.fused_step_supported(data)
+        if fused:
+            loss = model.fused_training_step(data, 0)
+        else:
+            loss = model.training_step(data, 0)
+            loss.backward()
+        torch.cuda.synchronize()
+        out.append((float(loss), flat.grad.clone(), model.train_acc.acc.clone(), model.lstm.seeds.clone()))
+    (la, ga, aa, sa), (lb, gb, ab, sb) = out
+    assert abs(la - lb) <= 1e-5 * abs(la), (la, lb)
+    torch.testing.assert_close(gb, ga, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(ab, aa, rtol=1e-6, atol=0)
+    assert torch.equal(sa, sb)  # dropout seeds advanced once by both paths
