@@ -29,10 +29,20 @@
 #ifndef MTA_STACK_STAMPS
 #define MTA_STACK_STAMPS 0
 #endif
+// s_sleep units (~64 cycles each) the helper waves wait after a step barrier before their MFMA product (the
+// forward input waves' W_ih x of layers >= 1, the backward gradient waves' dx): right after the barrier the
+// recurrent waves run their own MFMA chain on the same SIMDs, and two MFMA streams on one SIMD serialise.
+#ifndef MTA_STACK_GX_DELAY
+#define MTA_STACK_GX_DELAY 0
+#endif
+#ifndef MTA_STACK_DX_DELAY
+#define MTA_STACK_DX_DELAY 0
+#endif
 #if MTA_STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
 __device__ unsigned long long mta_stack_stamp_acc[2][2][8];
+__device__ int mta_stack_stamp_block[2];  // block whose waves are stamped, per direction (probe sets it)
 #define SSTAMP_DECL unsigned long long _ts_prev = 0, _ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SSTAMP(k)                                                                  \
   {                                                                                \
@@ -44,7 +54,7 @@ __device__ unsigned long long mta_stack_stamp_acc[2][2][8];
     __builtin_amdgcn_sched_barrier(0);                                             \
   }
 #define SSTAMP_FLUSH(dir, role, first_wave)                                        \
-  if (blockIdx.x == 0 && (first_wave) && (threadIdx.x & 63) == 0)                  \
+  if ((int)blockIdx.x == mta_stack_stamp_block[(dir)] && (first_wave) && (threadIdx.x & 63) == 0) \
     for (int _k = 0; _k < 8; ++_k) mta_stack_stamp_acc[(dir)][(role)][_k] = _ts_acc[_k];
 #else
 #define SSTAMP_DECL
@@ -342,6 +352,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       // the loop for step T-1); the slot is rewritten in interval t+2, after barrier t+1
       draw_mask(t);
       if (t + 1 < T) {
+        if constexpr (!FIRST && MTA_STACK_GX_DELAY > 0) __builtin_amdgcn_s_sleep(MTA_STACK_GX_DELAY);
         compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
         SSTAMP(1)
         if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
@@ -447,13 +458,23 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[3][i] = v.w;
     }
     SSTAMP(1)
-    // the hand-off stores issued at the previous top (a whole step ago)
-    if (stash && t >= 2) mta_wait_vmcnt<STASH>();
-    else mta_wait_vmem();
-    // progress: hand-off stores of step t-3 were drained by every recurrent wave's wait at the top of t-1, before
-    // the barrier that ended step t-1
-    if (!last && t >= 3 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(t - 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the hand-off stores issued two tops ago (~two steps of latency budget; one step cost ~200 cycles of
+    // drain per step, r2 stamp probe).  Newer than them: that step's 5 stash stores, the previous top's
+    // hand-offs (h, [masked h]) and its 5 stash stores (wave 0 also has a progress store in between, so
+    // its wait is one op more conservative).  The counts are immediates: branch on the uniform layout.
+    if (t >= 3) {
+      if (stash) {
+        if (xout) mta_wait_vmcnt<2 + 2 * STASH>();
+        else mta_wait_vmcnt<1 + 2 * STASH>();
+      } else {
+        if (xout) mta_wait_vmcnt<2>();
+        else mta_wait_vmcnt<1>();
+      }
+    }
+    // progress: hand-off stores of step t-4 were drained by every recurrent wave's wait at the top of t-1,
+    // before the barrier that ended step t-1
+    if (!last && t >= 4 && threadIdx.x == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)(t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     SSTAMP(2)
     if (t > 0) store_step(t - 1);
     __builtin_amdgcn_sched_barrier(0);
@@ -476,18 +497,22 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       // stages of 4 independent MFMAs (one per gate chain): per k-block [lo x hi, hi x lo,] hi x hi; the
       // stash stores go between stages
       constexpr int NSTAGE = KB * (PREC == PREC_BF16X3 ? 3 : 1);
+      // every A fragment first (the stage barriers below would otherwise expose each k-block's LDS latency)
+      bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
-        bf16x8 alo;
-        if constexpr (PREC == PREC_BF16X3) alo = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
+        ahi[kb] = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
+        if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
+      }
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
         for (int sg = 0; sg < (PREC == PREC_BF16X3 ? 3 : 1); ++sg) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            if (PREC == PREC_BF16X3 && sg == 0) acc[g] = mfma16x16x32(alo, Bhi[g][kb], acc[g]);
-            else if (PREC == PREC_BF16X3 && sg == 1) acc[g] = mfma16x16x32(ahi, Blo[g][kb], acc[g]);
-            else acc[g] = mfma16x16x32(ahi, Bhi[g][kb], acc[g]);
+            if (PREC == PREC_BF16X3 && sg == 0) acc[g] = mfma16x16x32(alo[kb], Bhi[g][kb], acc[g]);
+            else if (PREC == PREC_BF16X3 && sg == 1) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
+            else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
           }
           const int stage = kb * (PREC == PREC_BF16X3 ? 3 : 1) + sg;
           __builtin_amdgcn_sched_barrier(0);
@@ -661,10 +686,10 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
-    uint32_t mreg = 0x01010101u;
-    auto load_mask = [&](int t) {  // keep bytes of step t (rows 4q+i, unit u) for dx_step(t), one interval ahead
+    uint32_t mreg = 0x01010101u, mnext = 0x01010101u;
+    auto load_mask = [&](int t) {  // keep bytes of step t (rows 4q+i, unit u), used one interval later
       if constexpr (!BOTTOM) {
-        if (min) mreg = min[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u];
+        if (min) mnext = min[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u];
       }
     };
     auto stage_dh = [&](int t) {
@@ -710,24 +735,26 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       stage_dh(T - 1);
       if (T > 1) load_dh(T - 2);
     }
-    load_mask(T - 1);
     __syncthreads();  // B0
     SSTAMP_DECL
     for (int t = T - 1; t >= 0; --t) {
-      // ---- interval I(t) ----
+      // ---- interval I(t) ----  issue order: [flags, dH loads, keep-byte load, dx store].  The dx product runs
+      // last, while the recurrent waves are in their VALU phase (their dh MFMAs run right after A(t+1); two
+      // MFMA streams on one SIMD serialise, r2 stamp probe), and its store stays in flight across the barrier:
+      // vmcnt(1) waits for this wave's loads of the previous interval and everything older than its dx store.
       SSTAMP(0)
-      mta_wait_vmem();  // this wave's dH / keep-byte loads and its dx stores of the previous interval
+      if constexpr (BOTTOM) mta_wait_vmem();
+      else mta_wait_vmcnt<1>();
+      mreg = mnext;
       SSTAMP(1)
-      // progress: dx of steps >= t+3 (stored in I(t+2)) was drained by every gradient wave's wait in
+      // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait in
       // I(t+1), before barrier A(t+1)
-      if (!BOTTOM && t + 3 <= T - 1 && wave == NW && lane == 0)
-        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
+        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // dG progress: every recurrent wave passed its top-of-(t+1) vmcnt wait before A(t+1), which drains
       // its dG stores of steps >= t+4
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t + 1 <= T - 1) dx_step(t + 1);
-      SSTAMP(2)
       if constexpr (!TOP) {
         if (t >= 1) {
           stage_dh(t - 1);
@@ -735,11 +762,16 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         }
       }
       load_mask(t);  // for dx_step(t) in I(t-1)
+      SSTAMP(2)
+      if (MTA_STACK_DX_DELAY > 0 && !BOTTOM) __builtin_amdgcn_s_sleep(MTA_STACK_DX_DELAY);
+      if (t + 1 <= T - 1) dx_step(t + 1);
       SSTAMP(3)
       __syncthreads();  // A(t)
       SSTAMP(4)
     }
     SSTAMP_FLUSH(1, 1, w == 0)
+    mta_wait_vmem();
+    mreg = mnext;
     dx_step(0);
     mta_wait_vmem();
     __syncthreads();  // F

@@ -42,6 +42,9 @@ int main(int argc, char** argv) {
   const int L = argc > 2 ? atoi(argv[2]) : 2;
   const int prec = argc > 3 ? atoi(argv[3]) : PREC_BF16X3;
   const int T = argc > 4 ? atoi(argv[4]) : 60;
+  // mode 0: training with dropout 0.2 (the headline step); 1: training, no dropout; 2: inference (no stash)
+  const int mode = argc > 5 ? atoi(argv[5]) : 0;
+  const float p = mode == 0 ? 0.2f : 0.0f;
   const int Np = (N + 15) / 16 * 16;
   if (L < 2 || L > 8 || N < 1 || T < 4 || T > 1000) {
     printf("bad arguments\n");
@@ -59,18 +62,18 @@ int main(int argc, char** argv) {
     bih[l] = dev_rand(4 * H, k);
     bhh[l] = dev_rand(4 * H, k);
     hseq[l] = dev_zero((size_t)T * Np * H);
-    if (l >= 1) {
+    if (l >= 1 && mode == 0) {
       xdrop[l] = dev_zero((size_t)T * Np * H);
       CK(hipMalloc(&mask[l], (size_t)T * Np * H));
     }
     if (l < L - 1) dX[l] = dev_zero((size_t)T * Np * H);
-    stash[l] = dev_zero((size_t)T * Np * 5 * H);
+    stash[l] = mode == 2 ? nullptr : dev_zero((size_t)T * Np * 5 * H);
     dG[l] = dev_zero((size_t)T * Np * 4 * H);
     gwih[l] = dev_zero((size_t)4 * H * fin);
     gwhh[l] = dev_zero((size_t)4 * H * H);
     gbih[l] = dev_zero(4 * H);
     gbhh[l] = dev_zero(4 * H);
-    inp[l] = l == 0 ? x : xdrop[l];
+    inp[l] = l == 0 ? x : (mode == 0 ? xdrop[l] : hseq[l - 1]);
   }
   float* dh_last = dev_rand((size_t)N * H, 1.f);
   uint64_t* seeds;
@@ -83,6 +86,15 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&flags, nflags * 4));
   CK(hipMemset(flags, 0, nflags * 4));
 
+#if MTA_STACK_STAMPS
+  // stamp the last layer's first tile in the forward (its input waves run the W_ih MFMAs: the slowest layer)
+  // and the top layer's first tile in the backward (block 0: its gradient waves run the dx MFMAs)
+  const int ntiles = Np / 16, tr8 = (ntiles + 7) / 8 * 8;
+  const int which = argc > 6 ? atoi(argv[6]) : L - 1;
+  int sb[2] = {which * tr8, 0};
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(mta_stack_stamp_block), sb, sizeof(sb)));
+  printf("stamping forward layer %d (block %d), backward block 0 (top layer)\n", which, sb[0]);
+#endif
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -92,7 +104,7 @@ int main(int argc, char** argv) {
     float m;
     CK(hipEventRecord(a));
     int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                xdrop.data(), mask.data(), stash.data(), seeds, 0.2f, flags, N, Np, T, 0);
+                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -101,11 +113,12 @@ int main(int argc, char** argv) {
     }
     CK(hipEventElapsedTime(&m, a, b));
     if (rep >= skip) ms_f += m / (reps - skip);
+    if (mode == 2) continue;
     CK(hipEventRecord(a));
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
                             hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
-                            const_cast<const uint32_t* const*>(mask.data()), seeds, 0.2f,
-                            1, flags, N, Np, T, 0);
+                            const_cast<const uint32_t* const*>(mask.data()), seeds, p,
+                            mode == 0 ? 1 : 0, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -117,9 +130,9 @@ int main(int argc, char** argv) {
   }
   unsigned tmo = 0;
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
-  printf("N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
+  printf("mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
          "timeouts=%u\n",
-         N, L, T, prec, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         mode, N, L, T, prec, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
 #if MTA_STACK_STAMPS
   unsigned long long acc[2][2][8];
@@ -129,7 +142,7 @@ int main(int argc, char** argv) {
        {"", "mask+compute_gx", "load_input(poll)", "barrier", "", "", "", ""}},
       {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
         "mfma_dh"},
-       {"", "vmem_wait", "flags+dx", "stage+load_dh+mask", "barrier", "", "", ""}}};
+       {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
   const char* role[2][2] = {{"recurrent", "input"}, {"recurrent", "gradient"}};
   for (int d = 0; d < 2; ++d)

@@ -13,6 +13,12 @@ CLI (``key=value`` overrides, ``-m/--multirun``, ``--cfg job|hydra|all``,
 * ``gpu_pool`` – MI355X addition: every trial is a child process pinned to one
   GPU through ``HIP_VISIBLE_DEVICES`` (``jobs_per_device`` trials per GPU), so
   an 18-trial sweep (`sweeps/experiment_synthetic.sh`) fills an 8-GPU node.
+
+Failure handling of the child-process launchers: a trial that exits non-zero is re-queued up
+to ``max_retries`` times with ``resume=auto`` (it continues from its own ``last.ckpt`` when one exists);
+``heartbeat_timeout_s > 0`` additionally kills a trial whose heartbeat file (touched by the trainer at
+every epoch boundary and every 500 steps, ``MTA_HEARTBEAT_FILE``) went stale — a hung GPU or collective —
+and retries it the same way.  ``MTA_RETRY_ATTEMPT`` tells the child which attempt it is.
 """
 from __future__ import annotations
 
@@ -135,34 +141,58 @@ def _launch_children(jobs: List[List[Override]], sweep_dir: Path, launcher: Dict
         n = int(launcher.get("n_jobs", -1) or -1)
         n = os.cpu_count() if n < 0 else n
         slots = [None] * max(1, n)
-    pending = list(enumerate(jobs))
+    max_retries = int(launcher.get("max_retries", 0) or 0)
+    hb_timeout = float(launcher.get("heartbeat_timeout_s", 0) or 0)
+    pending = [(num, ovs, 0) for num, ovs in enumerate(jobs)]
     running = {}
     results = {}
     free = list(range(len(slots)))
     while pending or running:
         while pending and free:
             slot = free.pop(0)
-            num, ovs = pending.pop(0)
+            num, ovs, attempt = pending.pop(0)
             env = dict(os.environ)
             env[_ENV_CHILD] = "1"
+            env["MTA_RETRY_ATTEMPT"] = str(attempt)
+            # parallel CPU children must not oversubscribe the cores (spinning OpenMP pools starve each other)
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // len(slots))))
+            hb = sweep_dir / f"job{num}.heartbeat"
+            env["MTA_HEARTBEAT_FILE"] = str(hb)
+            hb.write_text(str(time.time()))
             if slots[slot] is not None:
                 env["HIP_VISIBLE_DEVICES"] = str(slots[slot])
-            cmd = [sys.executable, script_argv0, *base_flags, *[o.text() for o in ovs],
+            extra = ["resume=auto"] if attempt > 0 else []
+            cmd = [sys.executable, script_argv0, *base_flags, *[o.text() for o in ovs], *extra,
                    f"hydra.run.dir={sweep_dir}/{num}", f"hydra.job.num={num}"]
-            log_f = open(sweep_dir / f"job{num}.out", "w")
+            log_f = open(sweep_dir / f"job{num}.out", "a" if attempt else "w")
             p = subprocess.Popen(cmd, env=env, stdout=log_f, stderr=subprocess.STDOUT)
-            running[p] = (slot, num, log_f)
-            print(f"[launcher:{kind}] job #{num} on slot {slots[slot]}: {' '.join(o.text() for o in ovs)}", flush=True)
+            running[p] = (slot, num, ovs, attempt, log_f, hb)
+            print(f"[launcher:{kind}] job #{num} (attempt {attempt}) on slot {slots[slot]}: "
+                  f"{' '.join(o.text() for o in ovs)}", flush=True)
+        if hb_timeout > 0:
+            now = time.time()
+            for p, (slot, num, _, attempt, _, hb) in running.items():
+                try:
+                    stale = now - hb.stat().st_mtime
+                except OSError:
+                    stale = 0.0
+                if p.poll() is None and stale > hb_timeout:
+                    print(f"[launcher:{kind}] job #{num} heartbeat stale for {stale:.0f}s: killing it", flush=True)
+                    p.kill()
         done = [p for p in running if p.poll() is not None]
         if not done:
             time.sleep(0.2)
             continue
         for p in done:
-            slot, num, log_f = running.pop(p)
+            slot, num, ovs, attempt, log_f, hb = running.pop(p)
             log_f.close()
-            results[num] = p.returncode
             free.append(slot)
-            if p.returncode != 0:
+            results[num] = p.returncode
+            if p.returncode != 0 and attempt < max_retries:
+                print(f"[launcher:{kind}] job #{num} FAILED (exit {p.returncode}); retry {attempt + 1}/{max_retries} "
+                      f"with resume=auto", flush=True)
+                pending.append((num, ovs, attempt + 1))
+            elif p.returncode != 0:
                 print(f"[launcher:{kind}] job #{num} FAILED (exit {p.returncode}); see {sweep_dir}/job{num}.out",
                       flush=True)
     return [results[i] for i in range(len(jobs))]

@@ -91,6 +91,11 @@ class Trainer:
         self.default_root_dir = default_root_dir
         env_fail = os.environ.get("MTA_FAIL_AT_STEP")
         self.fail_at_step = int(env_fail) if env_fail else fail_at_step
+        # fault injection on the first MTA_FAIL_ATTEMPTS launcher attempts only (transient-failure tests)
+        attempts = os.environ.get("MTA_FAIL_ATTEMPTS")
+        if attempts is not None and int(os.environ.get("MTA_RETRY_ATTEMPT", "0")) >= int(attempts):
+            self.fail_at_step = None
+        self.heartbeat_file = os.environ.get("MTA_HEARTBEAT_FILE")
         self.deterministic = deterministic
         # state
         self.current_epoch = 0
@@ -429,6 +434,15 @@ class Trainer:
                 break
             self._eval_step(stage, loader, i, False, batch)
 
+    def heartbeat(self) -> None:
+        """Touch the launcher's heartbeat file (hang detection of the gpu_pool / joblib child launchers)."""
+        if self.heartbeat_file:
+            try:
+                with open(self.heartbeat_file, "w") as f:
+                    f.write(f"{time.time()} {self.global_step}\n")
+            except OSError:
+                pass
+
     def _check_device_health(self) -> None:
         """Raise if a pipelined LSTM launch gave up on a hand-off (its results were garbage)."""
         if self.device.type == "cuda":
@@ -474,6 +488,8 @@ class Trainer:
         def pre_step(i):
             if self.fail_at_step is not None and self.global_step == self.fail_at_step:
                 raise RuntimeError(f"fault injection: MTA_FAIL_AT_STEP={self.fail_at_step}")
+            if self.heartbeat_file and i % 500 == 0:
+                self.heartbeat()
             if self.enable_progress_bar and self.is_global_zero and (i % 500 == 0 or i == n_batches - 1):
                 sys.stdout.write(f"\rEpoch {epoch}: {i + 1}/{n_batches}")
                 sys.stdout.flush()
@@ -574,6 +590,7 @@ class Trainer:
                 for c in self.callbacks:
                     c.on_validation_end(self, model)
             model.on_train_epoch_end()
+            self.heartbeat()
             for c in self.callbacks:
                 c.on_train_epoch_end(self, model)
             self._step_scheduler(epoch)

@@ -144,9 +144,12 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
         return False
     H = weights[1].shape[1]
     N, T, F = x.shape
-    tr8 = -(-(padded_rows(N) // 16) // 8) * 8
-    # all L x tiles workgroups co-resident: one 8-wave workgroup per CU at 136-144 VGPRs, 256 CUs
-    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and num_layers * tr8 <= 256
+    # No co-residency cap: a hand-off's producer workgroup always has a lower block id than its consumers
+    # (layer-major ids; the backward lists the top layer first), so with in-order dispatch every resident
+    # spinning workgroup's producers are resident or finished.  Grids beyond one workgroup per CU (large
+    # batches: B=64 is 800 workgroups) run in waves instead of falling back to per-layer launches and
+    # T x Np x 4H gate tensors.
+    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and T < 4096
 
 
 _FLAGS = {}

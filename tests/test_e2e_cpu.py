@@ -126,3 +126,20 @@ def test_report_delta_and_best_ckpt(tmp_path):
     bad = _run([str(REPO / "train.py"), *TINY, "trainer.max_epochs=1", "test_ckpt=worst", "logger.version=bad"],
                tmp_path, ok=False)
     assert bad.returncode != 0 and "test_ckpt" in (bad.stdout + bad.stderr)
+
+
+def test_launcher_retries_failed_trial_with_auto_resume(tmp_path):
+    """SURVEY §5 failure handling: a trial that dies (fault injection on its first attempt only) is re-queued by
+    the child-process launcher with resume=auto and finishes from its own last.ckpt."""
+    r = _run([str(REPO / "train.py"), "-m", *TINY, "trainer.max_epochs=2", "model.learning_rate=0.001,0.0001",
+              "hydra/launcher=joblib", "hydra.launcher.n_jobs=2", "hydra.launcher.max_retries=1"], tmp_path,
+             env={"MTA_FAIL_AT_STEP": "90", "MTA_FAIL_ATTEMPTS": "1"})
+    assert r.stdout.count("retry 1/1 with resume=auto") == 2, r.stdout
+    outs = sorted((tmp_path / "multirun").glob("*/*/job*.out"))
+    assert len(outs) == 2
+    for o in outs:
+        text = o.read_text()
+        assert "fault injection" in text and "resuming from" in text and "Test MAE" in text
+    for v in ("mse_small_lr0.001_fast", "mse_small_lr0.0001_fast"):
+        ck = torch.load(tmp_path / "logs/FinancialLstm/synthetic" / v / "checkpoints/last.ckpt", weights_only=True)
+        assert ck["epoch"] == 1

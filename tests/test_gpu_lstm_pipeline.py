@@ -103,6 +103,29 @@ def test_pipelined_matches_fp64(prec, N, T, F, H, L):
         assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad w{i}: err {e} (scale {sc})"
 
 
+def test_pipelined_grid_beyond_one_workgroup_per_cu():
+    """L x tiles > 256 workgroups (not all co-resident): producers always precede consumers in block order, so
+    the grid drains in waves and stays exact (large batches take this path instead of per-layer launches)."""
+    from masters_thesis_amd.ops import lstm as op
+
+    torch.manual_seed(7)
+    N, T, F, H, L = 2100, 10, 3, 64, 3   # 132 tiles -> 136 x 3 = 408 workgroups per launch
+    x = torch.randn(N, T, F)
+    ws = _weights(F, H, L, seed=5)
+    R = torch.randn(N, H)
+    ref, w64 = _ref(x, ws, L)
+    (ref * R.double()).sum().backward()
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    assert op.pipeline_supported(x.to(DEV), wg, L)
+    out = op.lstm_last_hidden(x.to(DEV), wg, L, 0.0, True, "highest")
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    assert (out.double().cpu() - ref.detach()).abs().max().item() <= 2e-5 * max(ref.abs().max().item(), 1.0)
+    for a, b in zip(wg, w64):
+        assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-4 * max(b.grad.abs().max().item(), 1e-3)
+    op.check_pipeline_health()
+
+
 def test_pipelined_dropout_masks_match_counter_hash():
     from masters_thesis_amd.ops import lstm as op
 

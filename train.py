@@ -8,7 +8,8 @@
     python train.py -m loss=combined loss.mse_weight=0.3,0.5,0.7
     torchrun --nproc-per-node 8 train.py ...          # DDP, one process per MI355X (RCCL/xGMI)
 
-MI355X additions (all optional): ``resume=<ckpt>`` (full state), ``init_from=<ckpt>``
+MI355X additions (all optional): ``resume=<ckpt>|auto`` (full state; ``auto`` = this run's own
+last.ckpt if present, used by the launcher's retries), ``init_from=<ckpt>``
 (weights only: the thesis' synthetic->real warm-up), ``seed=<int>``,
 ``+trainer.use_hip_graphs=false``, ``+trainer.matmul_precision=highest|high|medium``,
 ``trainer.precision=bf16-mixed``, ``hydra/launcher=gpu_pool`` (one trial per GPU),
@@ -108,7 +109,13 @@ def main(cfg):
     print("\n" + "=" * 50)
     print("Starting Training...")
     print("=" * 50 + "\n")
-    trainer.fit(model, datamodule=dm, ckpt_path=cfg.get("resume"))
+    resume = cfg.get("resume")
+    if resume == "auto":
+        # launcher retries (max_retries): continue from this run's own last checkpoint when there is one
+        last = checkpoint_dir / "last.ckpt"
+        resume = str(last) if last.exists() else None
+        print(f"resume=auto: {'resuming from ' + resume if resume else 'no checkpoint yet, starting fresh'}")
+    trainer.fit(model, datamodule=dm, ckpt_path=resume)
 
     ckpt_cb = trainer.checkpoint_callback
     best = ckpt_cb.best_model_score
