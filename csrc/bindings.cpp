@@ -14,7 +14,9 @@ int mta_lstm_fwd_layer(int H, int prec, const float* x, const float* w_ih, const
 int mta_lstm_bwd_layer(int H, int prec, const float* stash, const float* w_hh, const float* dH, const float* dh_last,
                        float* dG, int N, int Np, int T, hipStream_t st);
 int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* inp, int inp_batch_first, int N, int Np,
-                   int T, int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, hipStream_t st);
+                   int T, int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, float* part,
+                   hipStream_t st);
+long mta_lstm_wgrad_part_floats(int fused, int T, int H, int F);
 void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
                    hipStream_t st);
 void mta_gather_batch(const float* const* src, float* const* dst, const long* row_floats, int ntensors,
@@ -65,8 +67,9 @@ int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const fl
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
-                       float* const* g_bih, float* const* g_bhh, const uint32_t* const* mask, uint64_t* seeds,
-                       float drop_p, int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st);
+                       float* const* g_bih, float* const* g_bhh, const uint32_t* const* mask, float* const* part,
+                       uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
+                       hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
@@ -153,7 +156,8 @@ void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor stash, at::Tensor w_hh, 
 }
 
 void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_first, int64_t N, int64_t Np,
-                int64_t T, int64_t H, at::Tensor g_wih, at::Tensor g_whh, at::Tensor g_bih, at::Tensor g_bhh) {
+                int64_t T, int64_t H, at::Tensor g_wih, at::Tensor g_whh, at::Tensor g_bih, at::Tensor g_bhh,
+                const OptT& part) {
   MTA_CHECK_F32(dG);
   MTA_CHECK_F32(hseq);
   MTA_CHECK_F32(inp);
@@ -169,7 +173,7 @@ void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bo
   const int rc = mta_lstm_wgrad((int)prec, dG.data_ptr<float>(), hseq.data_ptr<float>(), inp.data_ptr<float>(),
                                 inp_batch_first ? 1 : 0, (int)N, (int)Np, (int)T, (int)H, (int)F,
                                 g_wih.data_ptr<float>(), g_whh.data_ptr<float>(), g_bih.data_ptr<float>(),
-                                g_bhh.data_ptr<float>(), cur_stream());
+                                g_bhh.data_ptr<float>(), opt_mut(part), cur_stream());
   TORCH_CHECK(rc == 0, "lstm_wgrad: unsupported configuration (H=", H, ", F=", F, ")");
 }
 
@@ -586,8 +590,9 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
 void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor> stash, std::vector<at::Tensor> w_hh,
                     std::vector<at::Tensor> w_ih, at::Tensor dh_last, std::vector<at::Tensor> dG,
                     std::vector<at::Tensor> dX, std::vector<at::Tensor> hseq, std::vector<at::Tensor> inp,
-                    std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks, at::Tensor seeds,
-                    double drop_p, bool dropout, at::Tensor flags, int64_t N, int64_t Np, int64_t T) {
+                    std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks,
+                    std::vector<at::Tensor> parts, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
+                    int64_t N, int64_t Np, int64_t T) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
@@ -634,11 +639,23 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
       mk[l] = reinterpret_cast<const uint32_t*>(masks[l].data_ptr<uint8_t>());
     }
   }
+  // deterministic mode: per-layer partial buffers of mta_lstm_wgrad_part_floats(1, T, H, F) floats
+  std::vector<float*> pt;
+  if (!parts.empty()) {
+    TORCH_CHECK(fused && parts.size() == (size_t)L, "parts: one buffer per layer (fused weight gradients)");
+    for (int64_t l = 0; l < L; ++l) {
+      MTA_CHECK_F32(parts[l]);
+      TORCH_CHECK(parts[l].numel() >= mta_lstm_wgrad_part_floats(1, (int)T, (int)H, l == 0 ? (int)fin : (int)H),
+                  "parts buffer too small");
+      pt.push_back(parts[l].data_ptr<float>());
+    }
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dh_last.device());
   const int rc = mta_lstm_stack_bwd(
       (int)H, (int)prec, (int)L, (int)fin, cst.data(), cwh.data(), cwi.data(), dh_last.data_ptr<float>(), dg.data(),
       dx.data(), fused ? chs.data() : nullptr, fused ? cin.data() : nullptr, fused ? g0.data() : nullptr,
       fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr, mk.data(),
+      pt.empty() ? nullptr : pt.data(),
       reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p, dropout ? 1 : 0,
       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
@@ -769,6 +786,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_num_partials", &optim_num_partials);
   m.def("grad_sqnorm", &grad_sqnorm);
   m.def("adam", &adam);
+  m.def("lstm_wgrad_part_floats", [](int64_t fused, int64_t T, int64_t H, int64_t F) {
+    return (int64_t)mta_lstm_wgrad_part_floats((int)fused, (int)T, (int)H, (int)F);
+  });
   m.def("heads_losses_train", &heads_losses_train);
   m.def("adam_fused_partials", &adam_fused_partials);
   m.def("adam_fused", &adam_fused);

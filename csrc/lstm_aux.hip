@@ -107,8 +107,9 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
 
 extern "C" int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* inp, int inp_batch_first,
                               int N, int Np, int T, int H, int F, float* g_wih, float* g_whh, float* g_bih,
-                              float* g_bhh, hipStream_t st) {
+                              float* g_bhh, float* part, hipStream_t st) {
   WgArgs a;
+  a.part = part;
   a.dG = dG;
   a.hseq = hseq;
   a.inp = inp;
@@ -125,9 +126,7 @@ extern "C" int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, cons
   a.g_bhh = g_bhh;
   const int NB = H + a.FP;
   if (H % 16 || (4 * H) % CQ || NB / 16 > 16 || 4 * (CQ / 4) + NB > WG_MAX_UNITS_PER_THREAD * WG_THREADS) return 1;
-  // time steps per chunk: ~30 chunks (MTA_WGRAD_TC overrides, for tuning)
-  int tc = (T + 29) / 30;
-  if (const char* e = getenv("MTA_WGRAD_TC")) tc = atoi(e) > 0 ? atoi(e) : tc;
+  const int tc = wg_time_chunk(T, false);
   a.rows_per_chunk = tc * Np;
   a.nchunks = (T * Np + a.rows_per_chunk - 1) / a.rows_per_chunk;
   const int groups = (a.nchunks + 7) / 8;            // chunk groups of 8 (one per XCD)
@@ -142,7 +141,13 @@ extern "C" int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, cons
     if (prec == PREC_BF16X3) lstm_wgrad_kernel<PREC_BF16X3><<<blocks, WG_THREADS, 2 * plane, st>>>(a);
     else lstm_wgrad_kernel<PREC_BF16><<<blocks, WG_THREADS, plane, st>>>(a);
   }
+  if (part) wgrad_reduce_kernel<<<(int)((wg_part_elems(H, F) + 255) / 256), 256, 0, st>>>(a);
   return 0;
+}
+
+// floats of the deterministic-mode partial buffer of one layer (fused: the stack kernel's chunking)
+extern "C" long mta_lstm_wgrad_part_floats(int fused, int T, int H, int F) {
+  return (long)wg_nchunks(T, fused != 0) * wg_part_elems(H, F);
 }
 
 extern "C" void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um,

@@ -1068,8 +1068,8 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
                                   float* const* g_whh, float* const* g_bih, float* const* g_bhh,
-                                  const uint32_t* const* mask, uint64_t* seeds, float drop_p, int dropout,
-                                  unsigned* flags, int N, int Np, int T, hipStream_t st) {
+                                  const uint32_t* const* mask, float* const* part, uint64_t* seeds, float drop_p,
+                                  int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T >= (1 << EPOCH_SHIFT)) return -1;
   StackBwdArgs a{};
   for (int l = 0; l < L; ++l) {
@@ -1100,8 +1100,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
   if (g_whh) {
     // NWAVES = 2 H / 16 waves per workgroup -> CQ = 16 NWAVES gate columns, 4H / CQ = 2 blocks per chunk
     const int nwaves = H / 8, cq = 16 * nwaves;
-    int tc = (T + 59) / 60;  // time steps per chunk: short chunks keep the tail after the last layer small
-    if (const char* e = getenv("MTA_WGRAD_TC")) tc = atoi(e) > 0 ? atoi(e) : tc;
+    const int tc = mta_wgrad::wg_time_chunk(T, true);
     a.wg_nq = 4 * H / cq;
     for (int l = 0; l < L; ++l) {
       mta_wgrad::WgArgs& w = a.wg[l];
@@ -1121,6 +1120,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
       w.g_whh = g_whh[l];
       w.g_bih = g_bih[l];
       w.g_bhh = g_bhh[l];
+      w.part = part ? part[l] : nullptr;
       const int NB = H + w.FP;
       if (NB / 16 > 16 || cq + NB > mta_wgrad::WG_MAX_UNITS_PER_THREAD * 64 * nwaves) return -1;
       size_t bytes;
@@ -1135,6 +1135,13 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     }
     a.wg_per_layer = a.wg[0].nchunks * a.wg_nq;
   }
-  if (H == 32) return dispatch_bwd<32>(prec, a, wg_lds, st);
-  return dispatch_bwd<64>(prec, a, wg_lds, st);
+  const int rc = H == 32 ? dispatch_bwd<32>(prec, a, wg_lds, st) : dispatch_bwd<64>(prec, a, wg_lds, st);
+  if (rc == 0 && g_whh && part) {
+    // deterministic mode: the fused workgroups wrote per-chunk partials; add them in chunk order
+    for (int l = 0; l < L; ++l)
+      if (a.wg[l].part)
+        mta_wgrad::wgrad_reduce_kernel<<<(int)((mta_wgrad::wg_part_elems(H, a.wg[l].F) + 255) / 256), 256, 0, st>>>(
+            a.wg[l]);
+  }
+  return rc;
 }

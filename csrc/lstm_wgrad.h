@@ -2,6 +2,8 @@
 // backward stack kernel's fused weight-gradient workgroups (lstm_stack.hip).
 #pragma once
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mta_wgrad {
@@ -40,7 +42,24 @@ struct WgArgs {
   float* g_whh;       // (4H, H)
   float* g_bih;       // (4H)
   float* g_bhh;       // (4H)
+  // deterministic mode: per-chunk partials [chunk][4H (H + F) + 4H] written with plain stores instead of the
+  // f32 atomics; wgrad_reduce_kernel adds them to the gradients in chunk order (bit-reproducible runs)
+  float* part;
 };
+
+__host__ __device__ inline long wg_part_elems(int H, int F) { return 4L * H * (H + F) + 4L * H; }
+
+// time steps per row chunk: the standalone kernel aims at ~30 chunks, the stack kernel's fused workgroups at
+// ~60 (short chunks keep the tail after the last layer small); MTA_WGRAD_TC overrides (tuning)
+inline int wg_time_chunk(int T, bool fused) {
+  int tc = fused ? (T + 59) / 60 : (T + 29) / 30;
+  if (const char* e = getenv("MTA_WGRAD_TC")) tc = atoi(e) > 0 ? atoi(e) : tc;
+  return tc;
+}
+inline int wg_nchunks(int T, bool fused) {
+  const int tc = wg_time_chunk(T, fused);
+  return (T + tc - 1) / tc;
+}
 
 // One staging unit = 8 rows x 4 columns of one operand (A = dG, or B = [h_{t-1} | inp]).
 struct WgUnit {
@@ -296,7 +315,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       if (j < NT) {
         const int col = 16 * j + (lane & 15);
         const float v = acc[j][i];
-        if (col < H) {
+        if (a.part) {
+          if (col < H + a.F) a.part[chunk * wg_part_elems(H, a.F) + (size_t)r * (H + a.F) + col] = v;
+        } else if (col < H) {
           atomicAdd(a.g_whh + (size_t)r * H + col, v);
         } else if (col - H < a.F) {
           atomicAdd(a.g_wih + (size_t)r * a.F + (col - H), v);
@@ -319,12 +340,35 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       for (int c = 0; c < 4; ++c) {
         const int cp = cq0 + cg * 4 + c;
         const int r = (cp & 3) * H + (cp >> 2);
-        atomicAdd(a.g_bih + r, bias_acc[c]);
-        atomicAdd(a.g_bhh + r, bias_acc[c]);
+        if (a.part) {
+          a.part[chunk * wg_part_elems(H, a.F) + 4L * H * (H + a.F) + r] = bias_acc[c];
+        } else {
+          atomicAdd(a.g_bih + r, bias_acc[c]);
+          atomicAdd(a.g_bhh + r, bias_acc[c]);
+        }
       }
     }
   }
 }
 
+
+// deterministic mode: gradients += the per-chunk partials summed in chunk order (one thread per element)
+static __global__ void wgrad_reduce_kernel(WgArgs a) {
+  const long E = wg_part_elems(a.H, a.F);
+  const int HF = a.H + a.F;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < E; e += (long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int c = 0; c < a.nchunks; ++c) acc += a.part[c * E + e];
+    if (e < 4L * a.H * HF) {
+      const int r = (int)(e / HF), col = (int)(e % HF);
+      if (col < a.H) a.g_whh[(size_t)r * a.H + col] += acc;
+      else a.g_wih[(size_t)r * a.F + (col - a.H)] += acc;
+    } else {
+      const int r = (int)(e - 4L * a.H * HF);
+      a.g_bih[r] += acc;
+      a.g_bhh[r] += acc;
+    }
+  }
+}
 
 }  // namespace mta_wgrad

@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
     CK(hipEventRecord(a));
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
                             hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
-                            const_cast<const uint32_t* const*>(mask.data()), seeds, p,
+                            const_cast<const uint32_t* const*>(mask.data()), nullptr, seeds, p,
                             mode == 0 ? 1 : 0, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));

@@ -96,7 +96,16 @@ class Trainer:
         if attempts is not None and int(os.environ.get("MTA_RETRY_ATTEMPT", "0")) >= int(attempts):
             self.fail_at_step = None
         self.heartbeat_file = os.environ.get("MTA_HEARTBEAT_FILE")
-        self.deterministic = deterministic
+        # bit-reproducible runs: ordered weight-gradient reductions instead of f32 atomics (LSTM kernels) and no
+        # split-K atomics in the extras' GEMMs; the other reductions (norm, loss, heads) are ordered anyway
+        self.deterministic = bool(deterministic) or os.environ.get("MTA_DETERMINISTIC", "0") == "1"
+        if self.deterministic:
+            from ..ops import lstm as _lstm_op
+            from ..ops import extras as _extras_op
+
+            _lstm_op.set_deterministic(True)
+            if hasattr(_extras_op, "set_deterministic"):
+                _extras_op.set_deterministic(True)
         # state
         self.current_epoch = 0
         self.global_step = 0

@@ -58,8 +58,19 @@ def gemm(mode: int, A: Tensor, B: Tensor, M: int, N: int, K: int, lda: int, ldb:
                     out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad)
 
 
+_DETERMINISTIC = [False]
+
+
+def set_deterministic(flag: bool) -> None:
+    """Deterministic mode: weight-gradient GEMMs without split-K (no cross-workgroup f32 atomics).  The
+    LayerNorm/RMSNorm parameter gradients still reduce across workgroups with atomics (csrc/norm.hip)."""
+    _DETERMINISTIC[0] = bool(flag)
+
+
 def wgrad_split(M: int, N: int, K: int) -> int:
     """Split-K count for a weight-gradient GEMM: ~256 workgroups, >= 4 k-slices of 32 each."""
+    if _DETERMINISTIC[0]:
+        return 1
     tiles = -(-M // 64) * -(-N // 64)
     return max(1, min(256 // max(tiles, 1), K // 128))
 

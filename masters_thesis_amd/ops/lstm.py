@@ -28,6 +28,20 @@ from torch import Tensor
 from ._lib import lib, use_hip
 
 MATMUL_PRECISION = {"highest": 0, "high": 1, "medium": 2}
+# deterministic mode (Trainer(deterministic=True)): the weight-gradient chunks write partials that are summed
+# in chunk order by one extra launch instead of f32 atomics, so two runs are bit-identical
+_DETERMINISTIC = [False]
+
+
+def set_deterministic(flag: bool) -> None:
+    _DETERMINISTIC[0] = bool(flag)
+
+
+def _parts(C, fused: bool, T: int, H: int, fins, device):
+    if not _DETERMINISTIC[0]:
+        return []
+    return [torch.empty(C.lstm_wgrad_part_floats(int(fused), T, H, f), device=device, dtype=torch.float32)
+            for f in fins]
 FUSED_F = (3, 5)
 
 
@@ -112,8 +126,9 @@ class _LSTMStackFn(torch.autograd.Function):
             dG = torch.empty((T, Np, 4 * H), device=dh_last.device, dtype=torch.float32)
             C.lstm_bwd_layer(H, ctx.prec, stash, w_hh, dH, None if dH is not None else dh_last, dG, N, Np, T)
             fused0 = l == 0 and F in FUSED_F
+            part = _parts(C, False, T, H, [inp.shape[-1]], dG.device)
             C.lstm_wgrad(ctx.prec, dG, hseq, inp, fused0, N, Np, T, H, _grad_buffer(w_ih), _grad_buffer(w_hh),
-                         _grad_buffer(b_ih), _grad_buffer(b_hh))
+                         _grad_buffer(b_ih), _grad_buffer(b_hh), part[0] if part else None)
             dG2 = dG.view(T * Np, 4 * H)
             if l > 0:
                 dinp = dG2.mm(w_um)
@@ -243,8 +258,10 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
     flags = _stack_flags(C, Np, L, dev)
     inp = [st.x] + [st.xdrop[l] if drop else st.hseq[l - 1] for l in range(1, L)]
     grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
+    parts = _parts(C, True, T, H, [F] + [H] * (L - 1), dev)
     C.lstm_stack_bwd(H, prec, F, list(st.stash), list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
-                     list(st.hseq), inp, grads, list(st.masks) if drop else [], st.seeds, p, drop, flags, N, Np, T)
+                     list(st.hseq), inp, grads, list(st.masks) if drop else [], parts, st.seeds, p, drop, flags, N,
+                     Np, T)
 
 
 class _LSTMPipelinedFn(torch.autograd.Function):

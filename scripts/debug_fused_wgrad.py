@@ -37,14 +37,14 @@ def main():
         dh = torch.randn(N, H, device=dev)
         inp = [x] + hseq[:-1]
         ref = [[torch.zeros_like(ws[4 * l + kk]) for l in range(L)] for kk in range(4)]
-        C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], seeds, 0.0, False, flags,
+        C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], [], seeds, 0.0, False, flags,
                          N, Np, T)
         for l in range(L):
-            C.lstm_wgrad(1, dG[l], hseq[l], inp[l], l == 0, N, Np, T, H, ref[0][l], ref[1][l], ref[2][l], ref[3][l])
+            C.lstm_wgrad(1, dG[l], hseq[l], inp[l], l == 0, N, Np, T, H, ref[0][l], ref[1][l], ref[2][l], ref[3][l], None)
         dG_ref = [d.clone() for d in dG]
         for rep in range(3):
             got = [[torch.zeros_like(ws[4 * l + kk]) for l in range(L)] for kk in range(4)]
-            C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, got, [], seeds, 0.0, False,
+            C.lstm_stack_bwd(H, 1, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, got, [], [], seeds, 0.0, False,
                              flags, N, Np, T)
             torch.cuda.synchronize()
             errs = []

@@ -44,18 +44,18 @@ def run(C, L, prec):
     grads = [[torch.zeros_like(ws[4 * l + k]) for l in range(L)] for k in range(4)]
 
     def bwd():
-        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], seeds, 0.0, False, flags,
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], [], seeds, 0.0, False, flags,
                          N, Np, T)
 
     def bwd_fused():
-        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, [], seeds, 0.0, False,
+        C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, [], [], seeds, 0.0, False,
                          flags, N, Np, T)
 
     def bwd_wgrad():
         bwd()
         for l in range(L):
             C.lstm_wgrad(prec, dG[l], hseq[l], inp[l] if l else x, l == 0, N, Np, T, H, grads[0][l], grads[1][l],
-                         grads[2][l], grads[3][l])
+                         grads[2][l], grads[3][l], None)
 
     tf, tb = timeit(fwd), timeit(bwd)
     tbf, tbw = timeit(bwd_fused), timeit(bwd_wgrad)

@@ -29,7 +29,7 @@ def main():
                         os.environ["MTA_WGRAD_NOATOMIC"] = "1"
                     else:
                         os.environ.pop("MTA_WGRAD_NOATOMIC", None)
-                    t = timeit(lambda: C.lstm_wgrad(prec, dG, hseq, inp, bf, N, Np, T, H, *g))
+                    t = timeit(lambda: C.lstm_wgrad(prec, dG, hseq, inp, bf, N, Np, T, H, *g, None))
                     print(f"N={N} F={F} prec={prec} tc={tc} atomics={'off' if noat else 'on '} {t:7.1f} us",
                           flush=True)
     os.environ.pop("MTA_WGRAD_NOATOMIC", None)

@@ -97,3 +97,35 @@ def test_fused_training_step_matches_autograd(cls_name, B):
     torch.testing.assert_close(gb, ga, rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(ab, aa, rtol=1e-6, atol=0)
     assert torch.equal(sa, sb)  # dropout seeds advanced once by both paths
+
+
+def test_deterministic_mode_runs_are_bit_identical():
+    """Trainer(deterministic=True): ordered per-chunk weight-gradient reductions (csrc/lstm_wgrad.h
+    wgrad_reduce_kernel) instead of f32 atomics -> two training runs give bit-identical parameters; the
+    result matches the atomic (default) path to rounding."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import FinancialLstmCombined
+    from masters_thesis_amd.ops import lstm as op
+
+    def run(det):
+        torch.manual_seed(3)
+        model = FinancialLstmCombined(dropout=0.2)
+        ld = TensorBatchLoader([t.to(DEV) for t in _data(9)], 1, shuffle=True, seed=0)
+        tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=True, matmul_precision="high", deterministic=det)
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.lstm.seeds.copy_(torch.arange(8, device=DEV) + 17)
+        model.train()
+        step = tr.make_train_stepper(ld)
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize()
+        op.set_deterministic(False)
+        return tr.flat.data.clone()
+
+    a, b = run(True), run(True)
+    assert torch.equal(a, b)
+    torch.testing.assert_close(run(False), a, rtol=1e-4, atol=1e-6)
