@@ -19,6 +19,8 @@ namespace {
 
 constexpr int TPB = 1024;
 constexpr int NWAVES = TPB / 64;
+// LDS floats of the u_t scratch: u_t itself plus one partial row per wave
+inline size_t ut_floats(int n) { return (size_t)((n + 3) & ~3) + (size_t)NWAVES * n; }
 constexpr double LOG2PI = 1.8378770664093453;
 
 struct LossArgs {
@@ -81,8 +83,11 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const
     for (int wdw = 0; wdw < A.windows; ++wdw) {
       const float fm = A.factor[wdw * A.factor_stride], fv = A.factor[wdw * A.factor_stride + 1];
       const int i0 = wdw * A.kwin;
+      // u_t partials per wave (row wid of ut + n), summed in wave order below: no float atomics, so the
+      // loss and every gradient are bit-reproducible (deterministic mode relies on it)
+      float* utw = ut + ((n + 3) & ~3);
       __syncthreads();
-      for (int t = tid; t < n; t += TPB) ut[t] = 0.f;
+      for (int t = tid; t < NWAVES * n; t += TPB) utw[t] = 0.f;
       __syncthreads();
       // pass 1: u_t = sum_i w_i b_i D_it ; partials of s = sum w b^2, sum log w, sum w D^2
       double s_wbb = 0.0, s_logw = 0.0, s_wdd = 0.0;
@@ -95,7 +100,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const
         for (int t = lane; t < n; t += 64) {
           const float D = (YL ? ys[i * n + t].x : yi[t * C]) - mu;
           sdd = fmaf(D, D, sdd);
-          atomicAdd(&ut[t], wb * D);
+          utw[wid * n + t] = fmaf(wb, D, utw[wid * n + t]);
         }
         sdd = wave_sum_dpp(sdd);
         if (lane == 0) {
@@ -103,6 +108,12 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const
           s_logw += log((double)w);
           s_wdd += (double)w * sdd;
         }
+      }
+      __syncthreads();
+      for (int t = tid; t < n; t += TPB) {
+        float v = 0.f;
+        for (int k = 0; k < NWAVES; ++k) v += utw[k * n + t];
+        ut[t] = v;
       }
       __syncthreads();
       double s_u1 = 0.0, s_u2 = 0.0;
@@ -170,7 +181,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const
 }
 
 __global__ __launch_bounds__(TPB) void decoder_losses_kernel(const float* __restrict__ ab, LossArgs A) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // n floats
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // ut_floats(n)
   losses_body(ab, A, smem);
 }
 
@@ -264,8 +275,8 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
   float* ab = smem;                      // 2N
   float* gm = ab + N2;                   // 2N  d mse / d(alpha, beta)
   float* gn = gm + N2;                   // 2N  d nll / d(alpha, beta)
-  float* ut = gn + N2;                   // n
-  float2* ys = reinterpret_cast<float2*>(ut + ((n + 3) & ~3));  // (N, n) when YL
+  float* ut = gn + N2;                   // ut_floats(n)
+  float2* ys = reinterpret_cast<float2*>(ut + ((ut_floats(n) + 3) & ~(size_t)3));  // (N, n) when YL
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if constexpr (YL) {
     for (int e = tid; e < N * n; e += TPB) {
@@ -417,7 +428,7 @@ extern "C" void mta_decoder_losses(const float* ab, const float* y, const float*
                                    hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, gmse, gnll, acc};
-  decoder_losses_kernel<<<1, TPB, (size_t)((n + 3) & ~3) * sizeof(float), st>>>(ab, A);
+  decoder_losses_kernel<<<1, TPB, ut_floats(n) * sizeof(float), st>>>(ab, A);
 }
 
 extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb,
@@ -429,10 +440,10 @@ extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const f
              out, gmse, gnll, acc};
   if (heads_big(N, H)) {
     heads_kernel<<<(N + NWAVES - 1) / NWAVES, TPB, 0, st>>>(h, N, H, wa, ba, wb, bb, ab_out);
-    decoder_losses_kernel<<<1, TPB, (size_t)((n + 3) & ~3) * sizeof(float), st>>>(ab_out, A);
+    decoder_losses_kernel<<<1, TPB, ut_floats(n) * sizeof(float), st>>>(ab_out, A);
     return;
   }
-  const size_t lds = (size_t)(2 * ((N + 1) & ~1) + 4 + ((n + 3) & ~3)) * sizeof(float);
+  const size_t lds = ((size_t)(2 * ((N + 1) & ~1) + 4) + ut_floats(n)) * sizeof(float);
   heads_losses_kernel<<<1, TPB, lds, st>>>(h, H, wa, ba, wb, bb, ab_out, A);
 }
 
@@ -445,7 +456,7 @@ extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, co
                                       float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, nullptr, nullptr, acc};
-  const size_t base = (size_t)(3 * 2 * ((N + 1) & ~1) + ((n + 3) & ~3)) * sizeof(float);
+  const size_t base = ((size_t)(3 * 2 * ((N + 1) & ~1)) + ((ut_floats(n) + 3) & ~(size_t)3)) * sizeof(float);
   const size_t ybytes = (size_t)N * n * sizeof(float2);
   if (base + ybytes <= 96 * 1024) {
     heads_losses_train_kernel<true><<<1, TPB, base + ybytes, st>>>(h, H, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb,

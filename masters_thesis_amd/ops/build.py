@@ -7,6 +7,7 @@ includes torch; everything is linked with ``hipcc -shared``.  Objects are cached
 kernel recompiles one file.  No hipify, no CUDA paths: gfx950 only.
 
     python -m masters_thesis_amd.ops.build [-v] [--force] [--debug]
+    python -m masters_thesis_amd.ops.build --sanitize      # host runtime under ASan+UBSan and TSan (no GPU)
 """
 from __future__ import annotations
 
@@ -142,13 +143,47 @@ def build(verbose: bool = False, force: bool = False, debug: bool = False, jobs:
     return out
 
 
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"], "tsan": ["-fsanitize=thread"]}
+
+
+def build_host_sanitized(kinds=("asan", "tsan"), verbose: bool = False) -> List[Path]:
+    """Host-only C++ runtime (csrc/host/*.cpp) + its stress drivers (csrc/host/tests/*.cpp) under the
+    sanitizers, as plain g++ executables (no HIP, no torch): race / memory-error detection for the native
+    runtime pieces.  Returns the executables (build/sanitize/<driver>_<kind>)."""
+    # ROCm's clang++ first: its TSan runtime intercepts libstdc++'s condition variables (gcc 11's libtsan
+    # reports false 'double lock' / races on std::condition_variable waits)
+    rocm_clang = Path("/opt/rocm/lib/llvm/bin/clang++")
+    cxx = str(rocm_clang) if rocm_clang.exists() else (shutil.which("clang++") or shutil.which("g++"))
+    if cxx is None:
+        raise RuntimeError("no host C++ compiler for the sanitizer builds")
+    out_dir = REPO / "build" / "sanitize"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    outs = []
+    for drv in sorted((CSRC / "host" / "tests").glob("*.cpp")):
+        for kind in kinds:
+            exe = out_dir / f"{drv.stem}_{kind}"
+            cmd = [cxx, "-std=c++17", "-O1", "-g", *SANITIZERS[kind], "-pthread", str(drv),
+                   *[str(p) for p in host_sources()], "-o", str(exe)]
+            if verbose:
+                print("[build]", " ".join(cmd))
+            subprocess.run(cmd, check=True)
+            outs.append(exe)
+    return outs
+
+
 def main(argv=None) -> None:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=0)
+    ap.add_argument("--sanitize", action="store_true", help="host runtime sanitizer builds (+ run them)")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        for exe in build_host_sanitized(verbose=a.verbose):
+            r = subprocess.run([str(exe)], capture_output=True, text=True)
+            print(f"{exe.name}: rc={r.returncode} {r.stdout.strip()} {r.stderr.strip()[-2000:]}")
+        return
     print(build(verbose=a.verbose, force=a.force, debug=a.debug, jobs=a.jobs))
 
 

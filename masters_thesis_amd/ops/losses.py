@@ -196,7 +196,8 @@ def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, ba
 
 def train_decoder_fits(N: int, n: int) -> bool:
     """Whether :func:`heads_losses_train`'s one-workgroup kernel takes (N sequences, n target days)."""
-    base = (3 * 2 * ((N + 1) & ~1) + ((n + 3) & ~3)) * 4
+    ut = ((n + 3) & ~3) + 16 * n  # u_t + one partial row per wave (csrc/losses.hip ut_floats)
+    base = (3 * 2 * ((N + 1) & ~1) + ((ut + 3) & ~3)) * 4
     return base + N * n * 8 <= 96 * 1024 or base <= 60 * 1024
 
 

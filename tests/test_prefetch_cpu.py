@@ -59,3 +59,22 @@ def test_streaming_loader_cpu_fallback_matches_base():
     got = torch.cat([b[0] for b in ld])
     ref = torch.cat([b[0] for b in base])
     assert torch.equal(got, ref) and len(ld) == 4
+
+
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+def test_host_prefetcher_under_sanitizers(kind):
+    """SURVEY §5 race / memory-error detection for the native host runtime: the prefetcher's ring protocol
+    stress driver (csrc/host/tests/prefetch_stress.cpp) built with AddressSanitizer+UBSan and with
+    ThreadSanitizer (host code only; no GPU sanitizers on this pool) must run clean."""
+    import shutil
+    import subprocess
+
+    from masters_thesis_amd.ops.build import build_host_sanitized
+
+    if shutil.which("g++") is None and shutil.which("clang++") is None:
+        pytest.skip("no host C++ compiler")
+    (exe,) = build_host_sanitized((kind,))
+    env = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=1", "UBSAN_OPTIONS": "halt_on_error=1",
+           "TSAN_OPTIONS": "halt_on_error=1"}
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "prefetch_stress: OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
