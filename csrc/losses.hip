@@ -20,7 +20,7 @@ namespace {
 constexpr int TPB = 1024;
 constexpr int NWAVES = TPB / 64;
 // LDS floats of the u_t scratch: u_t itself plus one partial row per wave
-inline size_t ut_floats(int n) { return (size_t)((n + 3) & ~3) + (size_t)NWAVES * n; }
+__host__ __device__ inline size_t ut_floats(int n) { return (size_t)((n + 3) & ~3) + (size_t)NWAVES * n; }
 constexpr double LOG2PI = 1.8378770664093453;
 
 struct LossArgs {
