@@ -129,6 +129,18 @@ def main(argv=None):
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = pdist.all_reduce_max(elapsed, dev)
+    # gradient all-reduce alone (world > 1): mean over 50 back-to-back syncs of the flat bucket, after the
+    # timed region (the timed steps include it)
+    allreduce_us = None
+    if world > 1 and dev.type == "cuda":
+        for _ in range(5):
+            trainer.ddp.allreduce_grads()
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        for _ in range(50):
+            trainer.ddp.allreduce_grads()
+        torch.cuda.synchronize()
+        allreduce_us = pdist.all_reduce_max((time.perf_counter() - a0) / 50 * 1e6, dev)
     step_ms = sorted(a.elapsed_time(b) for a, b in evs) if evs else [elapsed * 1e3 / args.steps]
     p50 = pdist.all_reduce_max(step_ms[len(step_ms) // 2], dev)
     p90 = pdist.all_reduce_max(step_ms[min(len(step_ms) - 1, (len(step_ms) * 9) // 10)], dev)
@@ -156,6 +168,9 @@ def main(argv=None):
                             if key in SAME_NODE_TORCH_EAGER and args.backend == "auto" else None),
             "baseline": "same-node PyTorch-ROCm reference path (MIOpen nn.LSTM, autograd, eager), x n_gpus",
             "vs_cpu_yardstick": (round(value / YARDSTICK[key], 3) if key in YARDSTICK else None),
+            "allreduce": trainer.ddp.backend_name,
+            "allreduce_us": round(allreduce_us, 2) if allreduce_us is not None else None,
+            "grad_bucket_bytes": int(trainer.flat.padded * 4),
             "dtype": ("bf16" if (cfg.model.get("arch", "lstm") != "lstm" and dev.type == "cuda")
                       or cfg.trainer.precision != "32-true" else "fp32"),
             "data": "synthetic (reference DGP, generated on device), random-init weights",

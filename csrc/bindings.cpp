@@ -71,6 +71,16 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
                        hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
+// allreduce.hip (one-shot all-reduce over xGMI peer memory)
+int mta_xgmi_alloc(long bytes, void** out);
+int mta_xgmi_free(void* p);
+int mta_xgmi_ipc_handle(void* p, unsigned char* out64);
+int mta_xgmi_ipc_open(const unsigned char* in64, void** out);
+int mta_xgmi_ipc_close(void* p);
+long mta_xgmi_layout(int world, long cap, long* flags_off);
+int mta_xgmi_ctl_words();
+int mta_xgmi_allreduce(float* grad, long n, long cap, void* const* bufs, int rank, int world, unsigned* ctl,
+                       hipStream_t st);
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
             float idio_loc, float idio_scale, float a_loc, float a_scale, float b_loc, float b_scale, float* r_market,
@@ -662,6 +672,50 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
 }
 
 
+// ------------------------------------------------------------------------------- xGMI all-reduce
+int64_t xgmi_buffer_bytes(int64_t world, int64_t cap) {
+  long off = 0;
+  return (int64_t)mta_xgmi_layout((int)world, (long)cap, &off);
+}
+
+int64_t xgmi_alloc(int64_t bytes) {
+  void* p = nullptr;
+  const int rc = mta_xgmi_alloc((long)bytes, &p);
+  TORCH_CHECK(rc == 0, "xgmi_alloc: fine-grained allocation failed (rc=", rc, ")");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void xgmi_free(int64_t p) { mta_xgmi_free(reinterpret_cast<void*>(p)); }
+
+at::Tensor xgmi_ipc_handle(int64_t p) {
+  at::Tensor out = at::zeros({64}, at::TensorOptions().dtype(at::kByte));
+  const int n = mta_xgmi_ipc_handle(reinterpret_cast<void*>(p), out.data_ptr<uint8_t>());
+  TORCH_CHECK(n > 0, "hipIpcGetMemHandle failed");
+  return out;
+}
+
+int64_t xgmi_ipc_open(at::Tensor handle) {
+  TORCH_CHECK(handle.scalar_type() == at::kByte && handle.numel() == 64 && !handle.is_cuda(), "64-byte CPU handle");
+  void* p = nullptr;
+  TORCH_CHECK(mta_xgmi_ipc_open(handle.contiguous().data_ptr<uint8_t>(), &p) == 0, "hipIpcOpenMemHandle failed");
+  return reinterpret_cast<int64_t>(p);
+}
+
+void xgmi_ipc_close(int64_t p) { mta_xgmi_ipc_close(reinterpret_cast<void*>(p)); }
+
+// in-place sum of `grad` over the ranks; bufs: every rank's comm buffer as mapped in this process;
+// ctl: int32[xgmi_ctl_words] zero-initialised once (epoch, arrival counter, timeout count)
+void xgmi_allreduce(at::Tensor grad, int64_t cap, std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl) {
+  MTA_CHECK_F32(grad);
+  TORCH_CHECK(ctl.is_cuda() && ctl.scalar_type() == at::kInt && ctl.numel() >= mta_xgmi_ctl_words(), "ctl words");
+  std::vector<void*> b;
+  for (auto v : bufs) b.push_back(reinterpret_cast<void*>(v));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
+  const int rc = mta_xgmi_allreduce(grad.data_ptr<float>(), (long)grad.numel(), (long)cap, b.data(), (int)rank,
+                                    (int)b.size(), reinterpret_cast<unsigned*>(ctl.data_ptr<int>()), cur_stream());
+  TORCH_CHECK(rc == 0, "xgmi_allreduce: bad arguments (rc=", rc, ")");
+}
+
 // ------------------------------------------------------------------------------- dataset build
 void dgp(int64_t seed, int64_t mkt_df, double mkt_loc, double mkt_scale, int64_t idio_df, double idio_loc,
          double idio_scale, double a_loc, double a_scale, double b_loc, double b_scale, at::Tensor r_market,
@@ -786,6 +840,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("optim_num_partials", &optim_num_partials);
   m.def("grad_sqnorm", &grad_sqnorm);
   m.def("adam", &adam);
+  m.def("xgmi_buffer_bytes", &xgmi_buffer_bytes);
+  m.def("xgmi_alloc", &xgmi_alloc);
+  m.def("xgmi_free", &xgmi_free);
+  m.def("xgmi_ipc_handle", &xgmi_ipc_handle);
+  m.def("xgmi_ipc_open", &xgmi_ipc_open);
+  m.def("xgmi_ipc_close", &xgmi_ipc_close);
+  m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.def("xgmi_ctl_words", []() { return (int64_t)mta_xgmi_ctl_words(); });
   m.def("lstm_wgrad_part_floats", [](int64_t fused, int64_t T, int64_t H, int64_t F) {
     return (int64_t)mta_lstm_wgrad_part_floats((int)fused, (int)T, (int)H, (int)F);
   });

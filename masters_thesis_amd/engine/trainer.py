@@ -233,7 +233,10 @@ class Trainer:
                 and getattr(self.model, "graph_capturable", True))
 
     def _allreduce_in_graph(self) -> bool:
-        return self.ddp.world == 1 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1"
+        # the xGMI one-shot all-reduce is a plain kernel: the whole step (sync + optimizer) is one graph.
+        # RCCL stays outside unless MTA_GRAPH_ALLREDUCE=1 (graph capture of RCCL is not exercised here).
+        return (self.ddp.world == 1 or getattr(self.ddp, "graph_safe", False)
+                or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1")
 
     def _seed_grad(self, loss: torch.Tensor) -> torch.Tensor:
         # a persistent ones tensor: no fill node per step for autograd's implicit seed
@@ -456,8 +459,10 @@ class Trainer:
         """Raise if a pipelined LSTM launch gave up on a hand-off (its results were garbage)."""
         if self.device.type == "cuda":
             from ..ops.lstm import check_pipeline_health
+            from ..parallel.xgmi import check_all_health
 
             check_pipeline_health()
+            check_all_health()
 
     def _run_eval(self, stage: str, loader, limit=None) -> Dict[str, torch.Tensor]:
         model = self.model

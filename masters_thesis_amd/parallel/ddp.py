@@ -11,9 +11,14 @@ models (the MLP/transformer extras) the buffer is split into ``bucket_mb`` chunk
 xGMI is point-to-point (7 links x ~153 GB/s), so a ring all-reduce is per-link
 bound and a few large buckets beat many small ones — the default bucket is 64 MB,
 and buckets are issued asynchronously so RCCL can pipeline them.
+
+On one node the flat bucket goes through the one-shot xGMI all-reduce instead (``parallel/xgmi.py``: one
+kernel, every peer written directly over its own link, summed locally in rank order), which is also safe to
+capture inside the step's HIP graph (``graph_safe``); ``MTA_ALLREDUCE=rccl`` keeps RCCL.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import torch
@@ -31,6 +36,24 @@ class FlatDDP:
         per = max(1024, int(bucket_mb * (1 << 20) / 4) // 1024 * 1024)
         self.buckets: List[slice] = [slice(i, min(i + per, n)) for i in range(0, n, per)]
         self._gloo_cpu = self.world > 1 and dist.get_backend(group) == "gloo" and flat.grad.is_cuda
+        # one-shot xGMI all-reduce (csrc/allreduce.hip) for single-node GPU groups; None -> the group's all-reduce
+        self.xgmi = None
+        if self.world > 1 and flat.grad.is_cuda and (dist.get_backend(group) == "nccl"
+                                                     or os.environ.get("MTA_ALLREDUCE", "") == "xgmi"):
+            from .xgmi import XgmiAllReduce
+
+            self.xgmi = XgmiAllReduce.create(flat.padded, flat.grad.device, group)
+
+    @property
+    def backend_name(self) -> str:
+        if self.world == 1:
+            return "none"
+        return "xgmi" if self.xgmi is not None else dist.get_backend(self.group)
+
+    @property
+    def graph_safe(self) -> bool:
+        """The gradient sync can live inside the captured step graph (a plain kernel: xGMI one-shot)."""
+        return self.world == 1 or self.xgmi is not None
 
     @property
     def grad_scale(self) -> float:
@@ -52,6 +75,9 @@ class FlatDDP:
         if self.world == 1:
             return
         g = self.flat.grad
+        if self.xgmi is not None:
+            self.xgmi.allreduce_(g)
+            return
         if self._gloo_cpu:
             t = g.cpu()
             dist.all_reduce(t, group=self.group)
