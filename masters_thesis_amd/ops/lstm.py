@@ -164,7 +164,7 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
     # spinning workgroup's producers are resident or finished.  Grids beyond one workgroup per CU (large
     # batches: B=64 is 800 workgroups) run in waves instead of falling back to per-layer launches and
     # T x Np x 4H gate tensors.
-    return H in (32, 64) and F in FUSED_F and 2 <= num_layers <= 8 and T < 4096
+    return (H in (32, 64) or 8 <= H < 32) and F in FUSED_F and 1 <= num_layers <= 8 and T < 4096
 
 
 _FLAGS = {}
@@ -212,7 +212,37 @@ def check_pipeline_health(clear: bool = True) -> None:
 class PipelinedState:
     """What the pipelined backward needs from its forward (the autograd Function's ctx, or held by the
     trainer's fused step)."""
-    __slots__ = ("meta", "params", "seeds", "x", "stash", "hseq", "xdrop", "masks")
+    __slots__ = ("meta", "params", "seeds", "x", "stash", "hseq", "xdrop", "masks", "pad")
+
+
+def _padded_rows_index(H: int, Hp: int, device) -> Tensor:
+    """nn.LSTM gate row g*H + u of an H-unit layer -> row g*Hp + u of the zero-padded Hp-unit layer."""
+    return (torch.arange(4, device=device)[:, None] * Hp + torch.arange(H, device=device)[None, :]).reshape(-1)
+
+
+def _pad_weights(flat: Sequence[Tensor], H: int, Hp: int, F: int) -> List[Tensor]:
+    """Zero-pad an H-unit stack to Hp units.  Exact: a padded unit has zero weights and bias, so its gates are
+    (0.5, 0.5, 0, 0.5), its c stays 0 and its h is exactly 0; its outgoing weights are zero too, so it never
+    reaches a real unit, and every gradient of a padding weight is exactly 0 (the thesis grid's H=16 runs
+    on the H=32 kernels: SURVEY A.2, `tex/diplomski_rad.tex:1106-1122`)."""
+    idx = _padded_rows_index(H, Hp, flat[0].device)
+    out = []
+    for l in range(len(flat) // 4):
+        w_ih, w_hh, b_ih, b_hh = flat[4 * l: 4 * l + 4]
+        fin = F if l == 0 else H
+        fin_p = F if l == 0 else Hp
+        pw = w_ih.new_zeros((4 * Hp, fin_p))
+        pw[:, :fin].index_copy_(0, idx, w_ih.detach())
+        ph = w_hh.new_zeros((4 * Hp, Hp))
+        ph[:, :H].index_copy_(0, idx, w_hh.detach())
+        out += [pw, ph, b_ih.new_zeros(4 * Hp).index_copy_(0, idx, b_ih.detach()),
+                b_hh.new_zeros(4 * Hp).index_copy_(0, idx, b_hh.detach())]
+    return out
+
+
+def kernel_hidden(H: int) -> int:
+    """Hidden size the pipelined kernels run an H-unit stack at (native 32 / 64; H < 32 zero-padded to 32)."""
+    return H if H in (32, 64) else 32
 
 
 def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, training: bool, need_grad: bool,
@@ -220,7 +250,12 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     """One forward launch of every layer (csrc/lstm_stack.hip).  Returns (h_T of the top layer (N, H), state)."""
     L = len(flat) // 4
     N, T, F = x.shape
-    H = flat[1].shape[1]
+    H0 = flat[1].shape[1]
+    H = kernel_hidden(H0)
+    pad = None
+    if H != H0:
+        pad = (tuple(flat), H0)
+        flat = _pad_weights(flat, H0, H, F)
     Np = padded_rows(N)
     C = lib()
     dev = x.device
@@ -243,6 +278,9 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     st.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
     st.params, st.seeds, st.x = tuple(flat), seeds, x
     st.stash, st.hseq, st.xdrop, st.masks = stash, hseq, xdrop, masks
+    st.pad = pad
+    if pad is not None:
+        return hseq[L - 1][T - 1, :N, :H0], st
     return hseq[L - 1][T - 1, :N], st
 
 
@@ -253,6 +291,13 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
     C = lib()
     dev = dh_last.device
     flat = st.params
+    if st.pad is not None:  # zero-padded stack: pad dh, accumulate into padded buffers, scatter back below
+        H0 = st.pad[1]
+        dh_p = dh_last.new_zeros((N, H))
+        dh_p[:, :H0] = dh_last
+        dh_last = dh_p
+        for t in flat:
+            t.grad = torch.zeros_like(t)
     dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
     dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
     flags = _stack_flags(C, Np, L, dev)
@@ -262,6 +307,17 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
     C.lstm_stack_bwd(H, prec, F, list(st.stash), list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
                      list(st.hseq), inp, grads, list(st.masks) if drop else [], parts, st.seeds, p, drop, flags, N,
                      Np, T)
+    if st.pad is not None:
+        real, H0 = st.pad
+        idx = _padded_rows_index(H0, H, dev)
+        for l in range(L):
+            fin = F if l == 0 else H0
+            pw, ph, pbi, pbh = flat[4 * l: 4 * l + 4]
+            w_ih, w_hh, b_ih, b_hh = real[4 * l: 4 * l + 4]
+            _grad_buffer(w_ih).add_(pw.grad.index_select(0, idx)[:, :fin])
+            _grad_buffer(w_hh).add_(ph.grad.index_select(0, idx)[:, :H0])
+            _grad_buffer(b_ih).add_(pbi.grad.index_select(0, idx))
+            _grad_buffer(b_hh).add_(pbh.grad.index_select(0, idx))
 
 
 class _LSTMPipelinedFn(torch.autograd.Function):

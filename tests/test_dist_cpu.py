@@ -73,3 +73,30 @@ def test_ddp_two_ranks_equals_single_process_global_batch(tmp_path):
     s = torch.load(tmp_path / "single.pt", weights_only=True)
     torch.testing.assert_close(r0["params"], s["params"], rtol=1e-5, atol=1e-6)
     assert abs(r0["mse"] - s["mse"]) < 1e-5 * abs(s["mse"])
+
+
+@pytest.mark.timeout(600)
+def test_bench_four_gloo_ranks_whole_path(tmp_path):
+    """bench.py under torch.distributed.run with 4 gloo ranks on the CPU: the driver's multi-GPU contract
+    (one JSON line from rank 0, whole-job value, n_gpus, weak-scaling global batch, gradient all-reduce) on the
+    same code path the MI355X run takes, minus the devices."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), str(repo / "bench.py"), "--gpus", "4", "--steps", "3",
+           "--warmup", "1", "--n-samples", "20000"]
+    r = subprocess.run(cmd, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=540)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["warmup"] == 1 and rec["scaling"] == "weak"
+    assert rec["config"]["global_batch"] == 4 and rec["config"]["parallelism"] == "dp4"
+    assert rec["allreduce"] == "gloo" and rec["value"] > 0

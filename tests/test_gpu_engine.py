@@ -68,8 +68,8 @@ def test_trainer_streaming_equals_resident():
 
 
 @pytest.mark.parametrize("cls_name", ["FinancialLstmMse", "FinancialLstmNll", "FinancialLstmCombined"])
-@pytest.mark.parametrize("B", [1, 2])
-def test_fused_training_step_matches_autograd(cls_name, B):
+@pytest.mark.parametrize("B,H,L", [(1, 64, 2), (2, 64, 2), (1, 16, 2), (1, 16, 1), (2, 32, 1)])
+def test_fused_training_step_matches_autograd(cls_name, B, H, L):
     """models/lstm.py fused_training_step (pipelined fwd + one-launch decoder + pipelined bwd, no autograd)
     against training_step + loss.backward(): same loss, gradients and epoch-metric sums, dropout on."""
     import masters_thesis_amd.models as M
@@ -79,7 +79,7 @@ def test_fused_training_step_matches_autograd(cls_name, B):
     out = []
     for fused in (False, True):
         torch.manual_seed(11)
-        model = getattr(M, cls_name)(dropout=0.2).to(DEV)
+        model = getattr(M, cls_name)(hidden_size=H, num_layers=L, dropout=0.2).to(DEV)
         model.lstm.seeds.copy_(torch.arange(8, device=DEV) * 977 + 5)
         model.matmul_precision = "highest"
         flat = FlatParameters(model.parameters())

@@ -77,7 +77,11 @@ def _ref(x, ws, L, masks=None):
 
 @pytest.mark.parametrize("prec", ["highest", "high", "medium"])
 @pytest.mark.parametrize("N,T,F,H,L", [(100, 60, 3, 64, 2), (37, 20, 5, 64, 3), (40, 15, 3, 32, 8),
-                                       (300, 60, 3, 64, 4)])
+                                       (300, 60, 3, 64, 4),
+                                       # thesis grid (tex/diplomski_rad.tex:1106-1122): H in {16, 32}, L in {1, 2};
+                                       # H=16 runs zero-padded on the H=32 kernels, L=1 in the same launch
+                                       (100, 60, 3, 16, 1), (100, 60, 3, 16, 2), (100, 60, 3, 32, 1),
+                                       (100, 60, 3, 64, 1), (50, 20, 5, 24, 3)])
 def test_pipelined_matches_fp64(prec, N, T, F, H, L):
     from masters_thesis_amd.ops import lstm as op
 
