@@ -153,6 +153,8 @@ class FinancialLstm(LightningModule):
         grads), pipelined LSTM backward (+ weight grads)] without autograd: HIP path, pipelined kernel
         applicable, decoder small enough for one workgroup."""
         x, y = batch[0], batch[1]
+        if not isinstance(getattr(self, "lstm", None), LSTMStack):  # MLP / transformer encoders (models/extras.py)
+            return False
         if self.backend == "torch" or not use_hip(x) or not self.training:
             return False
         if any(p.grad is None for p in self.parameters()):

@@ -191,3 +191,36 @@ def test_extras_dropout_train_vs_eval_and_finite_grads():
         loss = m.training_step(batch, 0)
         loss.backward()
         assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+@pytest.mark.parametrize("arch", ["mlp", "transformer"])
+def test_extras_train_through_trainer_graph(arch):
+    """The extras encoders through the Trainer's captured training step (graph warm-up, capture, replays):
+    the fused-LSTM step must not be taken for them, and training must stay finite."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import get_model_class
+
+    g = torch.Generator().manual_seed(0)
+    W = 6
+    data = [torch.randn(W, 100, 60, 3, generator=g), torch.randn(W, 100, 30, 4, generator=g) * 0.01,
+            torch.stack([torch.randn(W, generator=g) * 0.01, torch.rand(W, generator=g) * 1e-3 + 1e-4], -1),
+            torch.rand(W, 100, generator=g) * 3 + 1]
+    cls = get_model_class("FinancialLstmCombined", arch)
+    kw = dict(input_size=3, hidden_size=128 if arch == "transformer" else 256, num_layers=2, dropout=0.1,
+              learning_rate=1e-4)
+    if arch == "transformer":
+        kw.update(num_heads=4, mlp_ratio=4)
+    model = cls(**kw)
+    tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False, use_hip_graphs=True)
+    tr._setup_env()
+    tr._setup_model(model)
+    tr._configure_optimizers(model)
+    model.train()
+    assert not model.fused_step_supported([t.to(DEV) for t in data])
+    step = tr.make_train_stepper(TensorBatchLoader([t.to(DEV) for t in data], 1, shuffle=True, seed=0))
+    for _ in range(8):
+        loss = step()
+    torch.cuda.synchronize()
+    assert torch.isfinite(tr.flat.data).all() and torch.isfinite(loss).all()
+    assert tr._graphs  # the step was captured and replayed
