@@ -61,6 +61,8 @@ def parse_args(argv=None):
                     help="torch = reference-equivalent PyTorch eager path (MIOpen LSTM) for A/B")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--n-samples", type=int, default=1_000_000, help="synthetic DGP days (reference: 1e6)")
+    ap.add_argument("--residency", default="device", choices=["device", "stream"],
+                    help="device: split resident in HBM; stream: pinned host ring + side-stream H2D per step")
     return ap.parse_args(argv)
 
 
@@ -81,7 +83,8 @@ def main(argv=None):
 
     cfg, _, _ = compose(REPO / "configs", "config", [
         f"model={args.model}", f"loss={args.loss}", f"trainer={args.trainer}",
-        f"datamodule.batch_size={args.batch}", f"datamodule.n_samples={args.n_samples}"])
+        f"datamodule.batch_size={args.batch}", f"datamodule.n_samples={args.n_samples}",
+        f"datamodule.residency={args.residency}"])
     if args.backend == "torch":
         cfg.model["backend"] = "torch"
     t_data = time.perf_counter()
@@ -188,6 +191,7 @@ def main(argv=None):
                 "matmul_precision": args.matmul_precision,
                 "backend": "hip" if args.backend == "auto" else "torch-miopen",
                 "hip_graphs": not args.no_graphs,
+                "residency": args.residency,
             },
         }
         print(json.dumps(rec), flush=True)

@@ -61,19 +61,20 @@ union Bf8 {
   __bf16 e[8];
 };
 
-template <int BM, int BN, bool AT, bool BT>
+template <int BM, int BN, int BKT, bool AT, bool BT>
 __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
+  constexpr int RST = BKT + 8;  // LDS row stride (bf16): BKT + 8 pad (16 B): conflict-free b128 rows
   constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
   // staging work items: non-transposed = 16-B chunks (row, 8 k); transposed = 8x8 blocks (8 k-rows x 8 cols)
-  constexpr int A_ITEMS = AT ? (BK / 8) * (BM / 8) : BM * (BK / 8);
-  constexpr int B_ITEMS = BT ? (BK / 8) * (BN / 8) : BN * (BK / 8);
+  constexpr int A_ITEMS = AT ? (BKT / 8) * (BM / 8) : BM * (BKT / 8);
+  constexpr int B_ITEMS = BT ? (BKT / 8) * (BN / 8) : BN * (BKT / 8);
   constexpr int A_PER = (A_ITEMS + GT - 1) / GT;
   constexpr int B_PER = (B_ITEMS + GT - 1) / GT;
   constexpr int A_REGS = AT ? 8 : 1;  // 16-B loads per item
   constexpr int B_REGS = BT ? 8 : 1;
 
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * RS];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * RS];
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * RST];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * RST];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -93,13 +94,13 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
       const int it = tid + p * GT;
       uint32_t msk = 0;
       if constexpr (!AT) {
-        const int r = it / (BK / 8), c = it % (BK / 8);
+        const int r = it / (BKT / 8), c = it % (BKT / 8);
         const int m = m0 + r, k = k0 + 8 * c;
         const bool ok = (it < A_ITEMS) & (m < g.M) & (k < kend);
         ra[p][0] = *reinterpret_cast<const uint4*>(g.A + (size_t)(ok ? m : 0) * g.lda + (ok ? k : 0));
         msk = ok ? 1u : 0u;
       } else {
-        const int kb = it % (BK / 8), mb8 = it / (BK / 8);
+        const int kb = it % (BKT / 8), mb8 = it / (BKT / 8);
         const int m = m0 + 8 * mb8;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -116,13 +117,13 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
       const int it = tid + p * GT;
       uint32_t msk = 0;
       if constexpr (!BT) {
-        const int r = it / (BK / 8), c = it % (BK / 8);
+        const int r = it / (BKT / 8), c = it % (BKT / 8);
         const int n = n0 + r, k = k0 + 8 * c;
         const bool ok = (it < B_ITEMS) & (n < g.N) & (k < kend);
         rb[p][0] = *reinterpret_cast<const uint4*>(g.B + (size_t)(ok ? n : 0) * g.ldb + (ok ? k : 0));
         msk = ok ? 1u : 0u;
       } else {
-        const int kb = it % (BK / 8), nb8 = it / (BK / 8);
+        const int kb = it % (BKT / 8), nb8 = it / (BKT / 8);
         const int n = n0 + 8 * nb8;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -143,10 +144,10 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
       const int it = tid + p * GT;
       if (it >= A_ITEMS) continue;
       if constexpr (!AT) {
-        const int r = it / (BK / 8), c = it % (BK / 8);
-        *reinterpret_cast<uint4*>(&As[r * RS + 8 * c]) = and_mask(ra[p][0], ma[p] & 1u);
+        const int r = it / (BKT / 8), c = it % (BKT / 8);
+        *reinterpret_cast<uint4*>(&As[r * RST + 8 * c]) = and_mask(ra[p][0], ma[p] & 1u);
       } else {
-        const int kb = it % (BK / 8), mb8 = it / (BK / 8);
+        const int kb = it % (BKT / 8), mb8 = it / (BKT / 8);
         Bf8 in[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) in[i].u = and_mask(ra[p][i], (ma[p] >> i) & 1u);
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
           Bf8 o;
 #pragma unroll
           for (int i = 0; i < 8; ++i) o.e[i] = in[i].e[j];
-          *reinterpret_cast<uint4*>(&As[(8 * mb8 + j) * RS + 8 * kb]) = o.u;
+          *reinterpret_cast<uint4*>(&As[(8 * mb8 + j) * RST + 8 * kb]) = o.u;
         }
       }
     }
@@ -164,10 +165,10 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
       const int it = tid + p * GT;
       if (it >= B_ITEMS) continue;
       if constexpr (!BT) {
-        const int r = it / (BK / 8), c = it % (BK / 8);
-        *reinterpret_cast<uint4*>(&Bs[r * RS + 8 * c]) = and_mask(rb[p][0], mb[p] & 1u);
+        const int r = it / (BKT / 8), c = it % (BKT / 8);
+        *reinterpret_cast<uint4*>(&Bs[r * RST + 8 * c]) = and_mask(rb[p][0], mb[p] & 1u);
       } else {
-        const int kb = it % (BK / 8), nb8 = it / (BK / 8);
+        const int kb = it % (BKT / 8), nb8 = it / (BKT / 8);
         Bf8 in[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) in[i].u = and_mask(rb[p][i], (mb[p] >> i) & 1u);
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
           Bf8 o;
 #pragma unroll
           for (int i = 0; i < 8; ++i) o.e[i] = in[i].e[j];
-          *reinterpret_cast<uint4*>(&Bs[(8 * nb8 + j) * RS + 8 * kb]) = o.u;
+          *reinterpret_cast<uint4*>(&Bs[(8 * nb8 + j) * RST + 8 * kb]) = o.u;
         }
       }
     }
@@ -193,25 +194,29 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   const bool want_rowsum = g.bias_grad != nullptr && blockIdx.x == 0 && wn == 0;
 
   load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
     __syncthreads();
     store();
     __syncthreads();
-    if (k0 + BK < kend) load(k0 + BK);
-    bf16x8 af[MT];
+    if (k0 + BKT < kend) load(k0 + BKT);
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      af[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WM + 16 * i + (lane & 15)) * RS + 8 * (lane >> 4)]);
-      if (want_rowsum) {
+    for (int ks = 0; ks < BKT / 32; ++ks) {
+      bf16x8 af[MT];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) rowsum[i] += (float)af[i][j];
+      for (int i = 0; i < MT; ++i) {
+        af[i] = *reinterpret_cast<const bf16x8*>(&As[(wm * WM + 16 * i + (lane & 15)) * RST + 32 * ks + 8 * (lane >> 4)]);
+        if (want_rowsum) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) rowsum[i] += (float)af[i][j];
+        }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(&Bs[(wn * WN + 16 * j + (lane & 15)) * RS + 8 * (lane >> 4)]);
+      for (int j = 0; j < NT; ++j) {
+        const bf16x8 bfr =
+            *reinterpret_cast<const bf16x8*>(&Bs[(wn * WN + 16 * j + (lane & 15)) * RST + 32 * ks + 8 * (lane >> 4)]);
 #pragma unroll
-      for (int i = 0; i < MT; ++i) acc[i][j] = mfma16x16x32(af[i], bfr, acc[i][j]);
+        for (int i = 0; i < MT; ++i) acc[i][j] = mfma16x16x32(af[i], bfr, acc[i][j]);
+      }
     }
   }
 
@@ -256,18 +261,26 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   }
 }
 
-template <int BM, int BN, bool AT, bool BT>
+template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ksplit);
-  gemm_bf16_kernel<BM, BN, AT, BT><<<grid, GT, 0, st>>>(g);
+  gemm_bf16_kernel<BM, BN, BKT, AT, BT><<<grid, GT, 0, st>>>(g);
 }
 
 template <bool AT, bool BT>
 void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
-  // 128x128 tiles once they already fill the chip; 64x64 otherwise (these encoders' GEMMs are small)
+  // 128x128 tiles once they already fill the chip; 64x64 otherwise (these encoders' GEMMs are small).
+  // K per workgroup >= 128: 128-deep k-steps (4 MFMA k-substeps per barrier pair) — the small-K GEMMs of the
+  // transformer (K = 128) then stage once instead of paying four dependent load -> LDS -> MFMA rounds
   const long tiles128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * ksplit;
-  if (tiles128 >= 256) launch<128, 128, AT, BT>(g, ksplit, st);
-  else launch<64, 64, AT, BT>(g, ksplit, st);
+  const bool deep = g.k_per_split >= 128;
+  if (tiles128 >= 256) {
+    if (deep) launch<128, 128, 64, AT, BT>(g, ksplit, st);
+    else launch<128, 128, 32, AT, BT>(g, ksplit, st);
+  } else {
+    if (deep) launch<64, 64, 128, AT, BT>(g, ksplit, st);
+    else launch<64, 64, 32, AT, BT>(g, ksplit, st);
+  }
 }
 
 }  // namespace
