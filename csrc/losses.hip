@@ -105,7 +105,7 @@ __device__ void losses_body(const float* ab, const LossArgs& A, float* ut, const
         sdd = wave_sum_dpp(sdd);
         if (lane == 0) {
           s_wbb += (double)wb * b;
-          s_logw += log((double)w);
+          s_logw += (double)logf(w);  // fp32 log (fp64 log is a long software sequence), fp64 sum
           s_wdd += (double)w * sdd;
         }
       }
@@ -277,12 +277,18 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
   float* gn = gm + N2;                   // 2N  d nll / d(alpha, beta)
   float* ut = gn + N2;                   // ut_floats(n)
   float2* ys = reinterpret_cast<float2*>(ut + ((ut_floats(n) + 3) & ~(size_t)3));  // (N, n) when YL
+  float* hl = reinterpret_cast<float*>(ys + (size_t)N * n);                       // (N, H) when YL
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if constexpr (YL) {
+    // one burst: every y pair and every h_T element in flight at once (the per-sequence loops below then
+    // read LDS instead of paying a dependent global round trip per iteration)
     for (int e = tid; e < N * n; e += TPB) {
       const float* yp = A.y + (size_t)e * A.C;
       ys[e] = make_float2(yp[0], yp[1]);
     }
+    for (int e = tid; e < N * H; e += TPB) hl[e] = h[e];
+    __syncthreads();
+    h = hl;
   }
   for (int i = wid; i < N; i += NWAVES) {
     float sa = 0.f, sb = 0.f;
@@ -457,7 +463,7 @@ extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, co
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, nullptr, nullptr, acc};
   const size_t base = ((size_t)(3 * 2 * ((N + 1) & ~1)) + ((ut_floats(n) + 3) & ~(size_t)3)) * sizeof(float);
-  const size_t ybytes = (size_t)N * n * sizeof(float2);
+  const size_t ybytes = (size_t)N * n * sizeof(float2) + (size_t)N * H * sizeof(float);  // y pairs + h_T
   if (base + ybytes <= 96 * 1024) {
     heads_losses_train_kernel<true><<<1, TPB, base + ybytes, st>>>(h, H, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb,
                                                                    g_bb);

@@ -134,10 +134,16 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
         break;
       }
     }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    // wave 0 reads the partials in parallel (lane b: b, b+64, ...; all loads in flight at once, not a chain of
+    // dependent round trips) and reduces them in a fixed order: the same norm on every workgroup and every run
     float sq = 0.f;
-    for (int b = 0; b < (int)gridDim.x; ++b)
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += 64)
       sq += __hip_atomic_load(partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_norm = sqrtf(sq);
+    sq = wave_sum_dpp(sq);
+    if (threadIdx.x == 0) s_norm = sqrtf(sq);
   }
   __syncthreads();
   const float norm = s_norm;

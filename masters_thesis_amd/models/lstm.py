@@ -163,7 +163,7 @@ class FinancialLstm(LightningModule):
         drop = self.lstm.dropout if self.lstm.num_layers > 1 else 0.0
         return (lstm_op.pipeline_supported(ctx, self.lstm.flat_weights, self.lstm.num_layers)
                 and (drop == 0.0 or self.lstm.seeds is not None)
-                and train_decoder_fits(ctx.shape[0], int(y.shape[2])))
+                and train_decoder_fits(ctx.shape[0], int(y.shape[2]), self.lstm.hidden_size))
 
     def fused_training_step(self, batch, batch_idx):
         """``training_step`` + ``loss.backward()`` in one go; gradients accumulate into the parameters' ``.grad``

@@ -194,11 +194,11 @@ def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, ba
     return res if with_total else res[:3]
 
 
-def train_decoder_fits(N: int, n: int) -> bool:
+def train_decoder_fits(N: int, n: int, H: int = 0) -> bool:
     """Whether :func:`heads_losses_train`'s one-workgroup kernel takes (N sequences, n target days)."""
     ut = ((n + 3) & ~3) + 16 * n  # u_t + one partial row per wave (csrc/losses.hip ut_floats)
     base = (3 * 2 * ((N + 1) & ~1) + ((ut + 3) & ~3)) * 4
-    return base + N * n * 8 <= 96 * 1024 or base <= 60 * 1024
+    return base + N * n * 8 + N * H * 4 <= 96 * 1024 or base <= 60 * 1024
 
 
 def heads_losses_train(h: Tensor, wa: Tensor, ba: Tensor, wb: Tensor, bb: Tensor, y: Tensor, factor: Tensor,
