@@ -222,6 +222,27 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
 
   // ---- epilogue ----
   const bool split = gridDim.z > 1;
+  // operands the epilogue reads (residual stream, GELU input of a DGELU) are fetched for the whole tile first:
+  // interleaved with the output stores the compiler must keep each load behind the previous (possibly
+  // aliasing) store, i.e. one dependent global round trip per element (r2 trace: 13 us per residual GEMM)
+  float pre_in[MT][NT][4];
+  const bool acc_rmw = (g.flags & EPI_ACCUM) && !split;  // read-modify-write of the fp32 output
+  if ((g.flags & (EPI_RESID | EPI_DGELU)) || acc_rmw) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n0 + wn * WN + 16 * j + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
+          const size_t o = (size_t)m * g.ldc + n;
+          const bool ok = m < g.M && n < g.n_store;
+          pre_in[i][j][r] = !ok ? 0.f : acc_rmw ? g.out_f32[o] : (g.flags & EPI_RESID) ? g.resid[o]
+                                                                                       : (float)g.aux_in[o];
+        }
+      }
+  }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
@@ -235,15 +256,15 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
         const size_t o = (size_t)m * g.ldc + n;
         if (g.flags & EPI_ACCUM) {
           if (split) atomicAdd(g.out_f32 + o, v);
-          else g.out_f32[o] += v;
+          else g.out_f32[o] = pre_in[i][j][r] + v;
           continue;
         }
         if (g.flags & EPI_BIAS) v += g.bias[n];
         if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
         if (g.flags & EPI_GELU) v = mta_gelu(v);
         if (g.flags & EPI_DROPOUT) v *= mta_dropout_scale(*g.seed, (uint32_t)m, (uint32_t)n, g.drop_p);
-        if (g.flags & EPI_DGELU) v *= mta_gelu_grad((float)g.aux_in[o]);
-        if (g.flags & EPI_RESID) v += g.resid[o];
+        if (g.flags & EPI_DGELU) v *= mta_gelu_grad(pre_in[i][j][r]);
+        if (g.flags & EPI_RESID) v += pre_in[i][j][r];
         if (g.out_f32) g.out_f32[o] = v;
         if (g.out_bf16) g.out_bf16[o] = (__bf16)v;
       }
@@ -293,6 +314,7 @@ extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int 
   if (n_store <= 0 || n_store > N) n_store = N;
   if (M % 8 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc < n_store) return 1;
   if ((flags & EPI_ACCUM) == 0 && ksplit > 1) return 2;
+  if ((flags & EPI_RESID) && (flags & EPI_DGELU)) return 7;  // one prefetched epilogue operand
   if (bias_grad && mode != 2) return 3;
   GemmArgs g;
   g.A = static_cast<const __bf16*>(A);

@@ -15,6 +15,21 @@
 // corrected per-window batched NLL is windows=B, kwin=K, factor_stride=2.
 #include "common.h"
 
+#ifndef MTA_LOSS_STAMPS
+#define MTA_LOSS_STAMPS 0
+#endif
+#if MTA_LOSS_STAMPS
+// diagnostic build only (csrc/tools/losses_probe.hip): s_memtime at the phase boundaries of the training decoder
+__device__ unsigned long long mta_loss_stamps[8];
+#define LSTAMP(k)                                                                  \
+  {                                                                                \
+    __syncthreads();                                                               \
+    if (threadIdx.x == 0) mta_loss_stamps[(k)] = __builtin_amdgcn_s_memtime();     \
+  }
+#else
+#define LSTAMP(k)
+#endif
+
 namespace {
 
 constexpr int TPB = 1024;
@@ -279,6 +294,7 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
   float2* ys = reinterpret_cast<float2*>(ut + ((ut_floats(n) + 3) & ~(size_t)3));  // (N, n) when YL
   float* hl = reinterpret_cast<float*>(ys + (size_t)N * n);                       // (N, H) when YL
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  LSTAMP(0)
   if constexpr (YL) {
     // one burst: every y pair and every h_T element in flight at once (the per-sequence loops below then
     // read LDS instead of paying a dependent global round trip per iteration)
@@ -290,6 +306,7 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
     __syncthreads();
     h = hl;
   }
+  LSTAMP(1)
   for (int i = wid; i < N; i += NWAVES) {
     float sa = 0.f, sb = 0.f;
     for (int k = lane; k < H; k += 64) {
@@ -304,17 +321,21 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
       ab[2 * i + 1] = sb;
     }
   }
+  LSTAMP(2)
   __syncthreads();
   LossArgs L = A;
   L.gmse = gm;
   L.gnll = gn;
   losses_body<YL>(ab, L, ut, ys);
+  LSTAMP(3)
   __syncthreads();
   const float cm = A.c_mse, cn = A.want_nll ? A.c_nll : 0.f;
   float* d = ab;  // alpha/beta are dead: reuse for d(alpha, beta)
   for (int k = tid; k < 2 * N; k += TPB) d[k] = cn != 0.f ? fmaf(cn, gn[k], cm * gm[k]) : cm * gm[k];
   __syncthreads();
+  LSTAMP(4)
   heads_bwd_body(d, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb, g_bb);
+  LSTAMP(5)
 }
 
 // backward: d(alpha, beta) from the saved per-sequence gradients, then dh_T and the head weight

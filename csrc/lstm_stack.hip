@@ -252,16 +252,22 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       nrow[i] = n < N ? n : N - 1;
       nmask[i] = n < N ? 1.f : 0.f;
     }
-    float xin0[4][FIRST ? FIN0 : 1];
-    float4 xr[FIRST ? 1 : XR];
+    // Layer inputs are prefetched THREE steps ahead into two register sets (step s in set s & 1): a
+    // write-through hand-off is read from beyond L2 (sc1 stores drop the line), ~1-2 us, i.e. more than the one
+    // interval the single-set form gave it (layer >= 1 input waves waited on it every step, r2 stamp probe).
+    struct XBuf {
+      float x0[4][FIRST ? FIN0 : 1];
+      float4 xr[FIRST ? 1 : XR];
+    };
+    XBuf xbA, xbB;
     unsigned seen = base;
-    auto load_input = [&](int t) {
+    auto load_input = [&](int t, XBuf& xb) {
       if constexpr (FIRST) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float* xs = a.x + ((size_t)nrow[i] * T + t) * FIN0;
 #pragma unroll
-          for (int f = 0; f < FIN0; ++f) xin0[i][f] = xs[f];
+          for (int f = 0; f < FIN0; ++f) xb.x0[i][f] = xs[f];
         }
       } else {
         // poll only when the last value seen does not cover step t (polling every step from every
@@ -272,11 +278,13 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         for (int v = 0; v < XR; ++v) {
           // bf16: float4 v covers k = 32 (v/2) + 8 q + 4 (v&1) .. +4;  f32: k = KF q + 4 v .. +4
           const int k = PREC == PREC_F32 ? KF * q + 4 * v : 32 * (v >> 1) + 8 * q + 4 * (v & 1);
-          xr[v] = load_sc1(xin, row * H + k);
+          xb.xr[v] = load_sc1(xin, row * H + k);
         }
       }
     };
-    auto compute_gx = [&](int slot) {
+    auto compute_gx = [&](int slot, const XBuf& xb) {
+      const auto& xin0 = xb.x0;
+      const auto& xr = xb.xr;
       f32x4 acc[4];
       if constexpr (FIRST) {
 #pragma unroll
@@ -341,25 +349,32 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         mout[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u] = kb;  // before this interval's loads
       }
     };
-    load_input(0);
-    compute_gx(0);
-    if (T > 1) load_input(1);
+    load_input(0, xbA);
+    compute_gx(0, xbA);
+    if (T > 1) load_input(1, xbB);
+    if (T > 2) load_input(2, xbA);
     __syncthreads();  // pre-loop barrier: gx_0 ready
     SSTAMP_DECL
-    for (int t = 0; t < T; ++t) {
+    // interval t computes gx_{t+1} from set (t+1) & 1 and refills that set with x_{t+3}; unrolled by two so
+    // the sets are static registers
+    auto interval = [&](int t, XBuf& xb) {
       SSTAMP(0)
       // step t's keep bytes, into slot t & 1: read by the recurrent waves at the top of step t+1 (and after
       // the loop for step T-1); the slot is rewritten in interval t+2, after barrier t+1
       draw_mask(t);
       if (t + 1 < T) {
         if constexpr (!FIRST && MTA_STACK_GX_DELAY > 0) __builtin_amdgcn_s_sleep(MTA_STACK_GX_DELAY);
-        compute_gx((t + 1) & 1);          // x_{t+1} arrived during step t-1
+        compute_gx((t + 1) & 1, xb);          // x_{t+1}, loaded two intervals ago
         SSTAMP(1)
-        if (t + 2 < T) load_input(t + 2); // (waits for the producer here, off the recurrent path)
+        if (t + 3 < T) load_input(t + 3, xb); // (waits for the producer here, off the recurrent path)
         SSTAMP(2)
       }
       __syncthreads();
       SSTAMP(3)
+    };
+    for (int t = 0; t < T; t += 2) {
+      interval(t, xbB);
+      if (t + 1 < T) interval(t + 1, xbA);
     }
     SSTAMP_FLUSH(0, 1, w == 0)
     __syncthreads();  // final barrier (the recurrent waves publish after it)
