@@ -338,6 +338,304 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
   LSTAMP(5)
 }
 
+// ---- register-resident training decoder (N <= 128, n <= 32, H in {16, 32, 64, 128}, <= 4 NLL windows) ----
+#ifndef MTA_DECODER_REG
+#define MTA_DECODER_REG 1  // 0: always the wave-per-sequence kernel above (kept for comparison in the probe)
+#endif
+// The wave-per-sequence kernel above loops 16 waves over the sequences with a full 64-lane reduction per
+// sequence and quantity, and stages y and h_T through LDS first: 12.9 us for the headline step's MSE decoder
+// (r2 rocprof), almost all of it dependent latency.  Here every input is loaded ONCE, straight into registers,
+// in one burst (h_T as float4 rows, G = H/4 lanes per sequence; y as (r, r_mkt) pairs, one 32-lane half-wave
+// per sequence, lane = target day), and every per-sequence quantity is a DPP half-wave (or G-lane) reduction
+// whose result lands in every lane that needs it — the only LDS traffic is alpha/beta, the Woodbury u_t
+// partials and d(alpha, beta).  Six block barriers in NLL mode, three in MSE mode.  All reductions run in a
+// fixed order (bit-reproducible).
+constexpr int RD_MAXP = 4, RD_MAXN = 128, RD_MAXW = 4;
+
+// sum over aligned groups of G lanes (G in 4..32), the result in every lane of the group; whole waves only
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+  v += mta_dpp<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += mta_dpp<0x4E>(v);  // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v += mta_dpp<0x141>(v);   // row_half_mirror: the other quad of the 8-lane half-row
+  if constexpr (G >= 16) v += mta_dpp<0x140>(v);  // row_mirror: the other half-row
+  if constexpr (G >= 32) v += __shfl_xor(v, 16);
+  return v;
+}
+
+template <int G>
+__global__ __launch_bounds__(TPB) void decoder_train_reg_kernel(
+    const float* __restrict__ h, const float* __restrict__ wa, const float* __restrict__ ba,
+    const float* __restrict__ wb, const float* __restrict__ bb, LossArgs A, float* __restrict__ dh,
+    float* __restrict__ g_wa, float* __restrict__ g_ba, float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  constexpr int H = 4 * G, SPP = TPB / G;  // sequences per h pass
+  __shared__ float2 ab[RD_MAXN], dab[RD_MAXN];
+  __shared__ float cpart[RD_MAXN * 33];    // w_i b_i D_it, row i (stride 33); later the head-gradient partials
+  __shared__ float upart[RD_MAXW][32][33];  // u_t partials: [window][sequence residue q][t]
+  __shared__ float4 sq[RD_MAXN];            // per sequence: w b^2, log w, w sum_t D^2
+  __shared__ float us[RD_MAXW][32];
+  __shared__ double wsum[RD_MAXW][8];       // per window: s_wbb, s_logw, s_wdd, U1, U2, den, nll
+  __shared__ double red[NWAVES][2];
+  const int N = A.N, n = A.n, C = A.C;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int t = tid & 31, hw = tid >> 5;   // y mapping: half-wave hw owns sequence p*32 + hw, lane t = day t
+  const int k4 = tid % G, hs = tid / G;    // h mapping: G lanes own sequence p*SPP + hs, float4 column k4
+  const int yp = (N + 31) >> 5, hp = (N + SPP - 1) / SPP;
+  const bool nll = A.want_nll != 0;
+  // ---- one load burst: y pairs, inverse idiosyncratic variances, h_T rows, head weights ----
+  float2 yv[RD_MAXP];
+  float psi[RD_MAXP], fmv[RD_MAXP];
+  float4 hv[RD_MAXP];
+#pragma unroll
+  for (int p = 0; p < RD_MAXP; ++p) {
+    const int i = p * 32 + hw;
+    yv[p] = make_float2(0.f, 0.f);
+    psi[p] = 1.f;
+    fmv[p] = 0.f;
+    if (p < yp && i < N) {
+      if (t < n) yv[p] = *reinterpret_cast<const float2*>(A.y + ((size_t)i * n + t) * C);
+      if (nll) {
+        psi[p] = A.inv_psi[i];
+        fmv[p] = A.factor[(i / A.kwin) * A.factor_stride];
+      }
+    }
+    const int ih = p * SPP + hs;
+    hv[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (p < hp && ih < N) hv[p] = *reinterpret_cast<const float4*>(h + (size_t)ih * H + 4 * k4);
+  }
+  // head weights are slices of the flat parameter buffer: scalar loads (no alignment to rely on)
+  const float4 wa4 = make_float4(wa[4 * k4], wa[4 * k4 + 1], wa[4 * k4 + 2], wa[4 * k4 + 3]);
+  const float4 wb4 = make_float4(wb[4 * k4], wb[4 * k4 + 1], wb[4 * k4 + 2], wb[4 * k4 + 3]);
+  const float bav = ba[0], bbv = bb[0];
+  // ---- heads: alpha_i = h_i . wa + ba, beta_i = h_i . wb + bb (G-lane reductions) ----
+#pragma unroll
+  for (int p = 0; p < RD_MAXP; ++p) {
+    if (p < hp) {  // uniform
+      const float4 x = hv[p];
+      float sa = x.x * wa4.x + x.y * wa4.y + x.z * wa4.z + x.w * wa4.w;
+      float sb = x.x * wb4.x + x.y * wb4.y + x.z * wb4.z + x.w * wb4.w;
+      sa = group_sum<G>(sa);
+      sb = group_sum<G>(sb);
+      const int i = p * SPP + hs;
+      if (k4 == 0 && i < N) ab[i] = make_float2(sa + bav, sb + bbv);
+    }
+  }
+  __syncthreads();  // #1 alpha, beta
+  // ---- MSE / MAE, NLL per-sequence terms (half-wave per sequence) ----
+  const float inv_cnt = 1.0f / ((float)N * (float)n);
+  float gma[RD_MAXP], gmb[RD_MAXP], sdv[RD_MAXP], dv[RD_MAXP];
+  float ss = 0.f, sa = 0.f;
+#pragma unroll
+  for (int p = 0; p < RD_MAXP; ++p) {
+    gma[p] = gmb[p] = sdv[p] = dv[p] = 0.f;
+    if (p < yp) {  // uniform
+      const int i = p * 32 + hw;
+      const bool seq = i < N, valid = seq && t < n;
+      const float2 abi = seq ? ab[i] : make_float2(0.f, 0.f);
+      const float r = yv[p].x, rm = yv[p].y;
+      const float e = valid ? fmaf(abi.y, rm, abi.x) - r : 0.f;
+      ss = fmaf(e, e, ss);
+      sa += fabsf(e);
+      gma[p] = 2.f * group_sum<32>(e) * inv_cnt;
+      gmb[p] = 2.f * group_sum<32>(e * rm) * inv_cnt;
+      if (nll) {
+        const float w = psi[p], mu = fmaf(abi.y, fmv[p], abi.x);
+        const float D = valid ? r - mu : 0.f;
+        dv[p] = D;
+        const float sdd = group_sum<32>(D * D);
+        sdv[p] = group_sum<32>(D);
+        if (seq) {
+          cpart[i * 33 + t] = w * abi.y * D;
+          if (t == 0) sq[i] = make_float4(w * abi.y * abi.y, logf(w), w * sdd, 0.f);
+        }
+      }
+    }
+  }
+  {
+    const double s1 = wave_sum_dpp((double)ss), s2 = wave_sum_dpp((double)sa);
+    if (lane == 0) {
+      red[wid][0] = s1;
+      red[wid][1] = s2;
+    }
+  }
+  const float cm = A.c_mse, cn = nll ? A.c_nll : 0.f;
+  if (nll) {
+    const int W = A.windows, kwin = A.kwin;
+    __syncthreads();  // #2 cpart, sq
+    // ---- u_t partials (thread (q, t) sums the window's sequences i0 + q, i0 + q + 32, ...) and the
+    //      per-window sequence sums (wave w) ----
+    for (int w = 0; w < W; ++w) {
+      float u = 0.f;
+      for (int k = hw; k < kwin; k += 32) u += cpart[(w * kwin + k) * 33 + t];
+      upart[w][hw][t] = u;
+    }
+    if (wid < W) {
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+      for (int k = lane; k < kwin; k += 64) {
+        const float4 q = sq[wid * kwin + k];
+        s0 += q.x;
+        s1 += q.y;
+        s2 += q.z;
+      }
+      s0 = wave_sum_dpp(s0);
+      s1 = wave_sum_dpp(s1);
+      s2 = wave_sum_dpp(s2);
+      if (lane == 0) {
+        wsum[wid][0] = s0;
+        wsum[wid][1] = s1;
+        wsum[wid][2] = s2;
+      }
+    }
+    __syncthreads();  // #3 upart, window sums
+    // ---- u_t, U1 = sum_t u_t, U2 = sum_t u_t^2 and the window's NLL (half-wave w) ----
+    if (hw < W) {
+      const int w = hw;
+      float u = 0.f;
+      for (int q = 0; q < 32; ++q) u += upart[w][q][t];
+      u = t < n ? u : 0.f;
+      us[w][t] = u;
+      const double U1 = group_sum<32>((double)u), U2 = group_sum<32>((double)u * u);
+      if (t == 0) {
+        const float fv = A.factor[w * A.factor_stride + 1];
+        const double den = 1.0 / (double)fv + wsum[w][0];
+        const double logdet = wsum[w][1] - log((double)fv * den);
+        wsum[w][3] = U1;
+        wsum[w][4] = U2;
+        wsum[w][5] = den;
+        wsum[w][6] = 0.5 * ((double)n * ((double)kwin * LOG2PI - logdet) + (wsum[w][2] - U2 / den));
+      }
+    }
+    __syncthreads();  // #4 u_t, U1, U2, den
+    // ---- d(alpha, beta) with the NLL gradients (derivation in ops/losses.py) ----
+#pragma unroll
+    for (int p = 0; p < RD_MAXP; ++p) {
+      if (p < yp) {
+        const int i = p * 32 + hw;
+        const int w = i < N ? i / kwin : 0;
+        const float ud = group_sum<32>(us[w][t] * dv[p]);
+        if (t == 0 && i < N) {
+          const float b = ab[i].y, wi = psi[p], fm = fmv[p], sd = sdv[p];
+          const float fden = (float)wsum[w][5], fU1 = (float)wsum[w][3], fU2 = (float)wsum[w][4];
+          const float wbi = wi * b;
+          const float gna = -wi * sd + wbi * fU1 / fden;
+          const float gnb = (float)n * wbi / fden - fm * (wi * sd - wbi * fU1 / fden) - wi * ud / fden +
+                            fU2 * wbi / (fden * fden);
+          dab[i] = cn != 0.f ? make_float2(fmaf(cn, gna, cm * gma[p]), fmaf(cn, gnb, cm * gmb[p]))
+                             : make_float2(cm * gma[p], cm * gmb[p]);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int p = 0; p < RD_MAXP; ++p) {
+      const int i = p * 32 + hw;
+      if (p < yp && t == 0 && i < N) dab[i] = make_float2(cm * gma[p], cm * gmb[p]);
+    }
+  }
+  __syncthreads();  // #5 d(alpha, beta)  (NLL) / #2 (MSE)
+  // ---- dh_T = d_alpha wa + d_beta wb; head-weight gradients: column sums over the sequences ----
+  float4 ga = make_float4(0.f, 0.f, 0.f, 0.f), gb = ga;
+#pragma unroll
+  for (int p = 0; p < RD_MAXP; ++p) {
+    const int i = p * SPP + hs;
+    if (p < hp && i < N) {
+      const float2 d = dab[i];
+      const float4 x = hv[p];
+      *reinterpret_cast<float4*>(dh + (size_t)i * H + 4 * k4) =
+          make_float4(d.x * wa4.x + d.y * wb4.x, d.x * wa4.y + d.y * wb4.y, d.x * wa4.z + d.y * wb4.z,
+                      d.x * wa4.w + d.y * wb4.w);
+      ga = make_float4(fmaf(d.x, x.x, ga.x), fmaf(d.x, x.y, ga.y), fmaf(d.x, x.z, ga.z), fmaf(d.x, x.w, ga.w));
+      gb = make_float4(fmaf(d.y, x.x, gb.x), fmaf(d.y, x.y, gb.y), fmaf(d.y, x.z, gb.z), fmaf(d.y, x.w, gb.w));
+    }
+  }
+#pragma unroll
+  for (int m = G; m < 64; m <<= 1) {  // the wave's sequences sharing column k4
+    ga.x += __shfl_xor(ga.x, m);
+    ga.y += __shfl_xor(ga.y, m);
+    ga.z += __shfl_xor(ga.z, m);
+    ga.w += __shfl_xor(ga.w, m);
+    gb.x += __shfl_xor(gb.x, m);
+    gb.y += __shfl_xor(gb.y, m);
+    gb.z += __shfl_xor(gb.z, m);
+    gb.w += __shfl_xor(gb.w, m);
+  }
+  float4* gpart = reinterpret_cast<float4*>(cpart);  // cpart is dead after barrier #3 / never used (MSE)
+  if (lane < G) {
+    gpart[(wid * 2) * G + lane] = ga;
+    gpart[(wid * 2 + 1) * G + lane] = gb;
+  }
+  __syncthreads();  // #6 head-gradient partials
+  if (tid < 2 * G) {  // ordered sum over the waves
+    const int which = tid / G, k = tid % G;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int w = 0; w < NWAVES; ++w) {
+      const float4 v = gpart[(w * 2 + which) * G + k];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    float* g = (which ? g_wb : g_wa) + 4 * k;  // a slice of the flat gradient: no alignment to rely on
+    g[0] += s.x;
+    g[1] += s.y;
+    g[2] += s.z;
+    g[3] += s.w;
+  } else if (wid == NWAVES - 1) {  // bias gradients: sum over the sequences
+    float sa2 = 0.f, sb2 = 0.f;
+    for (int i = lane; i < N; i += 64) {
+      sa2 += dab[i].x;
+      sb2 += dab[i].y;
+    }
+    sa2 = wave_sum_dpp(sa2);
+    sb2 = wave_sum_dpp(sb2);
+    if (lane == 0) {
+      g_ba[0] += sa2;
+      g_bb[0] += sb2;
+    }
+  } else if (tid == 2 * G) {  // losses + metric accumulators
+    double s_sse = 0.0, s_sae = 0.0, nll_total = 0.0;
+    for (int w = 0; w < NWAVES; ++w) {
+      s_sse += red[w][0];
+      s_sae += red[w][1];
+    }
+    if (nll)
+      for (int w = 0; w < A.windows; ++w) nll_total += wsum[w][6];
+    const double cnt = (double)N * n, mse = s_sse / cnt;
+    const double total = (double)A.c_nll * nll_total + (double)A.c_mse * mse;
+    A.out[0] = (float)mse;
+    A.out[1] = (float)nll_total;
+    A.out[2] = (float)(s_sae / cnt);
+    A.out[3] = (float)total;
+    if (A.acc) {
+      A.acc[0] += s_sse;
+      A.acc[1] += cnt;
+      A.acc[2] += nll_total;
+      A.acc[3] += 1.0;
+      A.acc[4] += total * A.batch_weight;
+      A.acc[5] += A.batch_weight;
+      A.acc[6] += s_sae;
+      A.acc[7] += cnt;
+    }
+  }
+}
+
+template <int G>
+static void launch_decoder_reg(const float* h, const float* wa, const float* ba, const float* wb, const float* bb,
+                               const LossArgs& A, float* dh, float* g_wa, float* g_ba, float* g_wb, float* g_bb,
+                               hipStream_t st) {
+  decoder_train_reg_kernel<G><<<1, TPB, 0, st>>>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb);
+}
+
+static bool decoder_reg_fits(const float* h, const float* y, const float* dh, const float* wa, const float* wb,
+                             int H, int N, int n, int C, int windows, int kwin, int want_nll) {
+  const auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
+  if (!MTA_DECODER_REG || N < 1 || N > RD_MAXN || n < 1 || n > 32 || C < 2 || (C & 1)) return false;
+  if (H != 16 && H != 32 && H != 64 && H != 128) return false;
+  if ((N + 31) / 32 > RD_MAXP || ((long)N * H / 4 + TPB - 1) / TPB > RD_MAXP) return false;
+  if (want_nll && (windows < 1 || windows > RD_MAXW || (long)windows * kwin != N)) return false;
+  return al(h, 16) && al(dh, 16) && al(y, 8);
+}
+
 // backward: d(alpha, beta) from the saved per-sequence gradients, then dh_T and the head weight
 // gradients (accumulated into the parameters' gradient views)
 __global__ __launch_bounds__(TPB) void heads_losses_bwd_kernel(
@@ -483,6 +781,15 @@ extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, co
                                       float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, nullptr, nullptr, acc};
+  if (decoder_reg_fits(h, y, dh, wa, wb, H, N, n, C, windows, kwin, want_nll)) {
+    switch (H) {
+      case 16: launch_decoder_reg<4>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb, st); break;
+      case 32: launch_decoder_reg<8>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb, st); break;
+      case 64: launch_decoder_reg<16>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb, st); break;
+      default: launch_decoder_reg<32>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb, st); break;
+    }
+    return 0;
+  }
   const size_t base = ((size_t)(3 * 2 * ((N + 1) & ~1)) + ((ut_floats(n) + 3) & ~(size_t)3)) * sizeof(float);
   const size_t ybytes = (size_t)N * n * sizeof(float2) + (size_t)N * H * sizeof(float);  // y pairs + h_T
   if (base + ybytes <= 96 * 1024) {

@@ -21,8 +21,8 @@ int main(int argc, char** argv) {
   const int N = argc > 1 ? atoi(argv[1]) : 100, n = 30, C = 4, H = 64;
   const int want_nll = argc > 2 ? atoi(argv[2]) : 0;
   std::vector<float> hy((size_t)N * n * C), hh((size_t)N * H), hw(H), hip(N, 1.5f), hf = {0.001f, 0.0002f};
-  for (size_t i = 0; i < hy.size(); ++i) hy[i] = 0.01f * (float)((i * 7919) % 101 - 50) / 50.f;
-  for (size_t i = 0; i < hh.size(); ++i) hh[i] = (float)((i * 104729) % 201 - 100) / 100.f;
+  for (size_t i = 0; i < hy.size(); ++i) hy[i] = 0.01f * (float)((long)((i * 7919) % 101) - 50) / 50.f;
+  for (size_t i = 0; i < hh.size(); ++i) hh[i] = (float)((long)((i * 104729) % 201) - 100) / 100.f;
   for (int i = 0; i < H; ++i) hw[i] = 0.1f * (float)((i * 31) % 17 - 8) / 8.f;
   float *y, *h, *wa, *wb, *ba, *bb, *fac, *ip, *out, *dh, *g;
   double* acc;
@@ -63,7 +63,21 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&m, a, b));
     if (r >= 20) ms += m / (reps - 20);
   }
-  printf("N=%d want_nll=%d: heads_losses_train %.2f us/launch\n", N, want_nll, ms * 1e3);
+  printf("N=%d want_nll=%d reg=%d: heads_losses_train %.2f us/launch\n", N, want_nll, MTA_DECODER_REG, ms * 1e3);
+  // one fresh call for the values (the head gradients accumulate)
+  CK(hipMemset(g, 0, (2 * H + 2) * 4));
+  mta_heads_losses_train(h, H, wa, ba, wb, bb, y, fac, ip, N, n, C, 1, N, 0, want_nll, 1.f, 1.f, 1.f, out, acc, dh,
+                         g, g + H, g + H + 1, g + 2 * H + 1, 0);
+  CK(hipDeviceSynchronize());
+  std::vector<float> ho(4), hdh((size_t)N * H), hg(2 * H + 2);
+  CK(hipMemcpy(ho.data(), out, 16, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hdh.data(), dh, hdh.size() * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(hg.data(), g, hg.size() * 4, hipMemcpyDeviceToHost));
+  double sdh = 0, sg = 0;
+  for (size_t i = 0; i < hdh.size(); ++i) sdh += hdh[i] * (1.0 + i % 7);
+  for (size_t i = 0; i < hg.size(); ++i) sg += hg[i] * (1.0 + i % 5);
+  printf("  out = %.9g %.9g %.9g %.9g  dh.w = %.9g  g.w = %.9g  g_ba = %.9g g_bb = %.9g\n", ho[0], ho[1], ho[2],
+         ho[3], sdh, sg, hg[H], hg[2 * H + 1]);
 #if MTA_LOSS_STAMPS
   unsigned long long st[8];
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(mta_loss_stamps), sizeof(st)));

@@ -61,6 +61,17 @@ class _Graph:
         return self.out
 
 
+def _group_sizes(events):
+    """(event pair, steps it covers): a grouped graph's pair is repeated once per step it ran."""
+    out = []
+    for ev in events:
+        if out and out[-1][0] is ev:
+            out[-1][1] += 1
+        else:
+            out.append([ev, 1])
+    return [(ev, n) for ev, n in out for _ in range(n)]
+
+
 class Trainer:
     def __init__(self, max_epochs: int = 1000, gradient_clip_val: Optional[float] = None,
                  precision: str = "32-true", enable_progress_bar: bool = True, enable_model_summary: bool = True,
@@ -70,7 +81,7 @@ class Trainer:
                  limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
                  limit_test_batches: Optional[int] = None, default_root_dir: str = ".",
                  max_steps: int = -1, fail_at_step: Optional[int] = None, deterministic: bool = False,
-                 log_every_n_steps: int = 50):
+                 log_every_n_steps: int = 50, steps_per_graph: int = 8):
         self.max_epochs = int(max_epochs)
         self.max_steps = int(max_steps)
         self.gradient_clip_val = float(gradient_clip_val or 0.0)
@@ -84,6 +95,10 @@ class Trainer:
         self.accelerator = accelerator
         self.use_hip_graphs = use_hip_graphs
         self.graph_warmup_steps = max(1, int(graph_warmup_steps))
+        # consecutive training steps captured into ONE graph (device-resident loaders only): one graph launch per
+        # S steps instead of per step — the ~19 us launch gap between back-to-back graph replays (r2 kernel
+        # trace) is paid once per group.  Every step still runs in full (gather, fwd, decoder, bwd, optimizer).
+        self.steps_per_graph = max(1, int(os.environ.get("MTA_STEPS_PER_GRAPH", steps_per_graph)))
         self.matmul_precision = matmul_precision
         self.limit_train_batches = limit_train_batches
         self.limit_val_batches = limit_val_batches
@@ -343,6 +358,28 @@ class Trainer:
             self._after_graph()
         return out
 
+    def _can_group(self, loader) -> bool:
+        """Whether training steps on ``loader`` may be captured S at a time: graphs on, an in-graph gather
+        without per-step host hooks (device residency), the optimizer inside the graph."""
+        if self.steps_per_graph <= 1 or not self._graphs_enabled() or not self._static_ok(loader):
+            return False
+        pre, post = self._static_hooks(loader)
+        return pre is None and post is None and self._allreduce_in_graph()
+
+    def _train_group(self, loader, batch_idx: int, S: int):
+        """S consecutive training steps as one graph (see ``steps_per_graph``); each step gathers its own batch
+        through the loader's device cursor."""
+        B = loader.batch_size
+        self.model._current_batch_size = B
+
+        def body(first):
+            out = self._train_body(first, batch_idx)
+            for k in range(1, S):
+                out = self._train_body(loader.gather_static(), batch_idx + k)
+            return out
+
+        return self._run(("train", B, True, id(loader), S), loader.gather_static, body, True, self.graph_warmup_steps)
+
     def _eval_step(self, stage: str, loader, batch_idx: int, static: bool, batch=None):
         model = self.model
         fn = model.validation_step if stage == "val" else model.test_step
@@ -382,21 +419,36 @@ class Trainer:
         static = self._static_ok(loader)
         state = {"epoch": -1, "left": 0, "i": 0, "it": None}
 
-        def step():
-            if state["left"] == 0:
-                state["epoch"] += 1
+        group = self._can_group(loader)
+
+        def step(n: int = 1):
+            """Run ``n`` steps (n == steps_per_graph: one grouped graph when the epoch has room; else singly)."""
+            out = None
+            while n > 0:
+                if state["left"] == 0:
+                    state["epoch"] += 1
+                    if static:
+                        state["left"] = loader.begin_epoch(state["epoch"])
+                    else:
+                        loader.set_epoch(state["epoch"])
+                        batches = [b for b in loader if _batch_size(b) == loader.batch_size]
+                        state["it"] = iter(batches)
+                        state["left"] = len(batches)
+                S = self.steps_per_graph
+                if group and n >= S and state["left"] >= S:
+                    out = self._train_group(loader, state["i"] + 1, S)
+                    state["left"] -= S
+                    state["i"] += S
+                    n -= S
+                    continue
+                state["left"] -= 1
+                state["i"] += 1
+                n -= 1
                 if static:
-                    state["left"] = loader.begin_epoch(state["epoch"])
+                    out = self._train_step(loader, state["i"], True)
                 else:
-                    loader.set_epoch(state["epoch"])
-                    batches = [b for b in loader if _batch_size(b) == loader.batch_size]
-                    state["it"] = iter(batches)
-                    state["left"] = len(batches)
-            state["left"] -= 1
-            state["i"] += 1
-            if static:
-                return self._train_step(loader, state["i"], True)
-            return self._train_step(loader, state["i"], False, next(state["it"]))
+                    out = self._train_step(loader, state["i"], False, next(state["it"]))
+            return out
 
         return step
 
@@ -510,12 +562,32 @@ class Trainer:
 
         if static:
             nfull = loader.begin_epoch(epoch)
-            for i in range(min(nfull, n_batches)):
+            S = self.steps_per_graph if self._can_group(loader) else 1
+            nrun = min(nfull, n_batches)
+            i = 0
+            while i < nrun:
                 if 0 <= self.max_steps <= self.global_step:
                     break
+                room = nrun - i
+                if self.max_steps >= 0:
+                    room = min(room, self.max_steps - self.global_step)
+                fail_in = (self.fail_at_step is not None
+                           and self.global_step <= self.fail_at_step < self.global_step + S)
+                if S > 1 and room >= S and not fail_in:
+                    for k in range(S):
+                        pre_step(i + k)
+                    first = i
+                    n_ev = len(events)
+                    timed(lambda: self._train_group(loader, first, S))
+                    if cuda:  # one event pair per group: StepTimer gets S equal per-step shares
+                        events.extend([events[n_ev]] * (S - 1))
+                    i += S
+                    self.global_step += S
+                    continue
                 pre_step(i)
                 timed(lambda: self._train_step(loader, i, True))
                 self.global_step += 1
+                i += 1
             if n_batches > nfull and not (0 <= self.max_steps <= self.global_step):
                 tail = loader.tail_batch()
                 if tail is not None:
@@ -535,7 +607,8 @@ class Trainer:
         if cuda:
             torch.cuda.synchronize()
             skip = self.graph_warmup_steps + 1
-            host_ms = [a.elapsed_time(b) for a, b in (events[skip:] if len(events) > skip else events)]
+            host_ms = [a.elapsed_time(b) / n for (a, b), n in _group_sizes(events[skip:] if len(events) > skip
+                                                                           else events)]
         if self.enable_progress_bar and self.is_global_zero:
             sys.stdout.write("\n")
         return host_ms, B

@@ -129,3 +129,39 @@ def test_deterministic_mode_runs_are_bit_identical():
     a, b = run(True), run(True)
     assert torch.equal(a, b)
     torch.testing.assert_close(run(False), a, rtol=1e-4, atol=1e-6)
+
+
+def test_grouped_step_graphs_match_single_steps():
+    """Trainer(steps_per_graph=S): S consecutive steps captured as one graph (one launch per group, each step
+    gathering its own batch through the device cursor) train exactly like S single-step replays —
+    bit-identical parameters in deterministic mode, across epoch roll-overs (9 batches per epoch)."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import FinancialLstmCombined
+    from masters_thesis_amd.ops import lstm as op
+
+    def run(S):
+        torch.manual_seed(3)
+        model = FinancialLstmCombined(dropout=0.2)
+        ld = TensorBatchLoader([t.to(DEV) for t in _data(9)], 1, shuffle=True, seed=0)
+        tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=True, matmul_precision="high", deterministic=True, steps_per_graph=S)
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.lstm.seeds.copy_(torch.arange(8, device=DEV) + 17)
+        model.train()
+        assert tr._can_group(ld) == (S > 1)
+        step = tr.make_train_stepper(ld)
+        for _ in range(24 // S):
+            step(S)
+        torch.cuda.synchronize()
+        op.set_deterministic(False)
+        acc = model.train_acc.acc.clone() if hasattr(model, "train_acc") else None
+        return tr.flat.data.clone(), acc, model.lstm.seeds.clone()
+
+    (pa, aa, sa), (pb, ab, sb) = run(1), run(4)
+    assert torch.equal(pa, pb)
+    assert torch.equal(sa, sb)
+    if aa is not None:
+        assert torch.equal(aa, ab)

@@ -222,6 +222,57 @@ def test_heads_losses_grads_and_metric_accumulator(coeffs):
         tot_r.item()) + 1e-3
 
 
+@pytest.mark.parametrize("N,B,mode,H", [(100, 1, "reference", 64), (37, 1, "reference", 16), (128, 1, "reference", 128),
+                                         (100, 2, "per_window", 32), (120, 3, "per_window", 64),
+                                         (200, 1, "reference", 64)])
+@pytest.mark.parametrize("coeffs", [(0.0, 1.0), (1.0, 100.0)])
+def test_training_decoder_matches_fp64(N, B, mode, H, coeffs):
+    """ops/losses.py heads_losses_train (one launch: heads, losses, metric sums, dh_T, head gradients; the
+    register-resident kernel for N <= 128, the LDS-staged one above) against fp64 autograd of heads_losses."""
+    from masters_thesis_amd.ops.losses import heads_losses, heads_losses_train
+
+    torch.manual_seed(N + H)
+    n = 30
+    h = torch.randn(N, H, dtype=torch.float64) * 0.5
+    wa, ba = torch.randn(1, H, dtype=torch.float64) * 0.1, torch.randn(1, dtype=torch.float64) * 0.1
+    wb, bb = torch.randn(1, H, dtype=torch.float64) * 0.1, torch.ones(1, dtype=torch.float64)
+    y = torch.randn(N, n, 4, dtype=torch.float64) * 0.02
+    factor = torch.stack([torch.randn(B) * 0.01, torch.rand(B) * 0.002 + 0.001], -1).double()
+    inv_psi = torch.rand(N, dtype=torch.float64) * 300 + 100
+    ref_in = [t.clone().requires_grad_(True) for t in (h, wa, ba, wb, bb)]
+    _, mse_r, nll_r, mae_r, tot_r = heads_losses(*ref_in, y, factor, inv_psi, batch_windows=B, nll_mode=mode,
+                                                 c_nll=coeffs[0], c_mse=coeffs[1])
+    tot_r.backward()
+    d = lambda t: t.float().to(DEV)  # noqa: E731
+    grads = [torch.zeros(H, device=DEV), torch.zeros(1, device=DEV), torch.zeros(H, device=DEV),
+             torch.zeros(1, device=DEV)]
+    acc = torch.zeros(8, dtype=torch.float64, device=DEV)
+    res = heads_losses_train(d(h), d(wa).flatten(), d(ba), d(wb).flatten(), d(bb), d(y), d(factor), d(inv_psi),
+                             batch_windows=B, want_nll=coeffs[0] != 0, nll_mode=mode, c_nll=coeffs[0],
+                             c_mse=coeffs[1], acc=acc, grads=grads)
+    assert res is not None
+    out, dh = res
+    torch.cuda.synchronize()
+    o = out.double().cpu()
+    assert abs(o[0] - mse_r.item()) <= 1e-5 * abs(mse_r.item())
+    assert abs(o[2] - mae_r.item()) <= 1e-5 * abs(mae_r.item())
+    if coeffs[0]:
+        assert abs(o[1] - nll_r.item()) <= 2e-5 * abs(nll_r.item()) + 1e-3
+    assert abs(o[3] - tot_r.item()) <= 3e-5 * abs(tot_r.item()) + 1e-3
+
+    def close(a, b):
+        err = (a.double().cpu() - b).abs().max().item()
+        assert err <= 2e-4 * b.abs().max().item() + 1e-7, err
+
+    close(dh, ref_in[0].grad)
+    close(grads[0], ref_in[1].grad.flatten())
+    close(grads[1], ref_in[2].grad)
+    close(grads[2], ref_in[3].grad.flatten())
+    close(grads[3], ref_in[4].grad)
+    a = acc.cpu()
+    assert a[3] == 1 and abs(a[0] / a[1] - mse_r.item()) <= 1e-5 * abs(mse_r.item())
+
+
 def test_gather_batch_kernel_and_cursor():
     from masters_thesis_amd.data.datamodule import TensorBatchLoader
 
