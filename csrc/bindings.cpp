@@ -17,6 +17,8 @@ int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* in
                    int T, int H, int F, float* g_wih, float* g_whh, float* g_bih, float* g_bhh, float* part,
                    hipStream_t st);
 long mta_lstm_wgrad_part_floats(int fused, int T, int H, int F);
+int mta_gemm_f32(int prec, const float* A, const float* B, const float* bias, const float* mask, float* C, int M,
+                 int N, int K, int b_kn, hipStream_t st);
 void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
                    hipStream_t st);
 void mta_gather_batch(const float* const* src, float* const* dst, const long* row_floats, int ntensors,
@@ -71,6 +73,7 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
                        hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
+int mta_lstm_stack_epoch_shift(int T);
 // allreduce.hip (one-shot all-reduce over xGMI peer memory)
 int mta_xgmi_alloc(long bytes, void** out);
 int mta_xgmi_free(void* p);
@@ -185,6 +188,33 @@ void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bo
                                 g_wih.data_ptr<float>(), g_whh.data_ptr<float>(), g_bih.data_ptr<float>(),
                                 g_bhh.data_ptr<float>(), opt_mut(part), cur_stream());
   TORCH_CHECK(rc == 0, "lstm_wgrad: unsupported configuration (H=", H, ", F=", F, ")");
+}
+
+// C = A . B^T (+ bias) (* mask); B is [N][K], or [K][N] with b_kn (csrc/gemm_f32.hip)
+void gemm_f32(int64_t prec, at::Tensor A, at::Tensor B, at::Tensor C, c10::optional<at::Tensor> bias,
+              c10::optional<at::Tensor> mask, bool b_kn) {
+  MTA_CHECK_F32(A);
+  MTA_CHECK_F32(B);
+  MTA_CHECK_F32(C);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f32: 2-D operands");
+  const int64_t M = A.size(0), K = A.size(1), N = b_kn ? B.size(1) : B.size(0);
+  TORCH_CHECK((b_kn ? B.size(0) : B.size(1)) == K && C.size(0) == M && C.size(1) == N, "gemm_f32: shape mismatch");
+  const float* pb = nullptr;
+  const float* pm = nullptr;
+  if (bias && bias->defined()) {
+    MTA_CHECK_F32((*bias));
+    TORCH_CHECK(bias->numel() == N, "gemm_f32: bias[N]");
+    pb = bias->data_ptr<float>();
+  }
+  if (mask && mask->defined()) {
+    MTA_CHECK_F32((*mask));
+    TORCH_CHECK(mask->numel() == M * N, "gemm_f32: mask[M][N]");
+    pm = mask->data_ptr<float>();
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  const int rc = mta_gemm_f32((int)prec, A.data_ptr<float>(), B.data_ptr<float>(), pb, pm, C.data_ptr<float>(),
+                              (int)M, (int)N, (int)K, b_kn ? 1 : 0, cur_stream());
+  TORCH_CHECK(rc == 0, "gemm_f32: unsupported configuration (", rc, ")");
 }
 
 void lstm_prep(at::Tensor w_ih, at::Tensor b_ih, at::Tensor b_hh, int64_t H, at::Tensor w_um, at::Tensor b_um) {
@@ -825,6 +855,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_fwd", &lstm_stack_fwd);
   m.def("lstm_stack_bwd", &lstm_stack_bwd);
   m.def("lstm_stack_flag_words", &lstm_stack_flag_words);
+  m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("cast_pad", &cast_pad);
   m.def("norm", &norm);
@@ -833,6 +864,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd_layer", &lstm_bwd_layer);
   m.def("lstm_wgrad", &lstm_wgrad);
   m.def("lstm_prep", &lstm_prep);
+  m.def("gemm_f32", &gemm_f32);
   m.def("gather_batch", &gather_batch);
   m.def("decoder_losses", &decoder_losses);
   m.def("heads_losses", &heads_losses);

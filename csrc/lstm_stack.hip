@@ -70,7 +70,14 @@ constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;  // default poll bound (env MTA_LSTM_SPIN_LIMIT overrides: fault tests)
 constexpr int FLAG_STRIDE = 32;
 constexpr int TRS = 20;  // row stride (floats) of the per-wave 16 x 16 transpose scratch (conflict-free writes)
-constexpr int EPOCH_SHIFT = 12;  // one 128-byte line per progress word (polled words never share a line)
+// progress words are E << eshift | steps: eshift = epoch_shift(T) >= 12 bits (long sequences take more step bits;
+// the flag buffer a launch uses is keyed by its shift on the host, ops/lstm.py _stack_flags)
+constexpr int MIN_EPOCH_SHIFT = 12, MAX_EPOCH_SHIFT = 22;
+inline int epoch_shift(int T) {
+  int s = MIN_EPOCH_SHIFT;
+  while (s < MAX_EPOCH_SHIFT && (1 << s) <= T + 8) ++s;
+  return s;
+}
 
 __device__ __forceinline__ size_t stash_index(int t, int tile, int ntiles, int w, int nw, int lane) {
   // component k of a lane at + 64 k: every stash store / load instruction covers 1 KB contiguous
@@ -91,24 +98,25 @@ __device__ __forceinline__ void store_sc1_x4(float* p, f32x4 v) {
 constexpr int CTL_TIMEOUT = 0, CTL_FWD_EPOCH = 32, CTL_FWD_DONE = 64, CTL_BWD_EPOCH = 96, CTL_BWD_DONE = 128;
 constexpr int CTL_WORDS = 160;
 
-__device__ __forceinline__ unsigned read_epoch_base(unsigned* ctl, int which) {
-  return __hip_atomic_load(ctl + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << EPOCH_SHIFT;
+__device__ __forceinline__ unsigned read_epoch_base(unsigned* ctl, int which, int eshift) {
+  return __hip_atomic_load(ctl + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << eshift;
 }
 // every workgroup arrives once after its work; the last one re-arms the counter and advances the epoch
 // (every workgroup read the epoch before arriving, so no launch sees a torn value)
-__device__ __forceinline__ bool finish_launch(unsigned* ctl, int epoch_word, int done_word, unsigned base) {
+__device__ __forceinline__ bool finish_launch(unsigned* ctl, int epoch_word, int done_word, unsigned base,
+                                              int eshift) {
   __syncthreads();
   if (threadIdx.x != 0) return false;
   const unsigned prev = __hip_atomic_fetch_add(ctl + done_word, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
   if (prev != gridDim.x - 1) return false;
   __hip_atomic_store(ctl + done_word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(ctl + epoch_word, (base >> EPOCH_SHIFT) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(ctl + epoch_word, (base >> eshift) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
 
 // Progress words are never reset: a launch reads its epoch E (control word, advanced by the launch's last
-// workgroup) and publishes E * 4096 + steps, so a stale word of an earlier launch always compares below
-// (wrap-safe signed difference, T < 4096).  No memset node per launch.
+// workgroup) and publishes (E << eshift) + steps, so a stale word of an earlier launch always compares below
+// (wrap-safe signed difference, T + 8 < 2^eshift).  No memset node per launch.
 __device__ __forceinline__ bool reached(unsigned seen, unsigned need) { return (int)(seen - need) >= 0; }
 
 // wait until *flag reaches need (relaxed agent-scope polls); returns the value seen.  A wait that exceeds
@@ -161,7 +169,7 @@ struct StackFwdArgs {
   unsigned* timeout;
   unsigned* ctl;
   unsigned spin_limit;
-  int N, Np, T, L, ntiles, tr8;
+  int N, Np, T, L, ntiles, tr8, eshift;
 };
 
 // Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
@@ -583,13 +591,13 @@ template <int H, int PREC, int FIN0>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
   const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
-  const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH);
+  const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
   __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
   if (tile < a.ntiles) {
     if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
     else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
   }
-  finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base);
+  finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -618,7 +626,7 @@ struct StackBwdArgs {
   unsigned* timeout;
   unsigned* ctl;
   unsigned spin_limit;
-  int N, Np, T, L, ntiles, tr8;
+  int N, Np, T, L, ntiles, tr8, eshift;
   // fused weight gradients: wg_per_layer workgroups per layer follow the L x tr8 recurrence workgroups
   mta_wgrad::WgArgs wg[MAXL];
   int wg_nq, wg_per_layer;
@@ -956,7 +964,7 @@ template <int H, int PREC>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwdArgs a) {
   // one dynamic LDS block: the recurrence image (BwdSmem) or a weight-gradient staging image
   extern __shared__ __attribute__((aligned(16))) char dyn_lds[];
-  const unsigned base = read_epoch_base(a.ctl, CTL_BWD_EPOCH);
+  const unsigned base = read_epoch_base(a.ctl, CTL_BWD_EPOCH, a.eshift);
   const int nrec = a.L * a.tr8;
   if ((int)blockIdx.x < nrec) {
     // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
@@ -984,7 +992,7 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     __syncthreads();
     mta_wgrad::wgrad_body<PREC, H / 8, true>(w, chunk, quarter, dyn_lds);
   }
-  if (finish_launch(a.ctl, CTL_BWD_EPOCH, CTL_BWD_DONE, base) && a.dropout) {
+  if (finish_launch(a.ctl, CTL_BWD_EPOCH, CTL_BWD_DONE, base, a.eshift) && a.dropout) {
     // fresh counter-hash masks for the next step (the graph needs no seed-update node)
     for (int l = 0; l < a.L; ++l) a.seeds[l] += 0x9E3779B97F4A7C15ull;
   }
@@ -1036,6 +1044,8 @@ unsigned spin_limit() {
 
 // flags (zero-initialised once, then never reset): [3][MAXL][tr8] progress words (forward, backward dX,
 // backward dG; FLAG_STRIDE apart) + CTL_WORDS control words (timeout, per-direction epoch + arrival counter).
+extern "C" int mta_lstm_stack_epoch_shift(int T) { return epoch_shift(T); }
+
 extern "C" long mta_lstm_stack_flag_words(int Np) {
   const int tr8 = (Np / S + 7) / 8 * 8;
   return 3L * FLAG_STRIDE * MAXL * tr8 + CTL_WORDS;
@@ -1068,7 +1078,8 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.L = L;
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;  // tile i of every layer gets the same block id modulo 8
-  if (T >= (1 << EPOCH_SHIFT)) return -1;
+  a.eshift = epoch_shift(T);
+  if (T + 8 >= (1 << a.eshift)) return -1;
   a.flags = flags;
   a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
@@ -1085,7 +1096,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   float* const* g_whh, float* const* g_bih, float* const* g_bhh,
                                   const uint32_t* const* mask, float* const* part, uint64_t* seeds, float drop_p,
                                   int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
-  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T >= (1 << EPOCH_SHIFT)) return -1;
+  if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T + 8 >= (1 << MAX_EPOCH_SHIFT)) return -1;
   StackBwdArgs a{};
   for (int l = 0; l < L; ++l) {
     a.stash[l] = stash[l];
@@ -1106,6 +1117,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
   a.L = L;
   a.ntiles = Np / S;
   a.tr8 = (a.ntiles + 7) / 8 * 8;
+  a.eshift = epoch_shift(T);
   a.flags = flags + FLAG_STRIDE * MAXL * a.tr8;
   a.dg_flags = flags + 2 * FLAG_STRIDE * MAXL * a.tr8;
   a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;

@@ -37,6 +37,7 @@ from ..ops.optim import FlatParameters, FusedAdam
 from ..parallel import dist as pdist
 from ..parallel.ddp import FlatDDP
 from .callbacks import Callback, ModelCheckpoint, StepTimer
+from ..utils.profiling import PhaseTimer, phase
 from .checkpoint import (LIGHTNING_COMPAT_VERSION, atomic_save, capture_rng_states, load_checkpoint,
                          restore_rng_states)
 from .schedulers import PlateauScheduler
@@ -81,7 +82,8 @@ class Trainer:
                  limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
                  limit_test_batches: Optional[int] = None, default_root_dir: str = ".",
                  max_steps: int = -1, fail_at_step: Optional[int] = None, deterministic: bool = False,
-                 log_every_n_steps: int = 50, steps_per_graph: int = 8):
+                 log_every_n_steps: int = 50, steps_per_graph: int = 8, profiler: Optional[str] = None,
+                 profile_steps: int = 20):
         self.max_epochs = int(max_epochs)
         self.max_steps = int(max_steps)
         self.gradient_clip_val = float(gradient_clip_val or 0.0)
@@ -147,6 +149,14 @@ class Trainer:
         self.fused_step = os.environ.get("MTA_FUSED_STEP", "1") != "0"
         self.step_timer = StepTimer()
         self.perf: Dict[str, float] = {}
+        # tracing (utils/profiling.py): "phases" = eager steps with per-phase HIP-event timers (gather / fwd /
+        # loss / bwd / allreduce / optim), "torch" = torch.profiler Chrome trace of the first profile_steps steps
+        self.profiler = (os.environ.get("MTA_PROFILER") or profiler or None)
+        if self.profiler not in (None, "phases", "torch"):
+            raise ValueError(f"profiler must be None, 'phases' or 'torch', got {self.profiler!r}")
+        self.profile_steps = int(profile_steps)
+        self.phase_timer: Optional[PhaseTimer] = None
+        self._torch_prof = None
         self._in_graph = False
 
     # ------------------------------------------------------------------ properties
@@ -244,7 +254,7 @@ class Trainer:
 
     # ------------------------------------------------------------------ step machinery
     def _graphs_enabled(self) -> bool:
-        return (self.use_hip_graphs and self.device.type == "cuda"
+        return (self.use_hip_graphs and self.device.type == "cuda" and self.profiler != "phases"
                 and getattr(self.model, "graph_capturable", True))
 
     def _allreduce_in_graph(self) -> bool:
@@ -271,10 +281,15 @@ class Trainer:
         if fused is not None and self.fused_step and self.model.fused_step_supported(batch):
             loss = fused(batch, batch_idx)  # forward + decoder + backward without autograd
         else:
+            phase("fwd")
             loss = self.model.training_step(batch, batch_idx)
+            phase("bwd")
             loss.backward(self._seed_grad(loss))
         if not self._in_graph or self._allreduce_in_graph():
+            if self.ddp.world > 1:
+                phase("allreduce")
             self.ddp.allreduce_grads()
+            phase("optim")
             self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
         return loss
 
@@ -292,6 +307,7 @@ class Trainer:
         buffers, otherwise it returns fresh tensors that are copied into the graph's inputs.
         """
         if not self._graphs_enabled():
+            phase("gather")
             return body(provider())
         g = self._graphs.get(key)
         if g is None:
@@ -538,7 +554,14 @@ class Trainer:
         host_ms: List[float] = []
         B = loader.batch_size
 
+        timer = self.phase_timer
+
         def timed(fn):
+            if timer is not None:
+                timer.begin_step()
+                fn()
+                timer.end_step()
+                return
             if cuda:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -552,6 +575,8 @@ class Trainer:
                 host_ms.append((time.perf_counter() - t0) * 1e3)
 
         def pre_step(i):
+            if self.profiler == "torch" and self.is_global_zero:
+                self._torch_profile_tick()
             if self.fail_at_step is not None and self.global_step == self.fail_at_step:
                 raise RuntimeError(f"fault injection: MTA_FAIL_AT_STEP={self.fail_at_step}")
             if self.heartbeat_file and i % 500 == 0:
@@ -604,6 +629,9 @@ class Trainer:
                 B = _batch_size(batch)
                 timed(lambda: self._train_step(loader, i, False, batch))
                 self.global_step += 1
+        if timer is not None:
+            self.perf_phases = timer.summarize(skip=2)
+            return [], B
         if cuda:
             torch.cuda.synchronize()
             skip = self.graph_warmup_steps + 1
@@ -649,9 +677,20 @@ class Trainer:
             for c in self.callbacks:
                 c.on_train_epoch_start(self, model)
             t_epoch = time.perf_counter()
-            step_ms, samples_per_batch = self._train_epoch(train_loader, epoch)
+            if self.profiler == "phases":
+                self.phase_timer = PhaseTimer(self.device)
+                with self.phase_timer:
+                    step_ms, samples_per_batch = self._train_epoch(train_loader, epoch)
+                self.phase_timer = None
+            else:
+                step_ms, samples_per_batch = self._train_epoch(train_loader, epoch)
             wall = time.perf_counter() - t_epoch
             perf = self.step_timer.summarize(step_ms, samples_per_batch, self.world_size)
+            if self.profiler == "phases":
+                perf.update(getattr(self, "perf_phases", {}))
+                steps = sum(v for k, v in perf.items() if k.startswith("perf/phase/"))
+                perf["perf/step_ms_p50"] = steps
+                perf["perf/samples_per_s"] = samples_per_batch * self.world_size * 1000.0 / max(steps, 1e-9)
             perf["perf/epoch_wall_s"] = wall
             self.perf = perf
             nonfinite = float(self.optimizer.nonfinite.item())
@@ -686,10 +725,33 @@ class Trainer:
                         f"{perf.get('perf/samples_per_s', 0):.1f} samples/s")
             if self.should_stop or (0 <= self.max_steps <= self.global_step):
                 break
+        if self._torch_prof not in (None, False):  # fewer steps than profile_steps: export what was recorded
+            self.global_step = max(self.global_step, self.graph_warmup_steps + 1 + self.profile_steps)
+            self._torch_profile_tick()
         for c in self.callbacks:
             c.on_fit_end(self, model)
         if self.logger is not None:
             self.logger.finalize()
+
+    def _torch_profile_tick(self) -> None:
+        """profiler="torch": start at the first step after the graph warm-up, stop + export after
+        ``profile_steps`` steps (Chrome trace in the logger's directory, else ``default_root_dir``)."""
+        start = self.graph_warmup_steps + 1
+        if self.global_step == start and self._torch_prof is None:
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._torch_prof = torch.profiler.profile(activities=acts)
+            self._torch_prof.start()
+        elif self._torch_prof not in (None, False) and self.global_step >= start + self.profile_steps:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            self._torch_prof.stop()
+            root = Path(self.logger.log_dir) if self.logger is not None else Path(self.default_root_dir)
+            root.mkdir(parents=True, exist_ok=True)
+            self.torch_trace_path = str(root / f"torch_trace_step{start}.json")
+            self._torch_prof.export_chrome_trace(self.torch_trace_path)
+            self._torch_prof = False  # done for this run
 
     def _step_scheduler(self, epoch: int) -> None:
         if self.scheduler is None:

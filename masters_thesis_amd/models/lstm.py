@@ -27,6 +27,7 @@ from ..metrics import (LinkedMAE, LinkedMSE, LinkedNLL, LinkedTotal, MeanAbsolut
 from ..ops import lstm as lstm_op
 from ..ops._lib import use_hip
 from ..ops.losses import heads_losses, heads_losses_train, train_decoder_fits
+from ..utils.profiling import phase
 
 
 class LSTMStack(torch.nn.Module):
@@ -171,16 +172,19 @@ class FinancialLstm(LightningModule):
         context, target, factor, inv_psi, B = self._unpack(batch)
         lstm = self.lstm
         drop = lstm.dropout if lstm.num_layers > 1 else 0.0
+        phase("fwd")
         h, st = lstm_op.pipelined_forward(context.contiguous(), lstm.seeds,
                                           lstm_op.precision_code(self.matmul_precision), float(drop), True, True,
                                           lstm.flat_weights)
         c_nll, c_mse = self.loss_coefficients
         grads = (self.alpha_head.weight.grad, self.alpha_head.bias.grad, self.beta_head.weight.grad,
                  self.beta_head.bias.grad)
+        phase("loss")
         out, dh = heads_losses_train(h, self.alpha_head.weight, self.alpha_head.bias, self.beta_head.weight,
                                      self.beta_head.bias, target, factor, inv_psi, batch_windows=B,
                                      want_nll=self.want_nll, nll_mode=self.nll_mode, c_nll=c_nll, c_mse=c_mse,
                                      acc=self.train_acc.acc, grads=grads)
+        phase("bwd")
         lstm_op.pipelined_backward(st, dh)
         self._log_stage("train", self.train_acc, self.train_log_names)
         return out[3]

@@ -98,7 +98,10 @@ class _LSTMStackFn(torch.autograd.Function):
                 w_um = torch.empty((4 * H, fin), device=dev, dtype=torch.float32)
                 b_um = torch.empty((4 * H,), device=dev, dtype=torch.float32)
                 C.lstm_prep(w_ih, b_ih, b_hh, H, w_um, b_um)
-                gx = torch.addmm(b_um, inp, w_um.t())
+                # time-parallel input projection on the MFMA GEMM at the op's precision (csrc/gemm_f32.hip)
+                inp = inp.contiguous()
+                gx = torch.empty((T * Np, 4 * H), device=dev, dtype=torch.float32)
+                C.gemm_f32(prec, inp, w_um, gx, b_um, None, False)
                 C.lstm_fwd_layer(H, prec, None, None, None, None, gx, stash, w_hh, hseq, N, Np, T)
             saved += [inp, stash if stash is not None else hseq, hseq, w_um]
             prev_h = hseq
@@ -131,13 +134,17 @@ class _LSTMStackFn(torch.autograd.Function):
                          _grad_buffer(b_ih), _grad_buffer(b_hh), part[0] if part else None)
             dG2 = dG.view(T * Np, 4 * H)
             if l > 0:
-                dinp = dG2.mm(w_um)
-                if ctx.dropout > 0.0 and ctx.training:
-                    dinp.mul_(masks[l - 1])
+                # dx = dG W_ih (x the input-dropout mask in the epilogue); W_um is [4H][H] = [K][N]
+                dinp = torch.empty((T * Np, H), device=dG.device, dtype=torch.float32)
+                C.gemm_f32(ctx.prec, dG2, w_um, dinp, None,
+                           masks[l - 1] if ctx.dropout > 0.0 and ctx.training else None, True)
                 dH = dinp.view(T, Np, H)
             elif ctx.needs_input_grad[0]:
                 perm = _unit_major_rows(H, dG.device)
-                dx = dG2.mm(w_ih.index_select(0, perm)).view(T, Np, F)[:, :N].transpose(0, 1)
+                w_sel = w_ih.index_select(0, perm).contiguous()
+                dx = torch.empty((T * Np, F), device=dG.device, dtype=torch.float32)
+                C.gemm_f32(ctx.prec, dG2, w_sel, dx, None, None, True)
+                dx = dx.view(T, Np, F)[:, :N].transpose(0, 1)
         return (dx, None, None, None, None, *([None] * (4 * L)))
 
 
@@ -164,14 +171,16 @@ def pipeline_supported(x: Tensor, weights: Sequence[Tensor], num_layers: int) ->
     # spinning workgroup's producers are resident or finished.  Grids beyond one workgroup per CU (large
     # batches: B=64 is 800 workgroups) run in waves instead of falling back to per-layer launches and
     # T x Np x 4H gate tensors.
-    return (H in (32, 64) or 8 <= H < 32) and F in FUSED_F and 1 <= num_layers <= 8 and T < 4096
+    # long sequences: progress words carry more step bits (csrc/lstm_stack.hip epoch_shift), the stash is O(T)
+    # (T = 100k, N = 100, H = 64: 14 GB per layer of 288 GB HBM)
+    return (H in (32, 64) or 8 <= H < 32) and F in FUSED_F and 1 <= num_layers <= 8 and T + 8 < (1 << 22)
 
 
 _FLAGS = {}
 _CTL_WORDS = 160  # control words at the end of the flag buffer (csrc/lstm_stack.hip CTL_*): [0] = timeout count
 
 
-def _stack_flags(C, Np: int, L: int, device) -> Tensor:
+def _stack_flags(C, Np: int, L: int, device, T: int = 60) -> Tensor:
     """Persistent, zero-initialised progress/epoch words of the pipelined kernels (never reset per launch:
     progress is epoch-stamped in-kernel, so a captured graph has no memset nodes).
 
@@ -179,8 +188,9 @@ def _stack_flags(C, Np: int, L: int, device) -> Tensor:
     that shares the buffer, so a stale word is always exactly one epoch behind and compares below the
     awaited value under the kernel's wrap-safe signed difference.  (A buffer shared between stack depths
     would leave the deeper layers' words at 0 while the epoch advances; once the epoch passes 2^19 such a
-    never-written word would read as 'reached'.)"""
-    key = (C.lstm_stack_flag_words(Np), int(L), str(device))
+    never-written word would read as 'reached'.)  The key includes the progress words' epoch shift (a function
+    of T): words written under one shift are never compared under another."""
+    key = (C.lstm_stack_flag_words(Np), int(L), str(device), int(C.lstm_stack_epoch_shift(int(T))))
     if key not in _FLAGS:
         _FLAGS[key] = torch.zeros(key[0], dtype=torch.int32, device=device)
     return _FLAGS[key]
@@ -197,7 +207,7 @@ def check_pipeline_health(clear: bool = True) -> None:
     The kernels bound every spin (the grid always drains) and count give-ups in a device word; the
     trainer calls this at every epoch end and ``bench.py`` after its timed loop."""
     bad = []
-    for (words, L, dev), f in _FLAGS.items():
+    for (words, L, dev, _shift), f in _FLAGS.items():
         n = stack_timeouts(f)
         if n:
             bad.append(f"L={L} on {dev}: {n} wait(s)")
@@ -271,7 +281,7 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     # dx masks (u32 words (T, ntiles, 4, H): byte i of a word = sequence 4q+i of a lane)
     masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
-    flags = _stack_flags(C, Np, L, dev)
+    flags = _stack_flags(C, Np, L, dev, T)
     C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]), hseq,
                      xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
     st = PipelinedState()
@@ -300,7 +310,7 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
             t.grad = torch.zeros_like(t)
     dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
     dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
-    flags = _stack_flags(C, Np, L, dev)
+    flags = _stack_flags(C, Np, L, dev, T)
     inp = [st.x] + [st.xdrop[l] if drop else st.hseq[l - 1] for l in range(1, L)]
     grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
     parts = _parts(C, True, T, H, [F] + [H] * (L - 1), dev)

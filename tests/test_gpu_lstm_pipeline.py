@@ -228,3 +228,28 @@ def test_handoff_timeout_is_reported_not_silent():
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "RAISED pipelined LSTM hand-off timed out" in r.stdout and "CLEARED" in r.stdout, r.stdout
+
+
+@pytest.mark.parametrize("T", [4100, 10000])
+def test_pipelined_long_sequence(T):
+    """Long context: T beyond the 12 step bits of a progress word (the epoch shift widens with T,
+    csrc/lstm_stack.hip epoch_shift) runs in the same two launches and stays exact against fp64."""
+    from masters_thesis_amd.ops import lstm as op
+
+    torch.manual_seed(11)
+    N, F, H, L = 32, 3, 32, 2
+    x = torch.randn(N, T, F) * 0.5
+    ws = _weights(F, H, L, seed=3)
+    R = torch.randn(N, H)
+    ref, w64 = _ref(x, ws, L)
+    (ref * R.double()).sum().backward()
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    assert op.pipeline_supported(x.to(DEV), wg, L)
+    out = op.lstm_last_hidden(x.to(DEV), wg, L, 0.0, True, "highest")
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    op.check_pipeline_health()
+    assert (out.double().cpu() - ref.detach()).abs().max().item() <= 1e-4 * max(ref.abs().max().item(), 1.0)
+    for a, b in zip(wg, w64):
+        # gradients sum T terms: relative to the gradient scale
+        assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-3 * max(b.grad.abs().max().item(), 1e-3)
