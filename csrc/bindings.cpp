@@ -7,6 +7,8 @@
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
 
+#include "batch_gather.h"
+
 extern "C" {
 int mta_lstm_fwd_layer(int H, int prec, const float* x, const float* w_ih, const float* b_ih, const float* b_hh,
                        int fin, const float* gx, float* stash, const float* w_hh, float* hseq, int N, int Np, int T,
@@ -62,6 +64,11 @@ int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps,
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
                   int D, int heads, float rope_base, hipStream_t st);
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
+int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
+                         const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                         float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
+                         const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
+                         const MtaBatchGather* gather, hipStream_t st);
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
@@ -585,11 +592,12 @@ std::vector<float*> ptrs_f32(const std::vector<at::Tensor>& v, const char* name)
 
 int64_t lstm_stack_flag_words(int64_t Np) { return mta_lstm_stack_flag_words((int)Np); }
 
-void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
-                    std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
-                    std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
-                    std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N,
-                    int64_t Np, int64_t T) {
+static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
+                                std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih,
+                                std::vector<at::Tensor> b_hh, std::vector<at::Tensor> hseq,
+                                std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
+                                std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags,
+                                int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(x);
   TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
@@ -617,12 +625,51 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
   for (int64_t l = 0; l < L; ++l)
     if (xdrop[l].numel()) mk[l] = reinterpret_cast<uint32_t*>(masks[l].data_ptr<uint8_t>());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int rc = mta_lstm_stack_fwd((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(), cwh.data(),
-                                    cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
-                                    reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
-                                    reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
-                                    cur_stream());
+  const int rc = mta_lstm_stack_fwd_g((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(),
+                                      cwh.data(), cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
+                                      reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
+                                      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
+                                      gather, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
+}
+
+void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
+                    std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
+                    std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
+                    std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N,
+                    int64_t Np, int64_t T) {
+  lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N, Np,
+                      T, nullptr);
+}
+
+// the same launch with the training step's batch gather folded in: src[k] (rows, ...) -> dst[k] (B, ...) at rows
+// perm[cursor * B + b]; x must be dst[0] (the static batch buffer), cursor advances once per launch
+void lstm_stack_fwd_gather(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
+                           std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
+                           std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop,
+                           std::vector<at::Tensor> masks, std::vector<at::Tensor> stash, at::Tensor seeds,
+                           double drop_p, at::Tensor flags, int64_t N, int64_t Np, int64_t T,
+                           std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::Tensor perm, at::Tensor cursor,
+                           int64_t B) {
+  TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 gathered tensors");
+  TORCH_CHECK(perm.is_cuda() && cursor.is_cuda() && perm.scalar_type() == at::kInt &&
+              cursor.scalar_type() == at::kInt, "perm/cursor: int32 GPU tensors");
+  TORCH_CHECK(dst[0].data_ptr() == x.data_ptr(), "x must be the static batch buffer dst[0]");
+  MtaBatchGather g{};
+  for (size_t k = 0; k < src.size(); ++k) {
+    MTA_CHECK_F32(src[k]);
+    MTA_CHECK_F32(dst[k]);
+    g.row[k] = (long)(src[k].numel() / src[k].size(0));
+    TORCH_CHECK(dst[k].numel() == B * g.row[k], "dst ", k, " must hold B rows");
+    g.src[k] = src[k].data_ptr<float>();
+    g.dst[k] = dst[k].data_ptr<float>();
+  }
+  g.nt = (int)src.size();
+  g.perm = perm.data_ptr<int>();
+  g.cursor = cursor.data_ptr<int>();
+  g.B = (int)B;
+  lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N, Np,
+                      T, &g);
 }
 
 // grads: [] (weight gradients by the caller) or 4 lists g_wih, g_whh, g_bih, g_bhh of per-layer gradient
@@ -853,6 +900,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgp", &dgp);
   m.def("ols_features", &ols_features);
   m.def("lstm_stack_fwd", &lstm_stack_fwd);
+  m.def("lstm_stack_fwd_gather", &lstm_stack_fwd_gather);
   m.def("lstm_stack_bwd", &lstm_stack_bwd);
   m.def("lstm_stack_flag_words", &lstm_stack_flag_words);
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });

@@ -170,6 +170,11 @@ struct StackFwdArgs {
   unsigned* ctl;
   unsigned spin_limit;
   int N, Np, T, L, ntiles, tr8, eshift;
+  // in-kernel batch gather (gather != 0): layer 0 reads x through the device permutation, the non-top-layer
+  // workgroups copy the batch rows into the static buffers after their recurrence (the decoder and the backward
+  // read those), the last workgroup advances the cursor: no separate gather launch per training step
+  int gather, copy_blocks;
+  MtaBatchGather g;
 };
 
 // Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
@@ -254,11 +259,22 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     }
     int nrow[4];
     float nmask[4];
+    const float* xbase[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int n = n0 + 4 * q + i;
       nrow[i] = n < N ? n : N - 1;
       nmask[i] = n < N ? 1.f : 0.f;
+      if constexpr (FIRST) {
+        if (a.gather) {
+          // sequence n = stock (n % K) of batch window b = n / K, read where the dataset holds it
+          const int K = N / a.g.B, b = nrow[i] / K, s = nrow[i] - b * K;
+          const int w = a.g.perm[a.g.cursor[0] * a.g.B + b];
+          xbase[i] = a.g.src[0] + (size_t)w * a.g.row[0] + (size_t)s * T * FIN0;
+        } else {
+          xbase[i] = a.x + (size_t)nrow[i] * T * FIN0;
+        }
+      }
     }
     // Layer inputs are prefetched THREE steps ahead into two register sets (step s in set s & 1): a
     // write-through hand-off is read from beyond L2 (sc1 stores drop the line), ~1-2 us, i.e. more than the one
@@ -273,7 +289,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       if constexpr (FIRST) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float* xs = a.x + ((size_t)nrow[i] * T + t) * FIN0;
+          const float* xs = xbase[i] + (size_t)t * FIN0;
 #pragma unroll
           for (int f = 0; f < FIN0; ++f) xb.x0[i][f] = xs[f];
         }
@@ -587,6 +603,29 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch)
+__device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P) {
+  const int cur = g.cursor[0];
+  const long stride = (long)P * blockDim.x, first = (long)p * blockDim.x + threadIdx.x;
+  for (int k = 0; k < g.nt; ++k) {
+    const long row = g.row[k], total = (long)g.B * row;
+    if ((row & 3) == 0 && ((((uintptr_t)g.src[k]) | ((uintptr_t)g.dst[k])) & 15) == 0) {
+      const long row4 = row / 4;
+      const float4* s4 = reinterpret_cast<const float4*>(g.src[k]);
+      float4* d4 = reinterpret_cast<float4*>(g.dst[k]);
+      for (long e = first; e < total / 4; e += stride) {
+        const long b = e / row4;
+        d4[e] = s4[(long)g.perm[cur * g.B + b] * row4 + (e - b * row4)];
+      }
+    } else {
+      for (long e = first; e < total; e += stride) {
+        const long b = e / row;
+        g.dst[k][e] = g.src[k][(long)g.perm[cur * g.B + b] * row + (e - b * row)];
+      }
+    }
+  }
+}
+
 template <int H, int PREC, int FIN0>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
@@ -597,7 +636,9 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwd
     if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
     else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
   }
-  finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift);
+  if (a.gather && (int)blockIdx.x < a.copy_blocks) batch_copy(a.g, blockIdx.x, a.copy_blocks);
+  // every workgroup read the cursor before arriving: the last one advances it
+  if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift) && a.gather) a.g.cursor[0] += 1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1051,14 +1092,22 @@ extern "C" long mta_lstm_stack_flag_words(int Np) {
   return 3L * FLAG_STRIDE * MAXL * tr8 + CTL_WORDS;
 }
 
-extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
-                                  const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
-                                  float* const* hseq, float* const* xdrop, uint32_t* const* mask,
-                                  float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                  int Np, int T, hipStream_t st) {
+// gather (nullable): x is then the static batch buffer the launch fills (layer 0 reads the dataset directly)
+extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
+                                    const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                                    float* const* hseq, float* const* xdrop, uint32_t* const* mask,
+                                    float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
+                                    int Np, int T, const MtaBatchGather* gather, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
   StackFwdArgs a{};
   a.x = x;
+  if (gather) {
+    if (gather->B < 1 || N % gather->B || gather->nt < 1 || gather->nt > 4 || gather->src[0] == nullptr ||
+        gather->row[0] != (long)(N / gather->B) * T * fin)
+      return -4;
+    a.gather = 1;
+    a.g = *gather;
+  }
   for (int l = 0; l < L; ++l) {
     a.w_ih[l] = w_ih[l];
     a.w_hh[l] = w_hh[l];
@@ -1084,8 +1133,19 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
   a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
   a.spin_limit = spin_limit();
+  // the copy goes to workgroups that finish before the top layer (all of them for one layer)
+  a.copy_blocks = (L > 1 ? L - 1 : 1) * a.tr8;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
+}
+
+extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
+                                  const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
+                                  float* const* hseq, float* const* xdrop, uint32_t* const* mask,
+                                  float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
+                                  int Np, int T, hipStream_t st) {
+  return mta_lstm_stack_fwd_g(H, prec, L, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, mask, stash, seeds, drop_p,
+                              flags, N, Np, T, nullptr, st);
 }
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's

@@ -95,6 +95,12 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
 constexpr int FUSED_MAX_BLOCKS = 256;
 constexpr unsigned FUSED_SPIN_LIMIT = 1u << 22;
 
+// REG: every thread's (at most REG_N) float4 of g, p, m, v are loaded in phase 1, before the grid-wide arrival
+// wait, so phase 2 is compute + stores only (the post-barrier HBM round trip of the re-reads was ~1.5 us of a
+// ~9 us launch for the 51K-parameter headline model)
+constexpr int REG_N = 4;
+
+template <bool REG>
 __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v, long n4,
                                                          float* __restrict__ partials,
@@ -107,12 +113,35 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
   __shared__ float s_norm;
   const long stride = (long)gridDim.x * TPB;
   float acc = 0.f;
-  for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
-    const float4 q = g[i];
-    acc = fmaf(q.x, q.x, acc);
-    acc = fmaf(q.y, q.y, acc);
-    acc = fmaf(q.z, q.z, acc);
-    acc = fmaf(q.w, q.w, acc);
+  float4 rg[REG ? REG_N : 1], rp[REG ? REG_N : 1], rm[REG ? REG_N : 1], rv[REG ? REG_N : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int r = 0; r < REG_N; ++r) {
+      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      if (i < n4) {
+        rg[r] = g[i];
+        rp[r] = p[i];
+        rm[r] = m[i];
+        rv[r] = v[i];
+      } else {
+        rg[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < REG_N; ++r) {
+      acc = fmaf(rg[r].x, rg[r].x, acc);
+      acc = fmaf(rg[r].y, rg[r].y, acc);
+      acc = fmaf(rg[r].z, rg[r].z, acc);
+      acc = fmaf(rg[r].w, rg[r].w, acc);
+    }
+  } else {
+    for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
+      const float4 q = g[i];
+      acc = fmaf(q.x, q.x, acc);
+      acc = fmaf(q.y, q.y, acc);
+      acc = fmaf(q.z, q.z, acc);
+      acc = fmaf(q.w, q.w, acc);
+    }
   }
   acc = block_sum(acc, scratch) * (scale * scale);
   // the step counter is read by every workgroup BEFORE it arrives; the last arriver advances it
@@ -161,6 +190,33 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
   const float bc2_sqrt = sqrtf(bc2);
   const float decay = adamw ? (1.0f - lr * wd) : 1.0f;
   const float l2 = adamw ? 0.0f : wd;
+  if constexpr (REG) {
+#pragma unroll
+    for (int r = 0; r < REG_N; ++r) {
+      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      if (i >= n4) continue;
+      float4 pp = rp[r], gg = rg[r], mm = rm[r], vv = rv[r];
+      float* pf = reinterpret_cast<float*>(&pp);
+      float* gf = reinterpret_cast<float*>(&gg);
+      float* mf = reinterpret_cast<float*>(&mm);
+      float* vf = reinterpret_cast<float*>(&vv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float gk = gf[k] * gs;
+        gf[k] = zero_grad ? 0.0f : gk;
+        gk = fmaf(l2, pf[k], gk);
+        mf[k] = fmaf(1.0f - beta1, gk - mf[k], mf[k]);
+        vf[k] = fmaf(beta2, vf[k], (1.0f - beta2) * gk * gk);
+        const float denom = sqrtf(vf[k]) / bc2_sqrt + eps;
+        pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
+      }
+      p[i] = pp;
+      g[i] = gg;
+      m[i] = mm;
+      v[i] = vv;
+    }
+    return;
+  }
   for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
     float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
     float* pf = reinterpret_cast<float*>(&pp);
@@ -182,6 +238,15 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     m[i] = mm;
     v[i] = vv;
   }
+}
+
+// register-resident form: one float4 per thread while that fills <= 256 workgroups, at most REG_N
+inline bool fused_reg(long n4) { return n4 <= (long)FUSED_MAX_BLOCKS * TPB * REG_N; }
+inline int fused_grid_reg(long n4) {
+  long blocks = (n4 + TPB - 1) / TPB;
+  if (blocks < 1) blocks = 1;
+  if (blocks > FUSED_MAX_BLOCKS) blocks = FUSED_MAX_BLOCKS;
+  return (int)blocks;
 }
 
 inline int fused_grid(long n4) {
@@ -239,8 +304,14 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
                                float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
                                float* norm_out, float* nonfinite, hipStream_t st) {
   const long n4 = n / 4;
-  adam_fused_kernel<<<fused_grid(n4), TPB, 0, st>>>(
-      reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
-      reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-      zero_grad, norm_out, nonfinite);
+  if (fused_reg(n4))
+    adam_fused_kernel<true><<<fused_grid_reg(n4), TPB, 0, st>>>(
+        reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
+        reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
+        zero_grad, norm_out, nonfinite);
+  else
+    adam_fused_kernel<false><<<fused_grid(n4), TPB, 0, st>>>(
+        reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
+        reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
+        zero_grad, norm_out, nonfinite);
 }

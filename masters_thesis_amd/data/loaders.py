@@ -125,7 +125,14 @@ class TensorBatchLoader:
         self._nfull = idx.numel() // self.batch_size
         return self._nfull
 
-    def gather_static(self) -> List[Tensor]:
+    def gather_static(self, defer: bool = False) -> List[Tensor]:
+        """Next batch in the static buffers (device gather, cursor advanced on the device).
+
+        ``defer``: launch nothing and return a :class:`DeferredBatch` — the consumer (the pipelined LSTM forward
+        of the fused training step) reads the rows through the permutation and fills the buffers itself, or
+        calls ``materialize()`` to run the gather kernel."""
+        if defer:
+            return DeferredBatch(self)
         _lib.lib().gather_batch(self.tensors, self._static, self._perm, self._cursor, self._arrive,
                                 self.batch_size, 0)
         return self._static
@@ -136,3 +143,31 @@ class TensorBatchLoader:
         if rest is None or rest.numel() == 0:
             return None
         return self._select(rest)
+
+
+class DeferredBatch(list):
+    """The static batch buffers of a loader whose gather has not run yet (``gather_static(defer=True)``).
+
+    ``gather_args()`` gives what a kernel needs to fold the gather in (source tensors, static buffers,
+    permutation, cursor, windows per batch); a consumer that does so calls ``consumed()``; any other consumer must
+    call ``materialize()`` first."""
+
+    def __init__(self, loader):
+        super().__init__(loader._static)
+        self._loader = loader
+        self.pending = True
+
+    def gather_args(self):
+        ld = self._loader
+        return list(ld.tensors), list(ld._static), ld._perm, ld._cursor, ld.batch_size
+
+    def consumed(self) -> None:
+        self.pending = False
+
+    def materialize(self) -> "DeferredBatch":
+        if self.pending:
+            ld = self._loader
+            _lib.lib().gather_batch(ld.tensors, ld._static, ld._perm, ld._cursor, ld._arrive, ld.batch_size, 0)
+            self.pending = False
+        return self
+

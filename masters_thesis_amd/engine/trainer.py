@@ -280,7 +280,11 @@ class Trainer:
         fused = getattr(self.model, "fused_training_step", None)
         if fused is not None and self.fused_step and self.model.fused_step_supported(batch):
             loss = fused(batch, batch_idx)  # forward + decoder + backward without autograd
+            if getattr(batch, "pending", False):
+                raise RuntimeError("fused training step left a deferred batch gather unconsumed")
         else:
+            if getattr(batch, "pending", False):
+                batch.materialize()
             phase("fwd")
             loss = self.model.training_step(batch, batch_idx)
             phase("bwd")
@@ -360,8 +364,8 @@ class Trainer:
             pre, post = self._static_hooks(loader)
             if pre is not None:
                 pre()
-            out = self._run(("train", B, True, id(loader)), loader.gather_static, lambda b: self._train_body(b, batch_idx), True,
-                            self.graph_warmup_steps)
+            out = self._run(("train", B, True, id(loader)), lambda: self._gather_train(loader),
+                            lambda b: self._train_body(b, batch_idx), True, self.graph_warmup_steps)
             if post is not None:
                 post()
         else:
@@ -391,10 +395,23 @@ class Trainer:
         def body(first):
             out = self._train_body(first, batch_idx)
             for k in range(1, S):
-                out = self._train_body(loader.gather_static(), batch_idx + k)
+                out = self._train_body(self._gather_train(loader), batch_idx + k)
             return out
 
-        return self._run(("train", B, True, id(loader), S), loader.gather_static, body, True, self.graph_warmup_steps)
+        return self._run(("train", B, True, id(loader), S), lambda: self._gather_train(loader), body, True,
+                         self.graph_warmup_steps)
+
+    def _gather_train(self, loader):
+        """Training batch from a static loader: the gather is deferred into the fused step's forward launch when
+        the model folds it in (``accepts_deferred_gather``; one launch less per step), else the gather kernel."""
+        defer = (self.fused_step and getattr(self.model, "accepts_deferred_gather", False)
+                 and os.environ.get("MTA_DEFER_GATHER", "1") != "0")
+        if defer:
+            try:
+                return loader.gather_static(defer=True)
+            except TypeError:  # loaders without the deferred protocol (streaming ring)
+                pass
+        return loader.gather_static()
 
     def _eval_step(self, stage: str, loader, batch_idx: int, static: bool, batch=None):
         model = self.model

@@ -80,6 +80,8 @@ class FinancialLstm(LightningModule):
     # (c_nll, c_mse) of the training loss; subclasses override
     loss_coefficients = (0.0, 1.0)
     want_nll = False
+    # the fused step folds a static loader's batch gather into its forward launch (engine/trainer.py _gather_train)
+    accepts_deferred_gather = True
 
     def __init__(self, input_size: int = 3, hidden_size: int = 64, num_layers: int = 2, dropout: float = 0.2,
                  learning_rate: float = 1e-4, weight_decay: float = 1e-5, *, backend: str = "auto",
@@ -172,10 +174,13 @@ class FinancialLstm(LightningModule):
         context, target, factor, inv_psi, B = self._unpack(batch)
         lstm = self.lstm
         drop = lstm.dropout if lstm.num_layers > 1 else 0.0
+        gather = batch.gather_args() if getattr(batch, "pending", False) else None
         phase("fwd")
-        h, st = lstm_op.pipelined_forward(context.contiguous(), lstm.seeds,
+        h, st = lstm_op.pipelined_forward(context if gather else context.contiguous(), lstm.seeds,
                                           lstm_op.precision_code(self.matmul_precision), float(drop), True, True,
-                                          lstm.flat_weights)
+                                          lstm.flat_weights, gather=gather)
+        if gather is not None:
+            batch.consumed()  # the forward launch filled the static batch buffers
         c_nll, c_mse = self.loss_coefficients
         grads = (self.alpha_head.weight.grad, self.alpha_head.bias.grad, self.beta_head.weight.grad,
                  self.beta_head.bias.grad)

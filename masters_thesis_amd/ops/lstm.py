@@ -256,8 +256,12 @@ def kernel_hidden(H: int) -> int:
 
 
 def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, training: bool, need_grad: bool,
-                      flat: Sequence[Tensor]):
-    """One forward launch of every layer (csrc/lstm_stack.hip).  Returns (h_T of the top layer (N, H), state)."""
+                      flat: Sequence[Tensor], gather=None):
+    """One forward launch of every layer (csrc/lstm_stack.hip).  Returns (h_T of the top layer (N, H), state).
+
+    ``gather`` = (src tensors, static buffers, perm, cursor, B) of a deferred static batch
+    (data/loaders.py DeferredBatch): the launch reads x through the permutation and fills the buffers itself
+    (``x`` must be the static x buffer, viewed (B*K, T, F))."""
     L = len(flat) // 4
     N, T, F = x.shape
     H0 = flat[1].shape[1]
@@ -282,8 +286,16 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
     flags = _stack_flags(C, Np, L, dev, T)
-    C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]), hseq,
-                     xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
+    if gather is not None:
+        src, dst, perm, cursor, B = gather
+        if x.data_ptr() != dst[0].data_ptr() or not x.is_contiguous():
+            raise ValueError("deferred gather: x must be the static batch buffer")
+        C.lstm_stack_fwd_gather(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]),
+                                list(flat[3::4]), hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T,
+                                src, dst, perm, cursor, B)
+    else:
+        C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
+                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
     st = PipelinedState()
     st.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
     st.params, st.seeds, st.x = tuple(flat), seeds, x

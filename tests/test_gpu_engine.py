@@ -165,3 +165,56 @@ def test_grouped_step_graphs_match_single_steps():
     assert torch.equal(sa, sb)
     if aa is not None:
         assert torch.equal(aa, ab)
+
+
+@pytest.mark.parametrize("B,L,dropout", [(1, 2, 0.2), (3, 1, 0.0), (2, 3, 0.2)])
+def test_deferred_gather_equals_gather_kernel(B, L, dropout, monkeypatch):
+    """The batch gather folded into the pipelined forward launch (layer 0 reads x through the permutation,
+    the static buffers are filled in-launch, the cursor advances once per launch) trains bit-identically to
+    the separate gather kernel, across an epoch roll-over and with grouped step graphs."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import FinancialLstmCombined
+
+    def run(defer):
+        monkeypatch.setenv("MTA_DEFER_GATHER", "1" if defer else "0")
+        torch.manual_seed(3)
+        model = FinancialLstmCombined(num_layers=L, dropout=dropout)
+        ld = TensorBatchLoader([t.to(DEV) for t in _data(19)], B, shuffle=True, seed=1)
+        tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=True, matmul_precision="high", steps_per_graph=4, deterministic=True)
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.train()
+        step = tr.make_train_stepper(ld)
+        launched = []
+        orig = ld.gather_static
+
+        def spy(defer=False):
+            launched.append(defer)
+            return orig(defer=defer)
+
+        ld.gather_static = spy
+        for _ in range(30):
+            step()
+        step(4)
+        torch.cuda.synchronize()
+        tr._check_device_health()
+        return [p.detach().clone() for p in model.parameters()], launched, [b.clone() for b in ld._static]
+
+    from masters_thesis_amd.ops import extras as extras_op
+    from masters_thesis_amd.ops import lstm as lstm_op
+
+    try:  # deterministic weight-gradient reductions: the two runs must agree bit for bit
+        p_def, l_def, s_def = run(True)
+        p_ref, l_ref, s_ref = run(False)
+    finally:
+        lstm_op.set_deterministic(False)
+        if hasattr(extras_op, "set_deterministic"):
+            extras_op.set_deterministic(False)
+    assert l_def and all(l_def) and not any(l_ref)
+    for a, b in zip(s_def, s_ref):  # the static buffers hold the same last batch
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, b in zip(p_def, p_ref):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
