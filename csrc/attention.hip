@@ -10,7 +10,11 @@
 // operand is one ds_read_b128; transposed images are written once at load time (V^T, K^T, Q^T, dO^T) or
 // straight from the accumulator layout (P^T, dS^T: four consecutive rows per lane = one 8-byte write).
 // Layout: qkv [M][3*D] bf16 with token row = seq*T + t, columns [q | k | v], head h at h*HD.
-// RoPE: interleaved pairs (2i, 2i+1), angle t * base^(-2i/HD).
+// RoPE: interleaved pairs (2i, 2i+1), angle t * base^(-2i/HD), from a host-built (cos, sin) table [T][HD/2]
+// (fp64-accurate; per-element sincosf/powf were ~1/4 of a launch).
+// Four waves per (sequence, head): the q / k / v (/ dO) rows are loaded and rotated by one wave each, then wave w
+// owns query tile w (scores, softmax, O; backward: P, dS) and token tile w (dV, dK, dQ): 4x the waves in flight
+// of the one-wave form, which left the launch latency-bound (28 us per call at 416 workgroups, r2 trace).
 #include "common.h"
 
 namespace {
@@ -71,20 +75,23 @@ struct AttnArgs {
   __bf16* dqkv;      // [M][3D]
   int T, D, heads;
   float scale, rope_base;
+  const float* rope;  // [T][HD/2] (cos, sin) pairs
 };
 
 // load this (seq, head)'s q, k, v rows (lane = token), apply RoPE (and the softmax scale to q), and write
 // the requested row-major (rm[i]) and transposed (tr[i]) images (nullptr = not needed)
 template <int HD>
-__device__ __forceinline__ void load_qkv(const AttnArgs& a, int seq, int h, __bf16* const rm[3], __bf16* const tr[3]) {
+__device__ __forceinline__ void load_qkv(const AttnArgs& a, int seq, int h, __bf16* const rm[3], __bf16* const tr[3],
+                                         int only) {
   constexpr int RLD = HD + 8;
   const int t = threadIdx.x & 63;
   const bool ok = t < a.T;
   const size_t row = (size_t)seq * a.T + (ok ? t : 0);
   const __bf16* base = a.qkv + row * 3 * a.D + h * HD;
+  const float2* rope = reinterpret_cast<const float2*>(a.rope) + (size_t)(ok ? t : 0) * (HD / 2);
 #pragma unroll
   for (int which = 0; which < 3; ++which) {
-    if (!rm[which] && !tr[which]) continue;
+    if (which != only || (!rm[which] && !tr[which])) continue;
     float x[HD];
 #pragma unroll
     for (int c = 0; c < HD; c += 8) {
@@ -95,9 +102,8 @@ __device__ __forceinline__ void load_qkv(const AttnArgs& a, int seq, int h, __bf
     if (which < 2) {
 #pragma unroll
       for (int i = 0; i < HD / 2; ++i) {
-        const float inv_freq = __powf(a.rope_base, -2.0f * (float)i / (float)HD);
-        float sn, cs;
-        sincosf((float)t * inv_freq, &sn, &cs);
+        const float2 r = rope[i];
+        const float cs = r.x, sn = r.y;
         const float x0 = x[2 * i], x1 = x[2 * i + 1];
         x[2 * i] = x0 * cs - x1 * sn;
         x[2 * i + 1] = x0 * sn + x1 * cs;
@@ -133,20 +139,20 @@ __device__ __forceinline__ f32x4 score_tile(const S& s, int qi, int ki, int T) {
 }
 
 template <int HD>
-__global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FwdSmem<HD>& s = *reinterpret_cast<FwdSmem<HD>*>(smem_raw);
   const int seq = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
-  const int l = threadIdx.x & 63;
+  const int l = threadIdx.x & 63, wave = threadIdx.x >> 6;
   {
     __bf16* const rm[3] = {s.q, s.k, nullptr};
     __bf16* const tr[3] = {nullptr, nullptr, s.vt};
-    load_qkv<HD>(a, seq, h, rm, tr);
+    load_qkv<HD>(a, seq, h, rm, tr, wave);  // wave 0: q, 1: k, 2: v^T
   }
   __syncthreads();
-  // scores + softmax, P -> LDS (row-major, the A operand of O = P V)
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) {
+  // scores + softmax of query tile qi = wave, P -> LDS (row-major, the A operand of O = P V)
+  {
+    const int qi = wave;
     f32x4 sc[4];
 #pragma unroll
     for (int ki = 0; ki < 4; ++ki) sc[ki] = score_tile<HD>(s, qi, ki, a.T);
@@ -172,10 +178,10 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
     for (int ki = 0; ki < 4; ++ki) put_rows(s.p, PLD, 16 * qi, 16 * ki, sc[ki]);
   }
   __syncthreads();
-  // O = P V  (B = V^T rows = features, k = tokens)
+  // O = P V  (B = V^T rows = features, k = tokens) for query tile qi = wave
   const size_t seqrow = (size_t)seq * a.T;
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) {
+  {
+    const int qi = wave;
 #pragma unroll
     for (int dj = 0; dj < HD / 16; ++dj) {
       const f32x4 o = mm(s.p, PLD, 16 * qi, s.vt, PLD, 16 * dj, TP, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -186,23 +192,22 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(AttnArgs a) {
       }
     }
   }
-  a.lse[(size_t)blockIdx.x * TP + l] = s.rowv[l];
+  if (wave == 0) a.lse[(size_t)blockIdx.x * TP + l] = s.rowv[l];
 }
 
 template <int HD>
-__global__ __launch_bounds__(64) void attn_bwd_kernel(AttnArgs a) {
+__global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   constexpr int RLD = HD + 8;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   BwdSmem<HD>& s = *reinterpret_cast<BwdSmem<HD>*>(smem_raw);
   const int seq = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
-  const int l = threadIdx.x & 63;
-  {
+  const int l = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave < 3) {
     __bf16* const rm[3] = {s.q, s.k, s.v};
     __bf16* const tr[3] = {s.qt, s.kt, nullptr};
-    load_qkv<HD>(a, seq, h, rm, tr);
-  }
-  // dO rows (row-major + transposed) and D = rowsum(dO o O)
-  {
+    load_qkv<HD>(a, seq, h, rm, tr, wave);  // wave 0: q, q^T; 1: k, k^T; 2: v
+  } else {
+    // wave 3: dO rows (row-major + transposed) and D = rowsum(dO o O)
     const int t = l;
     const bool ok = t < a.T;
     const size_t row = (size_t)seq * a.T + (ok ? t : 0);
@@ -227,9 +232,9 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(AttnArgs a) {
   }
   const float* lse = a.lse + (size_t)blockIdx.x * TP;
   __syncthreads();
-  // P (recomputed), dS = P (dP - D)  ->  P^T, dS, dS^T images
-#pragma unroll
-  for (int qi = 0; qi < 4; ++qi) {
+  // P (recomputed), dS = P (dP - D)  ->  P^T, dS, dS^T images, query tile qi = wave
+  {
+    const int qi = wave;
     float lrow[4], drow[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -255,20 +260,19 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(AttnArgs a) {
   // dV = P^T dO, dK = dS^T (scale q), dQ = scale dS K; inverse RoPE on dQ / dK; write dqkv
   const size_t seqrow = (size_t)seq * a.T;
   const int col = l & 15;
-#pragma unroll
-  for (int ti = 0; ti < 4; ++ti) {
+  {
+    const int ti = wave;  // token tile
 #pragma unroll
     for (int dj = 0; dj < HD / 16; ++dj) {
       const f32x4 dv = mm(s.pt, PLD, 16 * ti, s.dOt, PLD, 16 * dj, TP, f32x4{0.f, 0.f, 0.f, 0.f});
       f32x4 dk = mm(s.dst, PLD, 16 * ti, s.qt, PLD, 16 * dj, TP, f32x4{0.f, 0.f, 0.f, 0.f});
       f32x4 dq = mm(s.p, PLD, 16 * ti, s.kt, PLD, 16 * dj, TP, f32x4{0.f, 0.f, 0.f, 0.f});
       const int c = 16 * dj + col;       // feature index; RoPE pair (c & ~1, c | 1) sits in lanes l, l^1
-      const float inv_freq = __powf(a.rope_base, -2.0f * (float)(c >> 1) / (float)HD);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = 16 * ti + 4 * (l >> 4) + r;
-        float sn, cs;
-        sincosf((float)t * inv_freq, &sn, &cs);
+        const float2 rr = reinterpret_cast<const float2*>(a.rope)[(size_t)(t < a.T ? t : 0) * (HD / 2) + (c >> 1)];
+        const float cs = rr.x, sn = rr.y;
         const float pq = __shfl_xor(dq[r], 1, 64), pk = __shfl_xor(dk[r], 1, 64);
         // forward: y0 = x0 c - x1 s, y1 = x0 s + x1 c  =>  dx0 = dy0 c + dy1 s, dx1 = -dy0 s + dy1 c
         const float gq = (c & 1) ? (-pq * sn + dq[r] * cs) : (dq[r] * cs + pq * sn);
@@ -287,8 +291,8 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(AttnArgs a) {
 }  // namespace
 
 extern "C" int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq,
-                             int T, int D, int heads, float rope_base, hipStream_t st) {
-  if (T < 1 || T > TP || D % heads) return 1;
+                             int T, int D, int heads, float rope_base, const float* rope, hipStream_t st) {
+  if (T < 1 || T > TP || D % heads || !rope) return 1;
   const int HD = D / heads;
   AttnArgs a;
   a.qkv = static_cast<const __bf16*>(qkv);
@@ -301,10 +305,11 @@ extern "C" int mta_attention(int bwd, const void* qkv, void* out, float* lse, co
   a.heads = heads;
   a.scale = 1.0f / sqrtf((float)HD);
   a.rope_base = rope_base;
+  a.rope = rope;
   const int blocks = nseq * heads;
   if (HD == 32) {
-    if (bwd) attn_bwd_kernel<32><<<blocks, 64, sizeof(BwdSmem<32>), st>>>(a);
-    else attn_fwd_kernel<32><<<blocks, 64, sizeof(FwdSmem<32>), st>>>(a);
+    if (bwd) attn_bwd_kernel<32><<<blocks, 256, sizeof(BwdSmem<32>), st>>>(a);
+    else attn_fwd_kernel<32><<<blocks, 256, sizeof(FwdSmem<32>), st>>>(a);
   } else if (HD == 64) {
     // > 64 KB of dynamic LDS (gfx950 has 160 KB per CU): opt in once per kernel
     static bool attr = false;
@@ -314,8 +319,8 @@ extern "C" int mta_attention(int bwd, const void* qkv, void* out, float* lse, co
         return 3;
       attr = true;
     }
-    if (bwd) attn_bwd_kernel<64><<<blocks, 64, sizeof(BwdSmem<64>), st>>>(a);
-    else attn_fwd_kernel<64><<<blocks, 64, sizeof(FwdSmem<64>), st>>>(a);
+    if (bwd) attn_bwd_kernel<64><<<blocks, 256, sizeof(BwdSmem<64>), st>>>(a);
+    else attn_fwd_kernel<64><<<blocks, 256, sizeof(FwdSmem<64>), st>>>(a);
   } else {
     return 2;
   }

@@ -3,6 +3,10 @@
 // validates tensors and forwards the current PyTorch HIP stream, so every op is stream-ordered
 // with PyTorch and capturable into a HIP graph.
 #include <torch/extension.h>
+
+#include <cmath>
+#include <map>
+#include <tuple>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <hip/hip_runtime.h>
@@ -62,7 +66,7 @@ int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps,
              float drop_p, const float* dy, const float* dres, const void* pre, void* dx_bf16, float* dx_f32,
              float* dgamma, float* dbeta, hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
-                  int D, int heads, float rope_base, hipStream_t st);
+                  int D, int heads, float rope_base, const float* rope, hipStream_t st);
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
 int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
@@ -556,6 +560,26 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
   TORCH_CHECK(rc == 0, "norm: unsupported arguments (D=", D, ")");
 }
 
+// RoPE (cos, sin) table [T][HD/2] in fp64 -> fp32, built once per (device, T, HD, base) on the first (eager) call;
+// graph replays reuse the cached device tensor
+static const float* rope_table(const at::Device& dev, int64_t T, int64_t HD, double base) {
+  static std::map<std::tuple<int, int64_t, int64_t, double>, at::Tensor> cache;
+  const auto key = std::make_tuple((int)dev.index(), T, HD, base);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    auto host = at::empty({T * HD}, at::TensorOptions().dtype(at::kFloat));
+    float* h = host.data_ptr<float>();
+    for (int64_t t = 0; t < T; ++t)
+      for (int64_t i = 0; i < HD / 2; ++i) {
+        const double ang = (double)t * std::pow(base, -2.0 * (double)i / (double)HD);
+        h[(t * (HD / 2) + i) * 2] = (float)std::cos(ang);
+        h[(t * (HD / 2) + i) * 2 + 1] = (float)std::sin(ang);
+      }
+    it = cache.emplace(key, host.to(dev)).first;
+  }
+  return it->second.data_ptr<float>();
+}
+
 void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
                int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base) {
   MTA_CHECK_GPU(qkv, at::kBFloat16);
@@ -570,7 +594,8 @@ void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const O
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   const int rc = mta_attention(bwd ? 1 : 0, qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
                                opt_typed<void>(dout, at::kBFloat16, "dout"), opt_typed<void>(dqkv, at::kBFloat16, "dqkv"),
-                               (int)nseq, (int)T, (int)D, (int)heads, (float)rope_base, cur_stream());
+                               (int)nseq, (int)T, (int)D, (int)heads, (float)rope_base,
+                               rope_table(qkv.device(), T, D / heads, rope_base), cur_stream());
   TORCH_CHECK(rc == 0, "attention: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc, ")");
 }
 

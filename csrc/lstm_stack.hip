@@ -171,10 +171,11 @@ struct StackFwdArgs {
   unsigned* ctl;
   unsigned spin_limit;
   int N, Np, T, L, ntiles, tr8, eshift;
-  // in-kernel batch gather (gather != 0): layer 0 reads x through the device permutation, the non-top-layer
-  // workgroups copy the batch rows into the static buffers after their recurrence (the decoder and the backward
-  // read those), the last workgroup advances the cursor: no separate gather launch per training step
-  int gather, copy_blocks;
+  // in-kernel batch gather (gather != 0): layer 0 reads x through the device permutation, copy_blocks extra
+  // workgroups at the end of the grid copy the batch rows into the static buffers (the decoder and the backward
+  // read those) on otherwise idle CUs while the recurrence runs, the last workgroup advances the cursor: no
+  // separate gather launch per training step
+  int gather, copy_blocks, main_blocks;
   MtaBatchGather g;
   // projection workgroups (proj != 0): the input product, the x loads / hand-off polls and the dropout-mask hashes
   // move off the recurrent CU (see stack_fwd_body)
@@ -736,19 +737,30 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch)
+// batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch);
+// four independent 16-byte loads in flight per thread before their stores
 __device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P) {
   const int cur = g.cursor[0];
   const long stride = (long)P * blockDim.x, first = (long)p * blockDim.x + threadIdx.x;
   for (int k = 0; k < g.nt; ++k) {
     const long row = g.row[k], total = (long)g.B * row;
     if ((row & 3) == 0 && ((((uintptr_t)g.src[k]) | ((uintptr_t)g.dst[k])) & 15) == 0) {
-      const long row4 = row / 4;
+      const long row4 = row / 4, n4 = total / 4;
       const float4* s4 = reinterpret_cast<const float4*>(g.src[k]);
       float4* d4 = reinterpret_cast<float4*>(g.dst[k]);
-      for (long e = first; e < total / 4; e += stride) {
-        const long b = e / row4;
-        d4[e] = s4[(long)g.perm[cur * g.B + b] * row4 + (e - b * row4)];
+      for (long e0 = first; e0 < n4; e0 += 4 * stride) {
+        float4 v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const long e = e0 + r * stride;
+          if (e < n4) {
+            const long b = e / row4;
+            v[r] = s4[(long)g.perm[cur * g.B + b] * row4 + (e - b * row4)];
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (e0 + r * stride < n4) d4[e0 + r * stride] = v[r];
       }
     } else {
       for (long e = first; e < total; e += stride) {
@@ -764,6 +776,13 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwd
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident); in projection
   // mode each layer is [projection pw 0 x tr8, projection pw 1 x tr8, recurrent x tr8] (producers first again)
   int layer, tile, role = 0, pw = 0;
+  if ((int)blockIdx.x >= a.main_blocks) {
+    // batch-copy workgroup (gather mode): no hand-offs, only the copy and the launch arrival
+    const unsigned cbase = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
+    batch_copy(a.g, blockIdx.x - a.main_blocks, a.copy_blocks);
+    if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, cbase, a.eshift)) a.g.cursor[0] += 1;
+    return;
+  }
   if (a.proj) {
     const int G = 3 * a.tr8, j = blockIdx.x % G;
     layer = blockIdx.x / G;
@@ -784,7 +803,6 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwd
     if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base, role, pw);
     else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base, role, pw);
   }
-  if (a.gather && (int)blockIdx.x < a.copy_blocks) batch_copy(a.g, blockIdx.x, a.copy_blocks);
   // every workgroup read the cursor before arriving: the last one advances it
   if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift) && a.gather) a.g.cursor[0] += 1;
 }
@@ -1189,7 +1207,7 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
 
 template <int H, int PREC>
 int launch_fwd(int fin, const StackFwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.L * a.tr8 * (a.proj ? 3 : 1)), block((H / 16) * 128);  // recurrent + input waves
+  const dim3 grid(a.main_blocks + (a.gather ? a.copy_blocks : 0)), block((H / 16) * 128);  // + batch-copy blocks
   if (fin == 3) lstm_stack_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(a);
   else if (fin == 5) lstm_stack_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(a);
   else return -1;
@@ -1291,9 +1309,8 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
   a.timeout = a.ctl + CTL_TIMEOUT;
   a.spin_limit = spin_limit();
   a.pflags = flags + proj_flag_offset(a.tr8);
-  // the copy goes to workgroups that finish before the top layer (all of them for one layer; projection mode:
-  // the layer-0 projection workgroups, which run ahead of everything)
-  a.copy_blocks = a.proj ? 2 * a.tr8 : (L > 1 ? L - 1 : 1) * a.tr8;
+  a.main_blocks = a.L * a.tr8 * (a.proj ? 3 : 1);
+  a.copy_blocks = 16;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
 }
