@@ -17,8 +17,6 @@
 // into an fp32 output (weight gradients straight into the flat gradient buffer); the weight-gradient
 // form also produces the bias gradient (row sums of A over K) from the A fragments it already holds.
 // Requirements (checked by the launcher): M, N, K multiples of 8, 16-byte aligned rows.
-#include <cstdlib>
-
 #include "common.h"
 
 namespace {
@@ -49,7 +47,6 @@ struct GemmArgs {
   int ldc, n_store;        // columns [0, n_store) of C are written (N may include zero padding)
   int k_per_split;          // multiple of BK
   float* bias_grad;         // AT mode: += row sums of A over K  ([M])
-  int row_epi;              // non-split, non-accumulating, 16-B aligned rows: LDS-staged row epilogue
 };
 
 
@@ -76,13 +73,8 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int A_REGS = AT ? 8 : 1;  // 16-B loads per item
   constexpr int B_REGS = BT ? 8 : 1;
 
-  // one LDS block: the A / B staging images, reused after the k loop as the fp32 C tile of the row epilogue
-  __shared__ __attribute__((aligned(16))) __bf16 smem[(BM + BN) * RST];
-  __bf16* const As = smem;
-  __bf16* const Bs = smem + BM * RST;
-  constexpr int CLD = BN + 4;  // fp32 C-tile row stride
-  constexpr bool ROW_EPI_FITS = BM * CLD * 4 <= (BM + BN) * RST * 2 && (BM * BN) % (8 * GT) == 0;
-  constexpr int RCH = ROW_EPI_FITS ? BM * BN / (8 * GT) : 1;  // 8-column row chunks per thread
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * RST];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * RST];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -201,31 +193,6 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   for (int i = 0; i < MT; ++i) rowsum[i] = 0.f;
   const bool want_rowsum = g.bias_grad != nullptr && blockIdx.x == 0 && wn == 0;
 
-  // row epilogue: this thread's chunks (row, 8 columns); their residual / GELU-input operands are fetched now,
-  // under the k loop, as 16- / 32-byte row loads
-  const bool row_epi = ROW_EPI_FITS && g.row_epi && gridDim.z == 1;
-  float4 rpre[RCH][2];
-  if (row_epi && (g.flags & (EPI_RESID | EPI_DGELU))) {
-#pragma unroll
-    for (int c = 0; c < RCH; ++c) {
-      const int idx = tid + c * GT, r = idx / (BN / 8), cc = 8 * (idx % (BN / 8));
-      const int m = m0 + r, n = n0 + cc;
-      rpre[c][0] = rpre[c][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < g.M && n < g.n_store) {
-        const size_t o = (size_t)m * g.ldc + n;
-        if (g.flags & EPI_RESID) {
-          rpre[c][0] = *reinterpret_cast<const float4*>(g.resid + o);
-          rpre[c][1] = *reinterpret_cast<const float4*>(g.resid + o + 4);
-        } else {
-          Bf8 v;
-          v.u = *reinterpret_cast<const uint4*>(g.aux_in + o);
-          rpre[c][0] = make_float4((float)v.e[0], (float)v.e[1], (float)v.e[2], (float)v.e[3]);
-          rpre[c][1] = make_float4((float)v.e[4], (float)v.e[5], (float)v.e[6], (float)v.e[7]);
-        }
-      }
-    }
-  }
-
   load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += BKT) {
     __syncthreads();
@@ -251,63 +218,6 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
         for (int i = 0; i < MT; ++i) acc[i][j] = mfma16x16x32(af[i], bfr, acc[i][j]);
       }
     }
-  }
-
-  if (row_epi) {
-    // ---- row epilogue: accumulators -> fp32 C tile in LDS -> each thread finishes (row, 8 columns) chunks with
-    // 16-byte loads / stores (the per-element form wrote 2- or 4-byte fragments at a row stride) ----
-    float* Cs = reinterpret_cast<float*>(smem);
-    __syncthreads();  // every wave is done with the A / B images
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          Cs[(wm * WM + 16 * i + 4 * (lane >> 4) + r) * CLD + wn * WN + 16 * j + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < RCH; ++c) {
-      const int idx = tid + c * GT, r = idx / (BN / 8), cc = 8 * (idx % (BN / 8));
-      const int m = m0 + r, n = n0 + cc;
-      if (m >= g.M || n >= g.n_store) continue;
-      const float4 c0 = *reinterpret_cast<const float4*>(&Cs[r * CLD + cc]);
-      const float4 c1 = *reinterpret_cast<const float4*>(&Cs[r * CLD + cc + 4]);
-      float v[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-      const float pre[8] = {rpre[c][0].x, rpre[c][0].y, rpre[c][0].z, rpre[c][0].w,
-                            rpre[c][1].x, rpre[c][1].y, rpre[c][1].z, rpre[c][1].w};
-      const size_t o = (size_t)m * g.ldc + n;
-      float bv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (g.flags & EPI_BIAS) {
-        const float4 b0 = *reinterpret_cast<const float4*>(g.bias + n);
-        const float4 b1 = *reinterpret_cast<const float4*>(g.bias + n + 4);
-        bv[0] = b0.x; bv[1] = b0.y; bv[2] = b0.z; bv[3] = b0.w;
-        bv[4] = b1.x; bv[5] = b1.y; bv[6] = b1.z; bv[7] = b1.w;
-      }
-      Bf8 apre;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float x = g.alpha * v[e] + bv[e];
-        apre.e[e] = (__bf16)x;
-        if (g.flags & EPI_GELU) x = mta_gelu(x);
-        if (g.flags & EPI_DROPOUT) x *= mta_dropout_scale(*g.seed, (uint32_t)m, (uint32_t)(n + e), g.drop_p);
-        if (g.flags & EPI_DGELU) x *= mta_gelu_grad(pre[e]);
-        if (g.flags & EPI_RESID) x += pre[e];
-        v[e] = x;
-      }
-      if (g.aux_pre) *reinterpret_cast<uint4*>(g.aux_pre + o) = apre.u;
-      if (g.out_f32) {
-        *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<float4*>(g.out_f32 + o + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      }
-      if (g.out_bf16) {
-        Bf8 ob;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ob.e[e] = (__bf16)v[e];
-        *reinterpret_cast<uint4*>(g.out_bf16 + o) = ob.u;
-      }
-    }
-    return;
   }
 
   // ---- epilogue ----
@@ -434,13 +344,6 @@ extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int 
   ksplit = (K + kps - 1) / kps;
   g.k_per_split = kps;
   g.bias_grad = bias_grad;
-  // row epilogue: whole 8-column chunks and 16-byte aligned rows of every operand it touches
-  {
-    auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-    g.row_epi = ksplit == 1 && !(flags & EPI_ACCUM) && !bias_grad && n_store % 8 == 0 && ldc % 8 == 0 &&
-                al16(bias) && al16(resid) && al16(aux_in) && al16(out_bf16) && al16(out_f32) && al16(aux_pre) &&
-                !(getenv("MTA_GEMM_ROW_EPI") && getenv("MTA_GEMM_ROW_EPI")[0] == '0');
-  }
   if (mode == 0) dispatch<false, false>(g, ksplit, st);
   else if (mode == 1) dispatch<false, true>(g, ksplit, st);
   else if (mode == 2) dispatch<true, true>(g, ksplit, st);
