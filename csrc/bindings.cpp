@@ -72,7 +72,7 @@ int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const 
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                          float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
                          const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
-                         float* const* gxg, const MtaBatchGather* gather, hipStream_t st);
+                         const MtaBatchGather* gather, hipStream_t st);
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
@@ -622,8 +622,7 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
                                 std::vector<at::Tensor> b_hh, std::vector<at::Tensor> hseq,
                                 std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
                                 std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags,
-                                int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather,
-                                const std::vector<at::Tensor>* gxg = nullptr) {
+                                int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather) {
   const int64_t L = (int64_t)w_hh.size();
   MTA_CHECK_F32(x);
   TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
@@ -651,19 +650,11 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
   for (int64_t l = 0; l < L; ++l)
     if (xdrop[l].numel()) mk[l] = reinterpret_cast<uint32_t*>(masks[l].data_ptr<uint8_t>());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  std::vector<float*> gp;
-  if (gxg && !gxg->empty()) {
-    TORCH_CHECK(gxg->size() == (size_t)L, "gxg: one projection buffer per layer");
-    for (const auto& t : *gxg)
-      TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.numel() >= T * Np * 4 * H,
-                  "gxg: fp32[T * Np * 4H] per layer");
-    gp = ptrs_f32(*gxg, "gxg");
-  }
   const int rc = mta_lstm_stack_fwd_g((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(),
                                       cwh.data(), cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
                                       reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
                                       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
-                                      gp.empty() ? nullptr : gp.data(), gather, cur_stream());
+                                      gather, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
 }
 
@@ -678,19 +669,13 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
 
 // the same launch with the training step's batch gather folded in: src[k] (rows, ...) -> dst[k] (B, ...) at rows
 // perm[cursor * B + b]; x must be dst[0] (the static batch buffer), cursor advances once per launch
-void lstm_stack_fwd_ex(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
+void lstm_stack_fwd_gather(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vector<at::Tensor> w_ih,
                            std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
                            std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop,
                            std::vector<at::Tensor> masks, std::vector<at::Tensor> stash, at::Tensor seeds,
                            double drop_p, at::Tensor flags, int64_t N, int64_t Np, int64_t T,
                            std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::Tensor perm, at::Tensor cursor,
-                           int64_t B, std::vector<at::Tensor> gxg) {
-  // src empty: no gather (plain launch, optionally in projection mode with gxg)
-  if (src.empty()) {
-    lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N,
-                        Np, T, nullptr, &gxg);
-    return;
-  }
+                           int64_t B) {
   TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 gathered tensors");
   TORCH_CHECK(perm.is_cuda() && cursor.is_cuda() && perm.scalar_type() == at::kInt &&
               cursor.scalar_type() == at::kInt, "perm/cursor: int32 GPU tensors");
@@ -709,7 +694,7 @@ void lstm_stack_fwd_ex(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::
   g.cursor = cursor.data_ptr<int>();
   g.B = (int)B;
   lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N, Np,
-                      T, &g, &gxg);
+                      T, &g);
 }
 
 // grads: [] (weight gradients by the caller) or 4 lists g_wih, g_whh, g_bih, g_bhh of per-layer gradient
@@ -940,7 +925,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dgp", &dgp);
   m.def("ols_features", &ols_features);
   m.def("lstm_stack_fwd", &lstm_stack_fwd);
-  m.def("lstm_stack_fwd_ex", &lstm_stack_fwd_ex);
+  m.def("lstm_stack_fwd_gather", &lstm_stack_fwd_gather);
   m.def("lstm_stack_bwd", &lstm_stack_bwd);
   m.def("lstm_stack_flag_words", &lstm_stack_flag_words);
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });

@@ -69,7 +69,6 @@ constexpr int STASH = 5;
 constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;  // default poll bound (env MTA_LSTM_SPIN_LIMIT overrides: fault tests)
 constexpr int FLAG_STRIDE = 32;
-constexpr int PSPLIT = 4;  // projection waves per unit slice (step t goes to wave t mod PSPLIT; 2 workgroups)
 constexpr int TRS = 20;  // row stride (floats) of the per-wave 16 x 16 transpose scratch (conflict-free writes)
 // progress words are E << eshift | steps: eshift = epoch_shift(T) >= 12 bits (long sequences take more step bits;
 // the flag buffer a launch uses is keyed by its shift on the host, ops/lstm.py _stack_flags)
@@ -177,11 +176,6 @@ struct StackFwdArgs {
   // separate gather launch per training step
   int gather, copy_blocks, main_blocks;
   MtaBatchGather g;
-  // projection workgroups (proj != 0): the input product, the x loads / hand-off polls and the dropout-mask hashes
-  // move off the recurrent CU (see stack_fwd_body)
-  int proj;
-  float* gxg[MAXL];   // (T, ntiles, NW, 64 lanes, 4 sequences) float4 gate pre-activations per layer
-  unsigned* pflags;   // [MAXL][tr8][PSPLIT][NW] progress words of the projection waves
 };
 
 // Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
@@ -193,16 +187,6 @@ struct StackFwdArgs {
 // output (one step ahead, into LDS and the keep-byte words the backward reads): the hash's 32-bit multiplies
 // were ~30 % of a recurrent step when the recurrent waves drew them (r2 stamp probe).  Both roles execute
 // the same barriers (pre-loop, one per step, final).
-//
-// Projection mode (a.proj, small grids: the headline shape): per (layer, tile) two extra PROJECTION
-// workgroups, placed before the layer's recurrent workgroup in block order, on the same XCD (same block id mod 8),
-// compute gx_t = bias + W_ih x_t for every step and draw the layer's output dropout masks, independently per
-// wave (8 waves = 4 unit slices x 2 step parities per workgroup, so each (slice, t mod 4) is one wave, with no
-// barrier), and hand gx_t + the keep words to the recurrent workgroup through L2/HBM (sc1 stores, drained, then
-// a per-wave progress word).  The recurrent workgroup's input waves then only poll, load 68 B per lane per step
-// and fill the LDS slots: its SIMDs no longer share the matrix pipe with the input MFMAs (layers >= 1) nor the
-// VALU with the mask hashes (the r2 stamp probe put ~45 % of a layer-1 step in that contention).  The price is
-// one more hand-off of pipeline fill per layer.
 template <int H, int PREC>
 struct FwdSmem {
   static constexpr int ROWB = H + 8, ROWF = H + 4;
@@ -216,8 +200,7 @@ struct FwdSmem {
 
 template <int H, int PREC, int FIN0, bool FIRST>
 __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
-                                               FwdSmem<H, PREC>& sm, const unsigned base, const int role,
-                                               const int pw) {
+                                               FwdSmem<H, PREC>& sm, const unsigned base) {
   constexpr int NW = H / 16;
   constexpr int KB = H / 32;
   constexpr int KF = H / 4;
@@ -227,9 +210,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 
   const bool last = layer == a.L - 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool proj_wg = role == 1;  // projection workgroup: every wave is a projection wave
-  const bool input_wave = proj_wg || wave >= NW;
-  const int w = proj_wg ? wave % NW : input_wave ? wave - NW : wave;
+  const bool input_wave = wave >= NW;
+  const int w = input_wave ? wave - NW : wave;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
   const int n0 = tile * S;
@@ -325,9 +307,10 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         }
       }
     };
-    auto compute_acc = [&](const XBuf& xb, f32x4 (&acc)[4]) {
+    auto compute_gx = [&](int slot, const XBuf& xb) {
       const auto& xin0 = xb.x0;
       const auto& xr = xb.xr;
+      f32x4 acc[4];
       if constexpr (FIRST) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -373,140 +356,24 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           }
         }
       }
-    };
-    auto compute_gx = [&](int slot, const XBuf& xb) {
-      f32x4 acc[4];
-      compute_acc(xb, acc);
 #pragma unroll
       for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
     };
     // dropout keep bytes of this layer's output (the next layer's input) for the lanes of recurrent wave w
     uint32_t* mout = last ? nullptr : a.mask[layer + 1];
     const uint64_t seed_next = mout ? a.seeds[layer + 1] : 0;
-    auto draw_kb = [&](int t) {
-      uint32_t kb = 0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-        kb |= (mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p) != 0.f ? 1u : 0u) << (8 * i);
-      }
-      return kb;
-    };
     auto draw_mask = [&](int t) {
       if (mout) {
-        const uint32_t kb = draw_kb(t);
+        uint32_t kb = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
+          kb |= (mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p) != 0.f ? 1u : 0u) << (8 * i);
+        }
         sm.keep[t & 1][w][lane] = kb;
         mout[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u] = kb;  // before this interval's loads
       }
     };
-    if (proj_wg) {
-      // ------------------------- projection waves (own workgroups, no barriers) -------------------------
-      // wave (slice w, parity) of projection workgroup pw computes the steps t = r, r + PSPLIT, ... (r = 2 pw +
-      // parity): gx_t and the keep word of its lanes, write-through stores, drained, then its progress word
-      const int r = 2 * pw + wave / NW;
-      unsigned* my_pf = a.pflags + FLAG_STRIDE * (((layer * a.tr8 + tile) * PSPLIT + r) * NW + w);
-      float* gxo = a.gxg[layer];
-      XBuf xb;
-      if (r < T) load_input(r, xb);
-      int k = 0;
-      for (int t = r; t < T; t += PSPLIT, ++k) {
-        f32x4 acc[4];
-        compute_acc(xb, acc);
-        float* dst = gxo + ((((size_t)t * a.ntiles + tile) * NW + w) * 64 + lane) * 16;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) store_sc1_x4(dst + 4 * i, f32x4{acc[0][i], acc[1][i], acc[2][i], acc[3][i]});
-        if (mout)
-          __hip_atomic_store(mout + ((size_t)t * a.ntiles + tile) * 4 * H + q * H + u, draw_kb(t), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        if (t + PSPLIT < T) load_input(t + PSPLIT, xb);  // (polls the layer below for layers >= 1)
-        mta_wait_vmem();  // this step's stores are visible at agent scope
-        if (lane == 0)
-          __hip_atomic_store(my_pf, base + (unsigned)(k + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    if (a.proj) {
-      // ------------- input waves of a projection-mode recurrent workgroup: poll, load, fill LDS -------------
-      // gx_t and the keep word of step t come from projection wave (t mod PSPLIT, slice w); three steps ahead in
-      // two register sets, a one-step-stale copy of every producer's word so a poll is only paid when it waits
-      struct PBuf {
-        float4 g[4];
-        uint32_t kb;
-      };
-      PBuf pA, pB;
-      unsigned sp[PSPLIT];
-#pragma unroll
-      for (int i = 0; i < PSPLIT; ++i) sp[i] = base;
-      const float* gxi = a.gxg[layer];
-      auto pflag = [&](int r) { return a.pflags + FLAG_STRIDE * (((layer * a.tr8 + tile) * PSPLIT + r) * NW + w); };
-      auto need = [&](int t) { return base + (unsigned)(t / PSPLIT + 1); };
-      // pv: producer word of the NEXT step to load, read one interval ahead and issued before that interval's
-      // payload loads: using it then waits only for loads two intervals old (vmcnt counts in order: a poll that
-      // is waited on right away drains every prefetch in flight, one full round trip per step)
-      unsigned pv = base;
-      auto poll_issue = [&](int t, int r) {
-        if (t < T && !reached(sp[r], need(t)))
-          pv = __hip_atomic_load(pflag(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          pv = sp[r];
-      };
-      auto loadp = [&](int t, int r, PBuf& xb) {
-        if (!reached(sp[r], need(t))) sp[r] = wait_progress(pflag(r), need(t), pv, a.timeout, a.spin_limit);
-        const float* src = gxi + ((((size_t)t * a.ntiles + tile) * NW + w) * 64 + lane) * 16;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) xb.g[v] = load_sc1(src, 4 * v);
-        xb.kb = mout ? __hip_atomic_load(mout + ((size_t)t * a.ntiles + tile) * 4 * H + q * H + u, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : 0u;
-      };
-      auto put = [&](int t, const PBuf& xb) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) gxs[t & 1][4 * q + i][u] = xb.g[i];
-      };
-      uint32_t kb_pend;
-      poll_issue(0, 0);
-      loadp(0, 0, pA);
-      put(0, pA);
-      kb_pend = pA.kb;
-      if (T > 1) {
-        poll_issue(1, 1);
-        loadp(1, 1, pB);
-      }
-      if (T > 2) {
-        poll_issue(2, 2);
-        loadp(2, 2, pA);
-      }
-      poll_issue(3, 3);
-      __syncthreads();  // pre-loop barrier: gx_0 ready
-      // interval t: keep word of step t to LDS, gx_{t+1} to LDS, refill that set with step t+3 (producer r3 =
-      // (t+3) mod PSPLIT) confirmed by the poll issued last interval, then the poll of step t+4
-      auto pinterval = [&](int t, PBuf& xb, int r3) {
-        if (mout) sm.keep[t & 1][w][lane] = kb_pend;
-        if (t + 1 < T) {
-          put(t + 1, xb);
-          kb_pend = xb.kb;
-          if (t + 3 < T) {
-            const unsigned pv_t3 = pv;
-            __builtin_amdgcn_sched_barrier(0);
-            poll_issue(t + 4, (r3 + 1) % PSPLIT);  // issued before this interval's payload loads
-            const unsigned pv_next = pv;
-            __builtin_amdgcn_sched_barrier(0);
-            pv = pv_t3;
-            loadp(t + 3, r3, xb);
-            pv = pv_next;
-          }
-        }
-        __syncthreads();
-      };
-      for (int t = 0; t < T; t += 4) {
-        pinterval(t, pB, 3);
-        if (t + 1 < T) pinterval(t + 1, pA, 0);
-        if (t + 2 < T) pinterval(t + 2, pB, 1);
-        if (t + 3 < T) pinterval(t + 3, pA, 2);
-      }
-      __syncthreads();  // final barrier (the recurrent waves publish after it)
-      return;
-    }
     load_input(0, xbA);
     compute_gx(0, xbA);
     if (T > 1) load_input(1, xbB);
@@ -773,9 +640,7 @@ __device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P
 
 template <int H, int PREC, int FIN0>
 __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
-  // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident); in projection
-  // mode each layer is [projection pw 0 x tr8, projection pw 1 x tr8, recurrent x tr8] (producers first again)
-  int layer, tile, role = 0, pw = 0;
+  // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
   if ((int)blockIdx.x >= a.main_blocks) {
     // batch-copy workgroup (gather mode): no hand-offs, only the copy and the launch arrival
     const unsigned cbase = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
@@ -783,25 +648,12 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwd
     if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, cbase, a.eshift)) a.g.cursor[0] += 1;
     return;
   }
-  if (a.proj) {
-    const int G = 3 * a.tr8, j = blockIdx.x % G;
-    layer = blockIdx.x / G;
-    if (j < 2 * a.tr8) {
-      role = 1;
-      pw = j / a.tr8;
-      tile = j % a.tr8;
-    } else {
-      tile = j - 2 * a.tr8;
-    }
-  } else {
-    layer = blockIdx.x / a.tr8;
-    tile = blockIdx.x % a.tr8;
-  }
+  const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
   const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
   __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
   if (tile < a.ntiles) {
-    if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base, role, pw);
-    else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base, role, pw);
+    if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
+    else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
   }
   // every workgroup read the cursor before arriving: the last one advances it
   if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift) && a.gather) a.g.cursor[0] += 1;
@@ -1239,10 +1091,6 @@ int dispatch_bwd(int prec, const StackBwdArgs& a, size_t wg_lds, hipStream_t st)
   return launch_bwd<H, PREC_BF16>(a, wg_lds, st);
 }
 
-// flag buffer: [3][MAXL][tr8] hand-off progress words, [MAXL][tr8][PSPLIT][4] projection-wave words, control words
-inline long proj_flag_offset(int tr8) { return 3L * FLAG_STRIDE * MAXL * tr8; }
-inline long ctl_offset(int tr8) { return proj_flag_offset(tr8) + (long)FLAG_STRIDE * MAXL * tr8 * PSPLIT * 4; }
-
 unsigned spin_limit() {
   static const unsigned v = [] {
     const char* e = getenv("MTA_LSTM_SPIN_LIMIT");
@@ -1259,7 +1107,7 @@ extern "C" int mta_lstm_stack_epoch_shift(int T) { return epoch_shift(T); }
 
 extern "C" long mta_lstm_stack_flag_words(int Np) {
   const int tr8 = (Np / S + 7) / 8 * 8;
-  return ctl_offset(tr8) + CTL_WORDS;
+  return 3L * FLAG_STRIDE * MAXL * tr8 + CTL_WORDS;
 }
 
 // gather (nullable): x is then the static batch buffer the launch fills (layer 0 reads the dataset directly)
@@ -1267,8 +1115,7 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
                                     const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                     float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                     float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                    int Np, int T, float* const* gxg, const MtaBatchGather* gather,
-                                    hipStream_t st) {
+                                    int Np, int T, const MtaBatchGather* gather, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
   StackFwdArgs a{};
   a.x = x;
@@ -1289,11 +1136,7 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
     a.mask[l] = mask ? mask[l] : nullptr;
     if (a.xdrop[l] && !a.mask[l]) return -2;  // the backward reads the keep bytes
     a.stash[l] = stash ? stash[l] : nullptr;
-    a.gxg[l] = gxg ? gxg[l] : nullptr;
   }
-  a.proj = gxg != nullptr;
-  for (int l = 0; l < L && a.proj; ++l)
-    if (!a.gxg[l]) return -5;
   a.seeds = seeds;
   a.drop_p = drop_p;
   a.N = N;
@@ -1305,11 +1148,10 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
   a.eshift = epoch_shift(T);
   if (T + 8 >= (1 << a.eshift)) return -1;
   a.flags = flags;
-  a.ctl = flags + ctl_offset(a.tr8);
+  a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
   a.spin_limit = spin_limit();
-  a.pflags = flags + proj_flag_offset(a.tr8);
-  a.main_blocks = a.L * a.tr8 * (a.proj ? 3 : 1);
+  a.main_blocks = a.L * a.tr8;
   a.copy_blocks = 16;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
   return dispatch_fwd<64>(prec, fin, a, st);
@@ -1321,7 +1163,7 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
                                   float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
                                   int Np, int T, hipStream_t st) {
   return mta_lstm_stack_fwd_g(H, prec, L, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, mask, stash, seeds, drop_p,
-                              flags, N, Np, T, nullptr, nullptr, st);
+                              flags, N, Np, T, nullptr, st);
 }
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's
@@ -1356,7 +1198,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
   a.eshift = epoch_shift(T);
   a.flags = flags + FLAG_STRIDE * MAXL * a.tr8;
   a.dg_flags = flags + 2 * FLAG_STRIDE * MAXL * a.tr8;
-  a.ctl = flags + ctl_offset(a.tr8);
+  a.ctl = flags + 3 * FLAG_STRIDE * MAXL * a.tr8;
   a.timeout = a.ctl + CTL_TIMEOUT;
   a.spin_limit = spin_limit();
   size_t wg_lds = 0;

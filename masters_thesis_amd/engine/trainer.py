@@ -658,9 +658,20 @@ class Trainer:
             sys.stdout.write("\n")
         return host_ms, B
 
+    def _print_devices(self) -> None:
+        """Lightning's start-up device line (plus the GPU a pinned launcher trial was given)."""
+        cuda = self.device.type == "cuda"
+        extra = ""
+        if cuda:
+            extra = (f", device: {torch.cuda.get_device_name(self.device)}"
+                     f" (HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', 'all')}, rank {self.denv.rank}"
+                     f"/{self.denv.world_size})")
+        self._print(f"GPU available: {torch.cuda.is_available()} (rocm), used: {cuda}{extra}")
+
     def fit(self, model, datamodule=None, ckpt_path: Optional[str] = None, train_dataloaders=None,
             val_dataloaders=None) -> None:
         self._setup_env()
+        self._print_devices()
         dm = datamodule
         self.datamodule = dm
         if dm is not None:

@@ -250,20 +250,6 @@ def _pad_weights(flat: Sequence[Tensor], H: int, Hp: int, F: int) -> List[Tensor
     return out
 
 
-def projection_mode(Np: int, L: int) -> bool:
-    """Whether the pipelined forward runs with projection workgroups (3 workgroups per (layer, tile)): opt-in
-    (``MTA_LSTM_PROJ=1``) and only while the whole grid fits one workgroup per CU.  Measured slower than the
-    in-workgroup input waves at every depth on MI355X (headline shape, profiles/r2_proj_ab.txt: L=1 108 vs
-    69 us, L=2 137 vs 102 us): the extra write-through hand-off of gx costs more per step than the SIMD
-    sharing it removes, so the default stays off.  Bit-identical to the default path (GPU test)."""
-    import os
-
-    if os.environ.get("MTA_LSTM_PROJ", "0") != "1":
-        return False
-    tr8 = (Np // 16 + 7) // 8 * 8
-    return 3 * L * tr8 <= 256
-
-
 def kernel_hidden(H: int) -> int:
     """Hidden size the pipelined kernels run an H-unit stack at (native 32 / 64; H < 32 zero-padded to 32)."""
     return H if H in (32, 64) else 32
@@ -300,19 +286,16 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
     flags = _stack_flags(C, Np, L, dev, T)
-    # projection workgroups (csrc/lstm_stack.hip "Projection mode"): gx_t = b + W_ih x_t and the dropout masks on
-    # their own CUs, handed to the recurrent workgroups through one (T, Np, 4H) buffer per layer
-    gxg = ([torch.empty(T * Np * 4 * H, device=dev, dtype=torch.float32) for _ in range(L)]
-           if projection_mode(Np, L) else [])
     if gather is not None:
         src, dst, perm, cursor, B = gather
         if x.data_ptr() != dst[0].data_ptr() or not x.is_contiguous():
             raise ValueError("deferred gather: x must be the static batch buffer")
+        C.lstm_stack_fwd_gather(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]),
+                                list(flat[3::4]), hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T,
+                                src, dst, perm, cursor, B)
     else:
-        src, dst, perm, cursor, B = [], [], _empty(dev, torch.int32), _empty(dev, torch.int32), 1
-    C.lstm_stack_fwd_ex(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
-                        hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T, src, dst, perm, cursor, B,
-                        gxg)
+        C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
+                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
     st = PipelinedState()
     st.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
     st.params, st.seeds, st.x = tuple(flat), seeds, x

@@ -1,4 +1,5 @@
-"""A/B timing of the pipelined LSTM forward/backward: projection workgroups (MTA_LSTM_PROJ=1) vs in-workgroup input
+"""(Historical: the projection mode it A/Bs was removed after this measurement, profiles/r2_proj_ab.txt.)
+A/B timing of the pipelined LSTM forward/backward: projection workgroups (MTA_LSTM_PROJ=1) vs in-workgroup input
 waves (0), per (L, dropout), N=100 T=60 H=64 (the headline shape)."""
 import os
 import sys

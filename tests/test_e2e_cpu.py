@@ -143,3 +143,14 @@ def test_launcher_retries_failed_trial_with_auto_resume(tmp_path):
     for v in ("mse_small_lr0.001_fast", "mse_small_lr0.0001_fast"):
         ck = torch.load(tmp_path / "logs/FinancialLstm/synthetic" / v / "checkpoints/last.ckpt", weights_only=True)
         assert ck["epoch"] == 1
+
+
+def test_gpu_pool_launcher_pins_one_device_per_slot(tmp_path):
+    """hydra/launcher=gpu_pool: every trial is a child process with its own HIP_VISIBLE_DEVICES slot (two fake
+    devices here; on CPU the children train on the CPU), results land in per-job run dirs."""
+    r = _run([str(REPO / "train.py"), "-m", *TINY, "trainer.max_epochs=1", "model.learning_rate=0.001,0.0001",
+              "hydra/launcher=gpu_pool", "hydra.launcher.devices=2", "hydra.launcher.jobs_per_device=1"], tmp_path)
+    assert "[launcher:gpu_pool] job #0 (attempt 0) on slot 0" in r.stdout, r.stdout
+    assert "[launcher:gpu_pool] job #1 (attempt 0) on slot 1" in r.stdout, r.stdout
+    outs = sorted((tmp_path / "multirun").glob("*/*/job*.out"))
+    assert len(outs) == 2 and all("Test MAE" in o.read_text() for o in outs)

@@ -110,3 +110,18 @@ def test_gpu_test_py_on_gpu_checkpoint(runs):
     for t in ("scatter/recon_residuals", "scatter/alphas", "scatter/betas", "hist/recon_residuals", "hist/alphas",
               "hist/betas", "estimation/alpha", "estimation/beta"):
         assert t in tags, (t, sorted(tags))
+
+
+def test_gpu_pool_sweep_on_device(tmp_path):
+    """hydra/launcher=gpu_pool on the MI355X: two trials share GPU 0 (jobs_per_device=2), each a child process
+    pinned through HIP_VISIBLE_DEVICES, training on the HIP path (SURVEY §2.6 trial-level launcher)."""
+    out = _run([str(REPO / "train.py"), "-m", "datamodule.n_samples=20000", "seed=0", "trainer.max_epochs=1",
+                "trainer.enable_progress_bar=false", "model.learning_rate=0.001,0.0001", "hydra/launcher=gpu_pool",
+                "hydra.launcher.devices=[0]", "hydra.launcher.jobs_per_device=2"], tmp_path, timeout=400)
+    assert out.count("[launcher:gpu_pool] job #") == 2, out
+    logs = sorted((tmp_path / "multirun").glob("*/*/job*.out"))
+    assert len(logs) == 2
+    for lg in logs:
+        text = lg.read_text()
+        assert "used: True" in text and "HIP_VISIBLE_DEVICES=0" in text, text[-2000:]
+        assert "Test MAE" in text

@@ -253,37 +253,3 @@ def test_pipelined_long_sequence(T):
     for a, b in zip(wg, w64):
         # gradients sum T terms: relative to the gradient scale
         assert (a.grad.double().cpu() - b.grad).abs().max().item() <= 1e-3 * max(b.grad.abs().max().item(), 1e-3)
-
-
-@pytest.mark.parametrize("N,T,F,H,L,p", [(100, 60, 3, 64, 2, 0.2), (100, 60, 5, 64, 4, 0.2), (37, 9, 3, 32, 3, 0.0),
-                                         (100, 60, 3, 16, 1, 0.0), (200, 33, 3, 64, 4, 0.3),
-                                         (100, 20, 3, 64, 8, 0.2)])
-def test_projection_workgroups_bit_identical(N, T, F, H, L, p, monkeypatch):
-    """Projection mode (gx_t and the dropout masks computed on their own workgroups, handed to the recurrent
-    workgroups through HBM/L2) is the same arithmetic as the in-workgroup input waves: outputs and gradients
-    match bit for bit, and the forward's keep bytes are what the backward reads."""
-    from masters_thesis_amd.ops import lstm as op
-
-    torch.manual_seed(4)
-    x = torch.randn(N, T, F, device=DEV)
-    ws = [w.to(DEV) for w in _weights(F, H, L, seed=9)]
-    R = torch.randn(N, H, device=DEV)
-    monkeypatch.setenv("MTA_LSTM_PROJ", "1")
-    assert op.projection_mode(op.padded_rows(N), L)
-    outs = []
-    for proj in ("1", "0"):
-        monkeypatch.setenv("MTA_LSTM_PROJ", proj)
-        wg = [w.clone().requires_grad_(True) for w in ws]
-        op.set_deterministic(True)
-        try:
-            seeds = torch.full((8,), 12345, dtype=torch.int64, device=DEV)
-            out = op.lstm_last_hidden(x, wg, L, p, True, "high", seeds=seeds)
-            (out * R).sum().backward()
-        finally:
-            op.set_deterministic(False)
-        torch.cuda.synchronize()
-        outs.append((out.detach().clone(), [w.grad.clone() for w in wg]))
-    op.check_pipeline_health()
-    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=0, atol=0)
-    for a, b in zip(outs[0][1], outs[1][1]):
-        torch.testing.assert_close(a, b, rtol=0, atol=0)
