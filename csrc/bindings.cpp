@@ -58,7 +58,10 @@ void mta_scale(float* x, long n, float s, hipStream_t st);
 int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb, float alpha,
                   int flags, const float* bias, const float* resid, const void* aux_in, const uint64_t* seed,
                   float drop_p, void* out_bf16, float* out_f32, void* aux_pre, int ldc, int n_store, int ksplit,
-                  float* bias_grad, hipStream_t st);
+                  float* bias_grad, int defer, hipStream_t st);
+void mta_gemm_flush();
+void mta_norm_flush();
+void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
                  const int* rows_p, const int* cols_p, const int* ld_src, hipStream_t st);
 int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
@@ -470,7 +473,7 @@ void check_span(const at::Tensor& t, int64_t rows, int64_t ld, int64_t cols, con
 void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                double alpha, int64_t flags, const OptT& bias, const OptT& resid, const OptT& aux_in, const OptT& seed,
                double drop_p, const OptT& out_bf16, const OptT& out_f32, const OptT& aux_pre, int64_t ldc,
-               int64_t n_store, int64_t ksplit, const OptT& bias_grad) {
+               int64_t n_store, int64_t ksplit, const OptT& bias_grad, bool defer) {
   const int64_t NS = (n_store <= 0 || n_store > N) ? N : n_store;
   MTA_CHECK_GPU(A, at::kBFloat16);
   MTA_CHECK_GPU(B, at::kBFloat16);
@@ -501,7 +504,7 @@ void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, i
                                (float)drop_p, opt_typed<void>(out_bf16, at::kBFloat16, "out_bf16"),
                                opt_typed<float>(out_f32, at::kFloat, "out_f32"),
                                opt_typed<void>(aux_pre, at::kBFloat16, "aux_pre"), (int)ldc, (int)NS, (int)ksplit,
-                               opt_typed<float>(bias_grad, at::kFloat, "bias_grad"), cur_stream());
+                               opt_typed<float>(bias_grad, at::kFloat, "bias_grad"), defer ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "gemm_bf16: unsupported arguments (rc=", rc, ", M=", M, " N=", N, " K=", K, ")");
 }
 
@@ -930,6 +933,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_flag_words", &lstm_stack_flag_words);
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
+  m.def("gemm_flush", []() { mta_gemm_flush(); });
+  m.def("norm_defer", []() { mta_norm_defer(); });
+  m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad);
   m.def("norm", &norm);
   m.def("attention", &attention);

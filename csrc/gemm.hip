@@ -62,7 +62,8 @@ union Bf8 {
 };
 
 template <int BM, int BN, int BKT, bool AT, bool BT>
-__global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
+__device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const int by, const int bz, const int gz,
+                                          __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
   constexpr int RST = BKT + 8;  // LDS row stride (bf16): BKT + 8 pad (16 B): conflict-free b128 rows
   constexpr int WM = BM / 2, WN = BN / 2, MT = WM / 16, NT = WN / 16;
   // staging work items: non-transposed = 16-B chunks (row, 8 k); transposed = 8x8 blocks (8 k-rows x 8 cols)
@@ -73,13 +74,10 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   constexpr int A_REGS = AT ? 8 : 1;  // 16-B loads per item
   constexpr int B_REGS = BT ? 8 : 1;
 
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * RST];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * RST];
-
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
-  const int kbeg = blockIdx.z * g.k_per_split;
+  const int n0 = bx * BN, m0 = by * BM;
+  const int kbeg = bz * g.k_per_split;
   const int kend = min(g.K, kbeg + g.k_per_split);
   if (kbeg >= kend) return;
 
@@ -191,7 +189,7 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   float rowsum[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) rowsum[i] = 0.f;
-  const bool want_rowsum = g.bias_grad != nullptr && blockIdx.x == 0 && wn == 0;
+  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
 
   load(kbeg);
   for (int k0 = kbeg; k0 < kend; k0 += BKT) {
@@ -221,7 +219,7 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
   }
 
   // ---- epilogue ----
-  const bool split = gridDim.z > 1;
+  const bool split = gz > 1;
   // operands the epilogue reads (residual stream, GELU input of a DGELU) are fetched for the whole tile first:
   // interleaved with the output stores the compiler must keep each load behind the previous (possibly
   // aliasing) store, i.e. one dependent global round trip per element (r2 trace: 13 us per residual GEMM)
@@ -283,9 +281,63 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
 }
 
 template <int BM, int BN, int BKT, bool AT, bool BT>
+__global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * (BKT + 8)];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * (BKT + 8)];
+  gemm_body<BM, BN, BKT, AT, BT>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, As, Bs);
+}
+
+// Two independent GEMMs of one tile configuration in ONE launch (the backward's weight gradient and input
+// gradient of a Linear read the same dY): one launch gap instead of two, and both grids fill the chip together.
+// Blocks [0, n1) are problem 1 (x fastest, as a 3-D grid would be dispatched), [n1, n1 + n2) problem 2.
+struct PairGrid {
+  int nx1, ny1, nz1, nx2, ny2, nz2;
+};
+template <int BM, int BN, int BKT, bool AT1, bool BT1, bool AT2, bool BT2>
+__global__ __launch_bounds__(GT) void gemm_bf16_pair_kernel(GemmArgs g1, GemmArgs g2, PairGrid pg) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[BM * (BKT + 8)];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * (BKT + 8)];
+  const int n1 = pg.nx1 * pg.ny1 * pg.nz1;
+  int b = blockIdx.x;
+  if (b < n1) {
+    gemm_body<BM, BN, BKT, AT1, BT1>(g1, b % pg.nx1, (b / pg.nx1) % pg.ny1, b / (pg.nx1 * pg.ny1), pg.nz1, As, Bs);
+  } else {
+    b -= n1;
+    gemm_body<BM, BN, BKT, AT2, BT2>(g2, b % pg.nx2, (b / pg.nx2) % pg.ny2, b / (pg.nx2 * pg.ny2), pg.nz2, As, Bs);
+  }
+}
+
+template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ksplit);
   gemm_bf16_kernel<BM, BN, BKT, AT, BT><<<grid, GT, 0, st>>>(g);
+}
+
+// tile configuration of a problem: 0 = 128x128x64, 1 = 128x128x32, 2 = 64x64x128, 3 = 64x64x32
+inline int tile_config(const GemmArgs& g, int ksplit) {
+  const long tiles128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * ksplit;
+  const bool deep = g.k_per_split >= 128;
+  return tiles128 >= 256 ? (deep ? 0 : 1) : (deep ? 2 : 3);
+}
+
+template <int BM, int BN, int BKT>
+void launch_pair_cfg(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
+  PairGrid pg{(g1.N + BN - 1) / BN, (g1.M + BM - 1) / BM, k1, (g2.N + BN - 1) / BN, (g2.M + BM - 1) / BM, k2};
+  const int blocks = pg.nx1 * pg.ny1 * pg.nz1 + pg.nx2 * pg.ny2 * pg.nz2;
+  gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
+}
+
+// (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately
+bool launch_pair(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
+  const int c = tile_config(g1, k1);
+  if (c != tile_config(g2, k2)) return false;
+  switch (c) {
+    case 0: launch_pair_cfg<128, 128, 64>(g1, k1, g2, k2, st); break;
+    case 1: launch_pair_cfg<128, 128, 32>(g1, k1, g2, k2, st); break;
+    case 2: launch_pair_cfg<64, 64, 128>(g1, k1, g2, k2, st); break;
+    default: launch_pair_cfg<64, 64, 32>(g1, k1, g2, k2, st); break;
+  }
+  return true;
 }
 
 template <bool AT, bool BT>
@@ -304,13 +356,37 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   }
 }
 
+void dispatch_mode(int mode, const GemmArgs& g, int ksplit, hipStream_t st) {
+  if (mode == 0) dispatch<false, false>(g, ksplit, st);
+  else if (mode == 1) dispatch<false, true>(g, ksplit, st);
+  else dispatch<true, true>(g, ksplit, st);
+}
+
+// one deferred weight-gradient GEMM waiting for its input-gradient partner (stream-ordered, single-threaded use)
+struct Pending {
+  bool on = false;
+  GemmArgs g;
+  int ksplit;
+  hipStream_t st;
+} pending;
+
 }  // namespace
 
+// launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
+extern "C" void mta_gemm_flush() {
+  if (pending.on) {
+    pending.on = false;
+    dispatch_mode(2, pending.g, pending.ksplit, pending.st);
+  }
+}
+
+namespace {
+
 // mode: 0 = NN-linear forward (AT=0,BT=0), 1 = input grad (AT=0,BT=1), 2 = weight grad (AT=1,BT=1)
-extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb,
-                             float alpha, int flags, const float* bias, const float* resid, const void* aux_in,
-                             const uint64_t* seed, float drop_p, void* out_bf16, float* out_f32, void* aux_pre,
-                             int ldc, int n_store, int ksplit, float* bias_grad, hipStream_t st) {
+int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb,
+                   float alpha, int flags, const float* bias, const float* resid, const void* aux_in,
+                   const uint64_t* seed, float drop_p, void* out_bf16, float* out_f32, void* aux_pre,
+                   int ldc, int n_store, int ksplit, float* bias_grad, int defer, hipStream_t st) {
   if (n_store <= 0 || n_store > N) n_store = N;
   if (M % 8 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc < n_store) return 1;
   if ((flags & EPI_ACCUM) == 0 && ksplit > 1) return 2;
@@ -344,9 +420,35 @@ extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int 
   ksplit = (K + kps - 1) / kps;
   g.k_per_split = kps;
   g.bias_grad = bias_grad;
-  if (mode == 0) dispatch<false, false>(g, ksplit, st);
-  else if (mode == 1) dispatch<false, true>(g, ksplit, st);
-  else if (mode == 2) dispatch<true, true>(g, ksplit, st);
-  else return 4;
+  if (mode < 0 || mode > 2) return 4;
+  if (defer) {
+    // a weight-gradient GEMM held back for the next call (its input-gradient partner): one paired launch
+    if (mode != 2) return 8;
+    mta_gemm_flush();
+    pending.on = true;
+    pending.g = g;
+    pending.ksplit = ksplit;
+    pending.st = st;
+    return 0;
+  }
+  if (pending.on) {
+    pending.on = false;
+    if (!(mode == 1 && pending.st == st && launch_pair(pending.g, pending.ksplit, g, ksplit, st))) {
+      dispatch_mode(2, pending.g, pending.ksplit, pending.st);
+      dispatch_mode(mode, g, ksplit, st);
+    }
+    return 0;
+  }
+  dispatch_mode(mode, g, ksplit, st);
   return 0;
+}
+
+}  // namespace
+
+extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb,
+                             float alpha, int flags, const float* bias, const float* resid, const void* aux_in,
+                             const uint64_t* seed, float drop_p, void* out_bf16, float* out_f32, void* aux_pre,
+                             int ldc, int n_store, int ksplit, float* bias_grad, int defer, hipStream_t st) {
+  return gemm_bf16_impl(mode, A, B, M, N, K, lda, ldb, alpha, flags, bias, resid, aux_in, seed, drop_p, out_bf16,
+                        out_f32, aux_pre, ldc, n_store, ksplit, bias_grad, defer, st);
 }

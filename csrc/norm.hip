@@ -56,6 +56,9 @@ struct NormArgs {
   float* dx_f32;        // [M][ldx]
   float* dgamma;
   float* dbeta;
+  float* part;          // per-block partial rows of dgamma / dbeta: [2][blocks][part_ld]
+  int part_ld;
+  long part_pass;       // floats between the dgamma and dbeta planes
 };
 
 template <int VPL>
@@ -112,6 +115,10 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
 constexpr int NORM_BWD_MAX_BLOCKS = 512;
 // per-block column partials of dgamma / dbeta (static: no allocation, graph-capture safe; stream-ordered use)
 __device__ float mta_norm_part[2][NORM_BWD_MAX_BLOCKS][2048];
+// deferred reductions (D <= NORM_DEFER_D): each backward call gets its own slot and ONE batched launch sums every
+// pending slot at the end of the encoder backward (9 launches -> 1 for the 4-layer transformer)
+constexpr int NORM_DEFER_SLOTS = 12, NORM_DEFER_D = 256;
+__device__ float mta_norm_part_slots[NORM_DEFER_SLOTS][2][NORM_BWD_MAX_BLOCKS][NORM_DEFER_D];
 
 template <int VPL>
 __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
       for (int j = 0; j < 4; ++j) red[wave][4 * (lane + 64 * i) + j] = pass == 0 ? dg[i][j] : db[i][j];
     __syncthreads();
     for (int c = threadIdx.x; c < a.D; c += NT_THREADS)
-      mta_norm_part[pass][blockIdx.x][c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+      a.part[pass * a.part_pass + (long)blockIdx.x * a.part_ld + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
   }
 }
 
@@ -216,6 +223,40 @@ __global__ void norm_param_reduce_kernel(float* __restrict__ dgamma, float* __re
   s = wave_sum_dpp(s);
   if (lane == 0) dst[col] += s;
 }
+
+struct ReduceJob {
+  const float* part;
+  float* dgamma;
+  float* dbeta;
+  int D, blocks, ld;
+  long pass;
+};
+struct ReduceBatch {
+  ReduceJob job[NORM_DEFER_SLOTS];
+};
+
+// the same fixed-order column sums as norm_param_reduce_kernel, for every pending job (blockIdx.y)
+__global__ void norm_param_reduce_batch_kernel(ReduceBatch b) {
+  const ReduceJob& j = b.job[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (c >= 2 * j.D) return;
+  const int pass = c / j.D, col = c % j.D;
+  float* dst = pass == 0 ? j.dgamma : j.dbeta;
+  if (!dst) return;
+  float s = 0.f;
+  for (int r = lane; r < j.blocks; r += 64) s += j.part[pass * j.pass + (long)r * j.ld + col];
+  s = wave_sum_dpp(s);
+  if (lane == 0) dst[col] += s;
+}
+
+bool defer_next = false;
+
+struct DeferState {
+  int n = 0;
+  ReduceBatch batch;
+  hipStream_t st = nullptr;
+} deferred;
 
 int norm_blocks(int M, bool bwd) {
   const int rows_per_block = 4;
@@ -242,6 +283,15 @@ extern "C" int mta_cast_pad(int n, const float* const* src, void* const* dst, co
   bx = bx > 2048 ? 2048 : (bx < 1 ? 1 : bx);
   cast_pad_kernel<<<dim3(bx, n), 256, 0, st>>>(a);
   return 0;
+}
+
+// launch every deferred parameter reduction (one launch)
+extern "C" void mta_norm_flush() {
+  if (deferred.n == 0) return;
+  int maxD = 0;
+  for (int i = 0; i < deferred.n; ++i) maxD = deferred.batch.job[i].D > maxD ? deferred.batch.job[i].D : maxD;
+  norm_param_reduce_batch_kernel<<<dim3((2 * maxD + 3) / 4, deferred.n), 256, 0, deferred.st>>>(deferred.batch);
+  deferred.n = 0;
 }
 
 extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
@@ -273,6 +323,32 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
   a.dbeta = dbeta;
   const int vpl = (D + 255) / 256;
   const int blocks = norm_blocks(M, bwd != 0);
+  // deferred slot when the caller asked for it (dgamma pointer tagged by mta_norm_defer) and D fits
+  const bool defer = bwd && (dgamma || dbeta) && defer_next && D <= NORM_DEFER_D;
+  defer_next = false;
+  if (defer) {
+    if (deferred.n == NORM_DEFER_SLOTS || (deferred.n && deferred.st != st)) mta_norm_flush();
+    static float* base = [] {
+      float* p = nullptr;
+      (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_part_slots));
+      return p;
+    }();
+    a.part = base + (long)deferred.n * 2 * NORM_BWD_MAX_BLOCKS * NORM_DEFER_D;
+    a.part_ld = NORM_DEFER_D;
+    a.part_pass = (long)NORM_BWD_MAX_BLOCKS * NORM_DEFER_D;
+    deferred.batch.job[deferred.n] = ReduceJob{a.part, dgamma, dbeta, D, blocks, a.part_ld, a.part_pass};
+    deferred.st = st;
+    ++deferred.n;
+  } else {
+    static float* base = [] {
+      float* p = nullptr;
+      (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_part));
+      return p;
+    }();
+    a.part = base;
+    a.part_ld = 2048;
+    a.part_pass = (long)NORM_BWD_MAX_BLOCKS * 2048;
+  }
 #define MTA_NORM_LAUNCH(V)                                                      \
   if (bwd) norm_bwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);                \
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
@@ -286,7 +362,10 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
     MTA_NORM_LAUNCH(8)
   }
 #undef MTA_NORM_LAUNCH
-  if (bwd && (dgamma || dbeta))
+  if (bwd && (dgamma || dbeta) && !defer)
     norm_param_reduce_kernel<<<(2 * D + 3) / 4, 256, 0, st>>>(dgamma, dbeta, D, blocks);
   return 0;
 }
+
+// the next mta_norm backward call defers its parameter reduction to mta_norm_flush
+extern "C" void mta_norm_defer() { defer_next = true; }

@@ -53,9 +53,16 @@ def _r16(n: int) -> int:
 def gemm(mode: int, A: Tensor, B: Tensor, M: int, N: int, K: int, lda: int, ldb: int, *, flags: int = 0,
          alpha: float = 1.0, bias=None, resid=None, aux_in=None, seed=None, drop_p: float = 0.0, out_bf16=None,
          out_f32=None, aux_pre=None, ldc: Optional[int] = None, n_store: int = 0, ksplit: int = 1,
-         bias_grad=None) -> None:
+         bias_grad=None, defer: bool = False) -> None:
+    """``defer`` (weight-gradient GEMMs): hold the launch back and run it together with the NEXT gemm call (its
+    input-gradient partner, which reads the same dY) as one paired launch (csrc/gemm.hip); ``gemm_flush()``
+    launches a held-back GEMM alone."""
     lib().gemm_bf16(mode, A, B, M, N, K, lda, ldb, alpha, flags, bias, resid, aux_in, seed, drop_p, out_bf16,
-                    out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad)
+                    out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad, bool(defer))
+
+
+def gemm_flush() -> None:
+    lib().gemm_flush()
 
 
 _DETERMINISTIC = [False]
@@ -188,10 +195,12 @@ class _MlpEncoderFn(torch.autograd.Function):
                        _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]))
             # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre)
             gemm(2, dpre, Xs[i], D, kp[i], Mp, D, kp[i], flags=EPI_ACCUM, out_f32=_grad_view(params[per * i]),
-                 ldc=Din, n_store=Din, ksplit=wgrad_split(D, kp[i], Mp), bias_grad=_grad_view(params[per * i + 1]))
+                 ldc=Din, n_store=Din, ksplit=wgrad_split(D, kp[i], Mp), bias_grad=_grad_view(params[per * i + 1]),
+                 defer=i > 0)  # paired with the input-gradient GEMM below (same dPre)
             if i > 0:
                 dy = torch.empty((Mp, Din), device=dev, dtype=torch.float32)
                 gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], out_f32=dy)
+        gemm_flush()
         return (None,) * (7 + len(params))
 
 
@@ -346,6 +355,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
         dhp = torch.zeros((Np, d), device=dev, dtype=torch.float32)
         dhp[:N].copy_(dh)
         gf = params[2 + nb * L]
+        C.norm_defer()
         C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, Np, d, True, RMS_EPS, gf, None, None, None, None,
                stats[-1], None, 0.0, dhp, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
         dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
@@ -359,24 +369,25 @@ class _TransformerEncoderFn(torch.autograd.Function):
             r1, lse, r2 = stats[3 * l: 3 * l + 3]
             # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
             gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                 ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2))
+                 ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)
             dpre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
             fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
             gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1, seed=ctx.seeds[l:l + 1] if drop else None,
                  drop_p=p, out_bf16=dpre1)
             # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
             gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                 ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+                 ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), defer=True)
             dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
             gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
             # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
             dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            C.norm_defer()  # dgamma: one batched reduction launch at the end of the backward
             C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None, dX1b,
                    dX1, _grad_view(g2), None)
             # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
             gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
-                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo))
+                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), defer=True)
             do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
             # attention backward (RoPE inverse fused) -> dqkv
@@ -384,17 +395,20 @@ class _TransformerEncoderFn(torch.autograd.Function):
             C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
             # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
             gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
-                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv))
+                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), defer=True)
             dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
             gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
             # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
             dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
+            C.norm_defer()
             C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None, dXb,
                    dXn, _grad_view(g1), None)
             dX = dXn
         # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
         gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,
              ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]))
+        gemm_flush()
+        C.norm_flush()
         return (None,) * (7 + len(params))
 
 

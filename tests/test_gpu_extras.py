@@ -224,3 +224,32 @@ def test_extras_train_through_trainer_graph(arch):
     torch.cuda.synchronize()
     assert torch.isfinite(tr.flat.data).all() and torch.isfinite(loss).all()
     assert tr._graphs  # the step was captured and replayed
+
+
+@pytest.mark.parametrize("M,D,Din", [(6720, 128, 512), (6720, 384, 128), (300, 64, 72)])
+def test_paired_weight_and_input_grad_gemms(M, D, Din):
+    """A deferred weight-gradient GEMM runs together with the next (input-gradient) GEMM in one paired launch:
+    same results as two launches (split-K sums compared with a tolerance, the input gradient exactly)."""
+    from masters_thesis_amd.ops import extras as X
+
+    g = torch.Generator().manual_seed(M + D)
+    dY = _bf(torch.randn(M, D, generator=g))
+    Xa = _bf(torch.randn(M, Din, generator=g))
+    W = _bf(torch.randn(D, Din, generator=g) * 0.1)
+    outs = []
+    for defer in (False, True):
+        gw = torch.zeros(D, Din, device=DEV)
+        gb = torch.zeros(D, device=DEV)
+        dx = torch.empty(M, Din, device=DEV)
+        X.gemm(2, dY, Xa, D, Din, M, D, Din, flags=X.EPI_ACCUM, out_f32=gw, ldc=Din,
+               ksplit=X.wgrad_split(D, Din, M), bias_grad=gb, defer=defer)
+        X.gemm(1, dY, W, M, Din, D, D, Din, out_f32=dx)
+        X.gemm_flush()
+        torch.cuda.synchronize()
+        outs.append((gw, gb, dx))
+    (gw0, gb0, dx0), (gw1, gb1, dx1) = outs
+    torch.testing.assert_close(dx1, dx0, rtol=0, atol=0)
+    torch.testing.assert_close(gw1, gw0, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(gb1, gb0, rtol=1e-5, atol=1e-3)
+    ref = dY.double().t() @ Xa.double()
+    assert _rel(gw1, ref) < 1e-5
