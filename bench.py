@@ -63,6 +63,8 @@ def parse_args(argv=None):
     ap.add_argument("--steps-per-graph", type=int, default=None,
                     help="training steps captured per graph (default: the trainer config's steps_per_graph)")
     ap.add_argument("--n-samples", type=int, default=1_000_000, help="synthetic DGP days (reference: 1e6)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra config override (repeatable), e.g. --set model.dropout=0")
     ap.add_argument("--residency", default="device", choices=["device", "stream"],
                     help="device: split resident in HBM; stream: pinned host ring + side-stream H2D per step")
     return ap.parse_args(argv)
@@ -86,7 +88,7 @@ def main(argv=None):
     cfg, _, _ = compose(REPO / "configs", "config", [
         f"model={args.model}", f"loss={args.loss}", f"trainer={args.trainer}",
         f"datamodule.batch_size={args.batch}", f"datamodule.n_samples={args.n_samples}",
-        f"datamodule.residency={args.residency}"])
+        f"datamodule.residency={args.residency}", *args.set])
     if args.backend == "torch":
         cfg.model["backend"] = "torch"
     t_data = time.perf_counter()

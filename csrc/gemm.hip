@@ -55,6 +55,21 @@ __device__ __forceinline__ uint4 and_mask(uint4 v, bool keep) {
   return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
 }
 
+// GEMM-epilogue dropout (forward GELU epilogue and backward DGELU epilogue draw the same mask): one lowbias32 hash
+// per PAIR of rows (a lane's 4 accumulator rows are 2 pairs), 16-bit uniform per element, p resolved to 1/65536:
+// 2 multiplies per pair + 2 for the inputs instead of mta_hash3's 8 per element (the hash was ~30 us of the
+// transformer step, r2 trace with / without dropout)
+__device__ __forceinline__ uint32_t gemm_pair_hash(uint32_t s, uint32_t mpair, uint32_t n) {
+  const uint32_t b = n * 0x85EBCA77u;
+  uint32_t x = s ^ (mpair * 0x9E3779B1u) ^ ((b << 13) | (b >> 19));
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
 union Bf8 {
   bf16x8 v;
   uint4 u;
@@ -241,11 +256,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
         }
       }
   }
+  uint32_t dseed = 0, dthr = 0;
+  float dscale = 0.f;
+  if (g.flags & EPI_DROPOUT) {
+    const uint64_t sd = *g.seed;
+    dseed = (uint32_t)(sd ^ (sd >> 32));
+    dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
+    dscale = 1.0f / (1.0f - g.drop_p);
+  }
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const int n = n0 + wn * WN + 16 * j + (lane & 15);
+      uint32_t hp[2] = {0u, 0u};
+      if (g.flags & EPI_DROPOUT) {
+        const uint32_t mp = (uint32_t)(m0 + wm * WM + 16 * i + 4 * (lane >> 4)) >> 1;
+        hp[0] = gemm_pair_hash(dseed, mp, (uint32_t)n);
+        hp[1] = gemm_pair_hash(dseed, mp + 1, (uint32_t)n);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
@@ -260,7 +289,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
         if (g.flags & EPI_BIAS) v += g.bias[n];
         if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
         if (g.flags & EPI_GELU) v = mta_gelu(v);
-        if (g.flags & EPI_DROPOUT) v *= mta_dropout_scale(*g.seed, (uint32_t)m, (uint32_t)n, g.drop_p);
+        if (g.flags & EPI_DROPOUT) {
+          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+          v *= u16 >= dthr ? dscale : 0.f;
+        }
         if (g.flags & EPI_DGELU) v *= mta_gelu_grad(pre_in[i][j][r]);
         if (g.flags & EPI_RESID) v += pre_in[i][j][r];
         if (g.out_f32) g.out_f32[o] = v;

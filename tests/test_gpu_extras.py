@@ -226,7 +226,7 @@ def test_extras_train_through_trainer_graph(arch):
     assert tr._graphs  # the step was captured and replayed
 
 
-@pytest.mark.parametrize("M,D,Din", [(6720, 128, 512), (6720, 384, 128), (300, 64, 72)])
+@pytest.mark.parametrize("M,D,Din", [(6720, 128, 512), (6720, 384, 128), (304, 64, 72)])
 def test_paired_weight_and_input_grad_gemms(M, D, Din):
     """A deferred weight-gradient GEMM runs together with the next (input-gradient) GEMM in one paired launch:
     same results as two launches (split-K sums compared with a tolerance, the input gradient exactly)."""
@@ -253,3 +253,32 @@ def test_paired_weight_and_input_grad_gemms(M, D, Din):
     torch.testing.assert_close(gb1, gb0, rtol=1e-5, atol=1e-3)
     ref = dY.double().t() @ Xa.double()
     assert _rel(gw1, ref) < 1e-5
+
+
+def test_gemm_dropout_mask_forward_backward_consistent():
+    """The GEMM-epilogue dropout (pair hash, 16-bit uniform) keeps 1-p of the elements and the backward DGELU
+    epilogue zeroes exactly the elements the forward GELU epilogue dropped (same seed, same (row, col))."""
+    from masters_thesis_amd.ops import extras as X
+
+    M, N, K, p = 1024, 256, 64, 0.1
+    g = torch.Generator().manual_seed(1)
+    A = _bf(torch.randn(M, K, generator=g))
+    W = _bf(torch.randn(N, K, generator=g) * 0.2)
+    bias = torch.full((N,), 3.0, device=DEV)  # GELU(v) > 0 everywhere: zeros come from the mask only
+    seed = torch.tensor([0x1234_5678_9ABC], dtype=torch.int64, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    X.gemm(0, A, W, M, N, K, K, K, flags=X.EPI_BIAS | X.EPI_GELU | X.EPI_DROPOUT, bias=bias, seed=seed, drop_p=p,
+           out_bf16=out, aux_pre=pre)
+    # backward: dPre = (dOut W2 ...) here dOut = ones via A2 = identity-like product of ones
+    ones_a = _bf(torch.ones(M, 8))
+    ones_b = _bf(torch.ones(8, N) / 8)  # [K][N] layout of mode 1: dY (M x 8) . B (8 x N) = ones
+    dpre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    X.gemm(1, ones_a, ones_b, M, N, 8, 8, N, flags=X.EPI_DGELU | X.EPI_DROPOUT, aux_in=pre, seed=seed, drop_p=p,
+           out_bf16=dpre)
+    torch.cuda.synchronize()
+    kept_f = out.float() != 0
+    kept_b = dpre.float() != 0
+    assert torch.equal(kept_f, kept_b)
+    frac = kept_f.float().mean().item()
+    assert abs(frac - (1 - p)) < 0.01, frac
