@@ -89,7 +89,11 @@ class XgmiAllReduce:
 
     # ------------------------------------------------------------------ construction + self-check
     @classmethod
-    def create(cls, numel: int, device: torch.device, group=None, max_mb: float = 64.0) -> Optional["XgmiAllReduce"]:
+    def create(cls, numel: int, device: torch.device, group=None,
+               max_mb: float = float(os.environ.get("MTA_XGMI_MAX_MB", "4"))) -> Optional["XgmiAllReduce"]:
+        # one-shot pushes the whole bucket over every link (N-1 copies out per rank): latency-optimal for the LSTM
+        # (204 KB) and transformer (3.2 MB) buckets; above a few MB RCCL's ring / two-shot moves ~2x less per link
+        # (mlp_large's 52 MB bucket: ~1 ms one-shot vs ~0.25 ms ring at ~50 GB/s per xGMI link)
         """The xGMI all-reduce for this group, or None (with the reason printed once on rank 0) when the
         configuration does not allow it or its self-check against the group's all-reduce fails."""
         mode = os.environ.get("MTA_ALLREDUCE", "auto").lower()
