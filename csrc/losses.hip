@@ -745,6 +745,199 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
 // small problems (the reference config: N = 100, H = 64) stay in the single fused workgroup
 inline bool heads_big(int N, int H) { return (long)N * H > 32768 && H % 4 == 0; }
 
+// ---- grid-parallel losses for large N (B = 64 windows = 6,400 sequences): ----
+// decoder_losses_kernel is ONE workgroup whose 16 waves walk the sequences with a dependent y load per
+// iteration, three passes: 316 us per call for mlp_large B=64 (r2 trace) - 11 % of that step.  Here:
+//   L1 (windows x J blocks): per-sequence MSE gradient, block partials of sse / sae / sum w b^2 / sum log w /
+//       sum w D^2 and of u_t (lane t owns day t: n <= 64) -> partial row P[w][j]
+//   L2 (windows blocks): fixed-order sum of a window's J partial rows -> den, U1, U2, u_t, the window's NLL
+//   L3 (sequence blocks): per-sequence NLL gradient; block 0 adds the window NLLs and the sse / sae partials
+//       (fixed order) into the four loss scalars and the epoch metric accumulator
+// Every sum has a fixed order (no float atomics): bit-reproducible like the single-workgroup kernel.
+constexpr int LG_SEQ = 16;           // sequences per L1 block (4 per wave)
+constexpr int LG_MAXJ = 256;         // partial rows per window
+constexpr int LG_MAXP = 16384;       // partial rows in total
+constexpr int LG_MAXW = 4096;        // windows
+struct LgPart {
+  double s[5];   // sse, sae, sum w b^2, sum log w, sum w D^2
+  double pad[3];
+  float ut[64];
+};
+struct LgWin {
+  double nll;
+  float den, u1, u2, pad;
+  float ut[64];
+};
+__device__ LgPart mta_lg_part[LG_MAXP];
+__device__ LgWin mta_lg_win[LG_MAXW];
+
+inline bool losses_grid_ok(const LossArgs& A) {
+  if (getenv("MTA_LOSSES_SINGLE")) return false;
+  const int J = A.kwin <= 0 ? 0 : min(LG_MAXJ, (A.kwin + LG_SEQ - 1) / LG_SEQ);
+  return A.N >= 1024 && A.n <= 64 && A.n >= 1 && A.windows <= LG_MAXW && (long)A.windows * A.kwin == A.N &&
+         (long)A.windows * J <= LG_MAXP;
+}
+
+__global__ __launch_bounds__(256) void losses_grid_part_kernel(const float* __restrict__ ab, LossArgs A, int J, int S) {
+  __shared__ double red[4][5];
+  __shared__ float utp[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wdw = blockIdx.y, j = blockIdx.x;
+  const int n = A.n, C = A.C;
+  const float inv_cnt = 1.0f / ((float)A.N * (float)n);
+  const float fm = A.want_nll ? A.factor[wdw * A.factor_stride] : 0.f;
+  const int k0 = j * S, k1 = min(A.kwin, k0 + S);
+  double sse = 0.0, sae = 0.0, wbb = 0.0, logw = 0.0, wdd = 0.0;
+  float ut = 0.f;
+  const bool tl = lane < n;
+  for (int k = k0 + wave; k < k1; k += 4) {
+    const int i = wdw * A.kwin + k;
+    const float a = ab[2 * i], b = ab[2 * i + 1];
+    const float* yi = A.y + (size_t)i * n * C;
+    const float r = tl ? yi[lane * C] : 0.f, rm = tl ? yi[lane * C + 1] : 0.f;
+    const float e = tl ? fmaf(b, rm, a) - r : 0.f;
+    const float se = wave_sum_dpp(e);
+    const float serm = wave_sum_dpp(e * rm);
+    const float ss = wave_sum_dpp(e * e);
+    const float sa = wave_sum_dpp(fabsf(e));
+    if (lane == 0) {
+      A.gmse[2 * i] = 2.f * se * inv_cnt;
+      A.gmse[2 * i + 1] = 2.f * serm * inv_cnt;
+    }
+    sse += (double)ss;
+    sae += (double)sa;
+    if (A.want_nll) {
+      const float w = A.inv_psi[i];
+      const float mu = fmaf(b, fm, a), wb = w * b;
+      const float D = tl ? r - mu : 0.f;
+      const float sdd = wave_sum_dpp(D * D);
+      ut = fmaf(wb, D, ut);
+      wbb += (double)wb * b;
+      logw += (double)logf(w);
+      wdd += (double)w * sdd;
+    }
+  }
+  if (lane == 0) {
+    red[wave][0] = sse;
+    red[wave][1] = sae;
+    red[wave][2] = wbb;
+    red[wave][3] = logw;
+    red[wave][4] = wdd;
+  }
+  utp[wave][lane] = ut;
+  __syncthreads();
+  LgPart* P = mta_lg_part + (long)wdw * J + j;
+  if (wave == 0) {
+    P->ut[lane] = (utp[0][lane] + utp[1][lane]) + (utp[2][lane] + utp[3][lane]);
+    if (lane < 5) P->s[lane] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  }
+}
+
+__global__ __launch_bounds__(64) void losses_grid_window_kernel(LossArgs A, int J) {
+  const int lane = threadIdx.x, wdw = blockIdx.x, n = A.n;
+  const LgPart* P = mta_lg_part + (long)wdw * J;
+  float ut = 0.f;
+  for (int j = 0; j < J; ++j) ut += P[j].ut[lane];  // lane t = day t, rows in order
+  double s[3] = {0.0, 0.0, 0.0};                   // wbb, logw, wdd: lane-strided rows, then a fixed-order tree
+  for (int j = lane; j < J; j += 64)
+    for (int m = 0; m < 3; ++m) s[m] += P[j].s[2 + m];
+  for (int m = 0; m < 3; ++m) s[m] = wave_sum_dpp(s[m]);
+  const float utl = lane < n ? ut : 0.f;
+  const double u1 = wave_sum_dpp((double)utl), u2 = wave_sum_dpp((double)utl * utl);
+  LgWin* W = mta_lg_win + wdw;
+  W->ut[lane] = utl;
+  if (lane == 0) {
+    const double fv = A.factor[wdw * A.factor_stride + 1];
+    const double den = 1.0 / fv + s[0];
+    const double logdet = s[1] - log(fv * den);
+    const double quad = s[2] - u2 / den;
+    W->nll = 0.5 * ((double)n * ((double)A.kwin * LOG2PI - logdet) + quad);
+    W->den = (float)den;
+    W->u1 = (float)u1;
+    W->u2 = (float)u2;
+  }
+}
+
+__global__ __launch_bounds__(256) void losses_grid_grad_kernel(const float* __restrict__ ab, LossArgs A, int J,
+                                                               int nparts) {
+  __shared__ double red[4][3];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n = A.n, C = A.C;
+  if (A.want_nll) {
+    const int i = blockIdx.x * 4 + wave;
+    if (i < A.N) {
+      const int wdw = i / A.kwin;
+      const LgWin* W = mta_lg_win + wdw;
+      const float fm = A.factor[wdw * A.factor_stride];
+      const float a = ab[2 * i], b = ab[2 * i + 1], w = A.inv_psi[i];
+      const float mu = fmaf(b, fm, a);
+      const bool tl = lane < n;
+      const float D = tl ? A.y[(size_t)i * n * C + lane * C] - mu : 0.f;
+      const float sd = wave_sum_dpp(D);
+      const float ud = wave_sum_dpp(tl ? W->ut[lane] * D : 0.f);
+      if (lane == 0) {
+        const float fden = W->den, fU1 = W->u1, fU2 = W->u2, wb = w * b;
+        A.gnll[2 * i] = -w * sd + wb * fU1 / fden;
+        A.gnll[2 * i + 1] = (float)n * wb / fden - fm * (w * sd - wb * fU1 / fden) - w * ud / fden +
+                            fU2 * wb / (fden * fden);
+      }
+    }
+  }
+  if (blockIdx.x != 0) return;
+  // scalars: lane-strided partial rows / windows per wave, fixed-order wave and block sums
+  double sse = 0.0, sae = 0.0, nll = 0.0;
+  for (int p = threadIdx.x; p < nparts; p += 256) {
+    sse += mta_lg_part[p].s[0];
+    sae += mta_lg_part[p].s[1];
+  }
+  if (A.want_nll)
+    for (int w = threadIdx.x; w < A.windows; w += 256) nll += mta_lg_win[w].nll;
+  sse = wave_sum_dpp(sse);
+  sae = wave_sum_dpp(sae);
+  nll = wave_sum_dpp(nll);
+  if (lane == 0) {
+    red[wave][0] = sse;
+    red[wave][1] = sae;
+    red[wave][2] = nll;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double s_sse = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    const double s_sae = (red[0][1] + red[1][1]) + (red[2][1] + red[3][1]);
+    const double nll_total = A.want_nll ? (red[0][2] + red[1][2]) + (red[2][2] + red[3][2]) : 0.0;
+    const double cnt = (double)A.N * n;
+    const double mse = s_sse / cnt;
+    const double total = (double)A.c_nll * nll_total + (double)A.c_mse * mse;
+    A.out[0] = (float)mse;
+    A.out[1] = (float)nll_total;
+    A.out[2] = (float)(s_sae / cnt);
+    A.out[3] = (float)total;
+    if (A.acc) {
+      A.acc[0] += s_sse;
+      A.acc[1] += cnt;
+      A.acc[2] += nll_total;
+      A.acc[3] += 1.0;
+      A.acc[4] += total * A.batch_weight;
+      A.acc[5] += A.batch_weight;
+      A.acc[6] += s_sae;
+      A.acc[7] += cnt;
+    }
+  }
+}
+
+// the decoder losses of `ab` (global memory) on the grid path when it applies, else the single workgroup
+void launch_decoder_losses(const float* ab, const LossArgs& A, hipStream_t st) {
+  if (losses_grid_ok(A)) {
+    const int J = min(LG_MAXJ, (A.kwin + LG_SEQ - 1) / LG_SEQ);
+    const int S = (A.kwin + J - 1) / J;
+    losses_grid_part_kernel<<<dim3(J, A.windows), 256, 0, st>>>(ab, A, J, S);
+    if (A.want_nll) losses_grid_window_kernel<<<A.windows, 64, 0, st>>>(A, J);
+    losses_grid_grad_kernel<<<(A.N + 3) / 4, 256, 0, st>>>(ab, A, J, A.windows * J);
+    return;
+  }
+  decoder_losses_kernel<<<1, TPB, ut_floats(A.n) * sizeof(float), st>>>(ab, A);
+}
+
 }  // namespace
 
 extern "C" void mta_decoder_losses(const float* ab, const float* y, const float* factor, const float* inv_psi, int N,
@@ -753,7 +946,7 @@ extern "C" void mta_decoder_losses(const float* ab, const float* y, const float*
                                    hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
              out, gmse, gnll, acc};
-  decoder_losses_kernel<<<1, TPB, ut_floats(n) * sizeof(float), st>>>(ab, A);
+  launch_decoder_losses(ab, A, st);
 }
 
 extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb,
@@ -765,7 +958,7 @@ extern "C" void mta_heads_losses(const float* h, int H, const float* wa, const f
              out, gmse, gnll, acc};
   if (heads_big(N, H)) {
     heads_kernel<<<(N + NWAVES - 1) / NWAVES, TPB, 0, st>>>(h, N, H, wa, ba, wb, bb, ab_out);
-    decoder_losses_kernel<<<1, TPB, ut_floats(n) * sizeof(float), st>>>(ab_out, A);
+    launch_decoder_losses(ab_out, A, st);
     return;
   }
   const size_t lds = ((size_t)(2 * ((N + 1) & ~1) + 4) + ut_floats(n)) * sizeof(float);

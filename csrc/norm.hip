@@ -112,7 +112,188 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
   }
 }
 
-constexpr int NORM_BWD_MAX_BLOCKS = 512;
+// ---- wide rows (D >= 1024: the MLP-large encoder's D = 2048) ----
+// One wave per row holds 32+ floats per lane of each operand plus the dgamma/dbeta accumulators (~200 VGPRs,
+// 2 waves/SIMD) and pays one dependent round trip per float4 group of gamma/beta/pre/dres interleaved with its
+// stores (r2 trace, mlp_large B=64: fwd 61 us, bwd 152 us per call for 78 / 157 MB, 4-5x off the HBM rate).
+// Here a 256-thread workgroup spans a row (VPT float4 per thread), every operand of a row is loaded up front
+// (the backward also prefetches the NEXT row's operands before reducing the current one), the row sums go
+// through one LDS exchange (parity double-buffered: one barrier per row), and each column belongs to exactly
+// one thread, so the backward's dgamma/dbeta partials stay in registers and leave as one plain row per block.
+template <int VPT>
+__global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row = blockIdx.x;
+  const float invD = 1.0f / (float)a.D;
+  const float* xr = a.x + (size_t)row * a.ldx;
+  float4 v[VPT], gm[VPT], bt[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    const bool ok = c < a.D;
+    v[i] = ok ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gm[i] = (ok && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    bt[i] = (ok && a.beta) ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  s = wave_sum(s);
+  if (lane == 0) red[0][wave] = s;
+  __syncthreads();
+  const float mu = a.rms ? 0.f : ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * invD;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    if (4 * (tid + NT_THREADS * i) < a.D) {
+      const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
+      q += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+  }
+  q = wave_sum(q);
+  if (lane == 0) red[1][wave] = q;
+  __syncthreads();
+  const float rs = rsqrtf(((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * invD + a.eps);
+  if (tid == 0) {
+    if (a.mean) a.mean[row] = mu;
+    a.rstd[row] = rs;
+  }
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    if (c >= a.D) continue;
+    const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w}, bs[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
+    float o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] = (xs[j] - mu) * rs * gs[j] + bs[j];
+      if (a.seed) o[j] *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+    }
+    if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
+    if (a.y_bf16) {
+      bf16x4 b;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
+      *reinterpret_cast<bf16x4*>(a.y_bf16 + (size_t)row * a.D + c) = b;
+    }
+  }
+}
+
+template <int VPT>
+struct WideRow {
+  float4 x[VPT], dy[VPT], dr[VPT];
+  bf16x4 pre[VPT];
+  float mu, rs;
+};
+
+template <int VPT>
+__device__ __forceinline__ void wide_load(const NormArgs& a, int row, WideRow<VPT>& r) {
+  const int tid = threadIdx.x;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    const bool ok = c < a.D;
+    r.x[i] = ok ? *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c) : z;
+    r.dy[i] = ok ? *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c) : z;
+    r.dr[i] = (ok && a.dres) ? *reinterpret_cast<const float4*>(a.dres + (size_t)row * a.ldx + c) : z;
+    if (ok && a.pre) r.pre[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
+  }
+  r.mu = a.rms ? 0.f : a.mean[row];
+  r.rs = a.rstd[row];
+}
+
+template <int VPT>
+__global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, int rows_per_block) {
+  __shared__ float red[2][2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float invD = 1.0f / (float)a.D;
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
+  float4 gm[VPT];
+  float dg[VPT][4], db[VPT][4];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    gm[i] = (c < a.D && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+  }
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(a.M, r0 + rows_per_block);
+  WideRow<VPT> cur, nxt;
+  if (r0 < r1) wide_load<VPT>(a, r0, cur);
+  for (int row = r0; row < r1; ++row) {
+    if (row + 1 < r1) wide_load<VPT>(a, row + 1, nxt);
+    float xh[VPT][4], g[VPT][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = 4 * (tid + NT_THREADS * i);
+      const bool ok = c < a.D;
+      const float xs[4] = {cur.x[i].x, cur.x[i].y, cur.x[i].z, cur.x[i].w};
+      const float ds[4] = {cur.dy[i].x, cur.dy[i].y, cur.dy[i].z, cur.dy[i].w};
+      const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float d = ds[j];
+        if (a.seed && ok) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+        xh[i][j] = ok ? (xs[j] - cur.mu) * cur.rs : 0.f;
+        db[i][j] += d;
+        dg[i][j] += d * xh[i][j];
+        g[i][j] = d * gs[j];
+        s1 += g[i][j];
+        s2 += g[i][j] * xh[i][j];
+      }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    const int par = row & 1;
+    if (lane == 0) {
+      red[par][0][wave] = s1;
+      red[par][1][wave] = s2;
+    }
+    __syncthreads();
+    s1 = a.rms ? 0.f : ((red[par][0][0] + red[par][0][1]) + (red[par][0][2] + red[par][0][3])) * invD;
+    s2 = ((red[par][1][0] + red[par][1][1]) + (red[par][1][2] + red[par][1][3])) * invD;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = 4 * (tid + NT_THREADS * i);
+      if (c >= a.D) continue;
+      const float rv[4] = {cur.dr[i].x, cur.dr[i].y, cur.dr[i].z, cur.dr[i].w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) + rv[j];
+        if (a.pre) o[j] *= mta_gelu_grad((float)cur.pre[i][j]);
+      }
+      if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if (a.dx_bf16) {
+        bf16x4 b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
+        *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+      }
+    }
+    cur = nxt;
+  }
+  if (!a.dgamma && !a.dbeta) return;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    if (c >= a.D) continue;
+    if (a.dgamma)
+      *reinterpret_cast<float4*>(a.part + (long)blockIdx.x * a.part_ld + c) = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
+    if (a.dbeta)
+      *reinterpret_cast<float4*>(a.part + a.part_pass + (long)blockIdx.x * a.part_ld + c) =
+          make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
+  }
+}
+
+constexpr int NORM_BWD_MAX_BLOCKS = 1024;
+constexpr int NORM_BWD_NARROW_BLOCKS = 512;  // the one-wave-per-row backward's grid cap (tuned on the transformer)
 // per-block column partials of dgamma / dbeta (static: no allocation, graph-capture safe; stream-ordered use)
 __device__ float mta_norm_part[2][NORM_BWD_MAX_BLOCKS][2048];
 // deferred reductions (D <= NORM_DEFER_D): each backward call gets its own slot and ONE batched launch sums every
@@ -224,6 +405,31 @@ __global__ void norm_param_reduce_kernel(float* __restrict__ dgamma, float* __re
   if (lane == 0) dst[col] += s;
 }
 
+// the same column sums for the wide backward's many partial rows: lane = column (coalesced 256-B rows), the
+// workgroup's 16 waves take every 16th partial row (16 independent loads in flight per lane), then the 16 wave
+// partials are added in wave order through LDS (fixed order: bit-reproducible)
+__global__ __launch_bounds__(1024) void norm_param_reduce_wide_kernel(float* __restrict__ dgamma,
+                                                                       float* __restrict__ dbeta, int D, int blocks) {
+  __shared__ float part[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;  // over [0, 2D)
+  const int pass = c >= D ? 1 : 0, col = c - pass * D;
+  float* dst = pass == 0 ? dgamma : dbeta;
+  float s = 0.f;
+  if (c < 2 * D && dst) {
+#pragma unroll 16
+    for (int b = wave; b < blocks; b += 16) s += mta_norm_part[pass][b][col];
+  }
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < 2 * D && dst) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += part[w][lane];
+    dst[col] += t;
+  }
+}
+
 struct ReduceJob {
   const float* part;
   float* dgamma;
@@ -262,7 +468,7 @@ int norm_blocks(int M, bool bwd) {
   const int rows_per_block = 4;
   int b = (M + rows_per_block - 1) / rows_per_block;
   // backward: cap the grid so each wave reduces several rows before the per-column atomics
-  const int cap = bwd ? NORM_BWD_MAX_BLOCKS : 4096;
+  const int cap = bwd ? NORM_BWD_NARROW_BLOCKS : 4096;
   return b > cap ? cap : (b < 1 ? 1 : b);
 }
 
@@ -322,7 +528,17 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
   a.dgamma = dgamma;
   a.dbeta = dbeta;
   const int vpl = (D + 255) / 256;
-  const int blocks = norm_blocks(M, bwd != 0);
+  const bool wide = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr;
+  int rows_per_block = 1;
+  int blocks = norm_blocks(M, bwd != 0);
+  if (wide && bwd) {
+    // ~4 workgroups per CU, each a contiguous row range (partials: one row per block)
+    rows_per_block = (M + NORM_BWD_MAX_BLOCKS - 1) / NORM_BWD_MAX_BLOCKS;
+    if (rows_per_block < 2) rows_per_block = 2;
+    blocks = (M + rows_per_block - 1) / rows_per_block;
+  } else if (wide) {
+    blocks = M;
+  }
   // deferred slot when the caller asked for it (dgamma pointer tagged by mta_norm_defer) and D fits
   const bool defer = bwd && (dgamma || dbeta) && defer_next && D <= NORM_DEFER_D;
   defer_next = false;
@@ -352,7 +568,17 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
 #define MTA_NORM_LAUNCH(V)                                                      \
   if (bwd) norm_bwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);                \
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
-  if (vpl <= 1) {
+  if (wide) {
+    if (M > 0) {
+      if (bwd) {
+        if (D <= 1024) norm_bwd_wide_kernel<1><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+        else norm_bwd_wide_kernel<2><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+      } else {
+        if (D <= 1024) norm_fwd_wide_kernel<1><<<blocks, NT_THREADS, 0, st>>>(a);
+        else norm_fwd_wide_kernel<2><<<blocks, NT_THREADS, 0, st>>>(a);
+      }
+    }
+  } else if (vpl <= 1) {
     MTA_NORM_LAUNCH(1)
   } else if (vpl <= 2) {
     MTA_NORM_LAUNCH(2)
@@ -362,7 +588,9 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
     MTA_NORM_LAUNCH(8)
   }
 #undef MTA_NORM_LAUNCH
-  if (bwd && (dgamma || dbeta) && !defer)
+  if (bwd && (dgamma || dbeta) && wide)
+    norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
+  else if (bwd && (dgamma || dbeta) && !defer)
     norm_param_reduce_kernel<<<(2 * D + 3) / 4, 256, 0, st>>>(dgamma, dbeta, D, blocks);
   return 0;
 }

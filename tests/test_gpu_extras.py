@@ -71,14 +71,14 @@ def test_gemm_input_grad_dgelu_and_weight_grad_split():
 
 
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("D", [128, 256, 2048])
+@pytest.mark.parametrize("D", [128, 256, 1024, 1536, 2048])
 def test_norm_forward_backward(rms, D):
     from masters_thesis_amd.ops import _lib
     from masters_thesis_amd.ops.extras import LN_EPS, RMS_EPS
 
     C = _lib.lib()
     torch.manual_seed(2)
-    M = 300
+    M = 301
     x = (torch.randn(M, D) * 2 + 0.5).to(DEV)
     g, b = (torch.rand(D) + 0.5).to(DEV), torch.randn(D).to(DEV)
     dy = torch.randn(M, D).to(DEV)

@@ -88,7 +88,8 @@ def test_lstm_dropout_path():
     assert all(torch.isfinite(w.grad).all() for w in ws)
 
 
-@pytest.mark.parametrize("B,mode", [(1, "reference"), (3, "reference"), (3, "per_window")])
+@pytest.mark.parametrize("B,mode", [(1, "reference"), (3, "reference"), (3, "per_window"), (12, "reference"),
+                                    (12, "per_window")])
 def test_decoder_losses_match_dense_reference(B, mode):
     from masters_thesis_amd.data.common import gaussian_nll_dense, inverse_returns_covariance
     from masters_thesis_amd.ops.losses import decoder_losses
@@ -326,6 +327,34 @@ def test_train_step_graph_matches_eager():
     p_graph, acc_graph = run(True)
     torch.testing.assert_close(p_graph, p_eager, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(acc_graph, acc_eager, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("mode", ["reference", "per_window"])
+def test_grid_losses_match_single_workgroup(mode, monkeypatch):
+    """N >= 1024: the three-launch grid losses (csrc/losses.hip L1-L3) agree with the single-workgroup kernel."""
+    from masters_thesis_amd.ops.losses import decoder_losses
+
+    torch.manual_seed(5)
+    B, K, n = 64, 100, 30
+    N = B * K
+    ab = (torch.randn(N, 2) * 0.3 + torch.tensor([0.0, 1.0])).to(DEV)
+    y = torch.randn(N, n, 4, device=DEV)
+    factor = torch.stack([torch.randn(B) * 0.1, torch.rand(B) * 0.5 + 0.2], -1).to(DEV)
+    inv_psi = (torch.rand(N) * 5 + 1).to(DEV)
+
+    def run():
+        a = ab.clone().requires_grad_(True)
+        mse, nll, mae = decoder_losses(a, y, factor, inv_psi, batch_windows=B, nll_mode=mode)
+        (mse * 0.7 + nll * 1.3).backward()
+        return torch.stack([mse, nll, mae]).detach(), a.grad
+
+    s_grid, g_grid = run()
+    s_grid2, g_grid2 = run()
+    assert torch.equal(s_grid, s_grid2) and torch.equal(g_grid, g_grid2)  # fixed-order sums
+    monkeypatch.setenv("MTA_LOSSES_SINGLE", "1")
+    s_one, g_one = run()
+    torch.testing.assert_close(s_grid, s_one, rtol=2e-5, atol=1e-4)
+    torch.testing.assert_close(g_grid, g_one, rtol=1e-4, atol=1e-4 * g_one.abs().max().item())
 
 
 @pytest.mark.parametrize("B,H", [(64, 2048), (8, 512)])
