@@ -76,7 +76,7 @@ union Bf8 {
   __bf16 e[8];
 };
 
-template <int BM, int BN, int BKT, bool AT, bool BT>
+template <int BM, int BN, int BKT, bool AT, bool BT, bool PIPE = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const int by, const int bz, const int gz,
                                           __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
   constexpr int RST = BKT + 8;  // LDS row stride (bf16): BKT + 8 pad (16 B): conflict-free b128 rows
@@ -96,12 +96,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
   const int kend = min(g.K, kbeg + g.k_per_split);
   if (kbeg >= kend) return;
 
-  uint4 ra[A_PER][A_REGS];
-  uint4 rb[B_PER][B_REGS];
-  uint32_t ma[A_PER], mb[B_PER];  // validity bits (one per 16-B load)
+  typedef uint4 RegA[A_PER][A_REGS];
+  typedef uint4 RegB[B_PER][B_REGS];
+  RegA ra[PIPE ? 2 : 1];
+  RegB rb[PIPE ? 2 : 1];
+  uint32_t ma[PIPE ? 2 : 1][A_PER], mb[PIPE ? 2 : 1][B_PER];  // validity bits (one per 16-B load)
 
   // ---- global -> registers (raw values + masks; masks applied at LDS-store time) ----
-  auto load = [&](int k0) __attribute__((always_inline)) {
+  auto load = [&](RegA& ra, RegB& rb, uint32_t (&ma)[A_PER], uint32_t (&mb)[B_PER], int k0)
+      __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < A_PER; ++p) {
       const int it = tid + p * GT;
@@ -151,7 +154,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
   };
 
   // ---- registers -> LDS k-contiguous images (transposing 8x8 blocks for AT/BT) ----
-  auto store = [&]() __attribute__((always_inline)) {
+  auto store = [&](const RegA& ra, const RegB& rb, const uint32_t (&ma)[A_PER], const uint32_t (&mb)[B_PER],
+                   __bf16* __restrict__ As, __bf16* __restrict__ Bs) __attribute__((always_inline)) {
 #pragma unroll
     for (int p = 0; p < A_PER; ++p) {
       const int it = tid + p * GT;
@@ -206,12 +210,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
   for (int i = 0; i < MT; ++i) rowsum[i] = 0.f;
   const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
 
-  load(kbeg);
-  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
-    __syncthreads();
-    store();
-    __syncthreads();
-    if (k0 + BKT < kend) load(k0 + BKT);
+  auto compute = [&](const __bf16* __restrict__ As, const __bf16* __restrict__ Bs) __attribute__((always_inline)) {
 #pragma unroll
     for (int ks = 0; ks < BKT / 32; ++ks) {
       bf16x8 af[MT];
@@ -230,6 +229,43 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
 #pragma unroll
         for (int i = 0; i < MT; ++i) acc[i][j] = mfma16x16x32(af[i], bfr, acc[i][j]);
       }
+    }
+  };
+
+  if constexpr (!PIPE) {
+    load(ra[0], rb[0], ma[0], mb[0], kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+      __syncthreads();
+      store(ra[0], rb[0], ma[0], mb[0], As, Bs);
+      __syncthreads();
+      if (k0 + BKT < kend) load(ra[0], rb[0], ma[0], mb[0], k0 + BKT);
+      compute(As, Bs);
+    }
+  } else {
+    // Two LDS stages and two register sets: the k-slice stored at step t was loaded at step t - 2 (two slices of
+    // MFMA work between a load's issue and its use, instead of one), one barrier per k-step.
+    __bf16* const As1 = As + (BM + BN) * RST;
+    __bf16* const Bs1 = Bs + (BM + BN) * RST;
+    const int nk = (kend - kbeg + BKT - 1) / BKT;
+    load(ra[0], rb[0], ma[0], mb[0], kbeg);
+    if (nk > 1) load(ra[1], rb[1], ma[1], mb[1], kbeg + BKT);
+    store(ra[0], rb[0], ma[0], mb[0], As, Bs);
+    if (nk > 2) load(ra[0], rb[0], ma[0], mb[0], kbeg + 2 * BKT);
+    __syncthreads();
+    for (int t = 0; t < nk; t += 2) {
+      compute(As, Bs);
+      if (t + 1 < nk) {
+        store(ra[1], rb[1], ma[1], mb[1], As1, Bs1);
+        if (t + 3 < nk) load(ra[1], rb[1], ma[1], mb[1], kbeg + (t + 3) * BKT);
+      }
+      __syncthreads();
+      if (t + 1 >= nk) break;
+      compute(As1, Bs1);
+      if (t + 2 < nk) {
+        store(ra[0], rb[0], ma[0], mb[0], As, Bs);
+        if (t + 4 < nk) load(ra[0], rb[0], ma[0], mb[0], kbeg + (t + 4) * BKT);
+      }
+      __syncthreads();
     }
   }
 
@@ -312,11 +348,22 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
   }
 }
 
-template <int BM, int BN, int BKT, bool AT, bool BT>
-__global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * (BKT + 8)];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * (BKT + 8)];
-  gemm_body<BM, BN, BKT, AT, BT>(g, blockIdx.x, blockIdx.y, blockIdx.z, gridDim.z, As, Bs);
+// XCD-aware block order: the dispatcher deals workgroup ids round-robin over the 8 XCDs (each with its own L2);
+// remapping id -> (id % 8) * (nb / 8) + id / 8 gives every XCD a contiguous run of tiles (x fastest), so tiles that
+// share A rows (and the same B column tiles) meet in one L2 instead of eight
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int nb8 = nb & ~7;
+  return b < nb8 ? (b & 7) * (nb8 >> 3) + (b >> 3) : b;
+}
+
+template <int BM, int BN, int BKT, bool PIPE>
+constexpr int gemm_lds_elems() { return (PIPE ? 2 : 1) * (BM + BN) * (BKT + 8); }
+
+template <int BM, int BN, int BKT, bool AT, bool BT, bool PIPE>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_bf16_kernel(GemmArgs g, int nx, int ny, int nz) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT, PIPE>()];
+  const int b = xcd_remap(blockIdx.x, nx * ny * nz);
+  gemm_body<BM, BN, BKT, AT, BT, PIPE>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, smem, smem + BM * (BKT + 8));
 }
 
 // Two independent GEMMs of one tile configuration in ONE launch (the backward's weight gradient and input
@@ -325,24 +372,135 @@ __global__ __launch_bounds__(GT) void gemm_bf16_kernel(GemmArgs g) {
 struct PairGrid {
   int nx1, ny1, nz1, nx2, ny2, nz2;
 };
-template <int BM, int BN, int BKT, bool AT1, bool BT1, bool AT2, bool BT2>
-__global__ __launch_bounds__(GT) void gemm_bf16_pair_kernel(GemmArgs g1, GemmArgs g2, PairGrid pg) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[BM * (BKT + 8)];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[BN * (BKT + 8)];
+template <int BM, int BN, int BKT, bool AT1, bool BT1, bool AT2, bool BT2, bool PIPE>
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_bf16_pair_kernel(GemmArgs g1, GemmArgs g2, PairGrid pg) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT, PIPE>()];
+  __bf16* const As = smem;
+  __bf16* const Bs = smem + BM * (BKT + 8);
+  // XCD remap within each problem (a remap over the joint range deals the long weight-gradient tiles to the first
+  // XCDs only: 295 -> 690 us per mlp_large pair); the second problem's ids stay on their XCD when n1 % 8 == 0
   const int n1 = pg.nx1 * pg.ny1 * pg.nz1;
   int b = blockIdx.x;
+  b = b < n1 ? xcd_remap(b, n1) : ((n1 & 7) == 0 ? n1 + xcd_remap(b - n1, pg.nx2 * pg.ny2 * pg.nz2) : b);
   if (b < n1) {
-    gemm_body<BM, BN, BKT, AT1, BT1>(g1, b % pg.nx1, (b / pg.nx1) % pg.ny1, b / (pg.nx1 * pg.ny1), pg.nz1, As, Bs);
+    gemm_body<BM, BN, BKT, AT1, BT1, PIPE>(g1, b % pg.nx1, (b / pg.nx1) % pg.ny1, b / (pg.nx1 * pg.ny1), pg.nz1, As,
+                                           Bs);
   } else {
     b -= n1;
-    gemm_body<BM, BN, BKT, AT2, BT2>(g2, b % pg.nx2, (b / pg.nx2) % pg.ny2, b / (pg.nx2 * pg.ny2), pg.nz2, As, Bs);
+    gemm_body<BM, BN, BKT, AT2, BT2, PIPE>(g2, b % pg.nx2, (b / pg.nx2) % pg.ny2, b / (pg.nx2 * pg.ny2), pg.nz2, As,
+                                           Bs);
   }
+}
+
+// the two-stage pipelined main loop where it fits: 128x128 tiles (enough k-steps to pipeline) whose register
+// staging is one 16-B load per item (k-contiguous operands; the transposing staging holds 8 loads per item, and
+// a second register set of those would spill).  Opt-in (MTA_GEMM_PIPE=1): measured equal to the single-stage loop
+// (mlp_large forward 117.4 vs 117.0 us, 6400x2048x2048) at one more 73.7 KB LDS image per workgroup.
+inline bool pipe_on() {
+  static const bool on = [] {
+    const char* e = getenv("MTA_GEMM_PIPE");
+    return e && e[0] == '1';
+  }();
+  return on;
 }
 
 template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
-  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, ksplit);
-  gemm_bf16_kernel<BM, BN, BKT, AT, BT><<<grid, GT, 0, st>>>(g);
+  const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
+  const int blocks = nx * ny * ksplit;
+  if constexpr (BM == 128 && !AT && !BT) {
+    if (pipe_on()) {
+      gemm_bf16_kernel<BM, BN, BKT, AT, BT, true><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
+      return;
+    }
+  }
+  gemm_bf16_kernel<BM, BN, BKT, AT, BT, false><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
+}
+
+// ---- big transposed-operand problems -> k-contiguous copies + the NN kernel ----
+// The transposing register staging (8 loads per 8x8 block on half the threads, 64 byte moves per block) holds
+// the input-gradient (B^T) and weight-gradient (A^T, B^T) GEMMs of mlp_large at 345 / 248 TFLOP/s against 460
+// for the k-contiguous forward: above 2^31 MACs a 64x64-tile LDS transpose (~5.5 TB/s-class copy) into a
+// per-operand workspace plus the NN kernel is cheaper.  Workspaces grow outside graph capture only and are never
+// freed (a captured graph keeps pointing at the buffer it recorded); inside a capture that would need a larger one
+// the GEMM keeps the transposing path.
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* __restrict__ in, int R, int C, int ld_in,
+                                                             __bf16* __restrict__ out, int ld_out) {
+  __shared__ __attribute__((aligned(16))) __bf16 t[64][72];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+#pragma unroll
+  for (int q = threadIdx.x; q < 512; q += 256) {
+    const int r = q >> 3, ch = q & 7;
+    const int gr = r0 + r, gc = c0 + 8 * ch;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (gr < R && gc < C) v = *reinterpret_cast<const uint4*>(in + (size_t)gr * ld_in + gc);
+    *reinterpret_cast<uint4*>(&t[r][8 * ch]) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = threadIdx.x; q < 512; q += 256) {
+    const int c = q >> 3, ch = q & 7;  // output row c0 + c, input rows r0 + 8ch ... + 7
+    const int oc = c0 + c, orow = r0 + 8 * ch;
+    if (oc < C && orow < R) {
+      Bf8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o.e[i] = t[8 * ch + i][c];
+      *reinterpret_cast<uint4*>(out + (size_t)oc * ld_out + orow) = o.u;
+    }
+  }
+}
+
+struct Workspace {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+Workspace g_ws[3];  // 0: weight-grad A^T, 1: weight-grad B^T, 2: input-grad B^T
+
+__bf16* workspace(int slot, size_t bytes, hipStream_t st) {
+  Workspace& w = g_ws[slot];
+  if (bytes <= w.cap) return static_cast<__bf16*>(w.p);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  void* p = nullptr;
+  if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+  w.p = p;  // the previous buffer is intentionally leaked (graphs may reference it)
+  w.cap = bytes;
+  return static_cast<__bf16*>(p);
+}
+
+inline bool transpose_on() {
+  static const bool on = [] {
+    const char* e = getenv("MTA_GEMM_TRANSPOSE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// out[c][r] = in[r][c] for an R x C bf16 matrix (R, C multiples of 8)
+void transpose(const __bf16* in, int R, int C, int ld_in, __bf16* out, hipStream_t st) {
+  transpose_bf16_kernel<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, ld_in, out, R);
+}
+
+// rewrite a mode-1/2 problem as a mode-0 one over transposed copies; false = keep the transposing kernel
+bool to_nn(GemmArgs& g, int mode, hipStream_t st) {
+  if (mode == 0 || !transpose_on() || (long)g.M * g.N * g.K < (1L << 31)) return false;
+  if (mode == 2) {
+    __bf16* at = workspace(0, (size_t)g.M * g.K * sizeof(__bf16), st);
+    __bf16* bt = workspace(1, (size_t)g.N * g.K * sizeof(__bf16), st);
+    if (!at || !bt) return false;
+    transpose(g.A, g.K, g.M, g.lda, at, st);  // A stored [K][M]
+    transpose(g.B, g.K, g.N, g.ldb, bt, st);  // B stored [K][N]
+    g.A = at;
+    g.B = bt;
+  } else {
+    __bf16* bt = workspace(2, (size_t)g.N * g.K * sizeof(__bf16), st);
+    if (!bt) return false;
+    transpose(g.B, g.K, g.N, g.ldb, bt, st);  // B stored [K][N]
+    g.B = bt;
+  }
+  g.lda = g.K;
+  g.ldb = g.K;
+  return true;
 }
 
 // tile configuration of a problem: 0 = 128x128x64, 1 = 128x128x32, 2 = 64x64x128, 3 = 64x64x32
@@ -352,22 +510,41 @@ inline int tile_config(const GemmArgs& g, int ksplit) {
   return tiles128 >= 256 ? (deep ? 0 : 1) : (deep ? 2 : 3);
 }
 
-template <int BM, int BN, int BKT>
+template <int BM, int BN, int BKT, bool NN>
 void launch_pair_cfg(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   PairGrid pg{(g1.N + BN - 1) / BN, (g1.M + BM - 1) / BM, k1, (g2.N + BN - 1) / BN, (g2.M + BM - 1) / BM, k2};
   const int blocks = pg.nx1 * pg.ny1 * pg.nz1 + pg.nx2 * pg.ny2 * pg.nz2;
-  gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  if constexpr (NN) gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  else gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
 }
 
-// (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately
-bool launch_pair(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
-  const int c = tile_config(g1, k1);
-  if (c != tile_config(g2, k2)) return false;
+template <bool NN>
+void launch_pair_nn(int c, const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   switch (c) {
-    case 0: launch_pair_cfg<128, 128, 64>(g1, k1, g2, k2, st); break;
-    case 1: launch_pair_cfg<128, 128, 32>(g1, k1, g2, k2, st); break;
-    case 2: launch_pair_cfg<64, 64, 128>(g1, k1, g2, k2, st); break;
-    default: launch_pair_cfg<64, 64, 32>(g1, k1, g2, k2, st); break;
+    case 0: launch_pair_cfg<128, 128, 64, NN>(g1, k1, g2, k2, st); break;
+    case 1: launch_pair_cfg<128, 128, 32, NN>(g1, k1, g2, k2, st); break;
+    case 2: launch_pair_cfg<64, 64, 128, NN>(g1, k1, g2, k2, st); break;
+    default: launch_pair_cfg<64, 64, 32, NN>(g1, k1, g2, k2, st); break;
+  }
+}
+
+void dispatch_mode(int mode, const GemmArgs& g, int ksplit, hipStream_t st);
+
+// (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately.
+// Big pairs run on transposed copies (both NN) when both problems qualify.
+bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, hipStream_t st) {
+  const int c = tile_config(g1_in, k1);
+  if (c != tile_config(g2_in, k2)) return false;
+  GemmArgs g1 = g1_in, g2 = g2_in;
+  const bool nn1 = to_nn(g1, 2, st);
+  const bool nn2 = nn1 && to_nn(g2, 1, st);
+  if (nn1 && nn2) {
+    launch_pair_nn<true>(c, g1, k1, g2, k2, st);
+  } else if (nn1) {  // workspace for the second operand unavailable (capture): launch the two separately
+    dispatch_mode(0, g1, k1, st);
+    dispatch_mode(1, g2_in, k2, st);
+  } else {
+    launch_pair_nn<false>(c, g1, k1, g2, k2, st);
   }
   return true;
 }
@@ -388,7 +565,9 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   }
 }
 
-void dispatch_mode(int mode, const GemmArgs& g, int ksplit, hipStream_t st) {
+void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
+  GemmArgs g = g_in;
+  if (to_nn(g, mode, st)) mode = 0;
   if (mode == 0) dispatch<false, false>(g, ksplit, st);
   else if (mode == 1) dispatch<false, true>(g, ksplit, st);
   else dispatch<true, true>(g, ksplit, st);

@@ -24,7 +24,8 @@ def _rel(a, b):
     return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("M,N,K", [(112, 256, 184), (6000, 384, 128), (64, 64, 32), (200, 136, 520)])
+@pytest.mark.parametrize("M,N,K", [(112, 256, 184), (6000, 384, 128), (64, 64, 32), (200, 136, 520), (2048, 2048, 200),
+                                   (4104, 1032, 520), (4096, 1024, 136)])
 def test_gemm_forward_epilogues(M, N, K):
     from masters_thesis_amd.ops import extras as X
 
@@ -226,7 +227,10 @@ def test_extras_train_through_trainer_graph(arch):
     assert tr._graphs  # the step was captured and replayed
 
 
-@pytest.mark.parametrize("M,D,Din", [(6720, 128, 512), (6720, 384, 128), (304, 64, 72)])
+# (6400, 2048, *): above 2^31 MACs both products run on transposed copies through the NN kernel (csrc/gemm.hip
+# to_nn); 2048 pairs them in one launch, 1032 gives the two different tile configurations (separate launches)
+@pytest.mark.parametrize("M,D,Din", [(6720, 128, 512), (6720, 384, 128), (304, 64, 72), (6400, 2048, 2048),
+                                     (6400, 2048, 1032)])
 def test_paired_weight_and_input_grad_gemms(M, D, Din):
     """A deferred weight-gradient GEMM runs together with the next (input-gradient) GEMM in one paired launch:
     same results as two launches (split-K sums compared with a tolerance, the input gradient exactly)."""
@@ -253,6 +257,8 @@ def test_paired_weight_and_input_grad_gemms(M, D, Din):
     torch.testing.assert_close(gb1, gb0, rtol=1e-5, atol=1e-3)
     ref = dY.double().t() @ Xa.double()
     assert _rel(gw1, ref) < 1e-5
+    assert _rel(gb1, dY.double().sum(0)) < 1e-5
+    assert _rel(dx1, dY.double() @ W.double()) < 1e-5
 
 
 def test_gemm_dropout_mask_forward_backward_consistent():
