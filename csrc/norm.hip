@@ -292,8 +292,11 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, i
   }
 }
 
-constexpr int NORM_BWD_MAX_BLOCKS = 1024;
-constexpr int NORM_BWD_NARROW_BLOCKS = 512;  // the one-wave-per-row backward's grid cap (tuned on the transformer)
+constexpr int NORM_BWD_MAX_BLOCKS = 1024;    // partial-row capacity of the static workspaces below
+constexpr int NORM_BWD_WIDE_BLOCKS = 1024;   // the wide backward: ~4 workgroups per CU
+// the one-wave-per-row backward's grid cap: transformer B=1 (M = 6,272 rows, D = 128) 0.714 ms at 512, 0.702 at
+// 1024, 0.711 at 1,568 (one row per wave: the partial-row reduce grows) (profiles/r2_norm_bwd_cap_ab.txt)
+constexpr int NORM_BWD_NARROW_BLOCKS = 1024;
 // per-block column partials of dgamma / dbeta (static: no allocation, graph-capture safe; stream-ordered use)
 __device__ float mta_norm_part[2][NORM_BWD_MAX_BLOCKS][2048];
 // deferred reductions (D <= NORM_DEFER_D): each backward call gets its own slot and ONE batched launch sums every
@@ -468,7 +471,12 @@ int norm_blocks(int M, bool bwd) {
   const int rows_per_block = 4;
   int b = (M + rows_per_block - 1) / rows_per_block;
   // backward: cap the grid so each wave reduces several rows before the per-column atomics
-  const int cap = bwd ? NORM_BWD_NARROW_BLOCKS : 4096;
+  static const int bwd_cap = [] {  // MTA_NORM_BWD_BLOCKS: A/B knob for the one-wave-per-row backward's grid
+    const char* e = getenv("MTA_NORM_BWD_BLOCKS");
+    const int v = e ? atoi(e) : NORM_BWD_NARROW_BLOCKS;
+    return v < 1 ? 1 : (v > NORM_BWD_MAX_BLOCKS ? NORM_BWD_MAX_BLOCKS : v);
+  }();
+  const int cap = bwd ? bwd_cap : 4096;
   return b > cap ? cap : (b < 1 ? 1 : b);
 }
 
@@ -533,7 +541,7 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
   int blocks = norm_blocks(M, bwd != 0);
   if (wide && bwd) {
     // ~4 workgroups per CU, each a contiguous row range (partials: one row per block)
-    rows_per_block = (M + NORM_BWD_MAX_BLOCKS - 1) / NORM_BWD_MAX_BLOCKS;
+    rows_per_block = (M + NORM_BWD_WIDE_BLOCKS - 1) / NORM_BWD_WIDE_BLOCKS;
     if (rows_per_block < 2) rows_per_block = 2;
     blocks = (M + rows_per_block - 1) / rows_per_block;
   } else if (wide) {
