@@ -274,26 +274,28 @@ def test_training_decoder_matches_fp64(N, B, mode, H, coeffs):
     assert a[3] == 1 and abs(a[0] / a[1] - mse_r.item()) <= 1e-5 * abs(mse_r.item())
 
 
-def test_gather_batch_kernel_and_cursor():
+# (37 windows of 5 x 6 x 3, B = 4): 20 blocks; (300 windows of 100 x 60 x 3, B = 64): 1,280 blocks, two-level arrival
+@pytest.mark.parametrize("W,K,T,B,stop", [(37, 5, 6, 4, 33), (300, 100, 60, 64, 290)])
+def test_gather_batch_kernel_and_cursor(W, K, T, B, stop):
     from masters_thesis_amd.data.datamodule import TensorBatchLoader
 
-    W = 37
-    X = torch.randn(W, 5, 6, 3, device=DEV)
-    Y = torch.randn(W, 5, 4, 4, device=DEV)
+    X = torch.randn(W, K, T, 3, device=DEV)
+    Y = torch.randn(W, K, 4, 4, device=DEV)
     Fc = torch.randn(W, 2, device=DEV)
-    P = torch.randn(W, 5, device=DEV)
-    ld = TensorBatchLoader([X, Y, Fc, P], 4, shuffle=True, seed=3, start=2, stop=33)
+    P = torch.randn(W, K, device=DEV)
+    ld = TensorBatchLoader([X, Y, Fc, P], B, shuffle=True, seed=3, start=2, stop=stop)
     assert ld.supports_static()
-    nfull = ld.begin_epoch(1)
-    idx = ld._epoch_idx
-    for k in range(nfull):
-        bufs = ld.gather_static()
-        sel = idx[k * 4:(k + 1) * 4].to(DEV).long()
-        for s, b in zip((X, Y, Fc, P), bufs):
-            torch.testing.assert_close(b, s.index_select(0, sel), rtol=0, atol=0)
-    assert int(ld._cursor.item()) == nfull and int(ld._arrive.item()) == 0
+    for epoch in (1, 2):
+        nfull = ld.begin_epoch(epoch)
+        idx = ld._epoch_idx
+        for k in range(nfull):
+            bufs = ld.gather_static()
+            sel = idx[k * B:(k + 1) * B].to(DEV).long()
+            for s, b in zip((X, Y, Fc, P), bufs):
+                torch.testing.assert_close(b, s.index_select(0, sel), rtol=0, atol=0)
+        assert int(ld._cursor.item()) == nfull and int(ld._arrive.abs().sum().item()) == 0
     tail = ld.tail_batch()
-    assert tail is not None and tail[0].shape[0] == idx.numel() - 4 * nfull
+    assert tail is not None and tail[0].shape[0] == idx.numel() - B * nfull
 
 
 def test_train_step_graph_matches_eager():
