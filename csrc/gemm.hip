@@ -454,10 +454,13 @@ struct Workspace {
   void* p = nullptr;
   size_t cap = 0;
 };
-Workspace g_ws[3];  // 0: weight-grad A^T, 1: weight-grad B^T, 2: input-grad B^T
+constexpr int WS_MAX_DEVICES = 16;
+Workspace g_ws[WS_MAX_DEVICES][3];  // per device: 0 = weight-grad A^T, 1 = weight-grad B^T, 2 = input-grad B^T
 
 __bf16* workspace(int slot, size_t bytes, hipStream_t st) {
-  Workspace& w = g_ws[slot];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WS_MAX_DEVICES) return nullptr;
+  Workspace& w = g_ws[dev][slot];
   if (bytes <= w.cap) return static_cast<__bf16*>(w.p);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
@@ -556,8 +559,26 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   // transformer (K = 128) then stage once instead of paying four dependent load -> LDS -> MFMA rounds
   const long tiles128 = (long)((g.M + 127) / 128) * ((g.N + 127) / 128) * ksplit;
   const bool deep = g.k_per_split >= 128;
+  // Per-CU balance of the k-contiguous deep case: 6400 x 2048 is 800 tiles of 128x128 = 3.125 per CU, so the
+  // busiest CUs run 4 while the mean is 3.1 (78 %); 1,600 tiles of 128x64 = 6.25 per CU (89 %).  128x64 tiles cost
+  // ~10 % per FLOP at equal balance (4096^3: 251 vs 226 us), so they are taken when 0.9 x their balance beats the
+  // 128x128 balance: mlp_large forward 118 -> 108 us, step 1.69 -> 1.59 ms (profiles/r2_gemm_bn64_ab.txt).
+  // MTA_GEMM_BN64=0/1 forces the choice.
+  static const int bn64_env = [] {
+    const char* e = getenv("MTA_GEMM_BN64");
+    return e ? (e[0] == '1' ? 1 : 0) : -1;
+  }();
+  bool bn64 = false;
+  if (deep && !AT && !BT) {
+    constexpr long CUS = 256;
+    const long t64 = (long)((g.M + 127) / 128) * ((g.N + 63) / 64) * ksplit;
+    const double e128 = (double)tiles128 / (double)(CUS * ((tiles128 + CUS - 1) / CUS));
+    const double e64 = (double)t64 / (double)(CUS * ((t64 + CUS - 1) / CUS));
+    bn64 = bn64_env >= 0 ? bn64_env == 1 : 0.9 * e64 > e128;
+  }
   if (tiles128 >= 256) {
-    if (deep) launch<128, 128, 64, AT, BT>(g, ksplit, st);
+    if (bn64) launch<128, 64, 64, AT, BT>(g, ksplit, st);
+    else if (deep) launch<128, 128, 64, AT, BT>(g, ksplit, st);
     else launch<128, 128, 32, AT, BT>(g, ksplit, st);
   } else {
     if (deep) launch<64, 64, 128, AT, BT>(g, ksplit, st);
