@@ -713,13 +713,22 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
   for (int k = threadIdx.x; k < H; k += TPB) {
     const float a = wa[k], b = wb[k];
     float sa = 0.f, sb = 0.f;
-    for (int i = r0; i < r1; ++i) {
+    // the block's HB_ROWS h values of column k are loaded in one burst (a runtime-bounded row loop waited on each
+    // row's load in turn: 35.6 us per call at N = 6,400, H = 2,048)
+    float hv[HB_ROWS];
+    if (g_wa) {
+#pragma unroll
+      for (int r = 0; r < HB_ROWS; ++r) hv[r] = r0 + r < r1 ? h[(size_t)(r0 + r) * H + k] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < HB_ROWS; ++r) {
+      const int i = r0 + r;
+      if (i >= r1) break;
       const float da = dab[2 * i], db = dab[2 * i + 1];
       if (dh) dh[(size_t)i * H + k] = da * a + db * b;
       if (g_wa) {
-        const float hv = h[(size_t)i * H + k];
-        sa = fmaf(da, hv, sa);
-        sb = fmaf(db, hv, sb);
+        sa = fmaf(da, hv[r], sa);
+        sb = fmaf(db, hv[r], sb);
       }
     }
     if (g_wa) {
