@@ -147,6 +147,28 @@ __device__ __forceinline__ uint32_t mta_hash3(uint64_t seed, uint32_t a, uint32_
   h ^= h >> 16;
   return h;
 }
+// Cheaper dropout for hot recurrences: ONE lowbias32-style hash per (row pair, column) gives two 16-bit uniforms
+// (p resolved to 1/65536): 3 multiplies per two elements instead of mta_hash3's ~8 per element.  Row pair = row >> 1,
+// element e = row & 1 takes bits [16 e, 16 e + 16).  seed / column parts are loop-invariant (hoisted by callers).
+__device__ __forceinline__ uint32_t mta_pair_seed(uint64_t seed) {
+  return (uint32_t)seed ^ ((uint32_t)(seed >> 32) * 0x27D4EB2Fu);
+}
+__device__ __forceinline__ uint32_t mta_pair_col(uint32_t col) {
+  const uint32_t b = col * 0x85EBCA77u;
+  return (b << 13) | (b >> 19);
+}
+__device__ __forceinline__ uint32_t mta_pair_hash(uint32_t pseed, uint32_t pair, uint32_t pcol) {
+  uint32_t x = pseed ^ (pair * 0x9E3779B1u) ^ pcol;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ bool mta_pair_keep(uint32_t hash, int e, float p) {
+  return (float)((hash >> (16 * e)) & 0xFFFFu) * (1.0f / 65536.0f) >= p;
+}
 // 0 or 1/(1-p)
 __device__ __forceinline__ float mta_dropout_scale(uint64_t seed, uint32_t row, uint32_t col, float p) {
   const float u = (float)(mta_hash3(seed, row, col) >> 8) * (1.0f / 16777216.0f);

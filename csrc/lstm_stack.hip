@@ -38,6 +38,27 @@
 #ifndef MTA_STACK_DX_DELAY
 #define MTA_STACK_DX_DELAY 0
 #endif
+// timing-only debug switches (results are garbage): input / store waves only run their barriers, recurrent waves
+// skip the staging writes
+#ifndef MTA_DBG_NO_INPUT
+#define MTA_DBG_NO_INPUT 0
+#endif
+#ifndef MTA_DBG_NO_STORE
+#define MTA_DBG_NO_STORE 0
+#endif
+#ifndef MTA_DBG_NO_LOAD
+#define MTA_DBG_NO_LOAD 0
+#endif
+#ifndef MTA_DBG_INPUT_BF16
+#define MTA_DBG_INPUT_BF16 0
+#endif
+#ifndef MTA_DBG_NO_STAGE
+#define MTA_DBG_NO_STAGE 0
+#endif
+// static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD
+#ifndef MTA_STACK_PRIO
+#define MTA_STACK_PRIO 0
+#endif
 #if MTA_STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
@@ -160,8 +181,8 @@ struct StackFwdArgs {
   const float* b_hh[MAXL];
   float* hseq[MAXL];    // (T, Np, H) outputs of every layer
   float* xdrop[MAXL];   // xdrop[l] (l >= 1): dropout(h^{(l-1)}), the input of layer l (null: no dropout)
-  uint32_t* mask[MAXL]; // mask[l] (with xdrop[l]): keep bytes of that dropout, (T, ntiles, 4, H) words of the
-                        // 4 sequences 4q..4q+3 of a lane (byte i = sequence 4q+i), read by the backward
+  uint32_t* mask[MAXL]; // mask[l] (with xdrop[l]): keep bytes of that dropout, (T, ntiles, S, H/4) words
+                        // (stack_keep_index: byte e of word (t, tile, s, c) = unit 4c+e of sequence s), read by the backward
   float* stash[MAXL];   // BPTT stash per layer (null: inference)
   const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
   float drop_p;
@@ -178,15 +199,18 @@ struct StackFwdArgs {
   MtaBatchGather g;
 };
 
-// Forward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run the recurrence exactly like lstm.hip
-// (W_hh in VGPRs, h through LDS, one barrier per step); waves [H/16, 2 H/16) are INPUT waves: one step
-// ahead they wait for / load the layer input and compute the gate pre-activations
-// gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products for layer 0, MFMA for layers >= 1) into a
-// double-buffered LDS slot, so the recurrent critical path never sees the hand-off latency, the progress
-// polls or the input product.  The input waves also draw the counter-hash dropout masks of the layer's
-// output (one step ahead, into LDS and the keep-byte words the backward reads): the hash's 32-bit multiplies
-// were ~30 % of a recurrent step when the recurrent waves drew them (r2 stamp probe).  Both roles execute
-// the same barriers (pre-loop, one per step, final).
+// Forward workgroup = 3 x (H/16) waves in three roles (one wave of each role per SIMD):
+//   RECURRENT waves [0, NW): W_hh in VGPRs, h through LDS, one barrier per step -- and NO global memory
+//     operation inside the time loop: h_t (fp32) and the BPTT stash of step t go to LDS staging slots.
+//   INPUT waves [NW, 2 NW): one step ahead they wait for / load the layer input and compute the gate
+//     pre-activations gx_{t+1} = bias + W_ih x_{t+1} (fused F-wide dot products for layer 0, MFMA for layers
+//     >= 1) into a double-buffered LDS slot (hand-off latency, progress polls and the input product off the
+//     recurrent path).
+//   STORE waves [2 NW, 3 NW): during step t they write out step t-1 from the staging slots: h (write-through when
+//     a layer above consumes it), the dropout-masked copy for the next layer with its keep bytes (pair hash,
+//     common.h), the stash; they drain the write-through stores and publish the layer's progress word.
+// r2 stamp probe: store issue + vmcnt drain were ~700 of ~2600 cycles of a recurrent step when the recurrent
+// waves issued the stores themselves.  All roles execute the same barriers (pre-loop, one per step, final).
 template <int H, int PREC>
 struct FwdSmem {
   static constexpr int ROWB = H + 8, ROWF = H + 4;
@@ -194,9 +218,21 @@ struct FwdSmem {
   __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
-  uint32_t keep[2][H / 16][64];  // dropout keep bytes of step t (slot t & 1) per recurrent wave / lane
-  float tr[H / 16][2][S][TRS];   // per-wave transpose scratch of the h / masked-h store
+  float hout[3][S][ROWF];              // h_t in fp32, natural unit order (slot t % 3), for the store waves
+  float4 st[3][H / 16][STASH][64];     // BPTT stash of step t (slot t % 3), per recurrent wave, lane-major
 };
+
+// keep bits of the forward dropout on layer l's input (store layout: one word per (row, 4 units), byte e = unit
+// 4 c + e): row = t * Np + n, pair hash over column pairs (the backward reads the same words)
+__device__ __forceinline__ uint32_t stack_keep_word(uint32_t pseed, uint32_t row, int unit4, float p) {
+  const uint32_t h0 = mta_pair_hash(pseed, row, mta_pair_col((uint32_t)unit4 >> 1));
+  const uint32_t h1 = mta_pair_hash(pseed, row, mta_pair_col(((uint32_t)unit4 >> 1) + 1));
+  return (mta_pair_keep(h0, 0, p) ? 1u : 0u) | (mta_pair_keep(h0, 1, p) ? 1u << 8 : 0u) |
+         (mta_pair_keep(h1, 0, p) ? 1u << 16 : 0u) | (mta_pair_keep(h1, 1, p) ? 1u << 24 : 0u);
+}
+__device__ __forceinline__ size_t stack_keep_index(int t, int tile, int ntiles, int s, int H, int unit4) {
+  return (((size_t)t * ntiles + tile) * S + s) * (H / 4) + unit4 / 4;
+}
 
 template <int H, int PREC, int FIN0, bool FIRST>
 __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int layer, const int tile,
@@ -210,8 +246,9 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 
   const bool last = layer == a.L - 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool input_wave = wave >= NW;
-  const int w = input_wave ? wave - NW : wave;
+  const int role = wave / NW;  // 0 recurrent, 1 input, 2 store
+  const bool input_wave = role == 1;
+  const int w = wave - role * NW;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
   const int n0 = tile * S;
@@ -225,6 +262,75 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   float bias[4];
 #pragma unroll
   for (int g = 0; g < 4; ++g) bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
+
+  if (role == 2) {
+    // =========================== store waves ===========================
+    float* hseq = a.hseq[layer];
+    float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
+    float* xout = last ? nullptr : a.xdrop[layer + 1];
+    uint32_t* mout = xout ? a.mask[layer + 1] : nullptr;
+    const uint32_t pseed = mout ? mta_pair_seed(a.seeds[layer + 1]) : 0;
+    const float keep_scale = 1.0f / (1.0f - a.drop_p);
+    unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+    const int ts = lane >> 2, tc = 4 * (lane & 3), unit4 = 16 * w + tc;
+    // step t from staging slot t & 1: hand-offs first (h, masked h), then keep word and stash (issue order per
+    // interval, the loop-head vmcnt counts below depend on it)
+    auto store_step = [&](int t) {
+      const int slot = t % 3;
+      const float4 hv = *reinterpret_cast<const float4*>(&sm.hout[slot][ts][unit4]);
+      const size_t o = ((size_t)t * Np + n0 + ts) * H + unit4;
+      if (last) *reinterpret_cast<float4*>(hseq + o) = hv;  // consumed after the kernel: plain store
+      else store_sc1_x4(hseq + o, f32x4{hv.x, hv.y, hv.z, hv.w});
+      if (xout) {
+        const uint32_t kw = stack_keep_word(pseed, (uint32_t)(t * Np + n0 + ts), unit4, a.drop_p);
+        const f32x4 xv{hv.x * ((kw & 0xFFu) ? keep_scale : 0.f), hv.y * ((kw & 0xFF00u) ? keep_scale : 0.f),
+                       hv.z * ((kw & 0xFF0000u) ? keep_scale : 0.f), hv.w * ((kw & 0xFF000000u) ? keep_scale : 0.f)};
+        store_sc1_x4(xout + o, xv);
+        mout[stack_keep_index(t, tile, a.ntiles, ts, H, unit4)] = kw;
+      }
+      if (stash) {
+#pragma unroll
+        for (int k = 0; k < STASH; ++k)
+          stash[stash_index(t, tile, a.ntiles, w, NW, lane) + 64 * k] = sm.st[slot][w][k][lane];
+      }
+    };
+    __syncthreads();  // pre-loop barrier
+    SSTAMP_DECL
+    // interval t (between barriers B(t-1) and B(t), while the recurrent waves run step t) writes out step t-2:
+    // the recurrent waves stage step t-1 in its slot during step t (LDS writes beside their MFMA chain)
+    for (int t = 0; t < T; ++t) {
+      SSTAMP(0)
+      // drain the hand-offs issued two intervals ago (step t-4); newer: that interval's [keep word, stash] and
+      // the previous interval's [h, masked h, keep word, stash].  Immediates: branch on the uniform layout.
+      if (t >= 4) {
+        if (xout) {
+          if (stash) mta_wait_vmcnt<(1 + STASH) + (3 + STASH)>();
+          else mta_wait_vmcnt<1 + 3>();
+        } else {
+          if (stash) mta_wait_vmcnt<STASH + (1 + STASH)>();
+          else mta_wait_vmcnt<1>();
+        }
+      }
+      // progress: the hand-offs of step t-5 were drained by every store wave's wait at the top of interval
+      // t-1, before the barrier that ended it
+      if (!last && t >= 5 && wave == 2 * NW && lane == 0)
+        __hip_atomic_store(my_flag, base + (unsigned)(t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      SSTAMP(1)
+      if (t >= 2 && !MTA_DBG_NO_STORE) store_step(t - 2);
+      SSTAMP(2)
+      __syncthreads();
+      SSTAMP(3)
+    }
+    SSTAMP_FLUSH(0, 1, w == 0)
+    if (T >= 2) store_step(T - 2);
+    __syncthreads();  // F1: step T-1 staged
+    store_step(T - 1);
+    mta_wait_vmem();
+    __syncthreads();  // F2 (final)
+    if (!last && wave == 2 * NW && lane == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
 
   if (input_wave) {
     // =========================== input waves ===========================
@@ -297,6 +403,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       } else {
         // poll only when the last value seen does not cover step t (polling every step from every
         // consumer wave measured slower: the progress words share cache lines across tiles)
+        if (MTA_DBG_NO_LOAD) return;
         seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
         const size_t row = (size_t)t * Np + n0 + j;
 #pragma unroll
@@ -347,7 +454,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
             }
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              if constexpr (PREC == PREC_BF16X3) {
+              if constexpr (PREC == PREC_BF16X3 && !MTA_DBG_INPUT_BF16) {
                 acc[g] = mfma16x16x32(alo, Xhi[g][kb], acc[g]);
                 acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
               }
@@ -359,59 +466,34 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 #pragma unroll
       for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
     };
-    // dropout keep bytes of this layer's output (the next layer's input) for the lanes of recurrent wave w
-    uint32_t* mout = last ? nullptr : a.mask[layer + 1];
-    const uint64_t seed_next = mout ? a.seeds[layer + 1] : 0;
-    auto draw_mask = [&](int t) {
-      if (mout) {
-        uint32_t kb = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t row = (uint32_t)(t * Np + n0 + 4 * q + i);
-          kb |= (mta_dropout_scale(seed_next, row, (uint32_t)u, a.drop_p) != 0.f ? 1u : 0u) << (8 * i);
-        }
-        sm.keep[t & 1][w][lane] = kb;
-        mout[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u] = kb;  // before this interval's loads
-      }
-    };
     load_input(0, xbA);
     compute_gx(0, xbA);
     if (T > 1) load_input(1, xbB);
     if (T > 2) load_input(2, xbA);
     __syncthreads();  // pre-loop barrier: gx_0 ready
-    SSTAMP_DECL
     // interval t computes gx_{t+1} from set (t+1) & 1 and refills that set with x_{t+3}; unrolled by two so
     // the sets are static registers
     auto interval = [&](int t, XBuf& xb) {
-      SSTAMP(0)
-      // step t's keep bytes, into slot t & 1: read by the recurrent waves at the top of step t+1 (and after
-      // the loop for step T-1); the slot is rewritten in interval t+2, after barrier t+1
-      draw_mask(t);
-      if (t + 1 < T) {
+      if (t + 1 < T && !MTA_DBG_NO_INPUT) {
         if constexpr (!FIRST && MTA_STACK_GX_DELAY > 0) __builtin_amdgcn_s_sleep(MTA_STACK_GX_DELAY);
         compute_gx((t + 1) & 1, xb);          // x_{t+1}, loaded two intervals ago
-        SSTAMP(1)
         if (t + 3 < T) load_input(t + 3, xb); // (waits for the producer here, off the recurrent path)
-        SSTAMP(2)
       }
       __syncthreads();
-      SSTAMP(3)
     };
     for (int t = 0; t < T; t += 2) {
       interval(t, xbB);
       if (t + 1 < T) interval(t + 1, xbA);
     }
-    SSTAMP_FLUSH(0, 1, w == 0)
-    __syncthreads();  // final barrier (the recurrent waves publish after it)
+    __syncthreads();  // F1
+    __syncthreads();  // F2 (final; the store waves publish after it)
     return;
   }
 
   // =========================== recurrent waves ===========================
+  if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
   const float* w_hh = a.w_hh[layer];
-  float* hseq = a.hseq[layer];
-  float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
-  float* xout = last ? nullptr : a.xdrop[layer + 1];
-  unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+  const bool stash = a.stash[layer] != nullptr;
 
   bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
   float Bf[4][PREC == PREC_F32 ? KF : 1];
@@ -444,46 +526,21 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 pgi, pgf, pgg, pgo, pcc;
-  float ph[4];
-  // issue order per step: hand-off stores, then the 5 stash stores; the loop-head vmcnt(STASH) then drains
-  // the previous step's hand-offs (in-order completion) and leaves its stash stores another step
-  const float keep_scale = 1.0f / (1.0f - a.drop_p);
-  // h (and its dropout-masked copy) leave as ONE 16-byte store per lane: the wave's 16 x 16 (sequence, unit)
-  // block is transposed through its own LDS scratch (same-wave LDS ops are ordered: no barrier) so lane
-  // (s, c) holds units 4c..4c+3 of sequence s.  Four 4-byte write-through stores per value cost ~75 cycles
-  // each of recurrent-wave issue (r2 stamp probe), a 16-byte one about as much as a plain store.
-  float (*trh)[TRS] = sm.tr[w][0];
-  float (*trx)[TRS] = sm.tr[w][1];
-  const int ts = lane >> 2, tc = 4 * (lane & 3);
-  auto store_step = [&](int t) {
+  float h[4];
+  // step t-1's fp32 h and BPTT stash go to staging slot (t-1) % 3 at the top of step t, where their LDS transfer
+  // overlaps this step's MFMA chain (issued before the barrier they stalled the step ~600 cycles, r3 stamps)
+  auto stage = [&](int t) {
+    const int slot = t % 3;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) trh[4 * q + i][j] = ph[i];
-    if (xout) {
-      const uint32_t kb = sm.keep[t & 1][w][lane];  // drawn by the input waves during step t
-#pragma unroll
-      for (int i = 0; i < 4; ++i) trx[4 * q + i][j] = ph[i] * (((kb >> (8 * i)) & 0xFFu) ? keep_scale : 0.f);
-    }
-    const size_t o = ((size_t)t * Np + n0 + ts) * H + 16 * w + tc;
-    const float4 hv = *reinterpret_cast<const float4*>(&trh[ts][tc]);
-    if (xout) {
-      const float4 xv = *reinterpret_cast<const float4*>(&trx[ts][tc]);
-      store_sc1_x4(xout + o, f32x4{xv.x, xv.y, xv.z, xv.w});
-    }
-    if (last) *reinterpret_cast<float4*>(hseq + o) = hv;  // consumed after the kernel: plain store
-    else store_sc1_x4(hseq + o, f32x4{hv.x, hv.y, hv.z, hv.w});
-  };
-  // the 5 stash stores of step t-1 are spread over the MFMA chain of step t (one per gate group): issued
-  // together at the top they stalled the wave ~1000 cycles on the CU's store path (28 KB per step per
-  // workgroup, r2 stamp probe); between MFMAs the path drains in the background.  Issue order per step stays
-  // [hand-offs, 5 stash], so the loop-head vmcnt(STASH) is unchanged.
-  auto stash_store = [&](int t, int k) {
-    if (stash && t >= 0) {
-      float4* st = stash + stash_index(t, tile, a.ntiles, w, NW, lane) + 64 * k;
-      const f32x4 v = k == 0 ? pgi : k == 1 ? pgf : k == 2 ? pgg : k == 3 ? pgo : pcc;
-      *st = make_float4(v[0], v[1], v[2], v[3]);
+    for (int i = 0; i < 4; ++i) sm.hout[slot][4 * q + i][u] = h[i];
+    if (stash) {
+      sm.st[slot][w][0][lane] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
+      sm.st[slot][w][1][lane] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      sm.st[slot][w][2][lane] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      sm.st[slot][w][3][lane] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      sm.st[slot][w][4][lane] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
     }
   };
-
   SSTAMP_DECL
   for (int t = 0; t < T; ++t) {
     SSTAMP(0)
@@ -498,52 +555,25 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       acc[3][i] = v.w;
     }
     SSTAMP(1)
-    // the hand-off stores issued two tops ago (~two steps of latency budget; one step cost ~200 cycles of
-    // drain per step, r2 stamp probe).  Newer than them: that step's 5 stash stores, the previous top's
-    // hand-offs (h, [masked h]) and its 5 stash stores (wave 0 also has a progress store in between, so
-    // its wait is one op more conservative).  The counts are immediates: branch on the uniform layout.
-    if (t >= 3) {
-      if (stash) {
-        if (xout) mta_wait_vmcnt<2 + 2 * STASH>();
-        else mta_wait_vmcnt<1 + 2 * STASH>();
-      } else {
-        if (xout) mta_wait_vmcnt<2>();
-        else mta_wait_vmcnt<1>();
-      }
-    }
-    // progress: hand-off stores of step t-4 were drained by every recurrent wave's wait at the top of t-1,
-    // before the barrier that ended step t-1
-    if (!last && t >= 4 && threadIdx.x == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    SSTAMP(2)
-    if (t > 0) store_step(t - 1);
-    __builtin_amdgcn_sched_barrier(0);
-    SSTAMP(3)
-
     if constexpr (PREC == PREC_F32) {
+      if (t > 0 && !MTA_DBG_NO_STAGE) stage(t - 1);
       const float* hrow = &h_f[cur][j][q * KF];
 #pragma unroll
       for (int kk = 0; kk < KF; ++kk) {
         const float av = hrow[kk];
 #pragma unroll
         for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Bf[g][kk], acc[g]);
-        if (kk < STASH) {
-          __builtin_amdgcn_sched_barrier(0);
-          stash_store(t - 1, kk);
-          __builtin_amdgcn_sched_barrier(0);
-        }
       }
     } else {
-      // stages of 4 independent MFMAs (one per gate chain): per k-block [lo x hi, hi x lo,] hi x hi; the
-      // stash stores go between stages
-      constexpr int NSTAGE = KB * (PREC == PREC_BF16X3 ? 3 : 1);
-      // every A fragment first (the stage barriers below would otherwise expose each k-block's LDS latency)
+      // every A fragment first, then 4 independent MFMA chains (one per gate): per k-block [lo x hi, hi x lo,]
+      // hi x hi
       bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
         ahi[kb] = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
         if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
       }
+      if (t > 0 && !MTA_DBG_NO_STAGE) stage(t - 1);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
@@ -554,19 +584,11 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
             else if (PREC == PREC_BF16X3 && sg == 1) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
             else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
           }
-          const int stage = kb * (PREC == PREC_BF16X3 ? 3 : 1) + sg;
-          __builtin_amdgcn_sched_barrier(0);
-          // spread the 5 stores over the stages (all of them by the last stage)
-#pragma unroll
-          for (int k = stage * STASH / NSTAGE; k < (stage + 1) * STASH / NSTAGE; ++k) stash_store(t - 1, k);
-          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
-    SSTAMP(4)
-
+    SSTAMP(2)
     const int nb = (t + 1) & 1;
-    float h[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       pgi[i] = mta_sigmoid(acc[0][i]);
@@ -576,8 +598,9 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
       pcc[i] = c[i];
       h[i] = pgo[i] * mta_tanh(c[i]);
-      ph[i] = h[i];
     }
+    SSTAMP(3)
+    // next step's A operand first (the critical path), then the staging slots of the store waves
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s4 = 4 * q + i;
@@ -590,18 +613,14 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
       }
     }
-    SSTAMP(5)
+    SSTAMP(4)
     __syncthreads();
-    SSTAMP(6)
+    SSTAMP(5)
   }
   SSTAMP_FLUSH(0, 0, wave == 0)
-  store_step(T - 1);
-#pragma unroll
-  for (int k = 0; k < STASH; ++k) stash_store(T - 1, k);
-  mta_wait_vmem();
-  __syncthreads();  // final barrier
-  if (!last && threadIdx.x == 0)
-    __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stage(T - 1);
+  __syncthreads();  // F1
+  __syncthreads();  // F2 (final; the store waves have written step T-1)
 }
 
 // batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch);
@@ -639,7 +658,7 @@ __device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P
 }
 
 template <int H, int PREC, int FIN0>
-__global__ __launch_bounds__((H / 16) * 128) void lstm_stack_fwd_kernel(StackFwdArgs a) {
+__global__ __launch_bounds__((H / 16) * 192) void lstm_stack_fwd_kernel(StackFwdArgs a) {
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
   if ((int)blockIdx.x >= a.main_blocks) {
     // batch-copy workgroup (gather mode): no hand-offs, only the copy and the launch arrival
@@ -769,9 +788,10 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       }
     };
     uint32_t mreg = 0x01010101u, mnext = 0x01010101u;
-    auto load_mask = [&](int t) {  // keep bytes of step t (rows 4q+i, unit u), used one interval later
+    const int ts = lane >> 2, tc = 4 * (lane & 3);
+    auto load_mask = [&](int t) {  // keep bytes of step t (row ts, units 16 w + tc + e), used one interval later
       if constexpr (!BOTTOM) {
-        if (min) mnext = min[((size_t)t * a.ntiles + tile) * 4 * H + q * H + u];
+        if (min) mnext = min[stack_keep_index(t, tile, a.ntiles, ts, H, 16 * w + tc)];
       }
     };
     auto stage_dh = [&](int t) {
@@ -799,17 +819,18 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
             ax[kb & 1] = mfma16x16x32(ahi, Xhi[kb], ax[kb & 1]);
           }
         }
-        // one 16-byte write-through store per lane (transpose through the wave's own LDS scratch)
+        // one 16-byte write-through store per lane (transpose through the wave's own LDS scratch); the input
+        // dropout mask (keep words in this store layout) is applied after the transpose
         float (*tr)[TRS] = sm.tr[w];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
-          if (min) v *= ((mreg >> (8 * i)) & 0xFFu) ? keep_scale : 0.f;
-          tr[4 * q + i][j] = v;
-        }
-        const int ts = lane >> 2, tc = 4 * (lane & 3);
+        for (int i = 0; i < 4; ++i) tr[4 * q + i][j] = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
         const float4 dv = *reinterpret_cast<const float4*>(&tr[ts][tc]);
-        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, f32x4{dv.x, dv.y, dv.z, dv.w});
+        f32x4 o{dv.x, dv.y, dv.z, dv.w};
+        if (min) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= ((mreg >> (8 * e)) & 0xFFu) ? keep_scale : 0.f;
+        }
+        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
       }
     };
     if constexpr (!TOP) {
@@ -865,6 +886,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   }
 
   // =========================== recurrent waves ===========================
+  if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
   const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
   const float* w_hh = a.w_hh[layer];
   float* dG = a.dG[layer];
@@ -1059,7 +1081,7 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
 
 template <int H, int PREC>
 int launch_fwd(int fin, const StackFwdArgs& a, hipStream_t st) {
-  const dim3 grid(a.main_blocks + (a.gather ? a.copy_blocks : 0)), block((H / 16) * 128);  // + batch-copy blocks
+  const dim3 grid(a.main_blocks + (a.gather ? a.copy_blocks : 0)), block((H / 16) * 192);  // + batch-copy blocks
   if (fin == 3) lstm_stack_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(a);
   else if (fin == 5) lstm_stack_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(a);
   else return -1;

@@ -7,6 +7,7 @@
 // Stamp builds are slower than the real kernel (each stamp waits lgkmcnt): read the SHARES there and the
 // absolute times from the stamp-free build.
 #include <cstdio>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -46,7 +47,7 @@ int main(int argc, char** argv) {
   const int mode = argc > 5 ? atoi(argv[5]) : 0;
   const float p = mode == 0 ? 0.2f : 0.0f;
   const int Np = (N + 15) / 16 * 16;
-  if (L < 2 || L > 8 || N < 1 || T < 4 || T > 1000) {
+  if (L < 1 || L > 8 || N < 1 || T < 4 || T > 1000) {
     printf("bad arguments\n");
     return 1;
   }
@@ -128,6 +129,46 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&m, a, b));
     if (rep >= skip) ms_b += m / (reps - skip);
   }
+  // determinism: two forwards with the same seeds must agree bitwise (h of every layer at every step)
+  {
+    std::vector<std::vector<float>> ref(L), again(L);
+    for (int pass = 0; pass < 2; ++pass) {
+      CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
+      int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
+                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
+      CK(hipDeviceSynchronize());
+      if (rc) return 1;
+      for (int l = 0; l < L; ++l) {
+        auto& v = pass ? again[l] : ref[l];
+        v.resize((size_t)T * Np * H);
+        CK(hipMemcpy(v.data(), hseq[l], v.size() * 4, hipMemcpyDeviceToHost));
+      }
+    }
+    long bad = 0;
+    double maxd = 0;
+    for (int l = 0; l < L; ++l)
+      for (int t = 0; t < T; ++t)
+        for (int n = 0; n < N; ++n)
+          for (int u = 0; u < H; ++u) {
+            const size_t i = ((size_t)t * Np + n) * H + u;
+            const double d = fabs((double)ref[l][i] - again[l][i]);
+            if (d != 0) ++bad;
+            if (d > maxd) maxd = d;
+          }
+    printf("determinism: %ld of %ld h values differ between two identical forwards (max |d| %.3e)\n", bad,
+           (long)L * T * N * H, maxd);
+  }
+  // checksums (variants of the kernel must agree): last layer's h at T-1 and layer 0's W_hh gradient after reps runs
+  {
+    std::vector<float> hl((size_t)Np * H), gw((size_t)4 * H * H);
+    CK(hipMemcpy(hl.data(), hseq[L - 1] + (size_t)(T - 1) * Np * H, hl.size() * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(gw.data(), gwhh[0], gw.size() * 4, hipMemcpyDeviceToHost));
+    double s1 = 0, s2 = 0;
+    for (int n = 0; n < N; ++n)
+      for (int u = 0; u < H; ++u) s1 += (double)hl[(size_t)n * H + u] * (1 + (n * 7 + u) % 5);
+    for (size_t i = 0; i < gw.size(); ++i) s2 += (double)gw[i] * (1 + i % 3);
+    printf("checksum h=%.9e gwhh=%.9e\n", s1, s2);
+  }
   unsigned tmo = 0;
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
   printf("mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
@@ -138,13 +179,13 @@ int main(int argc, char** argv) {
   unsigned long long acc[2][2][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
   const char* seg[2][2][8] = {
-      {{"", "gx_lds_read", "vmcnt_drain", "store_issue", "mfma_chain", "act+lds_write", "barrier", ""},
-       {"", "mask+compute_gx", "load_input(poll)", "barrier", "", "", "", ""}},
+      {{"", "gx_lds_read", "mfma_chain", "activations", "lds_write", "barrier", "", ""},
+       {"", "vmcnt_drain+flag", "store_step", "barrier", "", "", "", ""}},
       {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
         "mfma_dh"},
        {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
-  const char* role[2][2] = {{"recurrent", "input"}, {"recurrent", "gradient"}};
+  const char* role[2][2] = {{"recurrent", "store"}, {"recurrent", "gradient"}};
   for (int d = 0; d < 2; ++d)
     for (int r = 0; r < 2; ++r) {
       unsigned long long tot = 0;

@@ -282,7 +282,7 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     xdrop = [E] + [torch.empty((T, Np, H), device=dev, dtype=torch.float32) if drop else E for _ in range(1, L)]
     EB = _empty(dev, torch.uint8)
     # keep bytes of every inter-layer dropout, drawn by the forward's input waves and read by the backward's
-    # dx masks (u32 words (T, ntiles, 4, H): byte i of a word = sequence 4q+i of a lane)
+    # dx keep bytes (u32 words (T, ntiles, 16, H/4): byte e of word (t, tile, s, c) = unit 4c+e of sequence s)
     masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
     flags = _stack_flags(C, Np, L, dev, T)

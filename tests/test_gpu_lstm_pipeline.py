@@ -21,31 +21,20 @@ def _weights(F, H, L, seed=0):
     return ws
 
 
-def _hash3(seed: int, a: np.ndarray, b: np.ndarray) -> np.ndarray:
-    """Python mirror of mta_hash3 (csrc/common.h)."""
+def _pair_hash(seed: int, rows: np.ndarray, cols: np.ndarray) -> np.ndarray:
+    """Python mirror of the LSTM keep-bit hash (csrc/common.h mta_pair_seed / mta_pair_col / mta_pair_hash,
+    csrc/lstm_stack.hip stack_keep_word): one hash per (row, column pair), 16-bit uniform per column."""
     M = np.uint64(0xFFFFFFFF)
-
-    def u32(v):
-        return np.asarray(v, dtype=np.uint64) & M
-
-    def rotl(x, r):
-        return ((x << np.uint64(r)) | (x >> np.uint64(32 - r))) & M
-
-    h = u32(np.full(a.shape, (seed & 0xFFFFFFFF) ^ 0x9E3779B9, dtype=np.uint64))
-    for k in (u32(np.full(a.shape, seed >> 32, dtype=np.uint64)), u32(a), u32(b)):
-        x = (k * np.uint64(0xCC9E2D51)) & M
-        x = rotl(x, 15)
-        x = (x * np.uint64(0x1B873593)) & M
-        h = h ^ x
-        h = rotl(h, 13)
-        h = (h * np.uint64(5) + np.uint64(0xE6546B64)) & M
-    h = h ^ np.uint64(12)
-    h = h ^ (h >> np.uint64(16))
-    h = (h * np.uint64(0x85EBCA6B)) & M
-    h = h ^ (h >> np.uint64(13))
-    h = (h * np.uint64(0xC2B2AE35)) & M
-    h = h ^ (h >> np.uint64(16))
-    return h
+    pseed = np.uint64((seed & 0xFFFFFFFF) ^ (((seed >> 32) * 0x27D4EB2F) & 0xFFFFFFFF))
+    b = (np.asarray(cols >> 1, dtype=np.uint64) * np.uint64(0x85EBCA77)) & M
+    pcol = ((b << np.uint64(13)) | (b >> np.uint64(19))) & M
+    x = pseed ^ ((np.asarray(rows, dtype=np.uint64) * np.uint64(0x9E3779B1)) & M) ^ pcol
+    x = x ^ (x >> np.uint64(16))
+    x = (x * np.uint64(0x7FEB352D)) & M
+    x = x ^ (x >> np.uint64(15))
+    x = (x * np.uint64(0x846CA68B)) & M
+    x = x ^ (x >> np.uint64(16))
+    return (x >> (np.uint64(16) * (np.asarray(cols, dtype=np.uint64) & np.uint64(1)))) & np.uint64(0xFFFF)
 
 
 def _mask(seed: int, T: int, Np: int, N: int, H: int, p: float) -> torch.Tensor:
@@ -55,8 +44,7 @@ def _mask(seed: int, T: int, Np: int, N: int, H: int, p: float) -> torch.Tensor:
     u = np.arange(H)[None, None, :]
     rows = np.broadcast_to(t * Np + n, (T, N, H))
     cols = np.broadcast_to(u, (T, N, H))
-    hv = _hash3(seed, rows, cols)
-    uni = (hv >> np.uint64(8)).astype(np.float64) / 16777216.0
+    uni = _pair_hash(seed, rows, cols).astype(np.float64) / 65536.0
     keep = (uni >= p).astype(np.float64) / (1.0 - p)
     return torch.from_numpy(keep).permute(1, 0, 2).contiguous()
 
