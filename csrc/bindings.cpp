@@ -88,16 +88,18 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 int mta_lstm_stack_epoch_shift(int T);
-// allreduce.hip (one-shot all-reduce over xGMI peer memory)
+// allreduce.hip (one-shot / two-shot all-reduce over xGMI peer memory, one channel per bucket)
 int mta_xgmi_alloc(long bytes, void** out);
 int mta_xgmi_free(void* p);
 int mta_xgmi_ipc_handle(void* p, unsigned char* out64);
 int mta_xgmi_ipc_open(const unsigned char* in64, void** out);
 int mta_xgmi_ipc_close(void* p);
-long mta_xgmi_layout(int world, long cap, long* flags_off);
+long mta_xgmi_buffer_bytes(int world, long cap, int channels);
 int mta_xgmi_ctl_words();
-int mta_xgmi_allreduce(float* grad, long n, long cap, void* const* bufs, int rank, int world, unsigned* ctl,
-                       hipStream_t st);
+int mta_xgmi_max_channels();
+int mta_xgmi_timeout_word();
+int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int channels, int twoshot,
+                       void* const* bufs, int rank, int world, unsigned* ctl, hipStream_t st);
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
             float idio_loc, float idio_scale, float a_loc, float a_scale, float b_loc, float b_scale, float* r_market,
@@ -778,9 +780,8 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
 
 
 // ------------------------------------------------------------------------------- xGMI all-reduce
-int64_t xgmi_buffer_bytes(int64_t world, int64_t cap) {
-  long off = 0;
-  return (int64_t)mta_xgmi_layout((int)world, (long)cap, &off);
+int64_t xgmi_buffer_bytes(int64_t world, int64_t cap, int64_t channels) {
+  return (int64_t)mta_xgmi_buffer_bytes((int)world, (long)cap, (int)channels);
 }
 
 int64_t xgmi_alloc(int64_t bytes) {
@@ -808,16 +809,19 @@ int64_t xgmi_ipc_open(at::Tensor handle) {
 
 void xgmi_ipc_close(int64_t p) { mta_xgmi_ipc_close(reinterpret_cast<void*>(p)); }
 
-// in-place sum of `grad` over the ranks; bufs: every rank's comm buffer as mapped in this process;
-// ctl: int32[xgmi_ctl_words] zero-initialised once (epoch, arrival counter, timeout count)
-void xgmi_allreduce(at::Tensor grad, int64_t cap, std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl) {
+// in-place sum of `grad` (a bucket at flat offset `off` of the gradient) over the ranks on the current stream;
+// bufs: every rank's comm buffer as mapped in this process; ctl: int32[xgmi_ctl_words] zero-initialised once
+// (per-channel epoch and arrival counters, the shared timeout count)
+void xgmi_allreduce(at::Tensor grad, int64_t off, int64_t cap, int64_t channel, int64_t channels, bool twoshot,
+                    std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl) {
   MTA_CHECK_F32(grad);
   TORCH_CHECK(ctl.is_cuda() && ctl.scalar_type() == at::kInt && ctl.numel() >= mta_xgmi_ctl_words(), "ctl words");
   std::vector<void*> b;
   for (auto v : bufs) b.push_back(reinterpret_cast<void*>(v));
   c10::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
-  const int rc = mta_xgmi_allreduce(grad.data_ptr<float>(), (long)grad.numel(), (long)cap, b.data(), (int)rank,
-                                    (int)b.size(), reinterpret_cast<unsigned*>(ctl.data_ptr<int>()), cur_stream());
+  const int rc = mta_xgmi_allreduce(grad.data_ptr<float>(), (long)grad.numel(), (long)off, (long)cap, (int)channel,
+                                    (int)channels, twoshot ? 1 : 0, b.data(), (int)rank, (int)b.size(),
+                                    reinterpret_cast<unsigned*>(ctl.data_ptr<int>()), cur_stream());
   TORCH_CHECK(rc == 0, "xgmi_allreduce: bad arguments (rc=", rc, ")");
 }
 
@@ -959,6 +963,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_ipc_close", &xgmi_ipc_close);
   m.def("xgmi_allreduce", &xgmi_allreduce);
   m.def("xgmi_ctl_words", []() { return (int64_t)mta_xgmi_ctl_words(); });
+  m.def("xgmi_max_channels", []() { return (int64_t)mta_xgmi_max_channels(); });
+  m.def("xgmi_timeout_word", []() { return (int64_t)mta_xgmi_timeout_word(); });
   m.def("lstm_wgrad_part_floats", [](int64_t fused, int64_t T, int64_t H, int64_t F) {
     return (int64_t)mta_lstm_wgrad_part_floats((int)fused, (int)T, (int)H, (int)F);
   });

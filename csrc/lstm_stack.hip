@@ -32,6 +32,22 @@
 // s_sleep units (~64 cycles each) the helper waves wait after a step barrier before their MFMA product (the
 // forward input waves' W_ih x of layers >= 1, the backward gradient waves' dx): right after the barrier the
 // recurrent waves run their own MFMA chain on the same SIMDs, and two MFMA streams on one SIMD serialise.
+// timeline build (probe only): s_memtime of every forward workgroup's recurrent wave 0 at entry, after the pre-loop
+// barrier, after step T/2 and at the end
+#ifndef MTA_STACK_TIMELINE
+#define MTA_STACK_TIMELINE 0
+#endif
+#if MTA_STACK_TIMELINE
+__device__ unsigned long long mta_stack_tl[2][64][4];
+#define STACK_TL(dir, k)                                                                      \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < 64) mta_stack_tl[(dir)][blockIdx.x][(k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define STACK_TL(dir, k) \
+  do {                   \
+  } while (0)
+#endif
 #ifndef MTA_STACK_GX_DELAY
 #define MTA_STACK_GX_DELAY 0
 #endif
@@ -62,7 +78,7 @@
 #if MTA_STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
-__device__ unsigned long long mta_stack_stamp_acc[2][2][8];
+__device__ unsigned long long mta_stack_stamp_acc[2][3][8];
 __device__ int mta_stack_stamp_block[2];  // block whose waves are stamped, per direction (probe sets it)
 #define SSTAMP_DECL unsigned long long _ts_prev = 0, _ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define SSTAMP(k)                                                                  \
@@ -218,6 +234,10 @@ struct FwdSmem {
   __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
+  // layers >= 1: the layer input x_t (slot t & 1) in the MFMA A-operand layout, filled a quarter per input wave
+  __bf16 x_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  __bf16 x_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  float x_f[2][S][PREC == PREC_F32 ? ROWF : 4];
   float hout[3][S][ROWF];              // h_t in fp32, natural unit order (slot t % 3), for the store waves
   float4 st[3][H / 16][STASH][64];     // BPTT stash of step t (slot t % 3), per recurrent wave, lane-major
 };
@@ -294,7 +314,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           stash[stash_index(t, tile, a.ntiles, w, NW, lane) + 64 * k] = sm.st[slot][w][k][lane];
       }
     };
-    __syncthreads();  // pre-loop barrier
+    __syncthreads();  // P0
+    __syncthreads();  // P1 (pre-loop)
     SSTAMP_DECL
     // interval t (between barriers B(t-1) and B(t), while the recurrent waves run step t) writes out step t-2:
     // the recurrent waves stage step t-1 in its slot during step t (LDS writes beside their MFMA chain)
@@ -466,31 +487,135 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 #pragma unroll
       for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
     };
-    load_input(0, xbA);
-    compute_gx(0, xbA);
-    if (T > 1) load_input(1, xbB);
-    if (T > 2) load_input(2, xbA);
-    __syncthreads();  // pre-loop barrier: gx_0 ready
-    // interval t computes gx_{t+1} from set (t+1) & 1 and refills that set with x_{t+3}; unrolled by two so
-    // the sets are static registers
-    auto interval = [&](int t, XBuf& xb) {
-      if (t + 1 < T && !MTA_DBG_NO_INPUT) {
-        if constexpr (!FIRST && MTA_STACK_GX_DELAY > 0) __builtin_amdgcn_s_sleep(MTA_STACK_GX_DELAY);
-        compute_gx((t + 1) & 1, xb);          // x_{t+1}, loaded two intervals ago
-        if (t + 3 < T) load_input(t + 3, xb); // (waits for the producer here, off the recurrent path)
+    SSTAMP_DECL
+    if constexpr (FIRST) {
+      load_input(0, xbA);
+      compute_gx(0, xbA);
+      if (T > 1) load_input(1, xbB);
+      if (T > 2) load_input(2, xbA);
+      __syncthreads();  // P0
+      __syncthreads();  // P1 (pre-loop): gx_0 ready
+      // interval t computes gx_{t+1} from set (t+1) & 1 and refills that set with x_{t+3}; unrolled by two so
+      // the sets are static registers
+      auto interval = [&](int t, XBuf& xb) {
+        SSTAMP(0)
+        if (t + 1 < T && !MTA_DBG_NO_INPUT) {
+          SSTAMP(1)
+          compute_gx((t + 1) & 1, xb);          // x_{t+1}, loaded two intervals ago
+          SSTAMP(2)
+          if (t + 3 < T) load_input(t + 3, xb);
+          SSTAMP(3)
+        }
+        __syncthreads();
+        SSTAMP(4)
+      };
+      for (int t = 0; t < T; t += 2) {
+        interval(t, xbB);
+        if (t + 1 < T) interval(t + 1, xbA);
       }
-      __syncthreads();
-    };
-    for (int t = 0; t < T; t += 2) {
-      interval(t, xbB);
-      if (t + 1 < T) interval(t + 1, xbA);
+    } else {
+      // Layers >= 1: every input wave loads a QUARTER of x_t (units [16w, 16w + 16) of the 16 sequences: one
+      // float4 per lane) and writes it split into the shared LDS image; every wave then reads its MFMA A
+      // fragments from the image.  4x fewer hand-off loads and splits per wave than each wave loading all of
+      // x_t (r3 stamps: that input work set the layer-1 pace).  x_s is polled + loaded 4 intervals ahead into
+      // register set s & 1, written into image slot s & 1 two intervals ahead, consumed one interval ahead.
+      const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
+      float4 xqA = make_float4(0.f, 0.f, 0.f, 0.f), xqB = xqA;
+      unsigned seen = base;
+      auto load_q = [&](int t, float4& xq) {
+        if (MTA_DBG_NO_LOAD) return;
+        seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
+        xq = load_sc1(xin, ((size_t)t * Np + n0 + ls) * H + lu);
+      };
+      auto write_q = [&](int t, const float4& xq) {
+        const int slot = t & 1;
+        if constexpr (PREC == PREC_F32) {
+          *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
+        } else {
+          const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
+          bf16x4 hi4, lo4;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            __bf16 hi, lo;
+            split_bf16(xv[e], hi, lo);
+            hi4[e] = hi;
+            lo4[e] = lo;
+          }
+          *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
+          if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
+        }
+      };
+      auto compute_gx_img = [&](int t) {  // gx_t from image slot t & 1 into gxs slot t & 1
+        const int slot = t & 1;
+        f32x4 acc[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
+        if constexpr (PREC == PREC_F32) {
+          const float* xr = &sm.x_f[slot][j][KF * q];
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) {
+            const float av = xr[kk];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
+          }
+        } else {
+          bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            ahi[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_hi[slot][j][32 * kb + 8 * q]);
+            if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_lo[slot][j][32 * kb + 8 * q]);
+          }
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if constexpr (PREC == PREC_BF16X3 && !MTA_DBG_INPUT_BF16) {
+                acc[g] = mfma16x16x32(alo[kb], Xhi[g][kb], acc[g]);
+                acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
+              }
+              acc[g] = mfma16x16x32(ahi[kb], Xhi[g][kb], acc[g]);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+      };
+      load_q(0, xqA);
+      if (T > 1) load_q(1, xqB);
+      write_q(0, xqA);
+      if (T > 1) write_q(1, xqB);
+      if (T > 2) load_q(2, xqA);
+      if (T > 3) load_q(3, xqB);
+      __syncthreads();  // P0: image slots 0 and 1 complete
+      compute_gx_img(0);
+      __syncthreads();  // P1 (pre-loop): gx_0 ready
+      // interval t: x_{t+2} (set t & 1) -> image slot t & 1 (x_t there was consumed in interval t-1); gx_{t+1}
+      // from slot (t+1) & 1; refill set t & 1 with x_{t+4}
+      auto interval = [&](int t, float4& xq) {
+        SSTAMP(0)
+        if (!MTA_DBG_NO_INPUT) {
+          if (t + 2 < T) write_q(t + 2, xq);
+          SSTAMP(1)
+          if (t + 1 < T) compute_gx_img(t + 1);
+          SSTAMP(2)
+          if (t + 4 < T) load_q(t + 4, xq);
+          SSTAMP(3)
+        }
+        __syncthreads();
+        SSTAMP(4)
+      };
+      for (int t = 0; t < T; t += 2) {
+        interval(t, xqA);
+        if (t + 1 < T) interval(t + 1, xqB);
+      }
     }
+    SSTAMP_FLUSH(0, 2, w == 0)
     __syncthreads();  // F1
     __syncthreads();  // F2 (final; the store waves publish after it)
     return;
   }
 
   // =========================== recurrent waves ===========================
+  STACK_TL(0, 0);
   if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
   const float* w_hh = a.w_hh[layer];
   const bool stash = a.stash[layer] != nullptr;
@@ -522,7 +647,9 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     if constexpr (PREC == PREC_BF16X3)
       for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
   }
-  __syncthreads();  // pre-loop barrier
+  __syncthreads();  // P0
+  __syncthreads();  // P1 (pre-loop)
+  STACK_TL(0, 1);
 
   float c[4] = {0.f, 0.f, 0.f, 0.f};
   f32x4 pgi, pgf, pgg, pgo, pcc;
@@ -616,11 +743,13 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     SSTAMP(4)
     __syncthreads();
     SSTAMP(5)
+    if (t == T / 2) STACK_TL(0, 2);
   }
   SSTAMP_FLUSH(0, 0, wave == 0)
   stage(T - 1);
   __syncthreads();  // F1
   __syncthreads();  // F2 (final; the store waves have written step T-1)
+  STACK_TL(0, 3);
 }
 
 // batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch);

@@ -129,6 +129,26 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&m, a, b));
     if (rep >= skip) ms_b += m / (reps - skip);
   }
+#if MTA_STACK_TIMELINE
+  {
+    // the last forward of the timed loop: per layer, min over tiles of entry / loop start / step T/2 / end
+    unsigned long long tl[2][64][4];
+    CK(hipMemcpyFromSymbol(tl, HIP_SYMBOL(mta_stack_tl), sizeof(tl)));
+    const int ntl = Np / 16, tr8l = (ntl + 7) / 8 * 8;
+    unsigned long long t0 = ~0ull;
+    for (int l = 0; l < L; ++l)
+      for (int i = 0; i < ntl && l * tr8l + i < 64; ++i) t0 = tl[0][l * tr8l + i][0] < t0 ? tl[0][l * tr8l + i][0] : t0;
+    for (int l = 0; l < L; ++l) {
+      double v[4] = {0, 0, 0, 0};
+      int cnt = 0;
+      for (int i = 0; i < ntl && l * tr8l + i < 64; ++i, ++cnt)
+        for (int k = 0; k < 4; ++k) v[k] += (double)(tl[0][l * tr8l + i][k] - t0);
+      printf("timeline fwd layer %d (cycles from first entry, mean of %d tiles): entry %.0f start %.0f mid %.0f end %.0f"
+             "  -> pace %.0f cycles/step (second half)\n",
+             l, cnt, v[0] / cnt, v[1] / cnt, v[2] / cnt, v[3] / cnt, (v[3] - v[2]) / cnt / (T - 1 - T / 2));
+    }
+  }
+#endif
   // determinism: two forwards with the same seeds must agree bitwise (h of every layer at every step)
   {
     std::vector<std::vector<float>> ref(L), again(L);
@@ -176,18 +196,21 @@ int main(int argc, char** argv) {
          mode, N, L, T, prec, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
 #if MTA_STACK_STAMPS
-  unsigned long long acc[2][2][8];
+  unsigned long long acc[2][3][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
-  const char* seg[2][2][8] = {
+  const char* seg[2][3][8] = {
       {{"", "gx_lds_read", "mfma_chain", "activations", "lds_write", "barrier", "", ""},
-       {"", "vmcnt_drain+flag", "store_step", "barrier", "", "", "", ""}},
+       {"", "vmcnt_drain+flag", "store_step", "barrier", "", "", "", ""},
+       {"", "write_x(load_wait)", "compute_gx", "poll+load_issue", "barrier", "", "", ""}},
       {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
         "mfma_dh"},
-       {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""}}};
+       {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""},
+       {"", "", "", "", "", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
-  const char* role[2][2] = {{"recurrent", "store"}, {"recurrent", "gradient"}};
+  const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "gradient", ""}};
   for (int d = 0; d < 2; ++d)
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < 3; ++r) {
+      if (!role[d][r][0]) continue;
       unsigned long long tot = 0;
       for (int s = 1; s < 8; ++s) tot += acc[d][r][s];
       printf("  %s %-9s cycles/step total=%6.0f :", dir[d], role[d][r], (double)tot / T);

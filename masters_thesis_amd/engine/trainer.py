@@ -258,7 +258,7 @@ class Trainer:
                 and getattr(self.model, "graph_capturable", True))
 
     def _allreduce_in_graph(self) -> bool:
-        # the xGMI one-shot all-reduce is a plain kernel: the whole step (sync + optimizer) is one graph.
+        # the xGMI all-reduce (one- or two-shot) is a plain kernel: the whole step (sync + optimizer) is one graph.
         # RCCL stays outside unless MTA_GRAPH_ALLREDUCE=1 (graph capture of RCCL is not exercised here).
         return (self.ddp.world == 1 or getattr(self.ddp, "graph_safe", False)
                 or os.environ.get("MTA_GRAPH_ALLREDUCE", "0") == "1")

@@ -12,9 +12,11 @@ xGMI is point-to-point (7 links x ~153 GB/s), so a ring all-reduce is per-link
 bound and a few large buckets beat many small ones — the default bucket is 64 MB,
 and buckets are issued asynchronously so RCCL can pipeline them.
 
-On one node the flat bucket goes through the one-shot xGMI all-reduce instead (``parallel/xgmi.py``: one
-kernel, every peer written directly over its own link, summed locally in rank order), which is also safe to
-capture inside the step's HIP graph (``graph_safe``); ``MTA_ALLREDUCE=rccl`` keeps RCCL.
+On one node every bucket goes through the xGMI all-reduce instead (``parallel/xgmi.py``: one kernel per
+bucket, one-shot for small buckets, reduce-scatter + all-gather over all 7 links for large ones, summed in rank
+order), which is also safe to capture inside the step's HIP graph (``graph_safe``), so grouped multi-step
+graphs stay on for world > 1 whatever the model size; ``MTA_ALLREDUCE=rccl`` keeps RCCL (eager, after the
+captured backward).
 """
 from __future__ import annotations
 
@@ -43,6 +45,9 @@ class FlatDDP:
             from .xgmi import XgmiAllReduce
 
             self.xgmi = XgmiAllReduce.create(flat.padded, flat.grad.device, group)
+        # xGMI buckets (4-float aligned ranges of the flat gradient, one channel each)
+        xper = max(4096, int(float(os.environ.get("MTA_XGMI_BUCKET_MB", "64")) * (1 << 20) / 4) // 4096 * 4096)
+        self.xgmi_buckets: List[slice] = [slice(i, min(i + xper, n)) for i in range(0, n, xper)]
 
     @property
     def backend_name(self) -> str:
@@ -76,7 +81,8 @@ class FlatDDP:
             return
         g = self.flat.grad
         if self.xgmi is not None:
-            self.xgmi.allreduce_(g)
+            for k, b in enumerate(self.xgmi_buckets):
+                self.xgmi.allreduce_(g[b], off=b.start, channel=k % self.xgmi.channels)
             return
         if self._gloo_cpu:
             t = g.cpu()

@@ -1,7 +1,7 @@
 #!/bin/bash
 # LSTM stack probe session: stamp / timing probes (tools_bin/stack_s0 = timing build, stack_s1 = s_memtime
 # stamp build; build both with scripts/build_probes.sh first), then optional GPU tests and headline bench.
-# OUT=<subdir of gpurun_out>  SPECS="N L prec T mode [stamp-layer];..."  PYTEST=1  BENCH=1  PROF=1
+# OUT=<subdir of gpurun_out>  SPECS="N L prec T mode [stamp-layer];..."  PYTEST=1 [PYTEST_K=expr]  BENCH=1  PROF=1
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${OUT:-probe}
 mkdir -p $OUT
@@ -15,7 +15,7 @@ for spec in "${SPEC_LIST[@]}"; do
   done
 done
 if [ -n "$PYTEST" ]; then
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1; rc=$?; st "pytest rc=$rc"; fatal $rc pytest
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > $OUT/pytest_gpu.log 2>&1; rc=$?; st "pytest rc=$rc"; fatal $rc pytest
 fi
 if [ -n "$BENCH" ]; then
   for b in ${BENCH_BATCHES:-1}; do
