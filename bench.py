@@ -11,7 +11,7 @@ step: batch gather, forward, fused loss, backward, RCCL gradient all-reduce
 (N > 1), clip + Adam, metric accumulation — replayed from the captured HIP graph
 exactly as ``train.py`` runs it.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model M] [--trainer T] [--concurrent k]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Weak scaling: ``--batch`` windows per GPU per step (global batch = B * N).
@@ -31,9 +31,13 @@ import torch
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO))
 
-# vs_baseline: the same-node reference-equivalent PyTorch path (``--backend torch --no-graphs``: nn.LSTM on
-# MIOpen + autograd, eager, 1 MI355X), measured by this bench (profiles/r2_bench_same_node_torch_vs_hip.jsonl);
-# samples/s per GPU keyed (model, loss, per-GPU batch).  Weak scaling: the baseline of N GPUs is N x this.
+# vs_baseline: the same-node reference-equivalent PyTorch path at its best -- ``--backend torch`` (nn.LSTM on MIOpen
+# + autograd, heads/loss/optimizer as here) with the whole step captured in a HIP graph, 1 MI355X -- measured by
+# this bench (profiles/r2_bench_same_node_torch_vs_hip.jsonl, hip_graphs=true rows); vs_torch_eager divides by the
+# same path run eagerly (``--no-graphs``).  samples/s per GPU keyed (model, loss, per-GPU batch); weak scaling:
+# the baseline of N GPUs is N x this.
+SAME_NODE_TORCH_GRAPH = {("small", "mse", 1): 508.881, ("medium", "mse", 1): 260.867, ("large", "mse", 1): 132.121,
+                         ("small", "mse", 8): 3090.277, ("small", "mse", 64): 4152.196}
 SAME_NODE_TORCH_EAGER = {("small", "mse", 1): 169.863, ("medium", "mse", 1): 85.333, ("large", "mse", 1): 44.098,
                          ("small", "mse", 8): 2047.487, ("small", "mse", 64): 4144.375}
 # the 8-vCPU CPU replica of the reference step (BASELINE.md yardstick rows); reported as vs_cpu_yardstick
@@ -67,11 +71,81 @@ def parse_args(argv=None):
                     help="extra config override (repeatable), e.g. --set model.dropout=0")
     ap.add_argument("--residency", default="device", choices=["device", "stream"],
                     help="device: split resident in HBM; stream: pinned host ring + side-stream H2D per step")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="k independent trainers, one process each, on ONE GPU (the sweep launcher's "
+                         "jobs_per_device); value = their summed samples/s over a common start barrier")
     return ap.parse_args(argv)
+
+
+def _child_barrier() -> None:
+    """--concurrent children: wait until every sibling finished its warm-up (file barrier), then time together."""
+    d = os.environ.get("MTA_BENCH_BARRIER")
+    if not d:
+        return
+    k, me = int(os.environ["MTA_BENCH_NCHILD"]), int(os.environ["MTA_BENCH_CHILD"])
+    Path(d, f"ready.{me}").touch()
+    t0 = time.time()
+    while len(list(Path(d).glob("ready.*"))) < k:
+        if time.time() - t0 > 900:
+            raise RuntimeError("concurrent bench: siblings never became ready")
+        time.sleep(0.01)
+
+
+def run_concurrent(args, argv) -> None:
+    """Spawn ``args.concurrent`` single-GPU bench processes on the same device and aggregate their lines."""
+    import subprocess
+    import tempfile
+
+    k = args.concurrent
+    if not 1 < k <= 8:
+        raise SystemExit("--concurrent: 2..8 processes per GPU")
+    raw = list(sys.argv[1:] if argv is None else argv)
+    child_argv, skip = [], False
+    for a in raw:
+        if skip:
+            skip = False
+            continue
+        if a == "--concurrent":
+            skip = True
+            continue
+        if a.startswith("--concurrent="):
+            continue
+        child_argv.append(a)
+    with tempfile.TemporaryDirectory(prefix="mta_bench_") as d:
+        procs = []
+        for i in range(k):
+            env = dict(os.environ, MTA_BENCH_BARRIER=d, MTA_BENCH_NCHILD=str(k), MTA_BENCH_CHILD=str(i))
+            for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+                env.pop(v, None)
+            procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *child_argv], env=env,
+                                          stdout=subprocess.PIPE, text=True))
+        outs = [p.communicate()[0] for p in procs]
+        rcs = [p.returncode for p in procs]
+    if any(rcs):
+        raise SystemExit(f"concurrent bench: child exit codes {rcs}")
+    recs = [json.loads([ln for ln in o.splitlines() if ln.startswith("{")][-1]) for o in outs]
+    rec = dict(recs[0])
+    total = sum(r["value"] for r in recs)
+    rec["value"] = round(total, 3)
+    rec["ms_per_step"] = round(max(r["ms_per_step"] for r in recs), 4)
+    rec["p50_step_ms"] = round(max(r["p50_step_ms"] for r in recs), 4)
+    rec["p90_step_ms"] = round(max(r["p90_step_ms"] for r in recs), 4)
+    rec["concurrent_trainers"] = k
+    rec["per_trainer_samples_per_s"] = [r["value"] for r in recs]
+    rec["vs_baseline"] = None if recs[0]["vs_baseline"] is None else round(
+        total / (recs[0]["value"] / recs[0]["vs_baseline"]), 3)
+    rec["vs_torch_eager"] = None
+    rec["vs_cpu_yardstick"] = None
+    rec["config"] = dict(rec["config"], parallelism=f"{k} independent trainers on 1 GPU (trial packing)",
+                         global_batch=rec["config"]["global_batch"] * k)
+    print(json.dumps(rec), flush=True)
 
 
 def main(argv=None):
     args = parse_args(argv)
+    if args.concurrent > 1 and not os.environ.get("MTA_BENCH_CHILD"):
+        run_concurrent(args, argv)
+        return
     from masters_thesis_amd.config import compose
     from masters_thesis_amd.data import FinancialLstmDataModule
     from masters_thesis_amd.engine import Trainer
@@ -122,6 +196,7 @@ def main(argv=None):
         step(S)
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    _child_barrier()
     pdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -167,6 +242,7 @@ def main(argv=None):
     nonfinite = float(trainer.optimizer.nonfinite.item())
     trainer._check_device_health()  # raises if a pipelined hand-off gave up (garbage steps)
     key = (args.model, args.loss, args.batch)
+    eff_prec = trainer._effective_matmul_precision()
     if denv.rank == 0:
         log(f"[bench] p50 step {p50:.3f} ms, mean {ms_per_step:.3f} ms, graphs={'on' if trainer._graphs else 'off'}, "
             f"nonfinite={nonfinite}, static_batches={trainer._static_ok(loader)}")
@@ -183,15 +259,21 @@ def main(argv=None):
             "host_issue_ms_per_step": round(host_issue_s * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (round(value / (world * SAME_NODE_TORCH_EAGER[key]), 3)
-                            if key in SAME_NODE_TORCH_EAGER and args.backend == "auto" else None),
-            "baseline": "same-node PyTorch-ROCm reference path (MIOpen nn.LSTM, autograd, eager), x n_gpus",
+            "vs_baseline": (round(value / (world * SAME_NODE_TORCH_GRAPH[key]), 3)
+                            if key in SAME_NODE_TORCH_GRAPH and args.backend == "auto" else None),
+            "baseline": "same-node PyTorch-ROCm reference path (MIOpen nn.LSTM + autograd, step captured in a HIP "
+                        "graph), x n_gpus",
+            "vs_torch_eager": (round(value / (world * SAME_NODE_TORCH_EAGER[key]), 3)
+                               if key in SAME_NODE_TORCH_EAGER and args.backend == "auto" else None),
             "vs_cpu_yardstick": (round(value / YARDSTICK[key], 3) if key in YARDSTICK else None),
             "allreduce": trainer.ddp.backend_name,
             "allreduce_us": round(allreduce_us, 2) if allreduce_us is not None else None,
             "grad_bucket_bytes": int(trainer.flat.padded * 4),
-            "dtype": ("bf16" if (cfg.model.get("arch", "lstm") != "lstm" and dev.type == "cuda")
-                      or cfg.trainer.precision != "32-true" else "fp32"),
+            # the compute dtype that actually ran: the extras' bf16 HIP kernels run only at matmul precision
+            # "medium" (bf16-mixed); under 32-true they run the fp32 graph.  The LSTM keeps fp32 parameters and
+            # activations; its recurrent matmuls run at matmul_precision (bf16x3 MFMA for "high")
+            "dtype": "bf16" if eff_prec == "medium" else "fp32",
+            "matmul_dtype": {"medium": "bf16", "high": "bf16x3 (fp32-accurate)", "highest": "fp32"}[eff_prec],
             "data": "synthetic (reference DGP, generated on device), random-init weights",
             "config": {
                 "model": f"{type(model).__name__} model={args.model} "
@@ -204,7 +286,7 @@ def main(argv=None):
                 "sequences_per_window": 100,
                 "trainer": args.trainer,
                 "precision": cfg.trainer.precision,
-                "matmul_precision": args.matmul_precision,
+                "matmul_precision": eff_prec,
                 "backend": "hip" if args.backend == "auto" else "torch-miopen",
                 "hip_graphs": not args.no_graphs,
                 "steps_per_graph": S,

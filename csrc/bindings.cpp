@@ -42,8 +42,10 @@ void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, c
                       int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
                       float batch_weight, float* out, float* gmse, float* gnll, double* acc, hipStream_t st);
 void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g_total, float c_nll, float c_mse, const float* gmse, const float* gnll,
-                          int has_nll, const float* h, int N, int H, const float* wa, const float* wb, float* dh,
-                          float* dab, float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st);
+                          int has_nll, const float* h, int N, int H, const float* wa, const float* wb, float* dh, float* dab,
+                          float* g_wa, float* g_ba, float* g_wb, float* g_bb, float* part, hipStream_t st);
+void mta_set_heads_deterministic(int on);
+long mta_heads_part_floats(int N, int H);
 int mta_optim_num_partials(long n);
 void mta_grad_sqnorm(const float* g, long n, float scale, float* partials, float* step, hipStream_t st);
 int mta_adam_fused_partials();
@@ -381,10 +383,13 @@ void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total,
   c10::hip::HIPGuardMasqueradingAsCUDA guard(gmse.device());
   // the grid-parallel path of wide heads stages d(alpha, beta) in global memory
   at::Tensor dab_buf = has(dab) ? *dab : at::empty({2 * N}, gmse.options());
+  // deterministic mode: per-block partials of the head parameter gradients, summed in block order
+  const long np = mta_heads_part_floats((int)N, (int)H);
+  at::Tensor part = np > 0 ? at::empty({np}, gmse.options()) : at::Tensor();
   mta_heads_losses_bwd(opt_ptr(g_mse), opt_ptr(g_nll), opt_ptr(g_total), (float)c_nll, (float)c_mse, gmse.data_ptr<float>(),
                        gnll.data_ptr<float>(), has_nll ? 1 : 0, opt_ptr(h), (int)N, (int)H, opt_ptr(wa), opt_ptr(wb),
                        opt_mut(dh), dab_buf.data_ptr<float>(), opt_mut(g_wa), opt_mut(g_ba), opt_mut(g_wb),
-                       opt_mut(g_bb), cur_stream());
+                       opt_mut(g_bb), np > 0 ? part.data_ptr<float>() : nullptr, cur_stream());
 }
 
 // ------------------------------------------------------------------------------------------- optimizer
@@ -963,6 +968,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_ipc_close", &xgmi_ipc_close);
   m.def("xgmi_allreduce", &xgmi_allreduce);
   m.def("xgmi_ctl_words", []() { return (int64_t)mta_xgmi_ctl_words(); });
+  m.def("set_heads_deterministic", [](bool on) { mta_set_heads_deterministic(on ? 1 : 0); });
   m.def("xgmi_max_channels", []() { return (int64_t)mta_xgmi_max_channels(); });
   m.def("xgmi_timeout_word", []() { return (int64_t)mta_xgmi_timeout_word(); });
   m.def("lstm_wgrad_part_floats", [](int64_t fused, int64_t T, int64_t H, int64_t F) {

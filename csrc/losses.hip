@@ -707,7 +707,11 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
                                                              const float* __restrict__ wa,
                                                              const float* __restrict__ wb, float* __restrict__ dh,
                                                              float* __restrict__ g_wa, float* __restrict__ g_ba,
-                                                             float* __restrict__ g_wb, float* __restrict__ g_bb) {
+                                                             float* __restrict__ g_wb, float* __restrict__ g_bb,
+                                                             float* __restrict__ part) {
+  // part (deterministic mode): this block's column partials [wa H | wb H | ba | bb] with plain stores, summed in
+  // block order by heads_part_reduce_kernel instead of the cross-block f32 atomics
+  float* my_part = part ? part + (size_t)blockIdx.x * (2 * H + 2) : nullptr;
   const int r0 = blockIdx.x * HB_ROWS;
   const int r1 = min(r0 + HB_ROWS, N);
   for (int k = threadIdx.x; k < H; k += TPB) {
@@ -732,8 +736,13 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
       }
     }
     if (g_wa) {
-      atomicAdd(g_wa + k, sa);
-      atomicAdd(g_wb + k, sb);
+      if (my_part) {
+        my_part[k] = sa;
+        my_part[H + k] = sb;
+      } else {
+        atomicAdd(g_wa + k, sa);
+        atomicAdd(g_wb + k, sb);
+      }
     }
   }
   if (g_ba && threadIdx.x < 64) {
@@ -745,11 +754,36 @@ __global__ __launch_bounds__(TPB) void heads_bwd_grid_kernel(const float* __rest
     da = wave_sum_dpp(da);
     db = wave_sum_dpp(db);
     if (threadIdx.x == 0) {
-      atomicAdd(g_ba, da);
-      atomicAdd(g_bb, db);
+      if (my_part) {
+        my_part[2 * H] = da;
+        my_part[2 * H + 1] = db;
+      } else {
+        atomicAdd(g_ba, da);
+        atomicAdd(g_bb, db);
+      }
     }
   }
 }
+
+// deterministic mode: column c of [g_wa | g_wb | g_ba | g_bb] += sum over blocks (in block order) of the partials
+__global__ __launch_bounds__(256) void heads_part_reduce_kernel(const float* __restrict__ part, int nblocks, int H,
+                                                               float* __restrict__ g_wa, float* __restrict__ g_ba,
+                                                               float* __restrict__ g_wb, float* __restrict__ g_bb,
+                                                               int has_w, int has_b) {
+  const int c = blockIdx.x * 256 + threadIdx.x, W = 2 * H + 2;
+  if (c >= W) return;
+  float acc = 0.f;
+  for (int b = 0; b < nblocks; ++b) acc += part[(size_t)b * W + c];
+  if (c < H) {
+    if (has_w) g_wa[c] += acc;
+  } else if (c < 2 * H) {
+    if (has_w) g_wb[c - H] += acc;
+  } else if (has_b) {
+    (c == 2 * H ? g_ba : g_bb)[0] += acc;
+  }
+}
+
+int g_heads_deterministic = 0;
 
 // small problems (the reference config: N = 100, H = 64) stay in the single fused workgroup
 inline bool heads_big(int N, int H) { return (long)N * H > 32768 && H % 4 == 0; }
@@ -1004,15 +1038,25 @@ extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, co
   return 0;
 }
 
+extern "C" void mta_set_heads_deterministic(int on) { g_heads_deterministic = on ? 1 : 0; }
+// floats of the partials buffer the deterministic grid path needs (0: none)
+extern "C" long mta_heads_part_floats(int N, int H) {
+  return heads_big(N, H) && g_heads_deterministic ? (long)((N + HB_ROWS - 1) / HB_ROWS) * (2 * H + 2) : 0;
+}
+
 extern "C" void mta_heads_losses_bwd(const float* g_mse, const float* g_nll, const float* g_total, float c_nll, float c_mse, const float* gmse,
                                      const float* gnll, int has_nll, const float* h, int N, int H, const float* wa,
                                      const float* wb, float* dh, float* dab, float* g_wa, float* g_ba, float* g_wb,
-                                     float* g_bb, hipStream_t st) {
+                                     float* g_bb, float* part, hipStream_t st) {
   if (heads_big(N, H) && dab) {
+    const int nb = (N + HB_ROWS - 1) / HB_ROWS;
     heads_dab_kernel<<<(2 * N + 255) / 256, 256, 0, st>>>(g_mse, g_nll, g_total, c_nll, c_mse, gmse, gnll, has_nll,
                                                           N, dab);
-    heads_bwd_grid_kernel<<<(N + HB_ROWS - 1) / HB_ROWS, TPB, 0, st>>>(dab, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb,
-                                                                       g_bb);
+    const bool det = part && (g_wa || g_ba);
+    heads_bwd_grid_kernel<<<nb, TPB, 0, st>>>(dab, h, N, H, wa, wb, dh, g_wa, g_ba, g_wb, g_bb, det ? part : nullptr);
+    if (det)
+      heads_part_reduce_kernel<<<(2 * H + 2 + 255) / 256, 256, 0, st>>>(part, nb, H, g_wa, g_ba, g_wb, g_bb,
+                                                                        g_wa ? 1 : 0, g_ba ? 1 : 0);
     return;
   }
   heads_losses_bwd_kernel<<<1, TPB, (size_t)(2 * N) * sizeof(float), st>>>(g_mse, g_nll, g_total, c_nll, c_mse, gmse, gnll, has_nll, h,

@@ -144,15 +144,18 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
   }
   acc = block_sum(acc, scratch) * (scale * scale);
-  // the step counter is read by every workgroup BEFORE it arrives; the last arriver advances it
-  const float t = step_ptr[0] + 1.0f;
+  // the step counter is read by every workgroup BEFORE it arrives (thread 0 loads it and its vmcnt(0) below
+  // completes the load before the ticket add; the workgroup reads it from LDS); the last arriver advances it
+  __shared__ float s_t;
   if (threadIdx.x == 0) {
+    const float t0 = step_ptr[0] + 1.0f;
+    s_t = t0;
     __hip_atomic_store(partials + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned long long prev =
         __hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long target = (prev / gridDim.x + 1) * gridDim.x;
-    if (prev + 1 == target) step_ptr[0] = t;
+    if (prev + 1 == target) step_ptr[0] = t0;
     unsigned long long seen = prev + 1;
     unsigned spins = 0;
     while (seen < target) {
@@ -165,6 +168,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
   }
   __syncthreads();
+  const float t = s_t;
   if (threadIdx.x < 64) {
     // wave 0 reads the partials in parallel (lane b: b, b+64, ...; all loads in flight at once, not a chain of
     // dependent round trips) and reduces them in a fixed order: the same norm on every workgroup and every run

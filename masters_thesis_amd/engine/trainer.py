@@ -62,14 +62,18 @@ class _Graph:
         return self.out
 
 
-def _group_sizes(events):
-    """(event pair, steps it covers): a grouped graph's pair is repeated once per step it ran."""
+def _group_sizes(events, skip_groups: int = 0):
+    """(event pair, steps it covers) per step: a grouped graph's pair is repeated once per step it ran.  The first
+    ``skip_groups`` launches (eager warm-up / capture groups) are dropped WHOLE, so a partially skipped group never
+    divides its time by the wrong step count."""
     out = []
     for ev in events:
         if out and out[-1][0] is ev:
             out[-1][1] += 1
         else:
             out.append([ev, 1])
+    if len(out) > skip_groups:
+        out = out[skip_groups:]
     return [(ev, n) for ev, n in out for _ in range(n)]
 
 
@@ -82,6 +86,7 @@ class Trainer:
                  limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
                  limit_test_batches: Optional[int] = None, default_root_dir: str = ".",
                  max_steps: int = -1, fail_at_step: Optional[int] = None, deterministic: bool = False,
+                 debug_serialize: bool = False,
                  log_every_n_steps: int = 50, steps_per_graph: int = 8, profiler: Optional[str] = None,
                  profile_steps: int = 20):
         self.max_epochs = int(max_epochs)
@@ -113,14 +118,24 @@ class Trainer:
         if attempts is not None and int(os.environ.get("MTA_RETRY_ATTEMPT", "0")) >= int(attempts):
             self.fail_at_step = None
         self.heartbeat_file = os.environ.get("MTA_HEARTBEAT_FILE")
-        # bit-reproducible runs: ordered weight-gradient reductions instead of f32 atomics (LSTM kernels) and no
-        # split-K atomics in the extras' GEMMs; the other reductions (norm, loss, heads) are ordered anyway
+        # bit-reproducible runs: ordered weight-gradient reductions instead of f32 atomics (LSTM kernels), no
+        # split-K atomics in the extras' GEMMs, block-ordered head-parameter partials (wide heads backward)
         self.deterministic = bool(deterministic) or os.environ.get("MTA_DETERMINISTIC", "0") == "1"
+        # serialize / launch-blocking debug mode (utils/debug.py): synchronous launches, no captured graphs
+        from ..utils.debug import apply_serialize_env, serialize_requested
+
+        self.debug_serialize = serialize_requested(debug_serialize)
+        if self.debug_serialize:
+            apply_serialize_env()
+            self.use_hip_graphs = False
+            self.steps_per_graph = 1
         if self.deterministic:
-            from ..ops import lstm as _lstm_op
             from ..ops import extras as _extras_op
+            from ..ops import losses as _losses_op
+            from ..ops import lstm as _lstm_op
 
             _lstm_op.set_deterministic(True)
+            _losses_op.set_deterministic(True)
             if hasattr(_extras_op, "set_deterministic"):
                 _extras_op.set_deterministic(True)
         # state
@@ -541,13 +556,22 @@ class Trainer:
                 pass
 
     def _check_device_health(self) -> None:
-        """Raise if a pipelined LSTM launch gave up on a hand-off (its results were garbage)."""
+        """Raise if a pipelined LSTM launch gave up on a hand-off, an xGMI all-reduce on a peer, or the single-launch
+        clip+Adam on its grid-wide norm arrival (that step's update used a partial norm): their results were
+        garbage."""
         if self.device.type == "cuda":
             from ..ops.lstm import check_pipeline_health
             from ..parallel.xgmi import check_all_health
 
             check_pipeline_health()
             check_all_health()
+            st = getattr(self.optimizer, "sync_timeouts", None)
+            if st is not None:
+                n = int(st.item())
+                if n:
+                    st.zero_()
+                    raise RuntimeError(f"fused clip+Adam: {n} grid-wide norm wait(s) gave up (those updates used a "
+                                       "partial gradient norm)")
 
     def _run_eval(self, stage: str, loader, limit=None) -> Dict[str, torch.Tensor]:
         model = self.model
@@ -651,9 +675,7 @@ class Trainer:
             return [], B
         if cuda:
             torch.cuda.synchronize()
-            skip = self.graph_warmup_steps + 1
-            host_ms = [a.elapsed_time(b) / n for (a, b), n in _group_sizes(events[skip:] if len(events) > skip
-                                                                           else events)]
+            host_ms = [a.elapsed_time(b) / n for (a, b), n in _group_sizes(events, self.graph_warmup_steps + 1)]
         if self.enable_progress_bar and self.is_global_zero:
             sys.stdout.write("\n")
         return host_ms, B

@@ -8,7 +8,10 @@ transformer encoder over its T tokens.  Everything else is the reference model: 
 ``FinancialMlp{Mse,Nll,Combined}`` and ``FinancialTransformer{Mse,Nll,Combined}``, selected by
 ``get_model_class(loss.module_class, arch)``.
 
-On the GPU the encoders run as bf16-mixed HIP kernels (``ops.extras``); on the CPU as fp32 PyTorch.
+On the GPU the encoders run as bf16-mixed HIP kernels (``ops.extras``) when the matmul precision the trainer
+resolves is "medium" (``trainer.precision=bf16-mixed``, e.g. ``trainer=gpu_fast``), and as the fp32 graph under
+``32-true`` (the reference trainers' precision, `configs/trainer/fast.yaml:3`); on the CPU as fp32 PyTorch.  A
+model used outside a Trainer defaults to "medium".
 """
 from __future__ import annotations
 
@@ -68,9 +71,11 @@ class MLPEncoder(torch.nn.Module):
             out += [lin.weight, lin.bias, nrm.weight] + ([nrm.bias] if self.norm == "layernorm" else [])
         return out
 
+    precision = "medium"  # set per call by the owning model (its matmul_precision)
+
     def forward(self, x: Tensor) -> Tensor:
         return xops.mlp_encode(x, self.flat_params(), self.seeds, self.num_layers, self.norm, self.dropout,
-                               self.training)
+                               self.training, self.precision)
 
 
 class _Block(torch.nn.Module):
@@ -113,7 +118,9 @@ class TransformerEncoder(torch.nn.Module):
         if x.shape[1] > 64:
             raise ValueError("transformer encoder supports lookback windows of up to 64 tokens")
         return xops.transformer_encode(x, self.flat_params(), self.seeds, self.num_layers, self.num_heads,
-                                       self.dropout, self.training)
+                                       self.dropout, self.training, self.precision)
+
+    precision = "medium"
 
 
 def _make(base, arch: str):
@@ -136,6 +143,7 @@ def _make(base, arch: str):
             self.beta_head = torch.nn.Linear(hidden_size, 1)
             self._hparams.clear()
             self.save_hyperparameters()
+            self.matmul_precision = "medium"
     else:
         def __init__(self, input_size: int = 3, hidden_size: int = 128, num_layers: int = 4, dropout: float = 0.1,
                      learning_rate: float = 1e-4, weight_decay: float = 1e-5, mse_weight: float = 1e2, *,
@@ -152,8 +160,10 @@ def _make(base, arch: str):
             self.beta_head = torch.nn.Linear(hidden_size, 1)
             self._hparams.clear()
             self.save_hyperparameters()
+            self.matmul_precision = "medium"
 
     def encode(self, x: Tensor) -> Tensor:
+        self.encoder.precision = self.matmul_precision
         return self.encoder(x)
 
     cls = type(name, (base,), {"__init__": __init__, "encode": encode, "__doc__": f"{base.__name__} with the {arch} "

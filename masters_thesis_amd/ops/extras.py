@@ -1,4 +1,5 @@
-"""MLP and transformer encoder ops for the ``BASELINE.json`` north-star extras (bf16-mixed on MI355X).
+"""MLP and transformer encoder ops for the ``BASELINE.json`` north-star extras (bf16-mixed on MI355X; fp32 under
+``32-true``).
 
 Not in the reference (it only has the LSTM, `src/model.py:88-94`); the north star asks for the
 ``src/model.py`` forward path as Linear/GEMM+bias, GELU and LayerNorm/RMSNorm HIP kernels and a
@@ -16,7 +17,9 @@ GPU path = one autograd Function per encoder, built from four hand-written HIP k
 * ``cast_pad`` -- fp32 master weights -> zero-padded bf16 operands, once per step.
 
 Precision: fp32 master weights (FlatParameters) and fp32 residual stream / gradients, bf16 GEMM
-operands with fp32 accumulation ("bf16-mixed").  Like the LSTM op, the weights' gradients are
+operands with fp32 accumulation ("bf16-mixed", matmul precision "medium").  Under ``32-true`` (matmul precision
+"high" / "highest") the encoders run the fp32 graph instead (``mlp_reference`` / ``transformer_reference`` on the
+device: fp32 GEMMs, norms and attention), so the trainer's precision is never silently lowered.  Like the LSTM op, the weights' gradients are
 accumulated inside the op and ``None`` is returned for them.
 
 CPU path: the same architectures in plain fp32 PyTorch (``mlp_reference`` / ``transformer_reference``),
@@ -205,8 +208,11 @@ class _MlpEncoderFn(torch.autograd.Function):
 
 
 def mlp_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, norm: str,
-               dropout: float, training: bool) -> Tensor:
-    if use_hip(x):
+               dropout: float, training: bool, precision: str = "medium") -> Tensor:
+    """``precision`` = the matmul precision the trainer resolved (``Trainer._effective_matmul_precision``): "medium"
+    (``bf16-mixed``, or an explicit medium) runs the bf16 HIP kernels; "high" / "highest" (``32-true``) runs the
+    fp32 graph (fp32 GEMMs, norms and attention) -- the trainer's precision is honoured, never silently lowered."""
+    if use_hip(x) and precision == "medium":
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _MlpEncoderFn.apply(x.contiguous(), seeds, num_layers, norm, float(dropout), bool(training),
                                    need_grad, *params)
@@ -413,8 +419,9 @@ class _TransformerEncoderFn(torch.autograd.Function):
 
 
 def transformer_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, heads: int,
-                       dropout: float, training: bool) -> Tensor:
-    if use_hip(x):
+                       dropout: float, training: bool, precision: str = "medium") -> Tensor:
+    """``precision``: as :func:`mlp_encode`."""
+    if use_hip(x) and precision == "medium":
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _TransformerEncoderFn.apply(x.contiguous(), seeds, num_layers, heads, float(dropout), bool(training),
                                            need_grad, *params)

@@ -45,6 +45,15 @@ from torch import Tensor
 
 from ._lib import lib, use_hip
 
+
+def set_deterministic(flag: bool) -> None:
+    """Deterministic mode: the wide-head backward (N * H > 32768: extras encoders, large batches) sums its per-block
+    head-parameter partials in block order (csrc/losses.hip heads_part_reduce_kernel) instead of f32 atomics."""
+    try:
+        lib().set_heads_deterministic(bool(flag))
+    except Exception:  # CPU-only process: the PyTorch path is deterministic already
+        pass
+
 LOG2PI = math.log(2 * math.pi)
 
 

@@ -213,7 +213,8 @@ def test_extras_train_through_trainer_graph(arch):
     if arch == "transformer":
         kw.update(num_heads=4, mlp_ratio=4)
     model = cls(**kw)
-    tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False, use_hip_graphs=True)
+    tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False, use_hip_graphs=True,
+                 precision="bf16-mixed")
     tr._setup_env()
     tr._setup_model(model)
     tr._configure_optimizers(model)
@@ -288,3 +289,80 @@ def test_gemm_dropout_mask_forward_backward_consistent():
     assert torch.equal(kept_f, kept_b)
     frac = kept_f.float().mean().item()
     assert abs(frac - (1 - p)) < 0.01, frac
+
+
+def test_extras_deterministic_mode_bit_identical_at_batch_64():
+    """Trainer(deterministic=True) with an extras encoder at B = 64 windows (N = 6,400 sequences: the wide-head
+    backward takes its grid path): no split-K GEMM atomics and block-ordered head-parameter partials
+    (csrc/losses.hip heads_part_reduce_kernel), so two runs give bit-identical parameters."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import get_model_class
+    from masters_thesis_amd.ops import extras as X
+    from masters_thesis_amd.ops import losses as L
+    from masters_thesis_amd.ops import lstm as op
+
+    g = torch.Generator().manual_seed(0)
+    W = 128
+    data = [torch.randn(W, 100, 60, 3, generator=g), torch.randn(W, 100, 30, 4, generator=g) * 0.01,
+            torch.stack([torch.randn(W, generator=g) * 0.01, torch.rand(W, generator=g) * 1e-3 + 1e-4], -1),
+            torch.rand(W, 100, generator=g) * 3 + 1]
+    dev_data = [t.to(DEV) for t in data]
+
+    def run():
+        torch.manual_seed(5)
+        cls = get_model_class("FinancialLstmCombined", "mlp")
+        model = cls(input_size=3, hidden_size=256, num_layers=2, dropout=0.1, learning_rate=1e-4)
+        tr = Trainer(gradient_clip_val=5.0, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=True, deterministic=True, precision="bf16-mixed")
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.train()
+        step = tr.make_train_stepper(TensorBatchLoader(dev_data, 64, shuffle=True, seed=0))
+        for _ in range(6):
+            step()
+        torch.cuda.synchronize()
+        return tr.flat.data.clone()
+
+    try:
+        a, b = run(), run()
+    finally:
+        op.set_deterministic(False)
+        X.set_deterministic(False)
+        L.set_deterministic(False)
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("arch", ["mlp", "transformer"])
+def test_extras_honour_trainer_precision(arch):
+    """under trainer precision 32-true the extras encoders run the fp32 graph (within 1e-4 of
+    fp32 PyTorch on the same weights); under bf16-mixed they run the bf16 HIP kernels (bf16 tolerance, not exact)."""
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import get_model_class
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(0)
+    cls = get_model_class("FinancialLstmMse", arch)
+    kw = dict(input_size=3, hidden_size=128, num_layers=2, dropout=0.0)
+    if arch == "transformer":
+        kw.update(num_heads=4)
+    x = torch.randn(200, 60, 3, device=DEV)
+    outs = {}
+    for prec in ("32-true", "bf16-mixed"):
+        model = cls(**kw)
+        tr = Trainer(enable_progress_bar=False, enable_model_summary=False, precision=prec)
+        tr._setup_env()
+        tr._setup_model(model)
+        model.eval()
+        with torch.no_grad():
+            h = model.encode(x)
+            params = model.encoder.flat_params()
+            if arch == "mlp":
+                ref = X.mlp_reference(x.double(), [p.double() for p in params], 2, model.encoder.norm, 0.0, False)
+            else:
+                ref = X.transformer_reference(x.double(), [p.double() for p in params], 2, 4, 0.0, False)
+        outs[prec] = (h.double() - ref).abs().max().item() / max(ref.abs().max().item(), 1.0)
+    assert outs["32-true"] <= 1e-4, outs
+    assert 1e-6 < outs["bf16-mixed"] <= 5e-2, outs

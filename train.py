@@ -50,7 +50,8 @@ def build_trainer(cfg, logger, callbacks):
         kw["check_val_every_n_epoch"] = t.check_val_every_n_epoch
     for k in ("use_hip_graphs", "matmul_precision", "limit_train_batches", "limit_val_batches",
               "limit_test_batches", "accelerator", "num_sanity_val_steps", "max_steps", "graph_warmup_steps",
-              "steps_per_graph", "deterministic", "log_every_n_steps", "profiler", "profile_steps"):
+              "steps_per_graph", "deterministic", "log_every_n_steps", "profiler", "profile_steps",
+              "debug_serialize"):
         if k in t:
             kw[k] = t[k]
     return Trainer(**kw)
