@@ -62,6 +62,7 @@ int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, i
                   float drop_p, void* out_bf16, float* out_f32, void* aux_pre, int ldc, int n_store, int ksplit,
                   float* bias_grad, int defer, hipStream_t st);
 void mta_gemm_flush();
+void mta_gemm_set_big(int on);
 void mta_norm_flush();
 void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
@@ -943,6 +944,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
+  m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad);

@@ -19,6 +19,8 @@
 // Requirements (checked by the launcher): M, N, K multiples of 8, 16-byte aligned rows.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int GT = 256;  // threads per workgroup
@@ -75,6 +77,83 @@ union Bf8 {
   uint4 u;
   __bf16 e[8];
 };
+
+// Epilogue of one wave's MT x NT grid of 16x16 accumulator tiles whose top-left output element is (mbase, nbase):
+// tile (i, j), register r of lane l holds C[mbase + 16 i + 4 (l >> 4) + r][nbase + 16 j + (l & 15)].  Rows are done
+// IC tiles at a time; the operands the epilogue reads (residual stream, GELU input of a DGELU, the fp32 output of a
+// non-split accumulate) are fetched for those IC x NT tiles first: interleaved with the output stores the compiler must
+// keep each load behind the previous (possibly aliasing) store, i.e. one dependent global round trip per element (r2
+// trace: 13 us per residual GEMM).
+template <int MT, int NT, int IC>
+__device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, const f32x4 (&acc)[MT][NT], const int mbase,
+                                              const int nbase, const bool split, const int lane) {
+  const bool acc_rmw = (g.flags & EPI_ACCUM) && !split;  // read-modify-write of the fp32 output
+  const bool prefetch = (g.flags & (EPI_RESID | EPI_DGELU)) || acc_rmw;
+  uint32_t dseed = 0, dthr = 0;
+  float dscale = 0.f;
+  if (g.flags & EPI_DROPOUT) {
+    const uint64_t sd = *g.seed;
+    dseed = (uint32_t)(sd ^ (sd >> 32));
+    dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
+    dscale = 1.0f / (1.0f - g.drop_p);
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < MT; i0 += IC) {
+    float pre_in[IC][NT][4];
+    if (prefetch) {
+#pragma unroll
+      for (int i = 0; i < IC; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const int n = nbase + 16 * j + (lane & 15);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = mbase + 16 * (i0 + i) + 4 * (lane >> 4) + r;
+            const size_t o = (size_t)m * g.ldc + n;
+            const bool ok = m < g.M && n < g.n_store;
+            pre_in[i][j][r] = !ok ? 0.f : acc_rmw ? g.out_f32[o] : (g.flags & EPI_RESID) ? g.resid[o]
+                                                                                         : (float)g.aux_in[o];
+          }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < IC; ++i) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = nbase + 16 * j + (lane & 15);
+        uint32_t hp[2] = {0u, 0u};
+        if (g.flags & EPI_DROPOUT) {
+          const uint32_t mp = (uint32_t)(mbase + 16 * (i0 + i) + 4 * (lane >> 4)) >> 1;
+          hp[0] = gemm_pair_hash(dseed, mp, (uint32_t)n);
+          hp[1] = gemm_pair_hash(dseed, mp + 1, (uint32_t)n);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = mbase + 16 * (i0 + i) + 4 * (lane >> 4) + r;
+          if (m >= g.M || n >= g.n_store) continue;
+          float v = g.alpha * acc[i0 + i][j][r];
+          const size_t o = (size_t)m * g.ldc + n;
+          if (g.flags & EPI_ACCUM) {
+            if (split) atomicAdd(g.out_f32 + o, v);
+            else g.out_f32[o] = pre_in[i][j][r] + v;
+            continue;
+          }
+          if (g.flags & EPI_BIAS) v += g.bias[n];
+          if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
+          if (g.flags & EPI_GELU) v = mta_gelu(v);
+          if (g.flags & EPI_DROPOUT) {
+            const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+            v *= u16 >= dthr ? dscale : 0.f;
+          }
+          if (g.flags & EPI_DGELU) v *= mta_gelu_grad(pre_in[i][j][r]);
+          if (g.flags & EPI_RESID) v += pre_in[i][j][r];
+          if (g.out_f32) g.out_f32[o] = v;
+          if (g.out_bf16) g.out_bf16[o] = (__bf16)v;
+        }
+      }
+    }
+  }
+}
 
 template <int BM, int BN, int BKT, bool AT, bool BT, bool PIPE = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const int by, const int bz, const int gz,
@@ -269,73 +348,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
     }
   }
 
-  // ---- epilogue ----
-  const bool split = gz > 1;
-  // operands the epilogue reads (residual stream, GELU input of a DGELU) are fetched for the whole tile first:
-  // interleaved with the output stores the compiler must keep each load behind the previous (possibly
-  // aliasing) store, i.e. one dependent global round trip per element (r2 trace: 13 us per residual GEMM)
-  float pre_in[MT][NT][4];
-  const bool acc_rmw = (g.flags & EPI_ACCUM) && !split;  // read-modify-write of the fp32 output
-  if ((g.flags & (EPI_RESID | EPI_DGELU)) || acc_rmw) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = n0 + wn * WN + 16 * j + (lane & 15);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
-          const size_t o = (size_t)m * g.ldc + n;
-          const bool ok = m < g.M && n < g.n_store;
-          pre_in[i][j][r] = !ok ? 0.f : acc_rmw ? g.out_f32[o] : (g.flags & EPI_RESID) ? g.resid[o]
-                                                                                       : (float)g.aux_in[o];
-        }
-      }
-  }
-  uint32_t dseed = 0, dthr = 0;
-  float dscale = 0.f;
-  if (g.flags & EPI_DROPOUT) {
-    const uint64_t sd = *g.seed;
-    dseed = (uint32_t)(sd ^ (sd >> 32));
-    dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
-    dscale = 1.0f / (1.0f - g.drop_p);
-  }
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const int n = n0 + wn * WN + 16 * j + (lane & 15);
-      uint32_t hp[2] = {0u, 0u};
-      if (g.flags & EPI_DROPOUT) {
-        const uint32_t mp = (uint32_t)(m0 + wm * WM + 16 * i + 4 * (lane >> 4)) >> 1;
-        hp[0] = gemm_pair_hash(dseed, mp, (uint32_t)n);
-        hp[1] = gemm_pair_hash(dseed, mp + 1, (uint32_t)n);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + 16 * i + 4 * (lane >> 4) + r;
-        if (m >= g.M || n >= g.n_store) continue;
-        float v = g.alpha * acc[i][j][r];
-        const size_t o = (size_t)m * g.ldc + n;
-        if (g.flags & EPI_ACCUM) {
-          if (split) atomicAdd(g.out_f32 + o, v);
-          else g.out_f32[o] = pre_in[i][j][r] + v;
-          continue;
-        }
-        if (g.flags & EPI_BIAS) v += g.bias[n];
-        if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
-        if (g.flags & EPI_GELU) v = mta_gelu(v);
-        if (g.flags & EPI_DROPOUT) {
-          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
-          v *= u16 >= dthr ? dscale : 0.f;
-        }
-        if (g.flags & EPI_DGELU) v *= mta_gelu_grad(pre_in[i][j][r]);
-        if (g.flags & EPI_RESID) v += pre_in[i][j][r];
-        if (g.out_f32) g.out_f32[o] = v;
-        if (g.out_bf16) g.out_bf16[o] = (__bf16)v;
-      }
-    }
-  }
+  gemm_epilogue<MT, NT, MT>(g, acc, m0 + wm * WM, n0 + wn * WN, gz > 1, lane);
   if (want_rowsum) {
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
@@ -364,6 +377,249 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
   __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT, PIPE>()];
   const int b = xcd_remap(blockIdx.x, nx * ny * nz);
   gemm_body<BM, BN, BKT, AT, BT, PIPE>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, smem, smem + BM * (BKT + 8));
+}
+
+// ---- 256 x 256 macro-tile GEMM: LDS-DMA ring, staggered wave groups, in-kernel transposed operands ----
+// The large problems (the mlp_large layers: 6400 x 2048 x 2048 and its two gradients) on one 512-thread workgroup per
+// CU:
+//   * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 outputs = 8 x 4 accumulators of v_mfma_f32_16x16x32_bf16
+//     (32 MFMAs per 32-deep k-tile against 12 fragment reads: the MFMA pipe, not LDS, is the limit);
+//   * operands go global -> LDS by global_load_lds (16 B per lane, no VGPR round trip) into a ring of AHEAD + 1 k-tile
+//     slots (A and B 16 KB each per slot; AHEAD = 4: 160 KB, the whole LDS), AHEAD k-tiles ahead of the one being
+//     multiplied, waited with COUNTED vmcnt (never 0 in the loop) and raw s_barrier so the DMA stays in flight across
+//     barriers (the latency to hide is an L2/MALL miss under full load, ~1-2 us);
+//   * the two wave rows run one barrier apart ("ping-pong"): every k-tile is a [fragment reads] segment and an
+//     [DMA issue + MFMA] segment separated by barriers, and the second wave row enters one barrier late, so on every
+//     SIMD one wave multiplies while its partner reads -- s_setprio(1) around each MFMA cluster keeps the compiler
+//     from moving MFMAs across the barriers;
+//   * k-contiguous operands ([rows][K]) land as [256 rows][32 k] images (64-B rows) whose 16-B chunks are XOR-swizzled
+//     by row bit 3 on the SOURCE address (the DMA writes lane-linear): conflict-free ds_read_b128 fragments;
+//   * k-strided operands ([K][rows]: the input-gradient W and both weight-gradient operands) land untransposed as
+//     [32 k][256 cols] images (512-B rows, 32-B chunks XOR-swizzled by k-row bits 0,1,3) and are read transposed by
+//     ds_read_b64_tr_b16 (two per fragment), conflict-free: no transpose kernels, no transposing register staging.
+// Ring hazards (j = k-tile; segments R = reads, M = DMA issue + MFMAs; row 0: R0 M0 R1 M1 ..., row 1: -- R0 M0 R1 ...):
+//   WAR: tile j+AHEAD is issued at the start of M_j into slot (j+AHEAD) % (AHEAD+1) = the slot of tile j-1; both rows
+//        retired their reads of it (lgkmcnt(0) ahead of their MFMAs of M_{j-1}) before a barrier that precedes M_j;
+//   RAW: row 0 first reads tile j+1 right after the barrier that closes its M_j, so at that barrier every wave has
+//        waited for all but the tiles it issued after tile j+1 (row 0 at the end of M_j, row 1 at the end of R_j).
+// Rows / columns beyond M, N are clamped on load (their outputs are not stored); K per split is a multiple of 32.
+namespace big {
+constexpr int TM = 256, TN = 256, KT = 32, THREADS = 512;
+#ifndef MTA_GEMM_BIG_AHEAD
+#define MTA_GEMM_BIG_AHEAD 4
+#endif
+constexpr int AHEAD = MTA_GEMM_BIG_AHEAD, SLOTS = AHEAD + 1;  // k-tiles in flight beyond the one multiplied
+constexpr int OP_BYTES = 256 * KT * 2;     // one operand's k-tile image: 16 KB
+constexpr int SLOT_BYTES = 2 * OP_BYTES;  // A | B
+constexpr int LDS_BYTES = SLOTS * SLOT_BYTES;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// per-lane source of the two DMA instructions this wave issues for one operand of one k-tile
+template <bool T>
+__device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, int r0, int kbeg, int wave, int lane,
+                                        const __bf16* (&src)[2]) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int ins = wave + 8 * q;  // 1-KB piece of the 16-KB image
+    if constexpr (!T) {
+      // 16 rows x 64 B; lane -> (row, physical chunk); the chunk it holds is the swizzled logical one
+      const int r = 16 * ins + (lane >> 2);
+      const int c = (lane & 3) ^ (((r >> 3) & 1) << 1);
+      const int row = min(r0 + r, rows - 1);
+      src[q] = base + (size_t)row * ld + kbeg + 8 * c;
+    } else {
+      // 2 k-rows x 512 B; lane -> (k-row, 16-B unit); 32-B chunk swizzled by k-row
+      const int kr = 2 * ins + (lane >> 5), u = lane & 31;
+      const int h = (kr & 3) | (((kr >> 3) & 1) << 2);
+      const int col = min(r0 + 16 * ((u >> 1) ^ h) + 8 * (u & 1), rows - 8);
+      src[q] = base + (size_t)(kbeg + kr) * ld + col;
+    }
+  }
+}
+
+// diagnostic build (csrc/tools/gemm_probe.hip): s_memtime stamps of the main loop's segments, summed per wave
+#ifdef MTA_GEMM_STAMPS
+__device__ unsigned long long stamp_acc[8][8];  // [wave][segment]
+#define GSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define GACC(i, a, b) dsum[i] += (unsigned)((b) - (a))
+#else
+#define GSTAMP(v)
+#define GACC(i, a, b)
+#endif
+
+__device__ __forceinline__ void dma16(const __bf16* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(static_cast<const void*>(src), (lds_void*)(lds), 16, 0, 0);
+}
+
+// MFMA operand fragment of 16 rows (m or n) starting at image row/col `rb`, k-chunk lane >> 4
+template <bool T>
+__device__ __forceinline__ bf16x8 frag(const char* img, int rb, int lane) {
+  if constexpr (!T) {
+    const int r = rb + (lane & 15);
+    const int p = (lane >> 4) ^ (((lane >> 3) & 1) << 1);
+    return *reinterpret_cast<const bf16x8*>(img + r * 64 + p * 16);
+  } else {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int lc = rb >> 4;
+    const int k0 = 8 * g + q, k1 = k0 + 4;
+    const int h0 = (k0 & 3) | (((k0 >> 3) & 1) << 2), h1 = (k1 & 3) | (((k1 >> 3) & 1) << 2);
+    // inline asm: the intrinsic form makes hipcc wait vmcnt(0) (every DMA in flight) before each transposed read;
+    // the caller waits lgkmcnt(0) itself before the MFMAs (tr_wait)
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 lo, hi;
+    const unsigned a0 = (unsigned)(uintptr_t)(img + k0 * 512 + ((lc ^ h0) << 5) + 8 * p);
+    const unsigned a1 = (unsigned)(uintptr_t)(img + k1 * 512 + ((lc ^ h1) << 5) + 8 * p);
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+    const u32x2 v8[2] = {lo, hi};
+    bf16x8 out;
+    __builtin_memcpy(&out, v8, 16);
+    return out;
+  }
+}
+
+__device__ __forceinline__ void barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// outstanding DMA k-tiles this wave may leave in flight at a wait (immediate operand: one branch per count)
+__device__ __forceinline__ void wait_tiles(int n) {
+  if (n >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AT, bool BT>
+__device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const bool row1 = wm == 1;
+  const int m0 = by * TM, n0 = bx * TN;
+  const int kbeg = bz * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg) / KT;
+  if (nk <= 0) return;
+
+  const __bf16* sa[2];
+  const __bf16* sb[2];
+  dma_src<AT>(g.A, g.lda, g.M, m0, kbeg, wave, lane, sa);
+  dma_src<BT>(g.B, g.ldb, g.N, n0, kbeg, wave, lane, sb);
+  const size_t stepA = AT ? (size_t)KT * g.lda : KT, stepB = BT ? (size_t)KT * g.ldb : KT;
+  auto stage = [&](int j, int slot_i) __attribute__((always_inline)) {
+    char* slot = lds + slot_i * SLOT_BYTES;
+    const size_t oa = (size_t)j * stepA, ob = (size_t)j * stepB;
+    dma16(sa[0] + oa, slot + wave * 1024);
+    dma16(sa[1] + oa, slot + (wave + 8) * 1024);
+    dma16(sb[0] + ob, slot + OP_BYTES + wave * 1024);
+    dma16(sb[1] + ob, slot + OP_BYTES + (wave + 8) * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
+  float rowsum[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rowsum[i] = 0.f;
+
+  // prologue: k-tiles 0 .. AHEAD-1 into slots 0 .. AHEAD-1; tile 0 landed (every wave) at the first barrier
+  const int pro = min(nk, AHEAD);
+  for (int t = 0; t < pro; ++t) stage(t, t);
+  wait_tiles(pro - 1);
+  barrier();
+  if (row1) barrier();  // the second wave row runs one barrier behind
+  int rd = 0, wr = AHEAD;  // ring slots of tile j and of tile j + AHEAD
+#ifdef MTA_GEMM_STAMPS
+  unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  GSTAMP(tloop0);
+#endif
+  for (int j = 0; j < nk; ++j) {
+    GSTAMP(t0);
+    // [reads] fragments of tile j
+    const char* slot = lds + rd * SLOT_BYTES;
+    bf16x8 af[8], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag<AT>(slot, wm * 128 + 16 * i, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = frag<BT>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
+    GSTAMP(t1);
+    // row 1 ends its read segment at the barrier before row 0 reads tile j + 1: everything up to it landed
+    if (row1) wait_tiles(min(nk - 1, j - 1 + AHEAD) - (j + 1));
+    GSTAMP(t2);
+    barrier();
+    GSTAMP(t3);
+    // [MFMA] tile j, with the DMA of tile j + AHEAD issued up front into the slot tile j - 1 used (both rows
+    // retired their reads of it: lgkmcnt(0) at their previous MFMA segments, and a barrier since)
+    if (j + AHEAD < nk) stage(j + AHEAD, wr);
+    if (want_rowsum) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rowsum[i] += (float)af[i][e];
+    }
+    if constexpr (AT || BT) {  // the transposed reads are inline asm: hipcc does not track them
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
+    __builtin_amdgcn_s_setprio(0);
+    GSTAMP(t4);
+    if (!row1) wait_tiles(min(nk - 1, j + AHEAD) - (j + 1));
+    GSTAMP(t5);
+    barrier();
+    GSTAMP(t6);
+    GACC(0, t0, t1);  // fragment reads (issue + completion: the stamp waits lgkmcnt)
+    GACC(1, t1, t2);  // row 1: DMA wait
+    GACC(2, t2, t3);  // barrier after the reads
+    GACC(3, t3, t4);  // DMA issue + MFMA issue
+    GACC(4, t4, t5);  // row 0: DMA wait
+    GACC(5, t5, t6);  // barrier after the MFMAs
+    rd = rd + 1 == SLOTS ? 0 : rd + 1;
+    wr = wr + 1 == SLOTS ? 0 : wr + 1;
+  }
+  if (!row1) barrier();
+#ifdef MTA_GEMM_STAMPS
+  GSTAMP(tloop1);
+  GACC(6, tloop0, tloop1);
+#endif
+
+  gemm_epilogue<8, 4, 2>(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, lane);
+  if (want_rowsum) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float s = rowsum[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const int m = m0 + wm * 128 + 16 * i + (lane & 15);
+      if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
+    }
+  }
+#ifdef MTA_GEMM_STAMPS
+  GSTAMP(tend);
+  GACC(7, tloop1, tend);  // epilogue
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
+#endif
+}
+}  // namespace big
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(big::THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_big_kernel(GemmArgs g, int nx, int ny, int nz) {
+  extern __shared__ __attribute__((aligned(16))) char big_lds[];
+  const int b = xcd_remap(blockIdx.x, nx * ny * nz);
+  big::body<AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, big_lds);
 }
 
 // Two independent GEMMs of one tile configuration in ONE launch (the backward's weight gradient and input
@@ -586,7 +842,53 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   }
 }
 
+// ---- routing to the 256 x 256 kernel ----
+// MTA_GEMM_BIG=0 disables it; mta_gemm_set_big(0/1) overrides at run time (tests compare the two paths in one process)
+int g_big_override = -1;
+inline bool big_on() {
+  static const bool env_on = [] {
+    const char* e = getenv("MTA_GEMM_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return g_big_override >= 0 ? g_big_override == 1 : env_on;
+}
+
+template <bool AT, bool BT>
+void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<AT, BT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, big::LDS_BYTES) == hipSuccess;
+  }();
+  (void)attr;
+  const int nx = (g.N + big::TN - 1) / big::TN, ny = (g.M + big::TM - 1) / big::TM;
+  gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(g, nx, ny, ksplit);
+}
+
+// true = launched on the 256 x 256 kernel: 32-deep k-tiles, and enough macro-tiles to fill at least half the CUs
+// (the split-K accumulating form re-splits K towards one wave of 256 workgroups, >= 8 k-tiles per split)
+bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
+  if (!big_on() || g_in.K % big::KT || g_in.M < 64 || g_in.N < 64) return false;
+  GemmArgs g = g_in;
+  const long tiles = (long)((g.M + big::TM - 1) / big::TM) * ((g.N + big::TN - 1) / big::TN);
+  if ((g.flags & EPI_ACCUM) && tiles * ksplit < 256) {
+    int ks = (int)std::max(1L, 256 / tiles);
+    ks = std::min(ks, std::max(1, g.K / 256));
+    if (ks > ksplit) {
+      int kps = (g.K + ks - 1) / ks;
+      kps = (kps + big::KT - 1) / big::KT * big::KT;
+      ksplit = (g.K + kps - 1) / kps;
+      g.k_per_split = kps;
+    }
+  }
+  if (tiles * ksplit < 128) return false;
+  if (mode == 0) launch_big_t<false, false>(g, ksplit, st);
+  else if (mode == 1) launch_big_t<false, true>(g, ksplit, st);
+  else launch_big_t<true, true>(g, ksplit, st);
+  return true;
+}
+
 void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
+  if (try_big(mode, g_in, ksplit, st)) return;
   GemmArgs g = g_in;
   if (to_nn(g, mode, st)) mode = 0;
   if (mode == 0) dispatch<false, false>(g, ksplit, st);
@@ -603,6 +905,8 @@ struct Pending {
 } pending;
 
 }  // namespace
+
+extern "C" void mta_gemm_set_big(int on) { g_big_override = on; }
 
 // launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
 extern "C" void mta_gemm_flush() {

@@ -47,6 +47,7 @@ def timeit(fn, reps=20, warm=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
+    ap.add_argument("--ab", action="store_true", help="every shape on the 256x256 kernel and on the 128-tile path")
     args = ap.parse_args()
     from masters_thesis_amd.ops import _lib
     from masters_thesis_amd.ops.extras import EPI_ACCUM, gemm, gemm_flush, wgrad_split
@@ -55,7 +56,9 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     rows = []
-    for name, mode, M, N, K in SHAPES:
+    variants = (1, 0) if args.ab else (-1,)
+    for (name, mode, M, N, K), big in [(sh, v) for sh in SHAPES for v in variants]:
+        _lib.lib().gemm_set_big(big)
         if mode == 0:
             A = torch.randn(M, K, device=dev).bfloat16()
             B = torch.randn(N, K, device=dev).bfloat16()
@@ -86,7 +89,7 @@ def main():
         err = ((out - ref).abs().max() / ref.abs().max()).item()
         us = timeit(fn)
         tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
-        row = {"shape": name, "mode": mode, "M": M, "N": N, "K": K, "ksplit": ks, "us": round(us, 2),
+        row = {"shape": name, "big": big, "mode": mode, "M": M, "N": N, "K": K, "ksplit": ks, "us": round(us, 2),
                "tflops": round(tf, 1), "rel_err": err}
         rows.append(row)
         print(json.dumps(row), flush=True)

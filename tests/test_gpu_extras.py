@@ -71,6 +71,72 @@ def test_gemm_input_grad_dgelu_and_weight_grad_split():
     assert _rel(gb - 1, dYb.float().sum(0)) < 2e-3
 
 
+def _ran_kernel(fn, name):
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return any(name in e.key for e in prof.key_averages())
+
+
+# the 256 x 256 LDS-DMA kernel (csrc/gemm.hip, namespace big) in its three operand layouts, on ragged shapes (M, N not
+# multiples of 256, K a multiple of 32 but not of 64, re-split K for the accumulating weight gradient), against an fp32
+# PyTorch product and against the 128-tile path of the same call
+@pytest.mark.parametrize("mode,M,N,K", [(0, 4000, 2056, 544), (0, 4096, 2048, 2048), (1, 4000, 2056, 544),
+                                        (1, 6400, 2048, 2048), (2, 1032, 776, 4000), (2, 2048, 2048, 6400)])
+def test_big_tile_gemm(mode, M, N, K):
+    from masters_thesis_amd.ops import _lib
+    from masters_thesis_amd.ops import extras as X
+
+    C = _lib.lib()
+    torch.manual_seed(mode * 7 + M)
+    if mode == 0:
+        A, B = _bf(torch.randn(M, K) * 0.5), _bf(torch.randn(N, K) * 0.1)
+        bias, res = torch.randn(N, device=DEV), torch.randn(M, N, device=DEV)
+        ref_pre = A.float() @ B.float().t() + bias
+        outs = []
+        for big in (1, 0):
+            C.gemm_set_big(big)
+            pre = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+            out = torch.empty(M, N, device=DEV)
+            fn = lambda: X.gemm(0, A, B, M, N, K, K, K, flags=X.EPI_BIAS | X.EPI_GELU | X.EPI_RESID,  # noqa: E731
+                                bias=bias, resid=res, aux_pre=pre, out_f32=out)
+            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _rel(pre.float(), ref_pre) < 5e-3
+            assert _rel(out, Fn.gelu(ref_pre) + res) < 2e-3
+            outs.append(out.clone())
+    elif mode == 1:
+        A, B = _bf(torch.randn(M, K)), _bf(torch.randn(K, N) * 0.1)  # dY [M][K], W [K=out][N=in]
+        pre = _bf(torch.randn(M, N))
+        p = pre.float().requires_grad_(True)
+        (ref,) = torch.autograd.grad(Fn.gelu(p), p, A.float() @ B.float())
+        outs = []
+        for big in (1, 0):
+            C.gemm_set_big(big)
+            out = torch.empty(M, N, device=DEV)
+            fn = lambda: X.gemm(1, A, B, M, N, K, K, N, flags=X.EPI_DGELU, aux_in=pre, out_f32=out)  # noqa: E731
+            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _rel(out, ref) < 3e-3
+            outs.append(out.clone())
+    else:
+        A, B = _bf(torch.randn(K, M)), _bf(torch.randn(K, N))  # dY [tokens][M], X [tokens][N]
+        ref = A.float().t() @ B.float()
+        outs = []
+        for big in (1, 0):
+            C.gemm_set_big(big)
+            gw = torch.ones(M, N, device=DEV)
+            gb = torch.ones(M, device=DEV)
+            fn = lambda: X.gemm(2, A, B, M, N, K, M, N, flags=X.EPI_ACCUM, out_f32=gw, ldc=N, n_store=N,  # noqa: E731
+                                ksplit=X.wgrad_split(M, N, K), bias_grad=gb)
+            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _rel(gw - 1, ref) < 2e-3
+            assert _rel(gb - 1, A.float().sum(0)) < 2e-3
+            outs.append(gw.clone())
+    C.gemm_set_big(-1)
+    assert _rel(outs[0], outs[1]) < 2e-3
+
+
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("D", [128, 256, 1024, 1536, 2048])
 def test_norm_forward_backward(rms, D):
