@@ -66,7 +66,7 @@ void mta_gemm_set_big(int on);
 void mta_norm_flush();
 void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
-                 const int* rows_p, const int* cols_p, const int* ld_src, hipStream_t st);
+                 const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds, hipStream_t st);
 int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
              const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
              float drop_p, const float* dy, const float* dres, const void* pre, void* dx_bf16, float* dx_f32,
@@ -516,7 +516,7 @@ void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, i
   TORCH_CHECK(rc == 0, "gemm_bf16: unsupported arguments (rc=", rc, ", M=", M, " N=", N, " K=", K, ")");
 }
 
-void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
+void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, const OptT& seeds) {
   TORCH_CHECK(src.size() == dst.size() && !src.empty() && src.size() <= 16, "cast_pad: 1..16 tensor pairs");
   std::vector<const float*> sp;
   std::vector<void*> dp;
@@ -537,8 +537,15 @@ void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
     ld.push_back((int)s2.stride(0));
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(src[0].device());
+  uint64_t* sd = nullptr;
+  int ns = 0;
+  if (seeds.has_value() && seeds->defined()) {
+    MTA_CHECK_GPU(*seeds, at::kLong);
+    sd = reinterpret_cast<uint64_t*>(seeds->data_ptr<int64_t>());
+    ns = (int)seeds->numel();
+  }
   TORCH_CHECK(mta_cast_pad((int)src.size(), sp.data(), dp.data(), rows.data(), cols.data(), rows_p.data(),
-                           cols_p.data(), ld.data(), cur_stream()) == 0, "cast_pad failed");
+                           cols_p.data(), ld.data(), sd, ns, cur_stream()) == 0, "cast_pad failed");
 }
 
 void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, double eps, const OptT& gamma,
@@ -947,7 +954,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
-  m.def("cast_pad", &cast_pad);
+  m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
   m.def("norm", &norm);
   m.def("attention", &attention);
   m.def("lstm_fwd_layer", &lstm_fwd_layer);

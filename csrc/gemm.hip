@@ -408,10 +408,16 @@ constexpr int TM = 256, TN = 256, KT = 32, THREADS = 512;
 #ifndef MTA_GEMM_BIG_AHEAD
 #define MTA_GEMM_BIG_AHEAD 4
 #endif
-constexpr int AHEAD = MTA_GEMM_BIG_AHEAD, SLOTS = AHEAD + 1;  // k-tiles in flight beyond the one multiplied
+#ifndef MTA_GEMM_DMA_IN_READS
+#define MTA_GEMM_DMA_IN_READS 0  // 1: issue the DMA in the read segment (needs one more ring slot)
+#endif
+constexpr int AHEAD = MTA_GEMM_BIG_AHEAD;                      // k-tiles in flight beyond the one multiplied
+constexpr int SLOTS = AHEAD + 1 + MTA_GEMM_DMA_IN_READS;
 constexpr int OP_BYTES = 256 * KT * 2;     // one operand's k-tile image: 16 KB
 constexpr int SLOT_BYTES = 2 * OP_BYTES;  // A | B
-constexpr int LDS_BYTES = SLOTS * SLOT_BYTES;
+constexpr int EPI_ROW = 68;                                   // staged row: 64 f32 + 4 pad (conflict-free writes)
+constexpr int EPI_WAVE_BYTES = 64 * EPI_ROW * 4;               // 64 rows of one wave's 128 x 64 tile per pass
+constexpr int LDS_BYTES = SLOTS * SLOT_BYTES > 8 * EPI_WAVE_BYTES ? SLOTS * SLOT_BYTES : 8 * EPI_WAVE_BYTES;
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -494,6 +500,146 @@ __device__ __forceinline__ void wait_tiles(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Epilogue through LDS (the ring is free once the loop's last barrier passed: every DMA and fragment read retired):
+// each wave stages 64 of its 128 x 64 output rows at a time as [row][64 f32] and reads them back row-contiguous, so
+//   * plain outputs / operand reads are 16-B (f32) or 8-B (bf16) per lane, four full 256-B row segments per
+//     instruction (the accumulator layout stores 4 rows x 64 B per instruction, 2-byte stores for bf16: the r3 probe
+//     measured ~83k cycles per 256 x 256 tile for the direct epilogue, 30-40 % of the kernel);
+//   * split-K atomics are one 256-B row segment per instruction (lane = column).
+// `vec` = every pointer / ldc allows the wide forms; otherwise the same walk with per-element accesses.
+__device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&acc)[8][4], const int mbase,
+                                             const int nbase, const bool split, const int lane, float* stage) {
+  const bool accum = (g.flags & EPI_ACCUM) != 0;
+  const bool vec = (g.ldc & 3) == 0 && ((uintptr_t)g.out_f32 & 15) == 0 && ((uintptr_t)g.out_bf16 & 7) == 0 &&
+                   ((uintptr_t)g.aux_pre & 7) == 0 && ((uintptr_t)g.resid & 15) == 0 && ((uintptr_t)g.aux_in & 7) == 0;
+  uint32_t dseed = 0, dthr = 0;
+  float dscale = 0.f;
+  if (g.flags & EPI_DROPOUT) {
+    const uint64_t sd = *g.seed;
+    dseed = (uint32_t)(sd ^ (sd >> 32));
+    dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
+    dscale = 1.0f / (1.0f - g.drop_p);
+  }
+  const int cc = 4 * (lane & 15);  // this lane's 4 columns in the row-contiguous walk
+  const int n = nbase + cc;
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!accum && (g.flags & EPI_BIAS)) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = n + e < g.N ? g.bias[n + e] : 0.f;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          stage[(16 * ii + 4 * (lane >> 4) + r) * EPI_ROW + 16 * j + (lane & 15)] = g.alpha * acc[4 * pass + ii][j][r];
+    const int mrow = mbase + 64 * pass;
+    // every LDS read of the pass BEFORE its first global access: hipcc waits vmcnt(0) ahead of an LDS access that
+    // follows outstanding vector-memory ops in a kernel that issues LDS-DMA (it cannot tell them apart), which
+    // serialised one store round trip per row quad (r3 stamp probe: ~65-100k cycles per tile)
+    if (accum && split) {
+      const int nc = nbase + lane;
+      float col[64];
+#pragma unroll
+      for (int rr = 0; rr < 64; ++rr) col[rr] = stage[rr * EPI_ROW + lane];
+#pragma unroll
+      for (int rr = 0; rr < 64; ++rr)
+        if (mrow + rr < g.M && nc < g.n_store) atomicAdd(g.out_f32 + (size_t)(mrow + rr) * g.ldc + nc, col[rr]);
+      continue;
+    }
+    float4 quad[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) quad[q] = *reinterpret_cast<const float4*>(&stage[(4 * q + (lane >> 4)) * EPI_ROW + cc]);
+    const bool prefetch = (g.flags & (EPI_RESID | EPI_DGELU)) || accum;
+#pragma unroll 2
+    for (int q0 = 0; q0 < 16; q0 += 8) {
+      float pin[8][4];
+      if (prefetch) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int m = mrow + 4 * (q0 + q) + (lane >> 4);
+          const size_t o = (size_t)m * g.ldc + n;
+          const bool rowok = m < g.M;
+          if (vec && rowok && n + 3 < g.n_store) {
+            if (accum || (g.flags & EPI_RESID)) {
+              const float4 t = *reinterpret_cast<const float4*>((accum ? g.out_f32 : g.resid) + o);
+              pin[q][0] = t.x; pin[q][1] = t.y; pin[q][2] = t.z; pin[q][3] = t.w;
+            } else {
+              Bf8 t;
+              t.u.x = reinterpret_cast<const uint2*>(g.aux_in + o)->x;
+              t.u.y = reinterpret_cast<const uint2*>(g.aux_in + o)->y;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) pin[q][e] = (float)t.e[e];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool ok = rowok && n + e < g.n_store;
+              pin[q][e] = !ok ? 0.f : accum ? g.out_f32[o + e] : (g.flags & EPI_RESID) ? g.resid[o + e]
+                                                                                      : (float)g.aux_in[o + e];
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int rr = 4 * (q0 + q) + (lane >> 4);
+        const int m = mrow + rr;
+        if (m >= g.M) continue;
+        const float4 t = quad[q0 + q];
+        float v[4] = {t.x, t.y, t.z, t.w};
+        float pre[4];
+        uint32_t hsh = 0;
+        if (g.flags & EPI_DROPOUT) hsh = (uint32_t)m;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (accum) {
+            v[e] += prefetch ? pin[q][e] : 0.f;
+            continue;
+          }
+          v[e] += bias4[e];
+          pre[e] = v[e];
+          if (g.flags & EPI_GELU) v[e] = mta_gelu(v[e]);
+          if (g.flags & EPI_DROPOUT) {
+            const uint32_t h = gemm_pair_hash(dseed, hsh >> 1, (uint32_t)(n + e));
+            const uint32_t u16 = (hsh & 1) ? (h >> 16) : (h & 0xFFFFu);
+            v[e] *= u16 >= dthr ? dscale : 0.f;
+          }
+          if (g.flags & EPI_DGELU) v[e] *= mta_gelu_grad(pin[q][e]);
+          if (g.flags & EPI_RESID) v[e] += pin[q][e];
+        }
+        const size_t o = (size_t)m * g.ldc + n;
+        if (vec && n + 3 < g.n_store) {
+          if (g.out_f32) *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+          if (!accum && g.out_bf16) {
+            Bf8 b;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)v[e];
+            *reinterpret_cast<uint2*>(g.out_bf16 + o) = make_uint2(b.u.x, b.u.y);
+          }
+          if (!accum && g.aux_pre) {
+            Bf8 b;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)pre[e];
+            *reinterpret_cast<uint2*>(g.aux_pre + o) = make_uint2(b.u.x, b.u.y);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n + e >= g.n_store) continue;
+            if (g.out_f32) g.out_f32[o + e] = v[e];
+            if (!accum && g.out_bf16) g.out_bf16[o + e] = (__bf16)v[e];
+            if (!accum && g.aux_pre) g.aux_pre[o + e] = (__bf16)pre[e];
+          }
+        }
+      }
+    }
+  }
+}
+
 template <bool AT, bool BT>
 __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -536,7 +682,7 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
   wait_tiles(pro - 1);
   barrier();
   if (row1) barrier();  // the second wave row runs one barrier behind
-  int rd = 0, wr = AHEAD;  // ring slots of tile j and of tile j + AHEAD
+  int rd = 0, wr = AHEAD % SLOTS;  // ring slots of tile j and of tile j + AHEAD
 #ifdef MTA_GEMM_STAMPS
   unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   GSTAMP(tloop0);
@@ -550,15 +696,23 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
     for (int i = 0; i < 8; ++i) af[i] = frag<AT>(slot, wm * 128 + 16 * i, lane);
 #pragma unroll
     for (int n = 0; n < 4; ++n) bfr[n] = frag<BT>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
+#if MTA_GEMM_DMA_IN_READS
+    if (j + AHEAD < nk) stage(j + AHEAD, wr);
+    GSTAMP(t1);
+    if (row1) wait_tiles(min(nk - 1, j + AHEAD) - (j + 1));
+#else
     GSTAMP(t1);
     // row 1 ends its read segment at the barrier before row 0 reads tile j + 1: everything up to it landed
     if (row1) wait_tiles(min(nk - 1, j - 1 + AHEAD) - (j + 1));
+#endif
     GSTAMP(t2);
     barrier();
     GSTAMP(t3);
     // [MFMA] tile j, with the DMA of tile j + AHEAD issued up front into the slot tile j - 1 used (both rows
     // retired their reads of it: lgkmcnt(0) at their previous MFMA segments, and a barrier since)
+#if !MTA_GEMM_DMA_IN_READS
     if (j + AHEAD < nk) stage(j + AHEAD, wr);
+#endif
     if (want_rowsum) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -569,12 +723,16 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
+#ifndef MTA_GEMM_NO_PRIO
     __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
+#ifndef MTA_GEMM_NO_PRIO
     __builtin_amdgcn_s_setprio(0);
+#endif
     GSTAMP(t4);
     if (!row1) wait_tiles(min(nk - 1, j + AHEAD) - (j + 1));
     GSTAMP(t5);
@@ -595,7 +753,8 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
   GACC(6, tloop0, tloop1);
 #endif
 
-  gemm_epilogue<8, 4, 2>(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, lane);
+  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, lane,
+               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
   if (want_rowsum) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {

@@ -23,10 +23,38 @@ struct CastItem {
 struct CastArgs {
   CastItem item[16];
   int n;
+  uint64_t* seeds;  // dropout seeds advanced by this launch (the step's first kernel of the encoder), or null
+  int nseeds;
 };
 
+// 8 consecutive columns per thread (16-B bf16 store; two 16-B loads when the source row allows), 32-bit index math;
+// rows past `rows` and columns past `cols` are written as zeros (the padded operand)
 __global__ void cast_pad_kernel(CastArgs a) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < a.nseeds)
+    a.seeds[threadIdx.x] += 0x9E3779B97F4A7C15ull;  // fresh counter-hash seed per step for every dropout site
   const CastItem it = a.item[blockIdx.y];
+  if ((it.cols_p & 7) == 0 && (long)it.rows_p * it.cols_p < (1L << 31)) {
+    const int c8 = it.cols_p >> 3;
+    const int total = it.rows_p * c8;
+    const bool vsrc = (it.ld_src & 3) == 0 && (((uintptr_t)it.src) & 15) == 0;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+      const int r = e / c8, c = (e - r * c8) * 8;
+      float v[8];
+      if (r < it.rows && vsrc && c + 8 <= it.cols) {
+        const float4 x0 = *reinterpret_cast<const float4*>(it.src + (size_t)r * it.ld_src + c);
+        const float4 x1 = *reinterpret_cast<const float4*>(it.src + (size_t)r * it.ld_src + c + 4);
+        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = (r < it.rows && c + k < it.cols) ? it.src[(size_t)r * it.ld_src + c + k] : 0.f;
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o[k] = (__bf16)v[k];
+      *reinterpret_cast<bf16x8*>(it.dst + (size_t)r * it.cols_p + c) = o;
+    }
+    return;
+  }
   const long total = (long)it.rows_p * it.cols_p;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int r = (int)(e / it.cols_p), c = (int)(e % it.cols_p);
@@ -483,14 +511,17 @@ int norm_blocks(int M, bool bwd) {
 }  // namespace
 
 extern "C" int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
-                            const int* rows_p, const int* cols_p, const int* ld_src, hipStream_t st) {
-  if (n < 1 || n > 16) return 1;
+                            const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds,
+                            hipStream_t st) {
+  if (n < 1 || n > 16 || nseeds < 0 || nseeds > 256 || (nseeds && !seeds)) return 1;
   CastArgs a;
   a.n = n;
+  a.seeds = seeds;
+  a.nseeds = nseeds;
   long maxe = 0;
   for (int i = 0; i < n; ++i) {
     a.item[i] = CastItem{src[i], static_cast<__bf16*>(dst[i]), rows[i], cols[i], rows_p[i], cols_p[i], ld_src[i]};
-    const long e = (long)rows_p[i] * cols_p[i];
+    const long e = (long)rows_p[i] * cols_p[i] / ((cols_p[i] & 7) == 0 ? 8 : 1);
     maxe = e > maxe ? e : maxe;
   }
   int bx = (int)((maxe + 255) / 256);

@@ -31,19 +31,27 @@ __global__ void fill_kernel(__bf16* p, size_t n, uint32_t seed) {
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096;
   const int K = argc > 3 ? atoi(argv[3]) : 4096, mode = argc > 4 ? atoi(argv[4]) : 0;
+  const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 1: the MLP forward epilogue (bias + GELU, bf16 pre-activation)
   __bf16 *A, *B;
   float* C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
   CK(hipMalloc(&B, (size_t)N * K * 2));
   CK(hipMalloc(&C, (size_t)M * N * 4));
+  __bf16* pre = nullptr;
+  float* bias = nullptr;
+  if (epi) {
+    CK(hipMalloc(&pre, (size_t)M * N * 2));
+    CK(hipMalloc(&bias, (size_t)N * 4));
+    CK(hipMemset(bias, 0, (size_t)N * 4));
+  }
   fill_kernel<<<1024, 256>>>(A, (size_t)M * K, 1u);
   fill_kernel<<<1024, 256>>>(B, (size_t)N * K, 2u);
   // mode 0: A [M][K], B [N][K]; 1: B [K][N]; 2: A [K][M], B [K][N] (accumulating, split-K)
   const int lda = mode == 2 ? M : K, ldb = mode == 0 ? K : N;
-  const int flags = mode == 2 ? 8 : 0;
+  const int flags = mode == 2 ? 8 : (epi ? 1 | 2 : 0);
   auto run = [&] {
-    const int rc = mta_gemm_bf16(mode, A, B, M, N, K, lda, ldb, 1.f, flags, nullptr, nullptr, nullptr, nullptr, 0.f,
-                                 nullptr, C, nullptr, N, N, 1, nullptr, 0, 0);
+    const int rc = mta_gemm_bf16(mode, A, B, M, N, K, lda, ldb, 1.f, flags, bias, nullptr, nullptr, nullptr, 0.f,
+                                 nullptr, C, pre, N, N, 1, nullptr, 0, 0);
     if (rc) {
       printf("gemm rc=%d\n", rc);
       exit(1);
@@ -66,7 +74,7 @@ int main(int argc, char** argv) {
   }
   std::sort(ts.begin(), ts.end());
   const double us = ts[ts.size() / 2];
-  printf("gemm_probe M=%d N=%d K=%d mode=%d: %.2f us  %.1f TFLOP/s\n", M, N, K, mode, us,
+  printf("gemm_probe M=%d N=%d K=%d mode=%d epi=%d: %.2f us  %.1f TFLOP/s\n", M, N, K, mode, epi, us,
          2.0 * M * N * K / (us * 1e-6) / 1e12);
 #ifdef MTA_GEMM_STAMPS
   unsigned long long zero[8][8] = {};

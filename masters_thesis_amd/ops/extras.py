@@ -85,19 +85,18 @@ def wgrad_split(M: int, N: int, K: int) -> int:
     return max(1, min(256 // max(tiles, 1), K // 128))
 
 
-def cast_pad(srcs: Sequence[Tensor], dsts: Sequence[Tensor]) -> None:
+def cast_pad(srcs: Sequence[Tensor], dsts: Sequence[Tensor], seeds: Optional[Tensor] = None) -> None:
+    """fp32 -> zero-padded bf16 operands (rows and columns past the source are zeros); ``seeds``: the encoder's
+    dropout seeds, advanced by the same launch (one fresh counter-hash seed per site and step, no ATen kernel)."""
     C = lib()
     for i in range(0, len(srcs), 16):
-        C.cast_pad(list(srcs[i:i + 16]), list(dsts[i:i + 16]))
+        C.cast_pad(list(srcs[i:i + 16]), list(dsts[i:i + 16]), seeds if i == 0 else None)
 
 
 def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
     return torch.empty((w.shape[0], cols_p), device=w.device, dtype=torch.bfloat16)
 
 
-def advance_seeds(seeds: Tensor) -> None:
-    # per-step, in-graph: every dropout site gets a fresh counter-hash seed
-    seeds.add_(0x9E3779B97F4A7C15 - (1 << 64))
 
 
 def _grad_view(p: Tensor) -> Tensor:
@@ -135,14 +134,12 @@ class _MlpEncoderFn(torch.autograd.Function):
         per = 4 if norm == "layernorm" else 3
         rms = norm != "layernorm"
         drop = dropout > 0 and training
-        if drop:
-            advance_seeds(seeds)
         K0 = x[0].numel()
         dims = [K0] + [params[per * i].shape[0] for i in range(L)]
         kp = [_r8(d) for d in dims]
         X0 = torch.empty((Mp, kp[0]), device=dev, dtype=torch.bfloat16)
         wb = [_padded_bf16(params[per * i], kp[i]) for i in range(L)]
-        cast_pad([x.reshape(N, K0)] + [params[per * i] for i in range(L)], [X0] + wb)
+        cast_pad([x.reshape(N, K0)] + [params[per * i] for i in range(L)], [X0] + wb, seeds if drop else None)
         Xs, pres, acts, means, rstds = [X0], [], [], [], []
         h = None
         for i in range(L):
@@ -186,8 +183,12 @@ class _MlpEncoderFn(torch.autograd.Function):
         Xs, pres, acts = saved[:L], saved[L:2 * L], saved[2 * L:]
         means, rstds = ctx.stats
         dev = dh.device
-        dy = torch.zeros((Mp, dims[-1]), device=dev, dtype=torch.float32)
-        dy[:N].copy_(dh)
+        if Mp == N and dh.dtype == torch.float32 and dh.is_contiguous():
+            dy = dh  # read-only below: no zero-fill + copy of the output gradient
+        else:
+            dy = torch.empty((Mp, dims[-1]), device=dev, dtype=torch.float32)
+            dy[:N].copy_(dh)
+            dy[N:].zero_()
         for i in range(L - 1, -1, -1):
             D, Din = dims[i + 1], dims[i]
             dpre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
@@ -279,8 +280,6 @@ class _TransformerEncoderFn(torch.autograd.Function):
         nb = len(BLOCK_NAMES)
         d = params[0].shape[0]
         drop = dropout > 0 and training
-        if drop:
-            advance_seeds(seeds)
         Fp = _r8(F)
         C = lib()
         # bf16 operands: input tokens + every matrix (padded along K only where needed)
@@ -290,10 +289,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
             base = 2 + nb * l
             mats += [params[base + 1], params[base + 3], params[base + 6], params[base + 8]]
         mats_b = [_padded_bf16(w, _r8(w.shape[1])) for w in mats]
-        xin_src = x.reshape(N * T, F)
-        if Np != N:
-            xin_src = torch.cat([xin_src, xin_src.new_zeros(((Np - N) * T, F))])
-        cast_pad([xin_src] + mats, [Xin] + mats_b)
+        # rows of the padded sequences (Np > N) are zero-filled by the cast itself
+        cast_pad([x.reshape(N * T, F)] + mats, [Xin] + mats_b, seeds if drop else None)
         xs = torch.empty((M, d), device=dev, dtype=torch.float32)
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]
