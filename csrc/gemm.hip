@@ -948,9 +948,71 @@ void launch_pair_nn(int c, const GemmArgs& g1, int k1, const GemmArgs& g2, int k
 
 void dispatch_mode(int mode, const GemmArgs& g, int ksplit, hipStream_t st);
 
+// ---- routing to the 256 x 256 kernel ----
+// MTA_GEMM_BIG=0 disables it; mta_gemm_set_big(0/1) overrides at run time (tests compare the two paths in one process)
+int g_big_override = -1;
+inline bool big_on() {
+  static const bool env_on = [] {
+    const char* e = getenv("MTA_GEMM_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return g_big_override >= 0 ? g_big_override == 1 : env_on;
+}
+
+template <bool AT, bool BT>
+void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<AT, BT>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, big::LDS_BYTES) == hipSuccess;
+  }();
+  (void)attr;
+  const int nx = (g.N + big::TN - 1) / big::TN, ny = (g.M + big::TM - 1) / big::TM;
+  gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(g, nx, ny, ksplit);
+}
+
+// Eligible for the 256 x 256 kernel: 32-deep k-tiles and enough macro-tiles to fill at least half the CUs; the
+// split-K accumulating form is re-split towards one wave of 256 workgroups (>= 8 k-tiles per split).  Returns the
+// split it runs with (g.k_per_split updated), 0 = not eligible.
+int big_split(GemmArgs& g, int ksplit) {
+  if (!big_on() || g.K % big::KT || g.M < 64 || g.N < 64) return 0;
+  const long tiles = (long)((g.M + big::TM - 1) / big::TM) * ((g.N + big::TN - 1) / big::TN);
+  if ((g.flags & EPI_ACCUM) && tiles * ksplit < 256) {
+    int ks = (int)std::max(1L, 256 / tiles);
+    ks = std::min(ks, std::max(1, g.K / 256));
+    if (ks > ksplit) {
+      int kps = (g.K + ks - 1) / ks;
+      kps = (kps + big::KT - 1) / big::KT * big::KT;
+      ksplit = (g.K + kps - 1) / kps;
+      g.k_per_split = kps;
+    }
+  }
+  return tiles * ksplit < 128 ? 0 : ksplit;
+}
+
+bool big_eligible(const GemmArgs& g_in, int ksplit) {
+  GemmArgs g = g_in;
+  return big_split(g, ksplit) > 0;
+}
+
+bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
+  GemmArgs g = g_in;
+  ksplit = big_split(g, ksplit);
+  if (ksplit <= 0) return false;
+  if (mode == 0) launch_big_t<false, false>(g, ksplit, st);
+  else if (mode == 1) launch_big_t<false, true>(g, ksplit, st);
+  else launch_big_t<true, true>(g, ksplit, st);
+  return true;
+}
+
 // (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately.
 // Big pairs run on transposed copies (both NN) when both problems qualify.
 bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, hipStream_t st) {
+  // big problems: the 256 x 256 kernel each (every one of them fills the chip on its own)
+  if (big_eligible(g1_in, k1) && big_eligible(g2_in, k2)) {
+    try_big(2, g1_in, k1, st);
+    try_big(1, g2_in, k2, st);
+    return true;
+  }
   const int c = tile_config(g1_in, k1);
   if (c != tile_config(g2_in, k2)) return false;
   GemmArgs g1 = g1_in, g2 = g2_in;
@@ -999,51 +1061,6 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
     if (deep) launch<64, 64, 128, AT, BT>(g, ksplit, st);
     else launch<64, 64, 32, AT, BT>(g, ksplit, st);
   }
-}
-
-// ---- routing to the 256 x 256 kernel ----
-// MTA_GEMM_BIG=0 disables it; mta_gemm_set_big(0/1) overrides at run time (tests compare the two paths in one process)
-int g_big_override = -1;
-inline bool big_on() {
-  static const bool env_on = [] {
-    const char* e = getenv("MTA_GEMM_BIG");
-    return !(e && e[0] == '0');
-  }();
-  return g_big_override >= 0 ? g_big_override == 1 : env_on;
-}
-
-template <bool AT, bool BT>
-void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
-  static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<AT, BT>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, big::LDS_BYTES) == hipSuccess;
-  }();
-  (void)attr;
-  const int nx = (g.N + big::TN - 1) / big::TN, ny = (g.M + big::TM - 1) / big::TM;
-  gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(g, nx, ny, ksplit);
-}
-
-// true = launched on the 256 x 256 kernel: 32-deep k-tiles, and enough macro-tiles to fill at least half the CUs
-// (the split-K accumulating form re-splits K towards one wave of 256 workgroups, >= 8 k-tiles per split)
-bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
-  if (!big_on() || g_in.K % big::KT || g_in.M < 64 || g_in.N < 64) return false;
-  GemmArgs g = g_in;
-  const long tiles = (long)((g.M + big::TM - 1) / big::TM) * ((g.N + big::TN - 1) / big::TN);
-  if ((g.flags & EPI_ACCUM) && tiles * ksplit < 256) {
-    int ks = (int)std::max(1L, 256 / tiles);
-    ks = std::min(ks, std::max(1, g.K / 256));
-    if (ks > ksplit) {
-      int kps = (g.K + ks - 1) / ks;
-      kps = (kps + big::KT - 1) / big::KT * big::KT;
-      ksplit = (g.K + kps - 1) / kps;
-      g.k_per_split = kps;
-    }
-  }
-  if (tiles * ksplit < 128) return false;
-  if (mode == 0) launch_big_t<false, false>(g, ksplit, st);
-  else if (mode == 1) launch_big_t<false, true>(g, ksplit, st);
-  else launch_big_t<true, true>(g, ksplit, st);
-  return true;
 }
 
 void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {

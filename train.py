@@ -19,6 +19,7 @@ last.ckpt if present, used by the launcher's retries), ``init_from=<ckpt>``
 from __future__ import annotations
 
 import os
+import time
 from pathlib import Path
 
 import torch
@@ -117,7 +118,14 @@ def main(cfg):
         last = checkpoint_dir / "last.ckpt"
         resume = str(last) if last.exists() else None
         print(f"resume=auto: {'resuming from ' + resume if resume else 'no checkpoint yet, starting fresh'}")
+    step0 = trainer.global_step
+    t_fit = time.perf_counter()
     trainer.fit(model, datamodule=dm, ckpt_path=resume)
+    t_fit = time.perf_counter() - t_fit
+    # one machine-readable line per trial (scripts/gpu_sweep_throughput.sh sums them over a sweep)
+    n_windows = (trainer.global_step - step0) * int(cfg.datamodule.batch_size)
+    print(f"[throughput] train_windows={n_windows} fit_s={t_fit:.3f} windows_per_s={n_windows / max(t_fit, 1e-9):.1f}",
+          flush=True)
 
     ckpt_cb = trainer.checkpoint_callback
     best = ckpt_cb.best_model_score
