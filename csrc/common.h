@@ -117,11 +117,22 @@ __device__ __forceinline__ void mta_wait_vmcnt() {
 }
 
 // GELU (erf form, torch.nn.GELU() default) and its derivative.
-__device__ __forceinline__ float mta_gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf(x / sqrt 2) for the exact (erf) GELU: Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7) on |z|, one exp (shared
+// with the GELU derivative's density) and one rcp instead of the library erff's branchy ~40-instruction sequence --
+// the GELU epilogue of the mlp_large forward GEMM was ~15 % of that kernel (r3 GEMM probe, epi=1 vs plain)
+__device__ __forceinline__ float mta_erf_sqrt1_2(float x, float e /* = exp(-x*x/2) */) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float p = t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f),
+                           0.254829592f);
+  return copysignf(1.0f - p * e, x);
+}
+__device__ __forceinline__ float mta_gelu(float x) {
+  return 0.5f * x * (1.0f + mta_erf_sqrt1_2(x, __expf(-0.5f * x * x)));
+}
 __device__ __forceinline__ float mta_gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const float e = __expf(-0.5f * x * x);
+  return 0.5f * (1.0f + mta_erf_sqrt1_2(x, e)) + x * 0.3989422804014327f * e;
 }
 
 // Counter-based dropout: keep(seed, row, col) from a stateless 32-bit hash (murmur3-style finaliser of

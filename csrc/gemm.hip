@@ -49,6 +49,7 @@ struct GemmArgs {
   int ldc, n_store;        // columns [0, n_store) of C are written (N may include zero padding)
   int k_per_split;          // multiple of BK
   float* bias_grad;         // AT mode: += row sums of A over K  ([M])
+  float* slab;              // split-K partials of the 256 x 256 kernel: [split][M][N] fp32 (null: f32 atomics)
 };
 
 
@@ -384,12 +385,12 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
 // CU:
 //   * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 outputs = 8 x 4 accumulators of v_mfma_f32_16x16x32_bf16
 //     (32 MFMAs per 32-deep k-tile against 12 fragment reads: the MFMA pipe, not LDS, is the limit);
-//   * operands go global -> LDS by global_load_lds (16 B per lane, no VGPR round trip) into a ring of AHEAD + 1 k-tile
-//     slots (A and B 16 KB each per slot; AHEAD = 4: 160 KB, the whole LDS), AHEAD k-tiles ahead of the one being
+//   * operands go global -> LDS by global_load_lds (16 B per lane, no VGPR round trip) into a ring of AHEAD + 2 k-tile
+//     slots (A and B 16 KB each per slot; AHEAD = 3: 160 KB, the whole LDS), AHEAD k-tiles ahead of the one being
 //     multiplied, waited with COUNTED vmcnt (never 0 in the loop) and raw s_barrier so the DMA stays in flight across
 //     barriers (the latency to hide is an L2/MALL miss under full load, ~1-2 us);
-//   * the two wave rows run one barrier apart ("ping-pong"): every k-tile is a [fragment reads] segment and an
-//     [DMA issue + MFMA] segment separated by barriers, and the second wave row enters one barrier late, so on every
+//   * the two wave rows run one barrier apart ("ping-pong"): every k-tile is a [fragment reads + DMA issue] segment
+//     and an [MFMA] segment separated by barriers, and the second wave row enters one barrier late, so on every
 //     SIMD one wave multiplies while its partner reads -- s_setprio(1) around each MFMA cluster keeps the compiler
 //     from moving MFMAs across the barriers;
 //   * k-contiguous operands ([rows][K]) land as [256 rows][32 k] images (64-B rows) whose 16-B chunks are XOR-swizzled
@@ -398,18 +399,22 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
 //     [32 k][256 cols] images (512-B rows, 32-B chunks XOR-swizzled by k-row bits 0,1,3) and are read transposed by
 //     ds_read_b64_tr_b16 (two per fragment), conflict-free: no transpose kernels, no transposing register staging.
 // Ring hazards (j = k-tile; segments R = reads, M = DMA issue + MFMAs; row 0: R0 M0 R1 M1 ..., row 1: -- R0 M0 R1 ...):
-//   WAR: tile j+AHEAD is issued at the start of M_j into slot (j+AHEAD) % (AHEAD+1) = the slot of tile j-1; both rows
-//        retired their reads of it (lgkmcnt(0) ahead of their MFMAs of M_{j-1}) before a barrier that precedes M_j;
+//   WAR: tile j+AHEAD is issued during R_j into slot (j+AHEAD) % (AHEAD+2) = the slot of tile j-2; both rows retired
+//        their reads of it (lgkmcnt(0) ahead of their MFMAs of M_{j-2}) before a barrier that precedes R_j (with the
+//        MTA_GEMM_DMA_IN_READS=0 form: issued at the head of M_j into the slot of tile j-1, AHEAD+1 slots);
 //   RAW: row 0 first reads tile j+1 right after the barrier that closes its M_j, so at that barrier every wave has
 //        waited for all but the tiles it issued after tile j+1 (row 0 at the end of M_j, row 1 at the end of R_j).
 // Rows / columns beyond M, N are clamped on load (their outputs are not stored); K per split is a multiple of 32.
 namespace big {
 constexpr int TM = 256, TN = 256, KT = 32, THREADS = 512;
+// DMA issued in the read segment, 3 k-tiles ahead, 5 slots (160 KB): r3 probe A/B against issuing it at the head of
+// the MFMA segment (4 ahead, 5 slots): main loop 1832 -> 1555 cycles per k-tile, 4096^3 858 -> 892..1038 TF,
+// mlp_large forward 545 -> 590 TF, input gradient 665 -> 707 TF (profiles/r3_gemm_variants.txt)
 #ifndef MTA_GEMM_BIG_AHEAD
-#define MTA_GEMM_BIG_AHEAD 4
+#define MTA_GEMM_BIG_AHEAD 3
 #endif
 #ifndef MTA_GEMM_DMA_IN_READS
-#define MTA_GEMM_DMA_IN_READS 0  // 1: issue the DMA in the read segment (needs one more ring slot)
+#define MTA_GEMM_DMA_IN_READS 1  // 0: issue the DMA at the head of the MFMA segment (one ring slot fewer)
 #endif
 constexpr int AHEAD = MTA_GEMM_BIG_AHEAD;                      // k-tiles in flight beyond the one multiplied
 constexpr int SLOTS = AHEAD + 1 + MTA_GEMM_DMA_IN_READS;
@@ -503,12 +508,128 @@ __device__ __forceinline__ void wait_tiles(int n) {
 // Epilogue through LDS (the ring is free once the loop's last barrier passed: every DMA and fragment read retired):
 // each wave stages 64 of its 128 x 64 output rows at a time as [row][64 f32] and reads them back row-contiguous, so
 //   * plain outputs / operand reads are 16-B (f32) or 8-B (bf16) per lane, four full 256-B row segments per
-//     instruction (the accumulator layout stores 4 rows x 64 B per instruction, 2-byte stores for bf16: the r3 probe
-//     measured ~83k cycles per 256 x 256 tile for the direct epilogue, 30-40 % of the kernel);
+//     instruction (the accumulator layout stores 4 rows x 64 B per instruction, 2-byte stores for bf16);
 //   * split-K atomics are one 256-B row segment per instruction (lane = column).
-// `vec` = every pointer / ldc allows the wide forms; otherwise the same walk with per-element accesses.
+// The read-back loops are ROLLED (the r3 stamp probe measured ~85k cycles per tile for fully unrolled epilogues of
+// ~30k instructions: every wave of the chip streams a cold instruction path at once) and read the staging image with
+// inline-asm ds_reads: hipcc would otherwise wait vmcnt(0) -- the previous iteration's stores -- ahead of every LDS
+// access in a kernel that issues LDS-DMA.  `vec` = every pointer / ldc allows the wide forms.
+__device__ __forceinline__ float4 stage_read4(const float* p) {
+  float4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float stage_read1(const float* p) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* stage, const int mrow, const int n,
+                                          const int lane, const bool vec, const bool split, const int bz,
+                                          const float (&bias4)[4],
+                                          const uint32_t dseed, const uint32_t dthr, const float dscale) {
+  const bool accum = (g.flags & EPI_ACCUM) != 0;
+  if (accum && split && g.slab) {
+    // split-K partial: plain 16-B stores into this split's slab; splitk_reduce_kernel adds the slabs afterwards
+    const int cc = 4 * (lane & 15);
+    float* slab = g.slab + (size_t)bz * g.M * g.N;
+#pragma unroll 1
+    for (int q = 0; q < 16; ++q) {
+      const int rr = 4 * q + (lane >> 4);
+      const float4 t = stage_read4(stage + rr * EPI_ROW + cc);
+      if (mrow + rr < g.M && n + 3 < g.N) *reinterpret_cast<float4*>(slab + (size_t)(mrow + rr) * g.N + n) = t;
+    }
+    return;
+  }
+  if (accum && split) {
+    const int nc = n - 4 * (lane & 15) + lane;  // lane = column of the 64-wide slice
+#pragma unroll 1
+    for (int rr = 0; rr < 64; ++rr) {
+      const float v = stage_read1(stage + rr * EPI_ROW + lane);
+      if (mrow + rr < g.M && nc < g.n_store) atomicAdd(g.out_f32 + (size_t)(mrow + rr) * g.ldc + nc, v);
+    }
+    return;
+  }
+  const int cc = 4 * (lane & 15);
+#pragma unroll 1
+  for (int q = 0; q < 16; ++q) {
+    const int rr = 4 * q + (lane >> 4);
+    const int m = mrow + rr;
+    const float4 t = stage_read4(stage + rr * EPI_ROW + cc);
+    if (m >= g.M) continue;
+    const size_t o = (size_t)m * g.ldc + n;
+    const bool wide = vec && n + 3 < g.n_store;
+    float pin[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((g.flags & (EPI_RESID | EPI_DGELU)) || accum) {
+      if (wide) {
+        if (accum || (g.flags & EPI_RESID)) {
+          const float4 x = *reinterpret_cast<const float4*>((accum ? g.out_f32 : g.resid) + o);
+          pin[0] = x.x; pin[1] = x.y; pin[2] = x.z; pin[3] = x.w;
+        } else {
+          Bf8 x;
+          const uint2 u = *reinterpret_cast<const uint2*>(g.aux_in + o);
+          x.u.x = u.x;
+          x.u.y = u.y;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pin[e] = (float)x.e[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (n + e < g.n_store)
+            pin[e] = accum ? g.out_f32[o + e] : (g.flags & EPI_RESID) ? g.resid[o + e] : (float)g.aux_in[o + e];
+      }
+    }
+    float v[4] = {t.x, t.y, t.z, t.w};
+    float pre[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (accum) {
+        v[e] += pin[e];
+        pre[e] = 0.f;
+        continue;
+      }
+      v[e] += bias4[e];
+      pre[e] = v[e];
+      if (g.flags & EPI_GELU) v[e] = mta_gelu(v[e]);
+      if (g.flags & EPI_DROPOUT) {
+        const uint32_t h = gemm_pair_hash(dseed, (uint32_t)m >> 1, (uint32_t)(n + e));
+        const uint32_t u16 = (m & 1) ? (h >> 16) : (h & 0xFFFFu);
+        v[e] *= u16 >= dthr ? dscale : 0.f;
+      }
+      if (g.flags & EPI_DGELU) v[e] *= mta_gelu_grad(pin[e]);
+      if (g.flags & EPI_RESID) v[e] += pin[e];
+    }
+    if (wide) {
+      if (g.out_f32) *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+      if (!accum && g.out_bf16) {
+        Bf8 b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)v[e];
+        *reinterpret_cast<uint2*>(g.out_bf16 + o) = make_uint2(b.u.x, b.u.y);
+      }
+      if (!accum && g.aux_pre) {
+        Bf8 b;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)pre[e];
+        *reinterpret_cast<uint2*>(g.aux_pre + o) = make_uint2(b.u.x, b.u.y);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (n + e >= g.n_store) continue;
+        if (g.out_f32) g.out_f32[o + e] = v[e];
+        if (!accum && g.out_bf16) g.out_bf16[o + e] = (__bf16)v[e];
+        if (!accum && g.aux_pre) g.aux_pre[o + e] = (__bf16)pre[e];
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&acc)[8][4], const int mbase,
-                                             const int nbase, const bool split, const int lane, float* stage) {
+                                             const int nbase, const bool split, const int bz, const int lane,
+                                             float* stage) {
   const bool accum = (g.flags & EPI_ACCUM) != 0;
   const bool vec = (g.ldc & 3) == 0 && ((uintptr_t)g.out_f32 & 15) == 0 && ((uintptr_t)g.out_bf16 & 7) == 0 &&
                    ((uintptr_t)g.aux_pre & 7) == 0 && ((uintptr_t)g.resid & 15) == 0 && ((uintptr_t)g.aux_in & 7) == 0;
@@ -520,8 +641,7 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
     dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
     dscale = 1.0f / (1.0f - g.drop_p);
   }
-  const int cc = 4 * (lane & 15);  // this lane's 4 columns in the row-contiguous walk
-  const int n = nbase + cc;
+  const int n = nbase + 4 * (lane & 15);  // this lane's 4 columns in the row-contiguous walk
   float bias4[4] = {0.f, 0.f, 0.f, 0.f};
   if (!accum && (g.flags & EPI_BIAS)) {
 #pragma unroll
@@ -536,107 +656,9 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           stage[(16 * ii + 4 * (lane >> 4) + r) * EPI_ROW + 16 * j + (lane & 15)] = g.alpha * acc[4 * pass + ii][j][r];
-    const int mrow = mbase + 64 * pass;
-    // every LDS read of the pass BEFORE its first global access: hipcc waits vmcnt(0) ahead of an LDS access that
-    // follows outstanding vector-memory ops in a kernel that issues LDS-DMA (it cannot tell them apart), which
-    // serialised one store round trip per row quad (r3 stamp probe: ~65-100k cycles per tile)
-    if (accum && split) {
-      const int nc = nbase + lane;
-      float col[64];
-#pragma unroll
-      for (int rr = 0; rr < 64; ++rr) col[rr] = stage[rr * EPI_ROW + lane];
-#pragma unroll
-      for (int rr = 0; rr < 64; ++rr)
-        if (mrow + rr < g.M && nc < g.n_store) atomicAdd(g.out_f32 + (size_t)(mrow + rr) * g.ldc + nc, col[rr]);
-      continue;
-    }
-    float4 quad[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) quad[q] = *reinterpret_cast<const float4*>(&stage[(4 * q + (lane >> 4)) * EPI_ROW + cc]);
-    const bool prefetch = (g.flags & (EPI_RESID | EPI_DGELU)) || accum;
-#pragma unroll 2
-    for (int q0 = 0; q0 < 16; q0 += 8) {
-      float pin[8][4];
-      if (prefetch) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int m = mrow + 4 * (q0 + q) + (lane >> 4);
-          const size_t o = (size_t)m * g.ldc + n;
-          const bool rowok = m < g.M;
-          if (vec && rowok && n + 3 < g.n_store) {
-            if (accum || (g.flags & EPI_RESID)) {
-              const float4 t = *reinterpret_cast<const float4*>((accum ? g.out_f32 : g.resid) + o);
-              pin[q][0] = t.x; pin[q][1] = t.y; pin[q][2] = t.z; pin[q][3] = t.w;
-            } else {
-              Bf8 t;
-              t.u.x = reinterpret_cast<const uint2*>(g.aux_in + o)->x;
-              t.u.y = reinterpret_cast<const uint2*>(g.aux_in + o)->y;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) pin[q][e] = (float)t.e[e];
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const bool ok = rowok && n + e < g.n_store;
-              pin[q][e] = !ok ? 0.f : accum ? g.out_f32[o + e] : (g.flags & EPI_RESID) ? g.resid[o + e]
-                                                                                      : (float)g.aux_in[o + e];
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int rr = 4 * (q0 + q) + (lane >> 4);
-        const int m = mrow + rr;
-        if (m >= g.M) continue;
-        const float4 t = quad[q0 + q];
-        float v[4] = {t.x, t.y, t.z, t.w};
-        float pre[4];
-        uint32_t hsh = 0;
-        if (g.flags & EPI_DROPOUT) hsh = (uint32_t)m;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (accum) {
-            v[e] += prefetch ? pin[q][e] : 0.f;
-            continue;
-          }
-          v[e] += bias4[e];
-          pre[e] = v[e];
-          if (g.flags & EPI_GELU) v[e] = mta_gelu(v[e]);
-          if (g.flags & EPI_DROPOUT) {
-            const uint32_t h = gemm_pair_hash(dseed, hsh >> 1, (uint32_t)(n + e));
-            const uint32_t u16 = (hsh & 1) ? (h >> 16) : (h & 0xFFFFu);
-            v[e] *= u16 >= dthr ? dscale : 0.f;
-          }
-          if (g.flags & EPI_DGELU) v[e] *= mta_gelu_grad(pin[q][e]);
-          if (g.flags & EPI_RESID) v[e] += pin[q][e];
-        }
-        const size_t o = (size_t)m * g.ldc + n;
-        if (vec && n + 3 < g.n_store) {
-          if (g.out_f32) *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
-          if (!accum && g.out_bf16) {
-            Bf8 b;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)v[e];
-            *reinterpret_cast<uint2*>(g.out_bf16 + o) = make_uint2(b.u.x, b.u.y);
-          }
-          if (!accum && g.aux_pre) {
-            Bf8 b;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)pre[e];
-            *reinterpret_cast<uint2*>(g.aux_pre + o) = make_uint2(b.u.x, b.u.y);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e >= g.n_store) continue;
-            if (g.out_f32) g.out_f32[o + e] = v[e];
-            if (!accum && g.out_bf16) g.out_bf16[o + e] = (__bf16)v[e];
-            if (!accum && g.aux_pre) g.aux_pre[o + e] = (__bf16)pre[e];
-          }
-        }
-      }
-    }
+    // the asm reads below are invisible to hipcc: order them behind the staging writes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    big_rows_out(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
   }
 }
 
@@ -682,6 +704,9 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
   wait_tiles(pro - 1);
   barrier();
   if (row1) barrier();  // the second wave row runs one barrier behind
+#ifdef MTA_GEMM_STATIC_PRIO
+  if (row1) __builtin_amdgcn_s_setprio(1);  // the younger half: no per-cluster flips (guide T5, static form)
+#endif
   int rd = 0, wr = AHEAD % SLOTS;  // ring slots of tile j and of tile j + AHEAD
 #ifdef MTA_GEMM_STAMPS
   unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -723,14 +748,14 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
-#ifndef MTA_GEMM_NO_PRIO
+#if !defined(MTA_GEMM_NO_PRIO) && !defined(MTA_GEMM_STATIC_PRIO)
     __builtin_amdgcn_s_setprio(1);
 #endif
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
-#ifndef MTA_GEMM_NO_PRIO
+#if !defined(MTA_GEMM_NO_PRIO) && !defined(MTA_GEMM_STATIC_PRIO)
     __builtin_amdgcn_s_setprio(0);
 #endif
     GSTAMP(t4);
@@ -753,7 +778,7 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
   GACC(6, tloop0, tloop1);
 #endif
 
-  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, lane,
+  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
                reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
   if (want_rowsum) {
 #pragma unroll
@@ -773,6 +798,30 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 #endif
 }
 }  // namespace big
+
+// out[m][n] += sum over the splits of slab[z][m][n] (n < n_store), 4 columns per thread
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ out, int ldc, int n_store, int M, int N,
+                                                            const float* __restrict__ slab, int splits) {
+  const int n4 = N >> 2;
+  const long total = (long)M * n4;
+  const size_t plane = (size_t)M * N;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+    const int m = (int)(e / n4), n = (int)(e - (long)m * n4) * 4;
+    float4 s = *reinterpret_cast<const float4*>(slab + (size_t)m * N + n);
+    for (int z = 1; z < splits; ++z) {
+      const float4 t = *reinterpret_cast<const float4*>(slab + z * plane + (size_t)m * N + n);
+      s.x += t.x;
+      s.y += t.y;
+      s.z += t.z;
+      s.w += t.w;
+    }
+    float* o = out + (size_t)m * ldc + n;
+    const float v[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (n + k < n_store) o[k] += v[k];
+  }
+}
 
 template <bool AT, bool BT>
 __global__ __launch_bounds__(big::THREADS) __attribute__((amdgpu_waves_per_eu(2, 2))) void gemm_big_kernel(GemmArgs g, int nx, int ny, int nz) {
@@ -870,7 +919,8 @@ struct Workspace {
   size_t cap = 0;
 };
 constexpr int WS_MAX_DEVICES = 16;
-Workspace g_ws[WS_MAX_DEVICES][3];  // per device: 0 = weight-grad A^T, 1 = weight-grad B^T, 2 = input-grad B^T
+Workspace g_ws[WS_MAX_DEVICES][4];  // per device: 0 = weight-grad A^T, 1 = weight-grad B^T, 2 = input-grad B^T,
+                                    // 3 = split-K slabs of the 256 x 256 kernel
 
 __bf16* workspace(int slot, size_t bytes, hipStream_t st) {
   int dev = 0;
@@ -959,6 +1009,17 @@ inline bool big_on() {
   return g_big_override >= 0 ? g_big_override == 1 : env_on;
 }
 
+// split-K of the 256 x 256 kernel through fp32 slabs + one reduce launch (default) instead of fp32 atomics, which
+// run at ~1 TB/s of added bytes chip-wide (mlp_large weight gradient: 64 MB of atomics = ~110k cycles per tile on
+// the r3 stamp probe); MTA_GEMM_SLABS=0 keeps the atomics
+inline bool slabs_on() {
+  static const bool on = [] {
+    const char* e = getenv("MTA_GEMM_SLABS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <bool AT, bool BT>
 void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
   static const bool attr = [] {
@@ -967,7 +1028,16 @@ void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
   }();
   (void)attr;
   const int nx = (g.N + big::TN - 1) / big::TN, ny = (g.M + big::TM - 1) / big::TM;
-  gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(g, nx, ny, ksplit);
+  GemmArgs ga = g;
+  ga.slab = nullptr;
+  if ((g.flags & EPI_ACCUM) && ksplit > 1 && slabs_on())
+    ga.slab = reinterpret_cast<float*>(workspace(3, (size_t)ksplit * g.M * g.N * sizeof(float), st));
+  gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(ga, nx, ny, ksplit);
+  if (ga.slab) {
+    const long work = (long)g.M * (g.N / 4);
+    const int blocks = (int)std::min<long>(4096, (work + 255) / 256);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(g.out_f32, g.ldc, g.n_store, g.M, g.N, ga.slab, ksplit);
+  }
 }
 
 // Eligible for the 256 x 256 kernel: 32-deep k-tiles and enough macro-tiles to fill at least half the CUs; the
@@ -1075,7 +1145,7 @@ void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
 // one deferred weight-gradient GEMM waiting for its input-gradient partner (stream-ordered, single-threaded use)
 struct Pending {
   bool on = false;
-  GemmArgs g;
+  GemmArgs g{};
   int ksplit;
   hipStream_t st;
 } pending;
@@ -1104,7 +1174,7 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   if ((flags & EPI_ACCUM) == 0 && ksplit > 1) return 2;
   if ((flags & EPI_RESID) && (flags & EPI_DGELU)) return 7;  // one prefetched epilogue operand
   if (bias_grad && mode != 2) return 3;
-  GemmArgs g;
+  GemmArgs g{};
   g.A = static_cast<const __bf16*>(A);
   g.B = static_cast<const __bf16*>(B);
   g.M = M;

@@ -292,6 +292,8 @@ class Trainer:
         The fused optimizer leaves the flat gradient zeroed, so a step that follows one needs no fill."""
         if not getattr(self.optimizer, "grads_zeroed", False):
             self.flat.grad.zero_()
+        if self.ddp.world > 1 and (not self._in_graph or self._allreduce_in_graph()):
+            self.ddp.begin_backward()  # arm the backward-overlapped gradient sync (parallel/overlap.py)
         fused = getattr(self.model, "fused_training_step", None)
         if fused is not None and self.fused_step and self.model.fused_step_supported(batch):
             loss = fused(batch, batch_idx)  # forward + decoder + backward without autograd

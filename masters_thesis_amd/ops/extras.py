@@ -34,6 +34,7 @@ import torch
 import torch.nn.functional as Fn
 from torch import Tensor
 
+from ..parallel.overlap import grad_ready
 from ._lib import lib, use_hip
 
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_ACCUM, EPI_DROPOUT, EPI_DGELU = 1, 2, 4, 8, 16, 32
@@ -204,6 +205,8 @@ class _MlpEncoderFn(torch.autograd.Function):
             if i > 0:
                 dy = torch.empty((Mp, Din), device=dev, dtype=torch.float32)
                 gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], out_f32=dy)
+            # W_i, b_i final (their GEMM is launched: deferred ones go with the input-gradient GEMM above)
+            grad_ready(params[per * i].grad, params[per * i + 1].grad)
         gemm_flush()
         return (None,) * (7 + len(params))
 
@@ -401,6 +404,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
                  ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), defer=True)
             dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
             gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
+            # this layer's matrices and biases are final (their norm gains are reduced at the end of the backward)
+            grad_ready(wqkv.grad, bqkv.grad, wo.grad, bo.grad, w1.grad, b1.grad, w2.grad, b2.grad)
             # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
             dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
             C.norm_defer()

@@ -27,6 +27,8 @@ import torch
 import torch.distributed as dist
 
 from ..ops.optim import FlatParameters
+from . import overlap as _ov
+from .overlap import grad_ready  # noqa: F401  (re-export)
 
 
 class FlatDDP:
@@ -48,6 +50,86 @@ class FlatDDP:
         # xGMI buckets (4-float aligned ranges of the flat gradient, one channel each)
         xper = max(4096, int(float(os.environ.get("MTA_XGMI_BUCKET_MB", "64")) * (1 << 20) / 4) // 4096 * 4096)
         self.xgmi_buckets: List[slice] = [slice(i, min(i + xper, n)) for i in range(0, n, xper)]
+
+        # backward-overlapped sync (xGMI only: a plain kernel, capturable on a side stream): ranges of the flat
+        # gradient reported final by grad_ready() during the backward are reduced there as they come
+        self.overlap = (self.xgmi is not None and os.environ.get("MTA_DDP_OVERLAP", "1") != "0")
+        self.overlap_min_bytes = int(float(os.environ.get("MTA_DDP_OVERLAP_MIN_KB", "256")) * 1024)
+        self._side: Optional[torch.cuda.Stream] = None
+        self._done: List[tuple] = []     # [start, stop) ranges already all-reduced this step
+        self._pending: List[tuple] = []  # ready ranges not yet launched (below the minimum size)
+        self._launches = 0
+        self._reduce_fn = None           # tests: replaces the xGMI launch (range -> None)
+
+    # ------------------------------------------------------------------ overlapped sync
+    def begin_backward(self) -> None:
+        """Arm grad_ready() for the coming backward (call before it; allreduce_grads() disarms)."""
+        self._done, self._pending, self._launches = [], [], 0
+        if self.overlap or self._reduce_fn is not None:
+            _ov.ACTIVE = self
+
+    def _range_of(self, t: torch.Tensor) -> Optional[tuple]:
+        g = self.flat.grad
+        if t is None or t.device != g.device or t.dtype != g.dtype or not t.is_contiguous():
+            return None
+        off = (t.data_ptr() - g.data_ptr()) // g.element_size()
+        if off < 0 or off + t.numel() > g.numel():
+            return None
+        return (off, off + t.numel())
+
+    def _ready(self, grads) -> None:
+        rs = sorted(r for r in (self._range_of(t) for t in grads) if r is not None)
+        for r in rs:
+            self._pending.append(r)
+        self._pending.sort()
+        merged: List[tuple] = []
+        for a, b in self._pending:
+            if merged and merged[-1][1] == a:
+                merged[-1] = (merged[-1][0], b)
+            else:
+                merged.append((a, b))
+        self._pending = []
+        for a, b in merged:
+            # 4-float-aligned interior goes now if it is big enough; the rest waits for the final sync
+            a4, b4 = -(-a // 4) * 4, b // 4 * 4
+            if (b4 - a4) * 4 >= self.overlap_min_bytes:
+                self._launch(a4, b4, side=True)
+                if a4 > a:
+                    self._pending.append((a, a4))
+                if b > b4:
+                    self._pending.append((b4, b))
+            else:
+                self._pending.append((a, b))
+
+    def _launch(self, a: int, b: int, side: bool) -> None:
+        self._done.append((a, b))
+        k = self._launches
+        self._launches += 1
+        if self._reduce_fn is not None:
+            self._reduce_fn(a, b)
+            return
+        g = self.flat.grad
+        if side:
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=g.device)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(g.device))
+            self._side.wait_event(ev)
+            with torch.cuda.stream(self._side):
+                self.xgmi.allreduce_(g[a:b], off=a, channel=k % self.xgmi.channels)
+        else:
+            self.xgmi.allreduce_(g[a:b], off=a, channel=k % self.xgmi.channels)
+
+    def _remaining(self, n: int) -> List[tuple]:
+        """[0, n) minus the ranges already reduced, in order."""
+        out, cur = [], 0
+        for a, b in sorted(self._done):
+            if a > cur:
+                out.append((cur, a))
+            cur = max(cur, b)
+        if cur < n:
+            out.append((cur, n))
+        return out
 
     @property
     def backend_name(self) -> str:
@@ -80,6 +162,18 @@ class FlatDDP:
         if self.world == 1:
             return
         g = self.flat.grad
+        if _ov.ACTIVE is self:
+            # overlapped: the rest of the buffer (xGMI-bucket-sized pieces) on the main stream, then join the side
+            # stream so the optimizer sees every reduced range
+            # (joined first: a channel is only ever reused in stream order)
+            _ov.ACTIVE = None
+            if self._side is not None and self._reduce_fn is None:
+                torch.cuda.current_stream(g.device).wait_stream(self._side)
+            xper = self.xgmi_buckets[0].stop - self.xgmi_buckets[0].start if self.xgmi_buckets else g.numel()
+            for a, b in self._remaining(g.numel()):
+                for s0 in range(a, b, xper):
+                    self._launch(s0, min(b, s0 + xper), side=False)
+            return
         if self.xgmi is not None:
             for k, b in enumerate(self.xgmi_buckets):
                 self.xgmi.allreduce_(g[b], off=b.start, channel=k % self.xgmi.channels)

@@ -15,6 +15,7 @@ case "$1" in
     hipcc $F -DMTA_GEMM_DMA_IN_READS=1 -DMTA_GEMM_BIG_AHEAD=3 csrc/tools/gemm_probe.hip -o tools_bin/gemm_probe_r &
     hipcc $F -DMTA_GEMM_DMA_IN_READS=1 -DMTA_GEMM_BIG_AHEAD=3 -DMTA_GEMM_STAMPS csrc/tools/gemm_probe.hip -o tools_bin/gemm_probe_rs &
     hipcc $F -DMTA_GEMM_NO_PRIO csrc/tools/gemm_probe.hip -o tools_bin/gemm_probe_np &
+    hipcc $F -DMTA_GEMM_STATIC_PRIO csrc/tools/gemm_probe.hip -o tools_bin/gemm_probe_sp &
     ;;
   *)
     hipcc $F csrc/tools/lstm_stack_probe.hip -o tools_bin/stack_s0 &

@@ -100,3 +100,40 @@ def test_bench_four_gloo_ranks_whole_path(tmp_path):
     assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["warmup"] == 1 and rec["scaling"] == "weak"
     assert rec["config"]["global_batch"] == 4 and rec["config"]["parallelism"] == "dp4"
     assert rec["allreduce"] == "gloo" and rec["value"] > 0
+
+
+def test_overlapped_sync_reduces_every_range_once():
+    """Backward-overlapped gradient sync bookkeeping (parallel/ddp.py + parallel/overlap.py): ranges reported by
+    grad_ready() are launched at once when large enough (4-float aligned interior), the rest of the flat gradient
+    goes at allreduce_grads(); together every element is reduced exactly once, in a rank-independent order."""
+    from masters_thesis_amd.ops.optim import FlatParameters
+    from masters_thesis_amd.parallel import overlap
+    from masters_thesis_amd.parallel.ddp import FlatDDP, grad_ready
+
+    torch.manual_seed(0)
+    params = [torch.nn.Parameter(torch.randn(*s)) for s in [(64, 33), (64,), (7,), (128, 64), (128,), (3, 5)]]
+    flat = FlatParameters(params)
+    ddp = FlatDDP(flat)
+    ddp.world = 2  # drive the multi-rank path with a recording reducer instead of a process group
+    ddp.overlap_min_bytes = 1024
+    calls = []
+    ddp._reduce_fn = lambda a, b: calls.append((a, b))
+    ddp.begin_backward()
+    assert overlap.ACTIVE is ddp
+    grad_ready(params[3].grad, params[4].grad)  # 128x64 + 128: launched now
+    early = list(calls)
+    assert len(early) == 1 and early[0][0] % 4 == 0 and early[0][1] % 4 == 0
+    grad_ready(params[2].grad)                  # 7 floats: too small, deferred to the final sync
+    assert calls == early
+    ddp.allreduce_grads()
+    assert overlap.ACTIVE is None
+    cover = torch.zeros(flat.padded, dtype=torch.int32)
+    for a, b in calls:
+        assert a % 4 == 0 and b % 4 == 0
+        cover[a:b] += 1
+    assert bool((cover == 1).all()), "every element of the flat gradient reduced exactly once"
+    # a second step re-arms cleanly
+    calls.clear()
+    ddp.begin_backward()
+    ddp.allreduce_grads()
+    assert sum(b - a for a, b in calls) == flat.padded

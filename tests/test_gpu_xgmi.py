@@ -105,3 +105,93 @@ def test_xgmi_allreduce_two_processes_one_gpu(n, rounds, twoshot):
     for rank, worst, err in res:
         assert err is None, (rank, err)
         assert worst <= 1e-5 * (1 + (n >= 1 << 24)), (rank, worst)
+
+
+def _overlap_worker(rank, world, port, q):
+    """FlatDDP backward-overlapped sync (parallel/ddp.py): layer gradients reported by grad_ready() during a
+    simulated backward are reduced on the side stream, the rest at allreduce_grads(); eager and captured + replayed."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), MTA_ALLREDUCE="xgmi")
+    try:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from masters_thesis_amd.ops.optim import FlatParameters
+        from masters_thesis_amd.parallel.ddp import FlatDDP, grad_ready
+
+        dev = torch.device("cuda", 0)
+        shapes = [(256, 184), (256,), (256,), (256,), (512, 256), (512,), (512,), (512,), (1, 512), (1,)]
+        params = [torch.nn.Parameter(torch.zeros(*s, device=dev)) for s in shapes]
+        flat = FlatParameters(params)
+        ddp = FlatDDP(flat)
+        assert ddp.xgmi is not None and ddp.overlap
+        ddp.overlap_min_bytes = 4096
+        srcs = [torch.zeros(p.numel(), device=dev) for p in params]
+
+        def step():
+            ddp.begin_backward()
+            for i in (9, 8, 7, 6, 5, 4):  # "top layer first", as a backward produces them
+                params[i].grad.view(-1).copy_(srcs[i] * 2.0)
+            grad_ready(params[4].grad, params[5].grad)          # overlapped (side stream)
+            for i in (3, 2, 1, 0):
+                params[i].grad.view(-1).copy_(srcs[i] * 2.0)
+            grad_ready(params[0].grad, params[1].grad)          # overlapped
+            ddp.allreduce_grads()                                # the rest + join
+
+        def fill(rnd):
+            for i, s in enumerate(srcs):
+                s.copy_(_data(s.numel(), rank, 100 * rnd + i).to(dev))
+
+        def check(rnd):
+            worst = 0.0
+            for i, p in enumerate(params):
+                exp = 2.0 * sum(_data(srcs[i].numel(), r, 100 * rnd + i).double() for r in range(world))
+                worst = max(worst, (p.grad.view(-1).double().cpu() - exp).abs().max().item())
+            return worst
+
+        worst = 0.0
+        fill(0)
+        step()
+        torch.cuda.synchronize()
+        worst = max(worst, check(0))
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
+            fill(1)
+            step()  # warm-up on the capture stream
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                step()
+        torch.cuda.synchronize()
+        for rnd in (2, 3):
+            fill(rnd)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            worst = max(worst, check(rnd))
+        assert ddp.xgmi.timeouts() == 0
+        q.put((rank, worst, None))
+        dist.barrier()
+        ddp.xgmi.close()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_overlapped_gradient_sync_two_processes_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, worst, err in res:
+        assert err is None, err
+        assert worst < 1e-4, (rank, worst)
