@@ -67,10 +67,15 @@ void mta_norm_flush();
 void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
                  const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds, hipStream_t st);
-int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
+int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps, const float* gamma,
              const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
-             float drop_p, const float* dy, const float* dres, const void* pre, void* dx_bf16, float* dx_f32,
-             float* dgamma, float* dbeta, hipStream_t st);
+             float drop_p, const void* dy, int dy_bf16, const float* dres, const void* pre, void* dx_bf16,
+             float* dx_f32, float* dgamma, float* dbeta, hipStream_t st);
+int mta_tr_layer_fwd(int nseq, int T, int d, int dff, int heads, const float* xs, const void* wqkv, const void* wo,
+                     const void* w1, const void* w2, const float* g1, const float* bqkv, const float* bo,
+                     const float* g2, const float* b1, const float* b2, float eps, void* xn, void* qkv, void* o,
+                     void* xn2, void* pre1, void* u, float* x1, float* x2, float* r1, float* r2, float* lse,
+                     const float* rope, const uint64_t* seed, float drop_p, hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
                   int D, int heads, float rope_base, const float* rope, hipStream_t st);
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
@@ -552,7 +557,11 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
           const OptT& beta, const OptT& y_bf16, const OptT& y_f32, const OptT& mean, at::Tensor rstd,
           const OptT& seed, double drop_p, const OptT& dy, const OptT& dres, const OptT& pre, const OptT& dx_bf16,
           const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat, "x must be fp32 GPU");
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
+              "x must be fp32 or bf16 GPU");
+  const bool xb = x.scalar_type() == at::kBFloat16;
+  const bool dyb = has(dy) && dy->scalar_type() == at::kBFloat16;
+  if (dyb) TORCH_CHECK(dy->is_cuda() && dy->is_contiguous(), "dy: contiguous GPU tensor");
   check_span(x, M, ldx, D, "x");
   MTA_CHECK_F32(rstd);
   TORCH_CHECK(rstd.numel() >= M, "rstd too small");
@@ -565,12 +574,13 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
     if (has(*o)) check_span(**o, M, ldx, D, "residual-stride tensor");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int rc = mta_norm(bwd ? 1 : 0, x.data_ptr<float>(), (int)ldx, (int)M, (int)D, rms ? 1 : 0, (float)eps,
+  const int rc = mta_norm(bwd ? 1 : 0, x.data_ptr(), xb ? 1 : 0, (int)ldx, (int)M, (int)D, rms ? 1 : 0, (float)eps,
                           opt_typed<float>(gamma, at::kFloat, "gamma"), opt_typed<float>(beta, at::kFloat, "beta"),
                           opt_typed<void>(y_bf16, at::kBFloat16, "y_bf16"), opt_typed<float>(y_f32, at::kFloat, "y_f32"),
                           opt_typed<float>(mean, at::kFloat, "mean"), rstd.data_ptr<float>(),
                           reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
-                          (float)drop_p, opt_typed<float>(dy, at::kFloat, "dy"),
+                          (float)drop_p, dyb ? dy->data_ptr() : (const void*)opt_typed<float>(dy, at::kFloat, "dy"),
+                          dyb ? 1 : 0,
                           opt_typed<float>(dres, at::kFloat, "dres"), opt_typed<void>(pre, at::kBFloat16, "pre"),
                           opt_typed<void>(dx_bf16, at::kBFloat16, "dx_bf16"),
                           opt_typed<float>(dx_f32, at::kFloat, "dx_f32"), opt_typed<float>(dgamma, at::kFloat, "dgamma"),
@@ -596,6 +606,36 @@ static const float* rope_table(const at::Device& dev, int64_t T, int64_t HD, dou
     it = cache.emplace(key, host.to(dev)).first;
   }
   return it->second.data_ptr<float>();
+}
+
+// one transformer block forward in one launch (csrc/transformer.hip); every saved activation written
+void tr_layer_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope_base, at::Tensor xs, at::Tensor wqkv,
+                  at::Tensor wo, at::Tensor w1, at::Tensor w2, at::Tensor g1, at::Tensor bqkv, at::Tensor bo,
+                  at::Tensor g2, at::Tensor b1, at::Tensor b2, at::Tensor xn, at::Tensor qkv, at::Tensor o,
+                  at::Tensor xn2, at::Tensor pre1, at::Tensor u, at::Tensor x1, at::Tensor x2, at::Tensor r1,
+                  at::Tensor r2, at::Tensor lse, const OptT& seed, double drop_p) {
+  const int64_t d = xs.size(-1), dff = w1.size(0), M = nseq * T;
+  for (auto* t : {&xs, &x1, &x2}) {
+    MTA_CHECK_F32(*t);
+    TORCH_CHECK(t->numel() >= M * d, "tr_layer_fwd: row tensor too small");
+  }
+  for (auto* t : {&wqkv, &wo, &w1, &w2, &xn, &qkv, &o, &xn2, &pre1, &u}) {
+    MTA_CHECK_GPU(*t, at::kBFloat16);
+  }
+  TORCH_CHECK(wqkv.size(0) == 3 * d && wqkv.size(1) == d && wo.size(0) == d && wo.size(1) == d && w1.size(1) == d &&
+                  w2.size(0) == d && w2.size(1) == dff, "tr_layer_fwd: weight shapes");
+  TORCH_CHECK(qkv.numel() >= M * 3 * d && pre1.numel() >= M * dff && u.numel() >= M * dff, "tr_layer_fwd: sizes");
+  TORCH_CHECK(lse.numel() >= nseq * heads * 64 && r1.numel() >= M && r2.numel() >= M, "tr_layer_fwd: stats");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(xs.device());
+  const int rc = mta_tr_layer_fwd(
+      (int)nseq, (int)T, (int)d, (int)dff, (int)heads, xs.data_ptr<float>(), wqkv.data_ptr(), wo.data_ptr(),
+      w1.data_ptr(), w2.data_ptr(), g1.data_ptr<float>(), bqkv.data_ptr<float>(), bo.data_ptr<float>(),
+      g2.data_ptr<float>(), b1.data_ptr<float>(), b2.data_ptr<float>(), (float)eps, xn.data_ptr(), qkv.data_ptr(),
+      o.data_ptr(), xn2.data_ptr(), pre1.data_ptr(), u.data_ptr(), x1.data_ptr<float>(), x2.data_ptr<float>(),
+      r1.data_ptr<float>(), r2.data_ptr<float>(), lse.data_ptr<float>(), rope_table(xs.device(), T, d / heads, rope_base),
+      reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")), (float)drop_p, cur_stream());
+  TORCH_CHECK(rc == 0, "tr_layer_fwd: unsupported configuration (d=", d, ", dff=", dff, ", heads=", heads, ", T=", T,
+              ", rc=", rc, ")");
 }
 
 void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
@@ -951,6 +991,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
+  m.def("tr_layer_fwd", &tr_layer_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("norm_flush", []() { mta_norm_flush(); });

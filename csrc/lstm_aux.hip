@@ -50,9 +50,9 @@ __global__ void lstm_prep_kernel(const float* __restrict__ w_ih, const float* __
 
 // ---------------------------------------------------------------------------------------------
 // batch gather: row perm[cursor*B + b] of tensor k -> dst_k[b].  Every (b, k) row is split over
-// GATHER_CHUNK-float4 blocks (grid.x = B * chunks of the longest row, grid.y = tensors), so all of a
-// step's loads are in flight at once (one 256-thread block per 16 KB: a 72 KB window row took 10 us as one
-// block's serial loop, r2 kernel trace).  Blocks past a shorter row's end only arrive.  The last block
+// GATHER_CHUNK-float4 pieces, `span` pieces per block (grid.x = B * chunks of the longest row, grid.y = tensors,
+// ~512 blocks), so all of a step's loads are in flight at once (one 256-thread block per 16 KB at B = 1: a 72 KB
+// window row took 10 us as one block's serial loop, r2 kernel trace).  Blocks past a shorter row's end only arrive.  The last block
 // to arrive advances the cursor (every block reads it before arriving, so the update is race-free).
 // ---------------------------------------------------------------------------------------------
 constexpr int GATHER_TPB = 256;
@@ -64,6 +64,7 @@ struct GatherArgs {
   long row_floats[4];
   int ntensors;
   int chunks;  // blocks per row (of the longest row)
+  int span;    // GATHER_CHUNK pieces per block
 };
 
 __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, const int* __restrict__ perm,
@@ -76,20 +77,24 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
   if ((n & 3) == 0 && ((((uintptr_t)s) | ((uintptr_t)d)) & 15) == 0) {
     const float4* s4 = reinterpret_cast<const float4*>(s);
     float4* d4 = reinterpret_cast<float4*>(d);
-    const long lo = (long)chunk * GATHER_CHUNK, hi = lo + GATHER_CHUNK < n / 4 ? lo + GATHER_CHUNK : n / 4;
-    float4 v[4];
+    for (int piece = chunk * a.span; piece < (chunk + 1) * a.span; ++piece) {
+      const long lo = (long)piece * GATHER_CHUNK, hi = lo + GATHER_CHUNK < n / 4 ? lo + GATHER_CHUNK : n / 4;
+      if (lo >= hi) break;
+      float4 v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long i = lo + r * GATHER_TPB + threadIdx.x;
-      if (i < hi) v[r] = s4[i];
-    }
+      for (int r = 0; r < 4; ++r) {
+        const long i = lo + r * GATHER_TPB + threadIdx.x;
+        if (i < hi) v[r] = s4[i];
+      }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long i = lo + r * GATHER_TPB + threadIdx.x;
-      if (i < hi) d4[i] = v[r];
+      for (int r = 0; r < 4; ++r) {
+        const long i = lo + r * GATHER_TPB + threadIdx.x;
+        if (i < hi) d4[i] = v[r];
+      }
     }
   } else {
-    const long lo = (long)chunk * GATHER_CHUNK * 4, hi = lo + GATHER_CHUNK * 4 < n ? lo + GATHER_CHUNK * 4 : n;
+    const long lo = (long)chunk * a.span * GATHER_CHUNK * 4;
+    const long hi = lo + (long)a.span * GATHER_CHUNK * 4 < n ? lo + (long)a.span * GATHER_CHUNK * 4 : n;
     for (long i = lo + threadIdx.x; i < hi; i += GATHER_TPB) d[i] = s[i];
   }
   __syncthreads();
@@ -166,6 +171,11 @@ extern "C" void mta_gather_batch(const float* const* src, float* const* dst, con
   a.ntensors = ntensors;
   long longest = 1;
   for (int k = 0; k < ntensors && k < 4; ++k) longest = row_floats[k] > longest ? row_floats[k] : longest;
-  a.chunks = (int)((longest + 4L * GATHER_CHUNK - 1) / (4L * GATHER_CHUNK));
+  const int pieces = (int)((longest + 4L * GATHER_CHUNK - 1) / (4L * GATHER_CHUNK));
+  // every block arrives on one counter (the last advances the cursor): keep the grid near 512 workgroups -- at
+  // B = 64 one block per 16-KB piece was ~5k same-word atomics, ~35 us per step (r3 mlp_large trace)
+  const int target = 512 / (B * (ntensors > 0 ? ntensors : 1)) > 1 ? 512 / (B * (ntensors > 0 ? ntensors : 1)) : 1;
+  a.span = (pieces + target - 1) / target;
+  a.chunks = (pieces + a.span - 1) / a.span;
   gather_batch_kernel<<<dim3(B * a.chunks, ntensors), GATHER_TPB, 0, st>>>(a, perm, cursor, arrive, B, row_offset);
 }

@@ -65,6 +65,7 @@ __global__ void cast_pad_kernel(CastArgs a) {
 
 struct NormArgs {
   const float* x;
+  const __bf16* xb;     // bf16 x instead of x (wide kernels): the MLP's GELU output stored in bf16
   int ldx;              // row stride of x (elements)
   int M, D, rms;
   float eps;
@@ -78,6 +79,7 @@ struct NormArgs {
   float drop_p;
   // backward
   const float* dy;      // [M][D]
+  const __bf16* dyb;    // bf16 dy instead of dy (wide kernels)
   const float* dres;    // [M][ldx] residual-stream gradient added to dx (or null)
   const __bf16* pre;    // [M][D] GELU input: dx *= gelu'(pre) (or null)
   __bf16* dx_bf16;      // [M][D]
@@ -88,6 +90,14 @@ struct NormArgs {
   int part_ld;
   long part_pass;       // floats between the dgamma and dbeta planes
 };
+
+__device__ __forceinline__ float4 ld4(const float* pf, const __bf16* pb, size_t i) {
+  if (pb) {
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(pb + i);
+    return make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+  }
+  return *reinterpret_cast<const float4*>(pf + i);
+}
 
 template <int VPL>
 __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
@@ -154,13 +164,12 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = blockIdx.x;
   const float invD = 1.0f / (float)a.D;
-  const float* xr = a.x + (size_t)row * a.ldx;
   float4 v[VPT], gm[VPT], bt[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     const bool ok = c < a.D;
-    v[i] = ok ? *reinterpret_cast<const float4*>(xr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[i] = ok ? ld4(a.x, a.xb, (size_t)row * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     gm[i] = (ok && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     bt[i] = (ok && a.beta) ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
@@ -225,8 +234,8 @@ __device__ __forceinline__ void wide_load(const NormArgs& a, int row, WideRow<VP
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     const bool ok = c < a.D;
-    r.x[i] = ok ? *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c) : z;
-    r.dy[i] = ok ? *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c) : z;
+    r.x[i] = ok ? ld4(a.x, a.xb, (size_t)row * a.ldx + c) : z;
+    r.dy[i] = ok ? ld4(a.dy, a.dyb, (size_t)row * a.D + c) : z;
     r.dr[i] = (ok && a.dres) ? *reinterpret_cast<const float4*>(a.dres + (size_t)row * a.ldx + c) : z;
     if (ok && a.pre) r.pre[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
   }
@@ -539,13 +548,16 @@ extern "C" void mta_norm_flush() {
   deferred.n = 0;
 }
 
-extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms, float eps, const float* gamma,
-                        const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd,
-                        const uint64_t* seed, float drop_p, const float* dy, const float* dres, const void* pre,
-                        void* dx_bf16, float* dx_f32, float* dgamma, float* dbeta, hipStream_t st) {
+extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps,
+                        const float* gamma, const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd,
+                        const uint64_t* seed, float drop_p, const void* dy, int dy_bf16, const float* dres,
+                        const void* pre, void* dx_bf16, float* dx_f32, float* dgamma, float* dbeta, hipStream_t st) {
   if (D % 4 || ldx % 4 || D > 2048) return 1;
-  NormArgs a;
-  a.x = x;
+  const bool wide_ok = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr;
+  if ((x_bf16 || dy_bf16) && !wide_ok) return 2;  // bf16 row inputs: wide kernels only
+  NormArgs a{};
+  a.x = x_bf16 ? nullptr : static_cast<const float*>(x);
+  a.xb = x_bf16 ? static_cast<const __bf16*>(x) : nullptr;
   a.ldx = ldx;
   a.M = M;
   a.D = D;
@@ -559,7 +571,8 @@ extern "C" int mta_norm(int bwd, const float* x, int ldx, int M, int D, int rms,
   a.rstd = rstd;
   a.seed = seed;
   a.drop_p = drop_p;
-  a.dy = dy;
+  a.dy = dy_bf16 ? nullptr : static_cast<const float*>(dy);
+  a.dyb = dy_bf16 ? static_cast<const __bf16*>(dy) : nullptr;
   a.dres = dres;
   a.pre = static_cast<const __bf16*>(pre);
   a.dx_bf16 = static_cast<__bf16*>(dx_bf16);

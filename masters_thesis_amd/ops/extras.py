@@ -28,6 +28,7 @@ which also serve as the numerics oracle of the GPU tests.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional, Sequence
 
 import torch
@@ -100,6 +101,20 @@ def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
 
 
 
+def _row_dtype(D: int) -> torch.dtype:
+    """Storage of a GEMM -> norm row tensor (activation or its gradient).  fp32: the bf16 form (MTA_BF16_ROWS=1, wide
+    norms only) measured slower end to end -- mlp_large B=64 1.277 -> 1.327 ms, the wide norm backward 50 -> 62 us
+    per call on 8-byte row loads, no gain in the GEMM epilogues (r3 trace, profiles/r3_bf16_rows_negative.txt)."""
+    return torch.bfloat16 if (_BF16_ROWS and D >= 1024) else torch.float32
+
+
+_BF16_ROWS = os.environ.get("MTA_BF16_ROWS", "0") == "1"
+
+
+def _row_out(t: Tensor) -> dict:
+    return {"out_bf16": t} if t.dtype == torch.bfloat16 else {"out_f32": t}
+
+
 def _grad_view(p: Tensor) -> Tensor:
     if p.grad is None:
         p.grad = torch.zeros_like(p)
@@ -147,9 +162,11 @@ class _MlpEncoderFn(torch.autograd.Function):
             D = dims[i + 1]
             assert D % 8 == 0, "MLP hidden size must be a multiple of 8"
             pre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
-            act = torch.empty((Mp, D), device=dev, dtype=torch.float32)
+            # wide layers keep the GELU output in bf16 (as autocast would): the GEMM writes, the norm's forward and
+            # backward read half the bytes (csrc/norm.hip wide kernels read bf16 rows)
+            act = torch.empty((Mp, D), device=dev, dtype=_row_dtype(D))
             gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU, bias=params[per * i + 1],
-                 aux_pre=pre, out_f32=act)
+                 aux_pre=pre, **_row_out(act))
             mean = None if rms else torch.empty(Mp, device=dev, dtype=torch.float32)
             rstd = torch.empty(Mp, device=dev, dtype=torch.float32)
             last = i == L - 1
@@ -203,8 +220,8 @@ class _MlpEncoderFn(torch.autograd.Function):
                  ldc=Din, n_store=Din, ksplit=wgrad_split(D, kp[i], Mp), bias_grad=_grad_view(params[per * i + 1]),
                  defer=i > 0)  # paired with the input-gradient GEMM below (same dPre)
             if i > 0:
-                dy = torch.empty((Mp, Din), device=dev, dtype=torch.float32)
-                gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], out_f32=dy)
+                dy = torch.empty((Mp, Din), device=dev, dtype=_row_dtype(Din))
+                gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], **_row_out(dy))
             # W_i, b_i final (their GEMM is launched: deferred ones go with the input-gradient GEMM above)
             grad_ready(params[per * i].grad, params[per * i + 1].grad)
         gemm_flush()
@@ -272,6 +289,20 @@ def transformer_reference(x: Tensor, params: Sequence[Tensor], num_layers: int, 
     return Fn.rms_norm(h[:, -1], (h.shape[-1],), gf, RMS_EPS)
 
 
+# fused block forward (csrc/transformer.hip) for the config it is built for: opt-in (MTA_TR_FUSED=1).  It replaces
+# 7 launches per block with one but measured 0.777 vs 0.719 ms per transformer B=1 step against the kernel chain
+# (70 us per block: the store-heavy epilogues with one wave per SIMD, profiles/r3_tr_fused_stamps.txt)
+_TR_FUSED = [os.environ.get("MTA_TR_FUSED", "0") == "1"]
+
+
+def set_transformer_fused(on: bool) -> None:
+    _TR_FUSED[0] = bool(on)
+
+
+def _tr_fused_ok(d: int, dff: int, heads: int, T: int) -> bool:
+    return _TR_FUSED[0] and d == 128 and dff == 512 and heads == 4 and 1 <= T <= 64
+
+
 class _TransformerEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, seeds, num_layers, heads, dropout, training, need_grad, *params):
@@ -298,12 +329,33 @@ class _TransformerEncoderFn(torch.autograd.Function):
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
+        fused = _tr_fused_ok(d, mats_b[3].shape[0] if L else 0, heads, T)
         for l in range(L):
             base = 2 + nb * l
             g1, bqkv, bo, g2, b1, b2 = (params[base], params[base + 2], params[base + 4], params[base + 5],
                                         params[base + 7], params[base + 9])
             wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
             dff = w1_b.shape[0]
+            if fused:
+                # the whole block in one launch (csrc/transformer.hip), same saved tensors as the chain below
+                xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                qkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
+                o = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+                u = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+                x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
+                x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
+                r1 = torch.empty(M, device=dev, dtype=torch.float32)
+                r2 = torch.empty(M, device=dev, dtype=torch.float32)
+                lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
+                C.tr_layer_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, wqkv_b, wo_b, w1_b, w2_b, g1, bqkv, bo, g2, b1,
+                               b2, xn, qkv, o, xn2, pre1, u, x1, x2, r1, r2, lse,
+                               seeds[l:l + 1] if drop else None, float(dropout))
+                saved += [xs, xn, qkv, o, x1, xn2, pre1, u]
+                stats += [r1, lse, r2]
+                xs = x2
+                continue
             xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             r1 = torch.empty(M, device=dev, dtype=torch.float32)
             C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,

@@ -239,6 +239,43 @@ def test_transformer_encoder_matches_fp32_reference():
     _encoder_parity(FinancialTransformerMse, dict(hidden_size=128, num_layers=2, num_heads=4, dropout=0.0), 3e-2, 8e-2)
 
 
+@pytest.mark.parametrize("dropout,N", [(0.0, 100), (0.2, 37)])
+def test_fused_transformer_block_matches_unfused(dropout, N):
+    """csrc/transformer.hip (one launch per block) against the 7-launch kernel chain on the same inputs, seeds and
+    weights: encoder output and every parameter gradient (the backward consumes the fused forward's saved
+    tensors), plus the fp32 PyTorch reference without dropout."""
+    from masters_thesis_amd.models.extras import FinancialTransformerMse
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(3)
+    m = FinancialTransformerMse(hidden_size=128, num_layers=2, num_heads=4, dropout=dropout).to(DEV)
+    enc = m.encoder
+    params = list(enc.flat_params()) if hasattr(enc, "flat_params") else [p for p in enc.parameters()]
+    x = torch.randn(N, 60, 3, device=DEV)
+    seeds0 = torch.randint(0, 2 ** 62, (8,), device=DEV, dtype=torch.int64)
+    outs, grads = [], []
+    try:
+        for fused in (True, False):
+            X.set_transformer_fused(fused)
+            for p in params:
+                p.grad = None
+            seeds = seeds0.clone()
+            h = X.transformer_encode(x, params, seeds, 2, 4, dropout, True)
+            g = torch.randn(h.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
+            h.backward(g)
+            outs.append(h.detach().clone())
+            grads.append([p.grad.detach().clone() for p in params])
+    finally:
+        X.set_transformer_fused(False)
+    assert _rel(outs[0], outs[1]) < 2e-3
+    for a, b in zip(*grads):
+        assert _rel(a, b) < 5e-3
+    if dropout == 0.0:
+        with torch.no_grad():
+            ref = X.transformer_reference(x.double(), [p.double() for p in params], 2, 4, 0.0, False)
+        assert _rel(outs[0], ref) < 3e-2
+
+
 def test_extras_dropout_train_vs_eval_and_finite_grads():
     from masters_thesis_amd.models.extras import FinancialMlpCombined, FinancialTransformerCombined
 
