@@ -115,6 +115,9 @@ def run_concurrent(args, argv) -> None:
         procs = []
         for i in range(k):
             env = dict(os.environ, MTA_BENCH_BARRIER=d, MTA_BENCH_NCHILD=str(k), MTA_BENCH_CHILD=str(i))
+            # trainers time-slicing one GPU: the pipelined LSTM's cross-workgroup waits may sit out another
+            # process's slice, so they poll 16x longer before giving up (a give-up still fails the run)
+            env.setdefault("MTA_LSTM_SPIN_LIMIT", str(1 << 25))
             for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
                 env.pop(v, None)
             procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *child_argv], env=env,

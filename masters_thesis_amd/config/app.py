@@ -161,6 +161,10 @@ def _launch_children(jobs: List[List[Override]], sweep_dir: Path, launcher: Dict
             hb.write_text(str(time.time()))
             if slots[slot] is not None:
                 env["HIP_VISIBLE_DEVICES"] = str(slots[slot])
+                if slots.count(slots[slot]) > 1:
+                    # trials sharing a GPU time-slice it: the pipelined LSTM's cross-workgroup waits poll 16x
+                    # longer before giving up (bench.py --concurrent does the same; a give-up fails the trial)
+                    env.setdefault("MTA_LSTM_SPIN_LIMIT", str(1 << 25))
             extra = ["resume=auto"] if attempt > 0 else []
             cmd = [sys.executable, script_argv0, *base_flags, *[o.text() for o in ovs], *extra,
                    f"hydra.run.dir={sweep_dir}/{num}", f"hydra.job.num={num}"]

@@ -44,4 +44,17 @@ if [ -n "$PMC" ]; then
     timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc_tr$i -o pmc -- python bench.py --model transformer_encoder --trainer gpu_fast --steps 8 --warmup 2 > $OUT/pmc_tr$i.log 2>&1 || exit $?
   done
 fi
+if [ -n "$GEMM_PMC" ]; then
+  # the 256 x 256 GEMM (tools_bin/gemm_probe, scripts/build_probes.sh gemm) at 4096^3 and the mlp_large shapes
+  G1="SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU_MFMA_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE"
+  G2="TCC_HIT_sum TCC_MISS_sum SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS GRBM_COUNT"
+  i=0
+  for P in "$G1" "$G2"; do
+    i=$((i+1))
+    for sh in "4096 4096 4096 0" "6400 2048 2048 0 1" "6400 2048 2048 1" "2048 2048 6400 2"; do
+      tag=$(echo $sh | tr ' ' '_')
+      timeout -s KILL 60 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc_gemm${i}_$tag -o pmc -- ./tools_bin/gemm_probe $sh > $OUT/pmc_gemm${i}_$tag.log 2>&1 || exit $?
+    done
+  done
+fi
 echo done >> $OUT/bench_all.err
