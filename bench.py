@@ -118,6 +118,8 @@ def run_concurrent(args, argv) -> None:
             # trainers time-slicing one GPU: the pipelined LSTM's cross-workgroup waits may sit out another
             # process's slice, so they poll 16x longer before giving up (a give-up still fails the run)
             env.setdefault("MTA_LSTM_SPIN_LIMIT", str(1 << 25))
+            env.setdefault("MTA_ADAM_SPIN_LIMIT", str(1 << 26))
+            env.setdefault("GPU_MAX_HW_QUEUES", "1")  # one hardware queue per trainer: k queues, no oversubscription
             for v in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
                 env.pop(v, None)
             procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *child_argv], env=env,

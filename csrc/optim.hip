@@ -94,6 +94,9 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
 // bounded only for safety (a give-up counts in nonfinite[1]).
 constexpr int FUSED_MAX_BLOCKS = 256;
 constexpr unsigned FUSED_SPIN_LIMIT = 1u << 22;
+// the bound actually used: MTA_ADAM_SPIN_LIMIT overrides it (trials time-slicing one GPU wait out another
+// process's slice; a give-up is still counted and fails the step)
+__device__ unsigned g_fused_spin_limit = FUSED_SPIN_LIMIT;
 
 // REG: every thread's (at most REG_N) float4 of g, p, m, v are loaded in phase 1, before the grid-wide arrival
 // wait, so phase 2 is compute + stores only (the post-barrier HBM round trip of the re-reads was ~1.5 us of a
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     while (seen < target) {
       __builtin_amdgcn_s_sleep(1);
       seen = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > FUSED_SPIN_LIMIT) {
+      if (++spins > g_fused_spin_limit) {
         if (nonfinite) atomicAdd(nonfinite + 1, 1.0f);
         break;
       }
@@ -308,6 +311,13 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
                                float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
                                float* norm_out, float* nonfinite, hipStream_t st) {
   const long n4 = n / 4;
+  static const bool spin_set = [] {
+    const char* e = getenv("MTA_ADAM_SPIN_LIMIT");
+    if (!e || atol(e) <= 0) return false;
+    const unsigned v = (unsigned)atol(e);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_spin_limit), &v, sizeof(v)) == hipSuccess;
+  }();
+  (void)spin_set;
   if (fused_reg(n4))
     adam_fused_kernel<true><<<fused_grid_reg(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),

@@ -165,6 +165,8 @@ def _launch_children(jobs: List[List[Override]], sweep_dir: Path, launcher: Dict
                     # trials sharing a GPU time-slice it: the pipelined LSTM's cross-workgroup waits poll 16x
                     # longer before giving up (bench.py --concurrent does the same; a give-up fails the trial)
                     env.setdefault("MTA_LSTM_SPIN_LIMIT", str(1 << 25))
+                    env.setdefault("MTA_ADAM_SPIN_LIMIT", str(1 << 26))
+                    env.setdefault("GPU_MAX_HW_QUEUES", "1")  # one hardware queue per trial
             extra = ["resume=auto"] if attempt > 0 else []
             cmd = [sys.executable, script_argv0, *base_flags, *[o.text() for o in ovs], *extra,
                    f"hydra.run.dir={sweep_dir}/{num}", f"hydra.job.num={num}"]
