@@ -991,6 +991,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
+  // contiguous tensor <- 0 through hipMemsetAsync on the current stream (no ATen fill kernel in a captured step)
+  m.def("zero_", [](at::Tensor t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
+    TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) == hipSuccess,
+                "zero_: hipMemsetAsync failed");
+  });
   m.def("tr_layer_fwd", &tr_layer_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });

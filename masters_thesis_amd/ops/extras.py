@@ -409,13 +409,14 @@ class _TransformerEncoderFn(torch.autograd.Function):
         Xin = saved[0]
         x_final = saved[-1]
         # final RMSNorm over the last-token rows -> residual-stream gradient (zero elsewhere)
-        dX = torch.zeros((M, d), device=dev, dtype=torch.float32)
-        dhp = torch.zeros((Np, d), device=dev, dtype=torch.float32)
-        dhp[:N].copy_(dh)
+        dX = torch.empty((M, d), device=dev, dtype=torch.float32)
+        C.zero_(dX)  # memset node, not an ATen fill kernel
+        # the N real sequences only (the padded ones have no output gradient): dh is read in place
+        dh = dh if (dh.dtype == torch.float32 and dh.is_contiguous()) else dh.float().contiguous()
         gf = params[2 + nb * L]
         C.norm_defer()
-        C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, Np, d, True, RMS_EPS, gf, None, None, None, None,
-               stats[-1], None, 0.0, dhp, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
+        C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, None, None,
+               stats[-1], None, 0.0, dh, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
         dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
         cast_pad([dX], [dXb])
         for l in range(L - 1, -1, -1):

@@ -14,6 +14,7 @@ run() {
   rc=$?
   if [ $rc -ne 0 ]; then echo "FAILED rc=$rc: $*" >> $OUT/bench_all.err; exit $rc; fi
 }
+if [ -z "$SKIP_MODELS" ]; then
 run --model small --loss mse
 run --model small --loss nll
 run --model small --loss combined
@@ -26,6 +27,7 @@ run --model mlp_large --loss mse --batch 64 --trainer gpu_fast
 run --model mlp_small --loss mse --trainer fast
 run --model transformer_encoder --loss mse --trainer gpu_fast
 run --model transformer_encoder --loss combined --batch 8 --trainer gpu_fast
+fi
 if [ -n "$CONCURRENT" ]; then
   for k in 2 4 8; do run --model small --loss mse --concurrent $k --steps 400; done
 fi
