@@ -157,7 +157,7 @@ def test_fused_adam_matches_torch_adam_with_clipping():
     assert float(opt.step_t.item()) == 5.0
 
 
-@pytest.mark.parametrize("n_params", [51_074, 3_000_000])
+@pytest.mark.parametrize("n_params", [51_074, 3_000_000, 12_980_226])  # small LSTM, mid, mlp_large
 def test_single_launch_adam_matches_two_launch_and_zeroes_grads(n_params, monkeypatch):
     """csrc/optim.hip adam_fused_kernel (in-launch norm ticket, grid <= 256 workgroups) against the two-launch
     norm + update pair, over several steps (the monotonic ticket spans launches), with grad zeroing."""
