@@ -63,6 +63,7 @@ int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, i
                   float* bias_grad, int defer, hipStream_t st);
 void mta_gemm_flush();
 void mta_gemm_set_big(int on);
+void mta_gemm_set_mid(int on);
 void mta_norm_flush();
 void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
@@ -1000,6 +1001,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("tr_layer_fwd", &tr_layer_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
+  m.def("gemm_set_mid", [](int64_t on) { mta_gemm_set_mid((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());

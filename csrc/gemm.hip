@@ -428,12 +428,14 @@ typedef __attribute__((address_space(3))) void lds_void;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 // per-lane source of the two DMA instructions this wave issues for one operand of one k-tile
-template <bool T>
+// (TW = image width in rows/columns: 256 for the macro-tile kernel, 128 for the mid kernel; WAVES issuing)
+template <bool T, int TW = 256, int WAVES = 8>
 __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, int r0, int kbeg, int wave, int lane,
                                         const __bf16* (&src)[2]) {
+  static_assert(TW / 16 == 2 * WAVES, "two 1-KB DMA pieces per wave and operand");
 #pragma unroll
   for (int q = 0; q < 2; ++q) {
-    const int ins = wave + 8 * q;  // 1-KB piece of the 16-KB image
+    const int ins = wave + WAVES * q;  // 1-KB piece of the image
     if constexpr (!T) {
       // 16 rows x 64 B; lane -> (row, physical chunk); the chunk it holds is the swizzled logical one
       const int r = 16 * ins + (lane >> 2);
@@ -441,8 +443,9 @@ __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, in
       const int row = min(r0 + r, rows - 1);
       src[q] = base + (size_t)row * ld + kbeg + 8 * c;
     } else {
-      // 2 k-rows x 512 B; lane -> (k-row, 16-B unit); 32-B chunk swizzled by k-row
-      const int kr = 2 * ins + (lane >> 5), u = lane & 31;
+      // 1024 / (2 TW) k-rows x 2 TW bytes; lane -> (k-row, 16-B unit); 32-B chunk swizzled by k-row
+      constexpr int UPR = TW / 8;  // 16-B units per k-row
+      const int kr = (1024 / (2 * TW)) * ins + lane / UPR, u = lane % UPR;
       const int h = (kr & 3) | (((kr >> 3) & 1) << 2);
       const int col = min(r0 + 16 * ((u >> 1) ^ h) + 8 * (u & 1), rows - 8);
       src[q] = base + (size_t)(kbeg + kr) * ld + col;
@@ -465,7 +468,7 @@ __device__ __forceinline__ void dma16(const __bf16* src, char* lds) {
 }
 
 // MFMA operand fragment of 16 rows (m or n) starting at image row/col `rb`, k-chunk lane >> 4
-template <bool T>
+template <bool T, int TW = 256>
 __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int lane) {
   if constexpr (!T) {
     const int r = rb + (lane & 15);
@@ -480,8 +483,8 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rb, int lane) {
     // the caller waits lgkmcnt(0) itself before the MFMAs (tr_wait)
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 lo, hi;
-    const unsigned a0 = (unsigned)(uintptr_t)(img + k0 * 512 + ((lc ^ h0) << 5) + 8 * p);
-    const unsigned a1 = (unsigned)(uintptr_t)(img + k1 * 512 + ((lc ^ h1) << 5) + 8 * p);
+    const unsigned a0 = (unsigned)(uintptr_t)(img + k0 * (2 * TW) + ((lc ^ h0) << 5) + 8 * p);
+    const unsigned a1 = (unsigned)(uintptr_t)(img + k1 * (2 * TW) + ((lc ^ h1) << 5) + 8 * p);
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
     asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
     const u32x2 v8[2] = {lo, hi};
@@ -797,7 +800,93 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
     for (int i = 0; i < 8; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
 #endif
 }
+// ---- 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each), same DMA images / swizzles / transposed reads as above ----
+// For the small weight-gradient products of the transformer (dY^T X: out <= 512 x 512, K = 6,272 tokens), which the
+// register-staged 128-tile path runs latency-bound (~2 us per 128-deep k-step: a transposing load -> LDS -> MFMA
+// round trip per step, r3 split-K A/B).  One barrier per 32-deep k-tile, the DMA AHEAD tiles in flight, several
+// workgroups per CU (32 KB LDS each) instead of ping-pong; split-K through the fp32 atomic epilogue (small outputs).
+namespace mid {
+constexpr int TM = 128, TN = 128, THREADS = 256, AHEAD = 3, SLOTS = AHEAD + 1;
+constexpr int OP_BYTES = 128 * KT * 2, SLOT_BYTES = 2 * OP_BYTES, LDS_BYTES = SLOTS * SLOT_BYTES;
+
+__device__ __forceinline__ void wait_tiles(int n) {  // 4 DMA instructions per wave per k-tile
+  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AT, bool BT>
+__device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = by * TM, n0 = bx * TN;
+  const int kbeg = bz * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg) / KT;
+  if (nk <= 0) return;
+  const __bf16* sa[2];
+  const __bf16* sb[2];
+  dma_src<AT, 128, 4>(g.A, g.lda, g.M, m0, kbeg, wave, lane, sa);
+  dma_src<BT, 128, 4>(g.B, g.ldb, g.N, n0, kbeg, wave, lane, sb);
+  const size_t stepA = AT ? (size_t)KT * g.lda : KT, stepB = BT ? (size_t)KT * g.ldb : KT;
+  auto stage = [&](int j) __attribute__((always_inline)) {
+    char* slot = lds + (j % SLOTS) * SLOT_BYTES;
+    const size_t oa = (size_t)j * stepA, ob = (size_t)j * stepB;
+    dma16(sa[0] + oa, slot + wave * 1024);
+    dma16(sa[1] + oa, slot + (wave + 4) * 1024);
+    dma16(sb[0] + ob, slot + OP_BYTES + wave * 1024);
+    dma16(sb[1] + ob, slot + OP_BYTES + (wave + 4) * 1024);
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
+  float rowsum[4] = {0.f, 0.f, 0.f, 0.f};
+  const int pro = min(nk, AHEAD);
+  for (int t = 0; t < pro; ++t) stage(t);
+  for (int j = 0; j < nk; ++j) {
+    wait_tiles(min(nk - 1, j + AHEAD - 1) - j);  // tile j landed (this wave's part)
+    barrier();                                    // ... every wave's part; every read of tile j - 1 retired
+    if (j + AHEAD < nk) stage(j + AHEAD);         // into the slot of tile j - 1
+    const char* slot = lds + (j % SLOTS) * SLOT_BYTES;
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag<AT, 128>(slot, wm * 64 + 16 * i, lane);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = frag<BT, 128>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
+    if constexpr (AT || BT) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (want_rowsum) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rowsum[i] += (float)af[i][e];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
+  }
+  gemm_epilogue<4, 4, 4>(g, acc, m0 + wm * 64, n0 + wn * 64, gz > 1, lane);
+  if (want_rowsum) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float s = rowsum[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      const int m = m0 + wm * 64 + 16 * i + (lane & 15);
+      if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
+    }
+  }
+}
+}  // namespace mid
 }  // namespace big
+
 
 // out[m][n] += sum over the splits of slab[z][m][n] (n < n_store), 4 columns per thread
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ out, int ldc, int n_store, int M, int N,
@@ -828,6 +917,13 @@ __global__ __launch_bounds__(big::THREADS) __attribute__((amdgpu_waves_per_eu(2,
   extern __shared__ __attribute__((aligned(16))) char big_lds[];
   const int b = xcd_remap(blockIdx.x, nx * ny * nz);
   big::body<AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, big_lds);
+}
+
+template <bool AT, bool BT>
+__global__ __launch_bounds__(big::mid::THREADS) void gemm_mid_kernel(GemmArgs g, int nx, int ny, int nz) {
+  extern __shared__ __attribute__((aligned(16))) char mid_lds[];
+  const int b = xcd_remap(blockIdx.x, nx * ny * nz);
+  big::mid::body<AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, mid_lds);
 }
 
 // Two independent GEMMs of one tile configuration in ONE launch (the backward's weight gradient and input
@@ -1074,6 +1170,40 @@ bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
   return true;
 }
 
+// ---- the 128 x 128 LDS-DMA kernel for weight gradients too small for the macro tiles ----
+// Opt-in (MTA_GEMM_MID=1): measured slower than the register-staged path on the transformer's weight gradients
+// (512 x 128 x 6272: 20.6 vs 16.9 us at the best split; ~0.45 us per 32-deep k-tile, the read -> MFMA latency of
+// one barrier-separated k-tile per iteration exposed with one workgroup per CU; profiles/r3_gemm_mid_negative.txt).
+// What it lacks: fragment double buffering across k-tiles (reads of tile j + 1 behind the MFMAs of tile j).
+int g_mid_override = -1;
+inline bool mid_on() {
+  static const bool env_on = [] {
+    const char* e = getenv("MTA_GEMM_MID");
+    return e && e[0] == '1';
+  }();
+  return g_mid_override >= 0 ? g_mid_override == 1 : env_on;
+}
+
+bool mid_eligible(int mode, const GemmArgs& g) {
+  return mid_on() && mode == 2 && (g.flags & EPI_ACCUM) && g.K % big::KT == 0 && g.M >= 64 && g.N >= 64;
+}
+
+// split towards ~256 workgroups with >= 4 k-tiles each (fp32 atomic epilogue: the outputs are small); a caller that
+// asked for no split (deterministic mode) gets none: the atomics' order would vary
+bool try_mid(int mode, const GemmArgs& g_in, int ksplit_in, hipStream_t st) {
+  if (!mid_eligible(mode, g_in)) return false;
+  GemmArgs g = g_in;
+  const int nx = (g.N + big::mid::TN - 1) / big::mid::TN, ny = (g.M + big::mid::TM - 1) / big::mid::TM;
+  int ks = std::max(1, std::min(ksplit_in, 256 / (nx * ny)));
+  ks = std::min(ks, std::max(1, g.K / (4 * big::KT)));
+  int kps = (g.K + ks - 1) / ks;
+  kps = (kps + big::KT - 1) / big::KT * big::KT;
+  ks = (g.K + kps - 1) / kps;
+  g.k_per_split = kps;
+  gemm_mid_kernel<true, true><<<nx * ny * ks, big::mid::THREADS, big::mid::LDS_BYTES, st>>>(g, nx, ny, ks);
+  return true;
+}
+
 // (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately.
 // Big pairs run on transposed copies (both NN) when both problems qualify.
 bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, hipStream_t st) {
@@ -1081,6 +1211,12 @@ bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, h
   if (big_eligible(g1_in, k1) && big_eligible(g2_in, k2)) {
     try_big(2, g1_in, k1, st);
     try_big(1, g2_in, k2, st);
+    return true;
+  }
+  // small weight gradient on the 128 x 128 LDS-DMA kernel, its input-gradient partner on its own path
+  if (!big_eligible(g1_in, k1) && mid_eligible(2, g1_in)) {
+    try_mid(2, g1_in, k1, st);
+    dispatch_mode(1, g2_in, k2, st);
     return true;
   }
   const int c = tile_config(g1_in, k1);
@@ -1135,6 +1271,7 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
 
 void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
   if (try_big(mode, g_in, ksplit, st)) return;
+  if (try_mid(mode, g_in, ksplit, st)) return;
   GemmArgs g = g_in;
   if (to_nn(g, mode, st)) mode = 0;
   if (mode == 0) dispatch<false, false>(g, ksplit, st);
@@ -1153,6 +1290,7 @@ struct Pending {
 }  // namespace
 
 extern "C" void mta_gemm_set_big(int on) { g_big_override = on; }
+extern "C" void mta_gemm_set_mid(int on) { g_mid_override = on; }
 
 // launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
 extern "C" void mta_gemm_flush() {

@@ -137,6 +137,34 @@ def test_big_tile_gemm(mode, M, N, K):
     assert _rel(outs[0], outs[1]) < 2e-3
 
 
+# the 128 x 128 LDS-DMA kernel (csrc/gemm.hip, namespace big::mid) for the transformer's small weight gradients:
+# against fp32 PyTorch and the register-staged path, split-K (atomics) and unsplit (deterministic mode)
+@pytest.mark.parametrize("M,N,K,ks", [(512, 128, 6272, 16), (128, 512, 6272, 16), (384, 128, 6272, 1), (200, 136, 4000, 8)])
+def test_mid_tile_weight_grad(M, N, K, ks):
+    from masters_thesis_amd.ops import _lib
+    from masters_thesis_amd.ops import extras as X
+
+    C = _lib.lib()
+    torch.manual_seed(M + N)
+    A, B = _bf(torch.randn(K, M)), _bf(torch.randn(K, N))
+    ref = A.float().t() @ B.float()
+    outs = []
+    try:
+        for mid in (1, 0):
+            C.gemm_set_mid(mid)
+            gw = torch.ones(M, N, device=DEV)
+            gb = torch.ones(M, device=DEV)
+            fn = lambda: X.gemm(2, A, B, M, N, K, M, N, flags=X.EPI_ACCUM, out_f32=gw, ldc=N, n_store=N,  # noqa: E731
+                                ksplit=ks, bias_grad=gb)
+            assert _ran_kernel(fn, "gemm_mid_kernel") == bool(mid)
+            assert _rel(gw - 1, ref) < 2e-3
+            assert _rel(gb - 1, A.float().sum(0)) < 2e-3
+            outs.append(gw.clone())
+    finally:
+        C.gemm_set_mid(-1)
+    assert _rel(outs[0], outs[1]) < 2e-3
+
+
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("D", [128, 256, 1024, 1536, 2048])
 def test_norm_forward_backward(rms, D):
