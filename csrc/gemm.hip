@@ -806,13 +806,24 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 // round trip per step, r3 split-K A/B).  One barrier per 32-deep k-tile, the DMA AHEAD tiles in flight, several
 // workgroups per CU (32 KB LDS each) instead of ping-pong; split-K through the fp32 atomic epilogue (small outputs).
 namespace mid {
-constexpr int TM = 128, TN = 128, THREADS = 256, AHEAD = 3, SLOTS = AHEAD + 1;
+// r3 stamps (csrc/tools/gemm_probe.hip, MTA_GEMM_MID=1, 512 x 128 x 6272): ~1380 cycles per k-tile whatever the
+// split (1, 8, 32) and the ring depth (AHEAD 4 or 8): DMA issue + fragment reads ~590, DMA wait ~460, MFMAs ~45 --
+// the per-CU load path of the [K][rows] operands (256-B row pieces) runs at ~12 B/clk here, so a deeper ring or
+// fewer, longer workgroups do not help (profiles/r3_gemm_mid_negative.txt)
+constexpr int TM = 128, TN = 128, THREADS = 256, AHEAD = 4, SLOTS = AHEAD + 1;  // 80 KB: two workgroups per CU
 constexpr int OP_BYTES = 128 * KT * 2, SLOT_BYTES = 2 * OP_BYTES, LDS_BYTES = SLOTS * SLOT_BYTES;
 
 __device__ __forceinline__ void wait_tiles(int n) {  // 4 DMA instructions per wave per k-tile
-  if (n >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  switch (n < 0 ? 0 : n > 7 ? 7 : n) {
+    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
 }
 
 template <bool AT, bool BT>
@@ -845,34 +856,72 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
   float rowsum[4] = {0.f, 0.f, 0.f, 0.f};
-  const int pro = min(nk, AHEAD);
-  for (int t = 0; t < pro; ++t) stage(t);
-  for (int j = 0; j < nk; ++j) {
-    wait_tiles(min(nk - 1, j + AHEAD - 1) - j);  // tile j landed (this wave's part)
-    barrier();                                    // ... every wave's part; every read of tile j - 1 retired
-    if (j + AHEAD < nk) stage(j + AHEAD);         // into the slot of tile j - 1
+  // fragments double-buffered in registers: the reads of k-tile j + 1 are issued right behind the MFMAs of tile j
+  // (issued asynchronously), so the LDS latency overlaps the matrix core instead of preceding every k-tile
+  bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
+  auto read_frags = [&](int j, bf16x8 (&fa)[4], bf16x8 (&fb)[4]) __attribute__((always_inline)) {
     const char* slot = lds + (j % SLOTS) * SLOT_BYTES;
-    bf16x8 af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = frag<AT, 128>(slot, wm * 64 + 16 * i, lane);
+    for (int i = 0; i < 4; ++i) fa[i] = frag<AT, 128>(slot, wm * 64 + 16 * i, lane);
 #pragma unroll
-    for (int n = 0; n < 4; ++n) bfr[n] = frag<BT, 128>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
-    if constexpr (AT || BT) {
+    for (int n = 0; n < 4; ++n) fb[n] = frag<BT, 128>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
+  };
+#ifdef MTA_GEMM_STAMPS
+  unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  auto step = [&](int j, bf16x8 (&fa)[4], bf16x8 (&fb)[4], bf16x8 (&na)[4], bf16x8 (&nb)[4])
+      __attribute__((always_inline)) {
+    GSTAMP(t0);
+    if constexpr (AT || BT) {  // the transposed reads are inline asm: hipcc does not track them
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
+    GSTAMP(t1);
     if (want_rowsum) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) rowsum[i] += (float)af[i][e];
+        for (int e = 0; e < 8; ++e) rowsum[i] += (float)fa[i][e];
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
+      for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(fa[i], fb[n], acc[i][n]);
+    GSTAMP(t2);
+    if (j + 1 < nk) {
+      wait_tiles(min(nk - 1, j - 1 + AHEAD) - (j + 1));  // tile j + 1 landed (this wave's part)
+      GSTAMP(t3);
+      barrier();  // ... every wave's part; every wave's reads of tile j done (waited before its MFMAs)
+      GSTAMP(t4);
+      if (j + AHEAD < nk) stage(j + AHEAD);  // into the slot of tile j - 1
+      read_frags(j + 1, na, nb);
+      GSTAMP(t5);
+      GACC(2, t2, t3);
+      GACC(3, t3, t4);
+      GACC(4, t4, t5);
+    }
+    GACC(0, t0, t1);
+    GACC(1, t1, t2);
+  };
+  const int pro = min(nk, AHEAD);
+  for (int t = 0; t < pro; ++t) stage(t);
+  wait_tiles(pro - 1);
+  barrier();
+  read_frags(0, fa0, fb0);
+  GSTAMP(tloop0);
+  for (int j = 0; j < nk; j += 2) {
+    step(j, fa0, fb0, fa1, fb1);
+    if (j + 1 < nk) step(j + 1, fa1, fb1, fa0, fb0);
   }
+  GSTAMP(tloop1);
   gemm_epilogue<4, 4, 4>(g, acc, m0 + wm * 64, n0 + wn * 64, gz > 1, lane);
+#ifdef MTA_GEMM_STAMPS
+  GACC(6, tloop0, tloop1);
+  GSTAMP(tend);
+  GACC(7, tloop1, tend);
+  if (lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
+#endif
   if (want_rowsum) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1172,9 +1221,9 @@ bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
 
 // ---- the 128 x 128 LDS-DMA kernel for weight gradients too small for the macro tiles ----
 // Opt-in (MTA_GEMM_MID=1): measured slower than the register-staged path on the transformer's weight gradients
-// (512 x 128 x 6272: 20.6 vs 16.9 us at the best split; ~0.45 us per 32-deep k-tile, the read -> MFMA latency of
-// one barrier-separated k-tile per iteration exposed with one workgroup per CU; profiles/r3_gemm_mid_negative.txt).
-// What it lacks: fragment double buffering across k-tiles (reads of tile j + 1 behind the MFMAs of tile j).
+// (512 x 128 x 6272: 19.0 vs 16.9 us at the best split, with fragment double buffering and an 8-deep ring tried;
+// the stamps put ~1050 of its ~1380 cycles per k-tile in the DMA issue / wait: load-path bound, not latency bound;
+// profiles/r3_gemm_mid_negative.txt).
 int g_mid_override = -1;
 inline bool mid_on() {
   static const bool env_on = [] {
@@ -1200,6 +1249,10 @@ bool try_mid(int mode, const GemmArgs& g_in, int ksplit_in, hipStream_t st) {
   kps = (kps + big::KT - 1) / big::KT * big::KT;
   ks = (g.K + kps - 1) / kps;
   g.k_per_split = kps;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid_kernel<true, true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               big::mid::LDS_BYTES) == hipSuccess;
+  (void)attr;
   gemm_mid_kernel<true, true><<<nx * ny * ks, big::mid::THREADS, big::mid::LDS_BYTES, st>>>(g, nx, ny, ks);
   return true;
 }

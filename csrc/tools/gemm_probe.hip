@@ -32,6 +32,7 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096;
   const int K = argc > 3 ? atoi(argv[3]) : 4096, mode = argc > 4 ? atoi(argv[4]) : 0;
   const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 1: the MLP forward epilogue (bias + GELU, bf16 pre-activation)
+  const int ksplit = argc > 6 ? atoi(argv[6]) : 1;  // mode 2 (the mid kernel with MTA_GEMM_MID=1): split-K
   __bf16 *A, *B;
   float* C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
@@ -51,7 +52,7 @@ int main(int argc, char** argv) {
   const int flags = mode == 2 ? 8 : (epi ? 1 | 2 : 0);
   auto run = [&] {
     const int rc = mta_gemm_bf16(mode, A, B, M, N, K, lda, ldb, 1.f, flags, bias, nullptr, nullptr, nullptr, 0.f,
-                                 nullptr, C, pre, N, N, 1, nullptr, 0, 0);
+                                 nullptr, C, pre, N, N, ksplit, nullptr, 0, 0);
     if (rc) {
       printf("gemm rc=%d\n", rc);
       exit(1);
@@ -83,8 +84,10 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
   unsigned long long acc[8][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(big::stamp_acc), sizeof(acc)));
-  const int blocks = ((M + 255) / 256) * ((N + 255) / 256);
-  const int nk = K / 32;
+  const char* mid = getenv("MTA_GEMM_MID");
+  const int tile = mid && mid[0] == '1' ? 128 : 256;  // the mid kernel's stamps: [wait lgkm, mfma, wait vm, barrier, dma+reads]
+  const int blocks = ((M + tile - 1) / tile) * ((N + tile - 1) / tile) * ksplit;
+  const int nk = K / 32 / ksplit;
   const char* names[8] = {"reads", "dma_wait_r1", "barrier1", "mfma_seg", "dma_wait_r0", "barrier2", "loop", "epilogue"};
   printf("cycles per k-tile (loop, epilogue: per tile) averaged over %d blocks, %d k-tiles\n", blocks, nk);
   printf("%-12s", "wave");
