@@ -11,6 +11,8 @@
 // the dgamma/dbeta partials stay in registers until one LDS reduction at the end.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int NT_THREADS = 256;
@@ -260,61 +262,71 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, i
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(a.M, r0 + rows_per_block);
-  WideRow<VPT> cur, nxt;
-  if (r0 < r1) wide_load<VPT>(a, r0, cur);
-  for (int row = r0; row < r1; ++row) {
-    if (row + 1 < r1) wide_load<VPT>(a, row + 1, nxt);
-    float xh[VPT][4], g[VPT][4];
-    float s1 = 0.f, s2 = 0.f;
+  if (r0 >= r1) return;
+  // three row buffers in a fully unrolled ring (static register names: no buffer copy, which made every row wait
+  // for the next row's loads), rows k + 1 and k + 2 in flight while row k is reduced; loads past the range re-read
+  // the last row (unconditional: the compiler's vmcnt accounting stays exact)
+  WideRow<VPT> rb[3];
+  wide_load<VPT>(a, r0, rb[0]);
+  wide_load<VPT>(a, min(r0 + 1, r1 - 1), rb[1]);
+  for (int base = r0; base < r1; base += 3) {
 #pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = 4 * (tid + NT_THREADS * i);
-      const bool ok = c < a.D;
-      const float xs[4] = {cur.x[i].x, cur.x[i].y, cur.x[i].z, cur.x[i].w};
-      const float ds[4] = {cur.dy[i].x, cur.dy[i].y, cur.dy[i].z, cur.dy[i].w};
-      const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+    for (int k = 0; k < 3; ++k) {
+      const int row = base + k;
+      if (row >= r1) break;
+      wide_load<VPT>(a, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
+      WideRow<VPT>& cur = rb[k];
+      float xh[VPT][4], g[VPT][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float d = ds[j];
-        if (a.seed && ok) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
-        xh[i][j] = ok ? (xs[j] - cur.mu) * cur.rs : 0.f;
-        db[i][j] += d;
-        dg[i][j] += d * xh[i][j];
-        g[i][j] = d * gs[j];
-        s1 += g[i][j];
-        s2 += g[i][j] * xh[i][j];
+      for (int i = 0; i < VPT; ++i) {
+        const int c = 4 * (tid + NT_THREADS * i);
+        const bool ok = c < a.D;
+        const float xs[4] = {cur.x[i].x, cur.x[i].y, cur.x[i].z, cur.x[i].w};
+        const float ds[4] = {cur.dy[i].x, cur.dy[i].y, cur.dy[i].z, cur.dy[i].w};
+        const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = ds[j];
+          if (a.seed && ok) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+          xh[i][j] = ok ? (xs[j] - cur.mu) * cur.rs : 0.f;
+          db[i][j] += d;
+          dg[i][j] += d * xh[i][j];
+          g[i][j] = d * gs[j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+        }
+      }
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      const int par = row & 1;
+      if (lane == 0) {
+        red[par][0][wave] = s1;
+        red[par][1][wave] = s2;
+      }
+      __syncthreads();
+      s1 = a.rms ? 0.f : ((red[par][0][0] + red[par][0][1]) + (red[par][0][2] + red[par][0][3])) * invD;
+      s2 = ((red[par][1][0] + red[par][1][1]) + (red[par][1][2] + red[par][1][3])) * invD;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int c = 4 * (tid + NT_THREADS * i);
+        if (c >= a.D) continue;
+        const float rv[4] = {cur.dr[i].x, cur.dr[i].y, cur.dr[i].z, cur.dr[i].w};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) + rv[j];
+          if (a.pre) o[j] *= mta_gelu_grad((float)cur.pre[i][j]);
+        }
+        if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
+        if (a.dx_bf16) {
+          bf16x4 b;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
+          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+        }
       }
     }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    const int par = row & 1;
-    if (lane == 0) {
-      red[par][0][wave] = s1;
-      red[par][1][wave] = s2;
-    }
-    __syncthreads();
-    s1 = a.rms ? 0.f : ((red[par][0][0] + red[par][0][1]) + (red[par][0][2] + red[par][0][3])) * invD;
-    s2 = ((red[par][1][0] + red[par][1][1]) + (red[par][1][2] + red[par][1][3])) * invD;
-#pragma unroll
-    for (int i = 0; i < VPT; ++i) {
-      const int c = 4 * (tid + NT_THREADS * i);
-      if (c >= a.D) continue;
-      const float rv[4] = {cur.dr[i].x, cur.dr[i].y, cur.dr[i].z, cur.dr[i].w};
-      float o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) + rv[j];
-        if (a.pre) o[j] *= mta_gelu_grad((float)cur.pre[i][j]);
-      }
-      if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
-      if (a.dx_bf16) {
-        bf16x4 b;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
-        *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
-      }
-    }
-    cur = nxt;
   }
   if (!a.dgamma && !a.dbeta) return;
 #pragma unroll
@@ -330,7 +342,141 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, i
 }
 
 constexpr int NORM_BWD_MAX_BLOCKS = 1024;    // partial-row capacity of the static workspaces below
-constexpr int NORM_BWD_WIDE_BLOCKS = 1024;   // the wide backward: ~4 workgroups per CU
+// The MLP's wide backward (pre != null, no residual gradient, x / dy both f32 or both bf16, D a multiple of
+// 4 x 256 x VPT): every load unconditional and unconverted until use, so hipcc's vmcnt accounting keeps rows k + 1
+// and k + 2 in flight while row k is reduced.  The generic kernel above branches per load (optional operands,
+// bf16 -> f32 conversion in the loading branch): its waits drained the whole prefetch every row (r3 ISA).
+template <int VPT, bool B16>
+struct FastRow {
+  typename std::conditional<B16, bf16x4, float4>::type x[VPT], dy[VPT];
+  bf16x4 pre[VPT];
+  float mu, rs;
+};
+
+template <int VPT, bool B16>
+__device__ __forceinline__ void fast_load(const NormArgs& a, const float* mean, int row, FastRow<VPT, B16>& r) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    if constexpr (B16) {
+      r.x[i] = *reinterpret_cast<const bf16x4*>(a.xb + (size_t)row * a.ldx + c);
+      r.dy[i] = *reinterpret_cast<const bf16x4*>(a.dyb + (size_t)row * a.D + c);
+    } else {
+      r.x[i] = *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c);
+      r.dy[i] = *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c);
+    }
+    r.pre[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
+  }
+  r.mu = mean[row];  // rstd when RMSNorm (selected at use)
+  r.rs = a.rstd[row];
+}
+
+template <bool B16>
+__device__ __forceinline__ void fast_f4(const typename std::conditional<B16, bf16x4, float4>::type& v, float (&o)[4]) {
+  if constexpr (B16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = (float)v[j];
+  } else {
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+}
+
+template <int VPT, bool B16>
+__global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs a, int rows_per_block) {
+  __shared__ float red[2][2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float invD = 1.0f / (float)a.D;
+  const uint64_t seed = a.seed ? *a.seed : 0ull;
+  const float* mean = a.rms ? a.rstd : a.mean;
+  float4 gm[VPT];
+  float dg[VPT][4], db[VPT][4];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    gm[i] = a.gamma ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+  }
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(a.M, r0 + rows_per_block);
+  if (r0 >= r1) return;
+  FastRow<VPT, B16> rb[3];
+  fast_load<VPT, B16>(a, mean, r0, rb[0]);
+  fast_load<VPT, B16>(a, mean, min(r0 + 1, r1 - 1), rb[1]);
+  for (int base = r0; base < r1; base += 3) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int row = base + k;
+      if (row >= r1) break;
+      fast_load<VPT, B16>(a, mean, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
+      const FastRow<VPT, B16>& cur = rb[k];
+      const float mu = a.rms ? 0.f : cur.mu;
+      float xh[VPT][4], g[VPT][4];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int c = 4 * (tid + NT_THREADS * i);
+        float xs[4], ds[4];
+        fast_f4<B16>(cur.x[i], xs);
+        fast_f4<B16>(cur.dy[i], ds);
+        const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float d = ds[j];
+          if (a.seed) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+          xh[i][j] = (xs[j] - mu) * cur.rs;
+          db[i][j] += d;
+          dg[i][j] += d * xh[i][j];
+          g[i][j] = d * gs[j];
+          s1 += g[i][j];
+          s2 += g[i][j] * xh[i][j];
+        }
+      }
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      const int par = row & 1;
+      if (lane == 0) {
+        red[par][0][wave] = s1;
+        red[par][1][wave] = s2;
+      }
+      __syncthreads();
+      s1 = a.rms ? 0.f : ((red[par][0][0] + red[par][0][1]) + (red[par][0][2] + red[par][0][3])) * invD;
+      s2 = ((red[par][1][0] + red[par][1][1]) + (red[par][1][2] + red[par][1][3])) * invD;
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) {
+        const int c = 4 * (tid + NT_THREADS * i);
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) * mta_gelu_grad((float)cur.pre[i][j]);
+        if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
+        if (a.dx_bf16) {
+          bf16x4 b;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
+          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+        }
+      }
+    }
+  }
+  if (!a.dgamma && !a.dbeta) return;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int c = 4 * (tid + NT_THREADS * i);
+    if (a.dgamma)
+      *reinterpret_cast<float4*>(a.part + (long)blockIdx.x * a.part_ld + c) = make_float4(dg[i][0], dg[i][1], dg[i][2], dg[i][3]);
+    if (a.dbeta)
+      *reinterpret_cast<float4*>(a.part + a.part_pass + (long)blockIdx.x * a.part_ld + c) =
+          make_float4(db[i][0], db[i][1], db[i][2], db[i][3]);
+  }
+}
+
+#ifndef MTA_NORM_BWD_WIDE_BLOCKS
+#define MTA_NORM_BWD_WIDE_BLOCKS 512
+#endif
+// the wide backward: ~2 workgroups per CU, each a contiguous row range with two rows in flight (fewer, longer
+// blocks: half the dgamma / dbeta partial rows of the r3 grid of 1024)
+constexpr int NORM_BWD_WIDE_BLOCKS = MTA_NORM_BWD_WIDE_BLOCKS;
 // the one-wave-per-row backward's grid cap: transformer B=1 (M = 6,272 rows, D = 128) 0.714 ms at 512, 0.702 at
 // 1024, 0.711 at 1,568 (one row per wave: the partial-row reduce grows) (profiles/r2_norm_bwd_cap_ab.txt)
 constexpr int NORM_BWD_NARROW_BLOCKS = 1024;
@@ -467,6 +613,45 @@ __global__ __launch_bounds__(1024) void norm_param_reduce_wide_kernel(float* __r
 #pragma unroll
     for (int w = 0; w < 16; ++w) t += part[w][lane];
     dst[col] += t;
+  }
+}
+
+// Column sums of the wide backward's partial rows, 16 columns per block (2D / 16 = 256 blocks at D = 2048): 16 rows x
+// 64 B per wave instruction, wave sums by a fixed xor tree, block sum in wave order (deterministic).  The 64-column
+// form (64 blocks, 4 B per lane) took 8.3 us per call at mlp_large; a two-level form with a last-arriver ticket
+// 12.9 us (its agent-scope release writes back the XCD's dirty L2 behind the norm backward) (r3 traces).
+__global__ __launch_bounds__(1024) void norm_param_reduce_cols_kernel(float* __restrict__ dgamma,
+                                                                      float* __restrict__ dbeta, int D, int blocks) {
+  __shared__ float4 red[16][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 16 + 4 * (lane & 3);  // over [0, 2D); D % 16 == 0: a block never straddles the planes
+  const int pass = c >= D ? 1 : 0, col = c - pass * D;
+  float* dst = pass == 0 ? dgamma : dbeta;
+  if (dst == nullptr) return;  // uniform over the block
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = wave * 16 + (lane >> 2); b < blocks; b += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(&mta_norm_part[pass][b][col]);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+#pragma unroll
+  for (int m = 4; m < 64; m <<= 1) {
+    s.x += __shfl_xor(s.x, m, 64);
+    s.y += __shfl_xor(s.y, m, 64);
+    s.z += __shfl_xor(s.z, m, 64);
+    s.w += __shfl_xor(s.w, m, 64);
+  }
+  if (lane < 4) red[wave][lane] = s;
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float4 t = red[0][threadIdx.x];
+    for (int w = 1; w < 16; ++w) {
+      const float4 v = red[w][threadIdx.x];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    dst[col] += t.x;  // parameter-gradient views need not be 16-B aligned
+    dst[col + 1] += t.y;
+    dst[col + 2] += t.z;
+    dst[col + 3] += t.w;
   }
 }
 
@@ -622,7 +807,19 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
   if (wide) {
     if (M > 0) {
-      if (bwd) {
+      const bool b16 = a.xb != nullptr;
+      static const bool generic = getenv("MTA_NORM_BWD_GENERIC") != nullptr;  // A/B switch
+      const bool fast = !generic && a.pre && !a.dres && b16 == (a.dyb != nullptr) &&
+                        (D == 1024 || D == 2048) && (a.rms || a.mean);
+      if (bwd && fast) {
+        if (D == 1024) {
+          if (b16) norm_bwd_wide_fast_kernel<1, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+          else norm_bwd_wide_fast_kernel<1, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+        } else {
+          if (b16) norm_bwd_wide_fast_kernel<2, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+          else norm_bwd_wide_fast_kernel<2, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+        }
+      } else if (bwd) {
         if (D <= 1024) norm_bwd_wide_kernel<1><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
         else norm_bwd_wide_kernel<2><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
       } else {
@@ -640,9 +837,13 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     MTA_NORM_LAUNCH(8)
   }
 #undef MTA_NORM_LAUNCH
-  if (bwd && (dgamma || dbeta) && wide)
-    norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
-  else if (bwd && (dgamma || dbeta) && !defer)
+  if (bwd && (dgamma || dbeta) && wide) {
+    static const bool cols64 = getenv("MTA_NORM_REDUCE_64") != nullptr;  // A/B switch
+    if (!cols64 && D % 16 == 0)
+      norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
+    else
+      norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
+  } else if (bwd && (dgamma || dbeta) && !defer)
     norm_param_reduce_kernel<<<(2 * D + 3) / 4, 256, 0, st>>>(dgamma, dbeta, D, blocks);
   return 0;
 }

@@ -199,13 +199,23 @@ def test_norm_forward_backward(rms, D):
     assert _rel(dgam, gg) < 1e-4
     if not rms:
         assert _rel(dbet, gb) < 1e-4
-    # GELU' fusion
+    # GELU' fusion (D = 1024 / 2048: the branch-free wide backward, with its parameter partials)
     dxb = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    dgam2 = torch.zeros(D, device=DEV)
+    dbet2 = torch.zeros(D, device=DEV)
     C.norm(True, x, D, M, D, rms, eps, g, None if rms else b, None, None, mean, rstd, None, 0.0, dy, None, pre, dxb,
-           None, None, None)
+           None, dgam2, None if rms else dbet2)
     p = pre.float().requires_grad_(True)
     (gp,) = torch.autograd.grad(Fn.gelu(p), p, gx)
     assert _rel(dxb.float(), gp) < 8e-3
+    assert _rel(dgam2, gg) < 1e-4
+    if not rms:
+        assert _rel(dbet2, gb) < 1e-4
+    # the parameter reduction is fixed-order (per-block partial rows, xor-tree + wave-order column sums): bit-identical reruns
+    dgam3 = torch.zeros(D, device=DEV)
+    C.norm(True, x, D, M, D, rms, eps, g, None if rms else b, None, None, mean, rstd, None, 0.0, dy, None, pre, dxb,
+           None, dgam3, None)
+    assert torch.equal(dgam2, dgam3)
 
 
 @pytest.mark.parametrize("T,heads,hd", [(60, 4, 32), (64, 2, 64), (17, 3, 32)])
