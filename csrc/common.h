@@ -27,10 +27,14 @@ enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2 };
 // Activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (1 ulp) instead of the ~10-instruction
 // IEEE division sequence a plain '1.0f / x' compiles to.
 __device__ __forceinline__ float mta_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-__device__ __forceinline__ float mta_sigmoid(float x) { return mta_rcp(1.0f + __expf(-x)); }
+// exp(-x) as v_exp_f32 (2^y) of one product: -log2(e) and -2 log2(e) folded into one constant each (hipcc keeps
+// `-2 * x` and the log2(e) scale of __expf as two multiplies: 8 extra VALU per LSTM step and lane)
+__device__ __forceinline__ float mta_sigmoid(float x) {
+  return mta_rcp(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
 __device__ __forceinline__ float mta_tanh(float x) {
   // 2*sigmoid(2x) - 1: saturates cleanly at +-1
-  return fmaf(2.0f, mta_rcp(1.0f + __expf(-2.0f * x)), -1.0f);
+  return fmaf(2.0f, mta_rcp(1.0f + __builtin_amdgcn_exp2f(x * -2.8853900817779268f)), -1.0f);
 }
 
 __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {

@@ -172,9 +172,15 @@ extern "C" void mta_gather_batch(const float* const* src, float* const* dst, con
   long longest = 1;
   for (int k = 0; k < ntensors && k < 4; ++k) longest = row_floats[k] > longest ? row_floats[k] : longest;
   const int pieces = (int)((longest + 4L * GATHER_CHUNK - 1) / (4L * GATHER_CHUNK));
-  // every block arrives on one counter (the last advances the cursor): keep the grid near 512 workgroups -- at
-  // B = 64 one block per 16-KB piece was ~5k same-word atomics, ~35 us per step (r3 mlp_large trace)
-  const int target = 512 / (B * (ntensors > 0 ? ntensors : 1)) > 1 ? 512 / (B * (ntensors > 0 ? ntensors : 1)) : 1;
+  // every block arrives on one counter (the last advances the cursor): keep the grid near 2048 workgroups -- at
+  // B = 64 one block per 16-KB piece was ~5k same-word atomics, ~35 us per step; mlp_large B = 64 gather with a
+  // target of 512 / 2048 / 8192 blocks: 27.1 / 23.6 / 23.4 us (r3 traces)
+  static const int grid_target = [] {
+    const char* e = getenv("MTA_GATHER_BLOCKS");  // A/B knob
+    return e ? atoi(e) : 2048;
+  }();
+  const int per = B * (ntensors > 0 ? ntensors : 1);
+  const int target = grid_target / per > 1 ? grid_target / per : 1;
   a.span = (pieces + target - 1) / target;
   a.chunks = (pieces + a.span - 1) / a.span;
   gather_batch_kernel<<<dim3(B * a.chunks, ntensors), GATHER_TPB, 0, st>>>(a, perm, cursor, arrive, B, row_offset);
