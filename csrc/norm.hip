@@ -105,6 +105,15 @@ template <int VPL>
 __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float invD = 1.0f / (float)a.D;
+  // gamma / beta in registers before the row loop: loaded after the row reduction they were a second dependent
+  // round trip per row (the transformer's rows are one per wave)
+  float4 gm[VPL], bt[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    gm[i] = (c < a.D && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    bt[i] = (c < a.D && a.beta) ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   for (int row = blockIdx.x * 4 + wave; row < a.M; row += gridDim.x * 4) {
     float4 v[VPL];
     const float* xr = a.x + (size_t)row * a.ldx;
@@ -134,12 +143,11 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
     for (int i = 0; i < VPL; ++i) {
       const int c = 4 * (lane + 64 * i);
       if (c >= a.D) continue;
-      float o[4] = {(v[i].x - mu) * rs, (v[i].y - mu) * rs, (v[i].z - mu) * rs, (v[i].w - mu) * rs};
+      float o[4] = {(v[i].x - mu) * rs * gm[i].x + bt[i].x, (v[i].y - mu) * rs * gm[i].y + bt[i].y,
+                    (v[i].z - mu) * rs * gm[i].z + bt[i].z, (v[i].w - mu) * rs * gm[i].w + bt[i].w};
+      if (a.seed) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (a.gamma) o[j] *= a.gamma[c + j];
-        if (a.beta) o[j] += a.beta[c + j];
-        if (a.seed) o[j] *= mta_dropout_scale(*a.seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+        for (int j = 0; j < 4; ++j) o[j] *= mta_dropout_scale(*a.seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
       }
       if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.y_bf16) {
@@ -498,22 +506,36 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
 
+  // gamma before the row loop; the residual gradient and the GELU input with the row's x / dy (one dependent
+  // round trip per row instead of three)
+  float4 gm[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    gm[i] = (c < a.D && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+  }
   for (int row = blockIdx.x * 4 + wave; row < a.M; row += gridDim.x * 4) {
     const float* xr = a.x + (size_t)row * a.ldx;
     const float* dyr = a.dy + (size_t)row * a.D;
     const float mu = a.rms ? 0.f : a.mean[row];
     const float rs = a.rstd[row];
     float xh[VPL][4], g[VPL][4];
+    float4 rv[VPL];
+    bf16x4 pv[VPL];
     float s1 = 0.f, s2 = 0.f;  // sum(g*gamma), sum(g*gamma*xhat)
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = 4 * (lane + 64 * i);
       float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
+      rv[i] = xv;
       if (c < a.D) {
         xv = *reinterpret_cast<const float4*>(xr + c);
         dv = *reinterpret_cast<const float4*>(dyr + c);
+        if (a.dres) rv[i] = *reinterpret_cast<const float4*>(a.dres + (size_t)row * a.ldx + c);
+        if (a.pre) pv[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
       }
       const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w};
+      const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float d = ds[j];
@@ -521,7 +543,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
         xh[i][j] = (xs[j] - mu) * rs;
         db[i][j] += d;
         dg[i][j] += d * xh[i][j];
-        const float gg = a.gamma && c < a.D ? d * a.gamma[c + j] : d;
+        const float gg = d * gs[j];
         g[i][j] = gg;
         s1 += gg;
         s2 += gg * xh[i][j];
@@ -536,17 +558,13 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = rs * (g[i][j] - s1 - xh[i][j] * s2);
-      if (a.dres) {
-        const float4 r = *reinterpret_cast<const float4*>(a.dres + (size_t)row * a.ldx + c);
-        o[0] += r.x;
-        o[1] += r.y;
-        o[2] += r.z;
-        o[3] += r.w;
-      }
+      o[0] += rv[i].x;
+      o[1] += rv[i].y;
+      o[2] += rv[i].z;
+      o[3] += rv[i].w;
       if (a.pre) {
-        const bf16x4 p = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= mta_gelu_grad((float)p[j]);
+        for (int j = 0; j < 4; ++j) o[j] *= mta_gelu_grad((float)pv[i][j]);
       }
       if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.dx_bf16) {
