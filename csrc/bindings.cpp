@@ -56,6 +56,7 @@ void mta_adam(float* p, float* g, float* m, float* v, long n, const float* parti
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
               float* norm_out, float* nonfinite, hipStream_t st);
 void mta_scale(float* x, long n, float s, hipStream_t st);
+void mta_zero_bytes(void* dst, long bytes, hipStream_t st);
 // gemm.hip / norm.hip / attention.hip (MLP + transformer encoders)
 int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb, float alpha,
                   int flags, const float* bias, const float* resid, const void* aux_in, const uint64_t* seed,
@@ -992,12 +993,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
-  // contiguous tensor <- 0 through hipMemsetAsync on the current stream (no ATen fill kernel in a captured step)
+  // contiguous tensor <- 0 by a zero-fill KERNEL on the current stream.  A captured hipMemsetAsync (memset graph
+  // node) was not ordered against the neighbouring kernel nodes on replay when several processes shared the GPU
+  // (4-rank graphed transformer NaN, profiles/r4_nan_root_cause.txt); MTA_ZERO_MEMSET=1 restores it for that A/B.
   m.def("zero_", [](at::Tensor t) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
-    TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) == hipSuccess,
-                "zero_: hipMemsetAsync failed");
+    static const bool memset_node = getenv("MTA_ZERO_MEMSET") && getenv("MTA_ZERO_MEMSET")[0] == '1';
+    const long bytes = (long)(t.numel() * t.element_size());
+    if (memset_node) {
+      TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, bytes, cur_stream()) == hipSuccess, "zero_: hipMemsetAsync failed");
+    } else {
+      mta_zero_bytes(t.data_ptr(), bytes, cur_stream());
+    }
   });
   m.def("tr_layer_fwd", &tr_layer_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });

@@ -9,6 +9,8 @@
 //                        clip = min(1, max_norm / (||g|| + 1e-6)), and updates its slice.
 // lr and step live in device memory, so the step is HIP-graph capturable and the plateau
 // scheduler only rewrites one float.  `scale` folds the DDP 1/world_size average in.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -295,6 +297,23 @@ extern "C" void mta_adam(float* p, float* g, float* m, float* v, long n, const f
                                             reinterpret_cast<float4*>(m), reinterpret_cast<float4*>(v), n4, partials,
                                             grid_for(n4), lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
                                             norm_out, nonfinite);
+}
+
+// dst[0, bytes) <- 0 as a KERNEL node (a captured hipMemsetAsync node was not ordered against the kernel nodes
+// around it on graph replay when several processes share the GPU: profiles/r4_nan_root_cause.txt)
+__global__ void zero_bytes_kernel(uint4* __restrict__ dst16, long n16, unsigned char* __restrict__ rest, long nrest) {
+  const long stride = (long)gridDim.x * blockDim.x, first = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (long i = first; i < n16; i += stride) dst16[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (long i = first; i < nrest; i += stride) rest[i] = 0;
+}
+
+extern "C" void mta_zero_bytes(void* dst, long bytes, hipStream_t st) {
+  if (bytes <= 0) return;
+  const long n16 = ((uintptr_t)dst & 15) ? 0 : bytes / 16;  // unaligned buffers: all bytes one by one
+  long blocks = (std::max(n16, bytes - n16 * 16) + 255) / 256;
+  blocks = blocks < 1 ? 1 : blocks > 2048 ? 2048 : blocks;
+  zero_bytes_kernel<<<(int)blocks, 256, 0, st>>>(reinterpret_cast<uint4*>(dst), n16,
+                                                 reinterpret_cast<unsigned char*>(dst) + n16 * 16, bytes - n16 * 16);
 }
 
 extern "C" void mta_scale(float* x, long n, float s, hipStream_t st) {

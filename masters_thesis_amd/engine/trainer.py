@@ -173,6 +173,11 @@ class Trainer:
         self.phase_timer: Optional[PhaseTimer] = None
         self._torch_prof = None
         self._in_graph = False
+        # MTA_DEBUG_FINITE=1: after every training step synchronise and name the first parameter whose local
+        # (pre-sync) gradient or updated value is non-finite, with rank and step (localises a bad kernel / race)
+        self.debug_finite = os.environ.get("MTA_DEBUG_FINITE", "0") == "1"
+        self._dbg_step = 0
+        self._dbg_reported = False
 
     # ------------------------------------------------------------------ properties
     @property
@@ -229,6 +234,7 @@ class Trainer:
         elif isinstance(conf, (list, tuple)):
             opt = conf[0]
         self.flat = FlatParameters(model.parameters(), device=self.device)
+        self.flat.names = [n for n, p in model.named_parameters() if p.requires_grad]
         g = opt.param_groups[0]
         adamw = isinstance(opt, torch.optim.AdamW)
         if not isinstance(opt, (torch.optim.Adam, torch.optim.AdamW)) or g.get("amsgrad"):
@@ -309,16 +315,54 @@ class Trainer:
         if not self._in_graph or self._allreduce_in_graph():
             if self.ddp.world > 1:
                 phase("allreduce")
+            self._debug_check("local grad (eager)", self.flat.grad)
             self.ddp.allreduce_grads()
+            self._debug_norm("summed grad", self.flat.grad)
             phase("optim")
             self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
+            self._debug_norm("optimizer", None)
         return loss
 
     def _after_graph(self) -> None:
         # world > 1: the RCCL all-reduce and the optimizer run outside the captured fwd/bwd graph
         if not self._allreduce_in_graph():
+            self._debug_check("local grad (replayed graph)", self.flat.grad)
             self.ddp.allreduce_grads()
+            self._debug_norm("summed grad", self.flat.grad)
             self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
+            self._debug_norm("optimizer", None)
+
+    def _debug_norm(self, what: str, buf: Optional[torch.Tensor]) -> None:
+        """MTA_DEBUG_FINITE: print the host fp64 norm of ``buf`` (or the optimizer's device norm) for early steps."""
+        if not self.debug_finite or self._in_graph or self._dbg_step > 12:
+            return
+        if buf is None:
+            torch.cuda.synchronize() if self.device.type == "cuda" else None
+            v = float(self.optimizer.grad_norm.item())
+        else:
+            v = float(buf.detach().double().norm().item())
+        print(f"[finite] rank {self.denv.rank} step {self._dbg_step}: {what} norm {v:.6g}", file=sys.stderr,
+              flush=True)
+
+    def _debug_check(self, what: str, buf: torch.Tensor) -> None:
+        """MTA_DEBUG_FINITE: report (once) the first parameter range of ``buf`` holding a NaN/Inf."""
+        if not self.debug_finite or self._dbg_reported or self._in_graph:
+            return
+        if what.startswith("local"):
+            self._debug_norm(what, buf)
+        torch.cuda.synchronize() if buf.is_cuda else None
+        host = buf.detach().float().cpu()
+        bad = ~torch.isfinite(host)
+        if not bool(bad.any()):
+            return
+        names = getattr(self.flat, "names", None) or [f"param{i}" for i in range(len(self.flat.params))]
+        for name, p, o in zip(names, self.flat.params, self.flat.offsets):
+            n = int(bad[o:o + p.numel()].sum())
+            if n:
+                print(f"[finite] rank {self.denv.rank} step {self._dbg_step}: {what}: first non-finite range "
+                      f"'{name}' ({n}/{p.numel()} elements)", file=sys.stderr, flush=True)
+                break
+        self._dbg_reported = True
 
     def _run(self, key: Tuple, provider: Callable[[], Sequence[torch.Tensor]], body: Callable, static: bool,
              warmup: int):
@@ -393,6 +437,8 @@ class Trainer:
         key = ("train", B, True, id(loader)) if static else ("train", B, False)
         if self._graphs_enabled() and key in self._graphs:
             self._after_graph()
+        self._dbg_step += 1
+        self._debug_check("parameters after the step", self.flat.data)
         return out
 
     def _can_group(self, loader) -> bool:

@@ -48,7 +48,9 @@ def _worker(rank, world, port, n, twoshot, rounds, q):
         dev = torch.device("cuda", 0)
         ar = XgmiAllReduce.create(n, dev)
         assert ar is not None
-        ar.force_twoshot = twoshot
+        ar.force_twoshot = twoshot  # None: the size / world based choice
+        if twoshot is None:
+            assert ar.twoshot(n) == (n * 4 > 512 * 1024 and world > 2)
         worst = 0.0
         for rnd in range(rounds):
             x = _data(n, rank, rnd).to(dev)
@@ -195,3 +197,24 @@ def test_overlapped_gradient_sync_two_processes_one_gpu():
     for rank, worst, err in res:
         assert err is None, err
         assert worst < 1e-4, (rank, worst)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("n", [4 * 262_147, 4 * 1_000_003])
+def test_xgmi_allreduce_four_processes_auto_two_shot_uneven(n):
+    """world = 4: the size-based choice (None = auto) picks two-shot for these > 512 KB buckets, and
+    n / 4 float4 is odd, so the reduce-scatter chunks are uneven (the last owner gets a short chunk)."""
+    world = 4
+    assert (n // 4) % world != 0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, None, 3, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=280) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, worst, err in res:
+        assert err is None, (rank, err)
+        assert worst <= 2e-5, (rank, worst)
