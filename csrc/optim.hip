@@ -10,6 +10,7 @@
 // lr and step live in device memory, so the step is HIP-graph capturable and the plateau
 // scheduler only rewrites one float.  `scale` folds the DDP 1/world_size average in.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -96,9 +97,15 @@ __global__ __launch_bounds__(TPB) void adam_kernel(float4* __restrict__ p, float
 // bounded only for safety (a give-up counts in nonfinite[1]).
 constexpr int FUSED_MAX_BLOCKS = 256;
 constexpr unsigned FUSED_SPIN_LIMIT = 1u << 22;
-// the bound actually used: MTA_ADAM_SPIN_LIMIT overrides it (trials time-slicing one GPU wait out another
-// process's slice; a give-up is still counted and fails the step)
-__device__ unsigned g_fused_spin_limit = FUSED_SPIN_LIMIT;
+// MTA_ADAM_SPIN_LIMIT overrides it (trials time-slicing one GPU wait out another process's slice; a give-up is still
+// counted and fails the step); passed as a kernel argument, so it holds on every device and inside captured graphs
+inline unsigned fused_spin_limit() {
+  static const unsigned v = [] {
+    const char* e = getenv("MTA_ADAM_SPIN_LIMIT");
+    return (e && atol(e) > 0) ? (unsigned)atol(e) : FUSED_SPIN_LIMIT;
+  }();
+  return v;
+}
 
 // REG: every thread's (at most REG_N) float4 of g, p, m, v are loaded in phase 1, before the grid-wide arrival
 // wait, so phase 2 is compute + stores only (the post-barrier HBM round trip of the re-reads was ~1.5 us of a
@@ -113,7 +120,8 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
                                                          const float* __restrict__ lr_ptr, float* __restrict__ step_ptr,
                                                          float beta1, float beta2, float eps, float wd,
                                                          float max_norm, float scale, int adamw, int zero_grad,
-                                                         float* __restrict__ norm_out, float* __restrict__ nonfinite) {
+                                                         float* __restrict__ norm_out, float* __restrict__ nonfinite,
+                                                         unsigned spin_limit) {
   __shared__ float scratch[TPB / 64];
   __shared__ float s_norm;
   const long stride = (long)gridDim.x * TPB;
@@ -166,7 +174,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     while (seen < target) {
       __builtin_amdgcn_s_sleep(1);
       seen = __hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (++spins > g_fused_spin_limit) {
+      if (++spins > spin_limit) {
         if (nonfinite) atomicAdd(nonfinite + 1, 1.0f);
         break;
       }
@@ -330,21 +338,15 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
                                float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
                                float* norm_out, float* nonfinite, hipStream_t st) {
   const long n4 = n / 4;
-  static const bool spin_set = [] {
-    const char* e = getenv("MTA_ADAM_SPIN_LIMIT");
-    if (!e || atol(e) <= 0) return false;
-    const unsigned v = (unsigned)atol(e);
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_fused_spin_limit), &v, sizeof(v)) == hipSuccess;
-  }();
-  (void)spin_set;
+  const unsigned spin = fused_spin_limit();
   if (fused_reg(n4))
     adam_fused_kernel<true><<<fused_grid_reg(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-        zero_grad, norm_out, nonfinite);
+        zero_grad, norm_out, nonfinite, spin);
   else
     adam_fused_kernel<false><<<fused_grid(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-        zero_grad, norm_out, nonfinite);
+        zero_grad, norm_out, nonfinite, spin);
 }

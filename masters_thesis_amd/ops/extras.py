@@ -164,8 +164,8 @@ class _MlpEncoderFn(torch.autograd.Function):
             D = dims[i + 1]
             assert D % 8 == 0, "MLP hidden size must be a multiple of 8"
             pre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
-            # wide layers keep the GELU output in bf16 (as autocast would): the GEMM writes, the norm's forward and
-            # backward read half the bytes (csrc/norm.hip wide kernels read bf16 rows)
+            # the GELU output rows are fp32 by default; bf16 only with MTA_BF16_ROWS=1 for wide layers (measured
+            # slower end to end, see _row_dtype)
             act = torch.empty((Mp, D), device=dev, dtype=_row_dtype(D))
             gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU, bias=params[per * i + 1],
                  aux_pre=pre, **_row_out(act))

@@ -60,6 +60,13 @@ class FlatDDP:
         self._pending: List[tuple] = []  # ready ranges not yet launched (below the minimum size)
         self._launches = 0
         self._reduce_fn = None           # tests: replaces the xGMI launch (range -> None)
+        # range -> channel, fixed for the life of this object.  csrc/allreduce.hip's parity double buffer protects
+        # consecutive calls of ONE channel only (inbox slots are indexed by flat offset, shared by all channels): a
+        # range reduced on channel c1 in one step and c2 in the next could let a fast peer overwrite a slot a slow
+        # rank is still reading.  So a range keeps the channel it was first given, in eager steps and
+        # (captured once) in graph replays alike.
+        self._chan_of: dict = {}
+        self._plan: List[tuple] = []      # the ranges of the last overlapped step, in launch order
 
     # ------------------------------------------------------------------ overlapped sync
     def begin_backward(self) -> None:
@@ -101,13 +108,28 @@ class FlatDDP:
             else:
                 self._pending.append((a, b))
 
+    def channel_of(self, a: int, b: int) -> int:
+        """The channel of range [a, b): assigned on first use, then never changed.  Every gradient element belongs to
+        ONE registered range for the life of this object (a range overlapping a different registered one raises):
+        that is what makes the per-channel parity double buffer sufficient."""
+        ch = self._chan_of.get((a, b))
+        if ch is None:
+            for (a2, b2) in self._chan_of:
+                if a < b2 and a2 < b:
+                    raise RuntimeError(f"xGMI channel invariant: range [{a}, {b}) overlaps the registered range "
+                                       f"[{a2}, {b2}) (the backward's ready ranges changed between steps)")
+            nch = self.xgmi.channels if self.xgmi is not None else 16
+            ch = len(self._chan_of) % nch
+            self._chan_of[(a, b)] = ch
+        return ch
+
     def _launch(self, a: int, b: int, side: bool) -> None:
         self._done.append((a, b))
-        k = self._launches
         self._launches += 1
         if self._reduce_fn is not None:
             self._reduce_fn(a, b)
             return
+        k = self.channel_of(a, b)
         g = self.flat.grad
         if side:
             if self._side is None:
@@ -116,9 +138,9 @@ class FlatDDP:
             ev.record(torch.cuda.current_stream(g.device))
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
-                self.xgmi.allreduce_(g[a:b], off=a, channel=k % self.xgmi.channels)
+                self.xgmi.allreduce_(g[a:b], off=a, channel=k)
         else:
-            self.xgmi.allreduce_(g[a:b], off=a, channel=k % self.xgmi.channels)
+            self.xgmi.allreduce_(g[a:b], off=a, channel=k)
 
     def _remaining(self, n: int) -> List[tuple]:
         """[0, n) minus the ranges already reduced, in order."""
@@ -173,10 +195,17 @@ class FlatDDP:
             for a, b in self._remaining(g.numel()):
                 for s0 in range(a, b, xper):
                     self._launch(s0, min(b, s0 + xper), side=False)
+            self._plan = list(self._done)
             return
         if self.xgmi is not None:
-            for k, b in enumerate(self.xgmi_buckets):
-                self.xgmi.allreduce_(g[b], off=b.start, channel=k % self.xgmi.channels)
+            if self._chan_of and self._plan:
+                # an un-armed sync after overlapped steps (bench.py's allreduce_us loop): the same ranges on the same
+                # channels as those steps, in stream order
+                for a, b in self._plan:
+                    self.xgmi.allreduce_(g[a:b], off=a, channel=self.channel_of(a, b))
+                return
+            for b in self.xgmi_buckets:
+                self.xgmi.allreduce_(g[b], off=b.start, channel=self.channel_of(b.start, b.stop))
             return
         if self._gloo_cpu:
             t = g.cpu()

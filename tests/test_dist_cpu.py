@@ -137,3 +137,21 @@ def test_overlapped_sync_reduces_every_range_once():
     ddp.begin_backward()
     ddp.allreduce_grads()
     assert sum(b - a for a, b in calls) == flat.padded
+
+
+def test_xgmi_range_channel_invariant():
+    """FlatDDP.channel_of: a range keeps its first channel; a range overlapping a different registered range raises
+    (csrc/allreduce.hip's parity double buffer is per channel, its inbox slots per flat offset: ADVICE r3)."""
+    import pytest
+    import torch
+
+    from masters_thesis_amd.ops.optim import FlatParameters
+    from masters_thesis_amd.parallel.ddp import FlatDDP
+
+    flat = FlatParameters([torch.nn.Parameter(torch.zeros(4096))])
+    ddp = FlatDDP(flat)
+    assert ddp.channel_of(0, 1024) == 0
+    assert ddp.channel_of(1024, 4096) == 1
+    assert ddp.channel_of(0, 1024) == 0 and ddp.channel_of(1024, 4096) == 1
+    with pytest.raises(RuntimeError, match="channel invariant"):
+        ddp.channel_of(0, 4096)
