@@ -71,6 +71,11 @@ __device__ unsigned long long mta_stack_tl[2][64][4];
 #ifndef MTA_DBG_NO_STAGE
 #define MTA_DBG_NO_STAGE 0
 #endif
+// backward dG stores: 0 = recurrent waves (r3), 1 = gradient waves before their dx product, 2 = gradient waves
+// after their dx product (default: profiles/r4_lstm_bwd_dg_ab.txt)
+#ifndef MTA_STACK_DG_MODE
+#define MTA_STACK_DG_MODE 2
+#endif
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD
 #ifndef MTA_STACK_PRIO
 #define MTA_STACK_PRIO 0
@@ -920,6 +925,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
     unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     const float* w_ih = a.w_ih[layer];
+    float* dG = a.dG[layer];
     constexpr int XKB = BOTTOM ? 1 : KB, XKF = BOTTOM ? 1 : KF;
     bf16x8 Xhi[PREC == PREC_F32 ? 1 : XKB], Xlo[PREC == PREC_BF16X3 ? XKB : 1];
     float Xf[PREC == PREC_F32 ? XKF : 1];
@@ -961,7 +967,41 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 #pragma unroll
       for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = dreg[i];
     };
-    auto dx_step = [&](int t) {  // dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
+    // dG_t (fp32, unit-major columns 4u + g) from the LDS image (t&1) -> write-through 16-byte stores: the fused
+    // weight-gradient workgroups read these rows.  Issued by the gradient waves (they wait at the step barrier
+    // for ~1,300 cycles, r3 stamps) instead of the recurrent waves, whose store issue + vmcnt waits were ~500
+    // cycles of every reverse step.  Lane li = 64 w + lane: row li / 16, columns 4 (li % 16) + 64 k.  bf16 images:
+    // dG = hi (+ lo) -- the weight-gradient product splits it into the same hi / lo pair again.
+    // (4 stores per lane for H = 32 and 64: NW waves cover 4 NW rows per pass, G4 / 64 column blocks per row)
+    auto store_dg = [&](int t) {
+      const int buf = t & 1, li = 64 * w + lane, c0 = 4 * (li & 15);
+#pragma unroll
+      for (int pass = 0; pass < 16 / (4 * NW); ++pass)
+#pragma unroll
+      for (int k = 0; k < G4 / 64; ++k) {
+        const int s = (li >> 4) + 4 * NW * pass;
+        float* row = dG + ((size_t)t * Np + n0 + s) * G4;
+        const int c = c0 + 64 * k;  // columns c .. c + 3 = gates 0..3 of unit c / 4
+        f32x4 v;
+        if constexpr (PREC == PREC_F32) {
+          const int uu = c >> 2;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = g_f[buf][s][(uu & 3) * KF + g * (H / 4) + (uu >> 2)];
+        } else {
+          const bf16x4 hi4 = *reinterpret_cast<const bf16x4*>(&g_hi[buf][s][c]);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = (float)hi4[g];
+          if constexpr (PREC == PREC_BF16X3) {
+            const bf16x4 lo4 = *reinterpret_cast<const bf16x4*>(&g_lo[buf][s][c]);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) v[g] += (float)lo4[g];
+          }
+        }
+        store_sc1_x4(row + c, v);
+      }
+    };
+    auto dx_step = [&](int t) {  // dG_t stores and dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
+      if constexpr (MTA_STACK_DG_MODE == 1) store_dg(t);
       if constexpr (!BOTTOM) {
         const int buf = t & 1;
         // four independent accumulation chains (even / odd k-blocks x hi / cross terms)
@@ -995,6 +1035,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         }
         store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
       }
+      if constexpr (MTA_STACK_DG_MODE == 2) store_dg(t);
     };
     if constexpr (!TOP) {
       load_dh(T - 1);
@@ -1009,16 +1050,23 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       // MFMA streams on one SIMD serialise, r2 stamp probe), and its store stays in flight across the barrier:
       // vmcnt(1) waits for this wave's loads of the previous interval and everything older than its dx store.
       SSTAMP(0)
-      if constexpr (BOTTOM) mta_wait_vmem();
-      else mta_wait_vmcnt<1>();
+      // the previous interval's dG stores (4 per lane) and dx store stay in flight; every older op (its dH and
+      // keep-byte loads, issued before them) is complete
+      if constexpr (MTA_STACK_DG_MODE == 0) {
+        if constexpr (BOTTOM) mta_wait_vmem();
+        else mta_wait_vmcnt<1>();
+      } else {
+        if constexpr (BOTTOM) mta_wait_vmcnt<4>();
+        else mta_wait_vmcnt<5>();
+      }
       mreg = mnext;
       SSTAMP(1)
-      // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait in
-      // I(t+1), before barrier A(t+1)
+      // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait at
+      // the top of I(t+1) (which leaves only I(t+2)'s stores in flight), before barrier A(t+1)
       if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // dG progress: every recurrent wave passed its top-of-(t+1) vmcnt wait before A(t+1), which drains
-      // its dG stores of steps >= t+4
+      // dG progress: dG_s is stored in the same dx_step(s) as dx_s, before it, so the drain argument above covers
+      // dG of steps >= t+4 too
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (!TOP) {
@@ -1052,7 +1100,6 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
   const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
   const float* w_hh = a.w_hh[layer];
-  float* dG = a.dG[layer];
   bf16x8 Bhi[PREC == PREC_F32 ? 1 : KB], Blo[PREC == PREC_BF16X3 ? KB : 1];
   float Bf[PREC == PREC_F32 ? KF : 1];
   if constexpr (PREC == PREC_F32) {
@@ -1082,15 +1129,16 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     }
   }
   float pdG[4][4] = {};
-  auto store_step = [&](int t) {  // write-through: the fused weight-gradient workgroups read these rows
+  [[maybe_unused]] float* dG = a.dG[layer];
+  auto store_step = [&](int t) {  // MTA_STACK_DG_MODE 0: write-through dG rows from the recurrent waves
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       store_sc1_x4(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u,
                    f32x4{pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]});
   };
   // stash of step t (i, f, g, o, c) plus c_{t-1}, prefetched ~two steps ahead into one of two register
-  // sets (even / odd steps); per step the issue order is [4 dG stores of t+1, 6 stash loads of t-2], so at
-  // the top of step t <= T-2 the loads it needs are followed by exactly 10 newer ops: vmcnt(10)
+  // sets (even / odd steps); a step issues the 6 stash loads of step t-2 (mode 0: after the 4 dG stores of step
+  // t+1), so at the top of step t the loads it needs are followed by exactly 6 (mode 0: 10) newer ops
   auto load_into = [&](int t, float4 (&sb)[STASH], float4& cb) {
     const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
 #pragma unroll
@@ -1110,11 +1158,15 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[t & 1][4 * q + i][u];
     SSTAMP(1)
-    if (t <= T - 2) mta_wait_vmcnt<10>();
-    else mta_wait_vmcnt<6>();
+    if constexpr (MTA_STACK_DG_MODE == 0) {
+      if (t <= T - 2) mta_wait_vmcnt<10>();
+      else mta_wait_vmcnt<6>();
+    } else {
+      mta_wait_vmcnt<6>();
+    }
     SSTAMP(2)
-    store_step(t < T - 1 ? t + 1 : t);  // unconditional (step T-1 stores its zero pdG to row T-1, which
-                                        // step T-2 then overwrites in order): keeps the count exact
+    // mode 0: unconditional (step T-1 stores its zero pdG to row T-1, which step T-2 then overwrites in order)
+    if constexpr (MTA_STACK_DG_MODE == 0) store_step(t < T - 1 ? t + 1 : t);
     __builtin_amdgcn_sched_barrier(0);
     SSTAMP(3)
     const float4* st = sb;
@@ -1199,7 +1251,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   }
   if (t == 0) step(0, sA, cA);
   SSTAMP_FLUSH(1, 0, wave == 0)
-  store_step(0);
+  if constexpr (MTA_STACK_DG_MODE == 0) store_step(0);
   mta_wait_vmem();
   __syncthreads();  // F
 }
