@@ -71,10 +71,11 @@ __device__ unsigned long long mta_stack_tl[2][64][4];
 #ifndef MTA_DBG_NO_STAGE
 #define MTA_DBG_NO_STAGE 0
 #endif
-// backward dG stores: 0 = recurrent waves (r3), 1 = gradient waves before their dx product, 2 = gradient waves
-// after their dx product (default: profiles/r4_lstm_bwd_dg_ab.txt)
+// backward dG stores: 0 = recurrent waves (default), 1 = gradient waves before their dx product, 2 = gradient
+// waves after it.  1 / 2 measured SLOWER (bwd 98 -> 109-116 us: the gradient waves' interval grew ~700 cycles and
+// became the step's critical path, profiles/r4_lstm_bwd_dg_negative.txt); kept as an A/B switch
 #ifndef MTA_STACK_DG_MODE
-#define MTA_STACK_DG_MODE 2
+#define MTA_STACK_DG_MODE 0
 #endif
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD
 #ifndef MTA_STACK_PRIO
