@@ -60,7 +60,7 @@ def parse_args(argv=None):
     ap.add_argument("--model", default="small")
     ap.add_argument("--loss", default="mse")
     ap.add_argument("--trainer", default="fast")
-    ap.add_argument("--matmul-precision", default="high", choices=["highest", "high", "medium"])
+    ap.add_argument("--matmul-precision", default="high", choices=["highest", "high", "bf16x3", "medium"])
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"],
                     help="torch = reference-equivalent PyTorch eager path (MIOpen LSTM) for A/B")
     ap.add_argument("--no-graphs", action="store_true")
@@ -278,7 +278,10 @@ def main(argv=None):
             # "medium" (bf16-mixed); under 32-true they run the fp32 graph.  The LSTM keeps fp32 parameters and
             # activations; its recurrent matmuls run at matmul_precision (bf16x3 MFMA for "high")
             "dtype": "bf16" if eff_prec == "medium" else "fp32",
-            "matmul_dtype": {"medium": "bf16", "high": "bf16x3 (fp32-accurate)", "highest": "fp32"}[eff_prec],
+            "matmul_dtype": {"medium": "bf16",
+                             "high": ("LSTM fwd fp16x2 (TF32-class: fp16 activations, fp16 hi+lo weights), bwd bf16x3"
+                                      if cfg.model.get("arch", "lstm") == "lstm" else "bf16x3"),
+                             "bf16x3": "bf16x3 (fp32-accurate)", "highest": "fp32"}[eff_prec],
             "data": "synthetic (reference DGP, generated on device), random-init weights",
             "config": {
                 "model": f"{type(model).__name__} model={args.model} "

@@ -11,16 +11,21 @@
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Matmul precision for fp32 recurrences, mirroring torch.set_float32_matmul_precision:
 //   PREC_F32    'highest' : exact f32-input MFMA (v_mfma_f32_16x16x4_f32, fmaf-chain numerics)
-//   PREC_BF16X3 'high'    : x = hi + lo split into two bf16, a*b ~= hi*hi + hi*lo + lo*hi (3 bf16 MFMAs,
+//   PREC_BF16X3 'bf16x3'  : x = hi + lo split into two bf16, a*b ~= hi*hi + hi*lo + lo*hi (3 bf16 MFMAs,
 //                           ~16 mantissa bits per product, fp32 accumulate; > TF32, which cuDNN uses)
 //   PREC_BF16   'medium'  : single bf16 MFMA pass, fp32 accumulate (the reference's own setting,
 //                           train.py:13 set_float32_matmul_precision('medium'))
-enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2 };
+//   PREC_F16X2  'high'    : LSTM forward only -- the activation operand (|h| < 1, |dropout(h)| < 1.5) as ONE fp16
+//                           (11-bit significand = TF32's), the weight as fp16 hi + lo (~22 bits): a*w ~= a*hi + a*lo,
+//                           2 f16 MFMAs instead of 3 bf16 ones.  TF32-class, i.e. what cuDNN's LSTM runs for the
+//                           reference by default (cudnn.allow_tf32), with the weights more exact than TF32's
+enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2, PREC_F16X2 = 3 };
 
 #define MTA_WAVE 64
 
@@ -42,8 +47,16 @@ __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(x - (float)hi);
 }
 
+__device__ __forceinline__ void split_bf16(float x, _Float16& hi, _Float16& lo) {  // fp16 hi + lo (PREC_F16X2)
+  hi = (_Float16)x;
+  lo = (_Float16)(x - (float)hi);
+}
+
 __device__ __forceinline__ f32x4 mfma16x16x32(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x16x32(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4 mfma16x16x4f32(float a, float b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);

@@ -195,6 +195,7 @@ extern "C" int mta_gemm_f32(int prec, const float* A, const float* B, const floa
                             int M, int N, int K, int b_kn, hipStream_t st) {
   if (M < 1 || N < 1 || K < 1 || (size_t)M * N >= (1ull << 40)) return -1;
   GemmF32Args p{A, B, bias, mask, C, M, N, K};
+  if (prec == PREC_F16X2) prec = PREC_BF16X3;  // an LSTM-forward mode (bounded activations); general operands: bf16x3
   if (prec == PREC_F32) launch<PREC_F32>(p, b_kn != 0, st);
   else if (prec == PREC_BF16X3) launch<PREC_BF16X3>(p, b_kn != 0, st);
   else if (prec == PREC_BF16) launch<PREC_BF16>(p, b_kn != 0, st);

@@ -474,6 +474,7 @@ template <int H>
 void dispatch_fwd(int prec, const float* x, const float* w_ih, const float* b_ih, const float* b_hh, int fin,
                   const float* gx, float* stash, const float* w_hh, float* hseq, int N, int Np, int T,
                   hipStream_t st) {
+  if (prec == PREC_F16X2) prec = PREC_BF16X3;  // per-layer kernels: no f16x2 form
   if (prec == PREC_F32) launch_fwd<H, PREC_F32>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
   else if (prec == PREC_BF16X3) launch_fwd<H, PREC_BF16X3>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
   else launch_fwd<H, PREC_BF16>(x, w_ih, b_ih, b_hh, fin, gx, stash, w_hh, hseq, N, Np, T, st);
@@ -491,6 +492,7 @@ void launch_bwd(const float* stash, const float* w_hh, const float* dH, const fl
 template <int H>
 void dispatch_bwd(int prec, const float* stash, const float* w_hh, const float* dH, const float* dh_last, float* dG,
                   int N, int Np, int T, hipStream_t st) {
+  if (prec == PREC_F16X2) prec = PREC_BF16X3;  // per-layer kernels: no f16x2 form
   if (prec == PREC_F32) launch_bwd<H, PREC_F32>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);
   else if (prec == PREC_BF16X3) launch_bwd<H, PREC_BF16X3>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);
   else launch_bwd<H, PREC_BF16>(stash, w_hh, dH, dh_last, dG, N, Np, T, st);

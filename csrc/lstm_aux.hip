@@ -113,6 +113,7 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
 extern "C" int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* inp, int inp_batch_first,
                               int N, int Np, int T, int H, int F, float* g_wih, float* g_whh, float* g_bih,
                               float* g_bhh, float* part, hipStream_t st) {
+  if (prec == PREC_F16X2) prec = PREC_BF16X3;
   WgArgs a;
   a.part = part;
   a.dG = dG;

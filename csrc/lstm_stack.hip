@@ -264,15 +264,34 @@ struct StackFwdArgs {
 //     common.h), the stash; they drain the write-through stores and publish the layer's progress word.
 // r2 stamp probe: store issue + vmcnt drain were ~700 of ~2600 cycles of a recurrent step when the recurrent
 // waves issued the stores themselves.  All roles execute the same barriers (pre-loop, one per step, final).
+// MFMA operand element / fragment types of a precision mode (PREC_F16X2: fp16, the others: bf16)
+template <int PREC>
+struct OpT {
+  using E = __bf16;
+  using V8 = bf16x8;
+};
+template <>
+struct OpT<PREC_F16X2> {
+  using E = _Float16;
+  using V8 = f16x8;
+};
+// the weight operand has a lo half (bf16x3: hi + lo of both operands; f16x2: hi + lo of the weight only)
+template <int PREC>
+constexpr bool kWeightLo = PREC == PREC_BF16X3 || PREC == PREC_F16X2;
+// MFMA passes per k-block: bf16x3 lo*Whi + hi*Wlo + hi*Whi; f16x2 a*Wlo + a*Whi; bf16 a*Whi
+template <int PREC>
+constexpr int kPasses = PREC == PREC_BF16X3 ? 3 : PREC == PREC_F16X2 ? 2 : 1;
+
 template <int H, int PREC>
 struct FwdSmem {
   static constexpr int ROWB = H + 8, ROWF = H + 4;
+  using E = typename OpT<PREC>::E;
   float4 gxs[2][S][H];  // gate pre-activations (i, f, g, o) per (sequence, unit)
-  __bf16 h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  E h_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 h_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float h_f[2][S][PREC == PREC_F32 ? ROWF : 4];
   // layers >= 1: the layer input x_t (slot t & 1) in the MFMA A-operand layout, filled a quarter per input wave
-  __bf16 x_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
+  E x_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 x_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float x_f[2][S][PREC == PREC_F32 ? ROWF : 4];
   float hout[3][S][ROWF];              // h_t in fp32, natural unit order (slot t % 3), for the store waves
@@ -301,6 +320,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   constexpr int ROWB = H + 8;
   constexpr int ROWF = H + 4;
 
+  using E = typename OpT<PREC>::E;
+  using V8 = typename OpT<PREC>::V8;
   const bool last = layer == a.L - 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int role = wave / NW;  // 0 recurrent, 1 input, 2 store
@@ -399,7 +420,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     const float* xin = FIRST ? nullptr : (a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1]);
     unsigned* in_flag = a.flags + FLAG_STRIDE * (FIRST ? 0 : (layer - 1) * a.tr8 + tile);
     constexpr int XKB = FIRST ? 1 : KB, XKF = FIRST ? 1 : KF;
-    bf16x8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][PREC == PREC_BF16X3 ? XKB : 1];
+    V8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][kWeightLo<PREC> ? XKB : 1];
     float Xf[4][PREC == PREC_F32 ? XKF : 1];
     float wi[4][FIRST ? FIN0 : 1];
     if constexpr (FIRST) {
@@ -419,10 +440,10 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            __bf16 hi, lo;
+            E hi, lo;
             split_bf16(w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
             Xhi[g][kb][e] = hi;
-            if constexpr (PREC == PREC_BF16X3) Xlo[g][kb][e] = lo;
+            if constexpr (kWeightLo<PREC>) Xlo[g][kb][e] = lo;
           }
     }
     int nrow[4];
@@ -505,10 +526,10 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           for (int kb = 0; kb < KB; ++kb) {
             const float4 v0 = xr[2 * kb], v1 = xr[2 * kb + 1];
             const float xv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-            bf16x8 ahi, alo;
+            V8 ahi, alo;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              __bf16 hi, lo;
+              E hi, lo;
               split_bf16(xv[e], hi, lo);
               ahi[e] = hi;
               alo[e] = lo;
@@ -519,6 +540,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
                 acc[g] = mfma16x16x32(alo, Xhi[g][kb], acc[g]);
                 acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
               }
+              if constexpr (PREC == PREC_F16X2) acc[g] = mfma16x16x32(ahi, Xlo[g][kb], acc[g]);
               acc[g] = mfma16x16x32(ahi, Xhi[g][kb], acc[g]);
             }
           }
@@ -573,16 +595,24 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
           *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
         } else {
           const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
-          bf16x4 hi4, lo4;
+          if constexpr (PREC == PREC_F16X2) {  // one fp16 per element (the activation operand is not split)
+            typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+            f16x4_t v4;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            __bf16 hi, lo;
-            split_bf16(xv[e], hi, lo);
-            hi4[e] = hi;
-            lo4[e] = lo;
+            for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
+            *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
+          } else {
+            bf16x4 hi4, lo4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              __bf16 hi, lo;
+              split_bf16(xv[e], hi, lo);
+              hi4[e] = hi;
+              lo4[e] = lo;
+            }
+            *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
+            if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
           }
-          *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
-          if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
         }
       };
       auto compute_gx_img = [&](int t) {  // gx_t from image slot t & 1 into gxs slot t & 1
@@ -599,10 +629,11 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
             for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
           }
         } else {
-          bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
+          V8 ahi[KB];
+          bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
 #pragma unroll
           for (int kb = 0; kb < KB; ++kb) {
-            ahi[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_hi[slot][j][32 * kb + 8 * q]);
+            ahi[kb] = *reinterpret_cast<const V8*>(&sm.x_hi[slot][j][32 * kb + 8 * q]);
             if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_lo[slot][j][32 * kb + 8 * q]);
           }
 #pragma unroll
@@ -613,6 +644,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
                 acc[g] = mfma16x16x32(alo[kb], Xhi[g][kb], acc[g]);
                 acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
               }
+              if constexpr (PREC == PREC_F16X2) acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
               acc[g] = mfma16x16x32(ahi[kb], Xhi[g][kb], acc[g]);
             }
         }
@@ -660,7 +692,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   const float* w_hh = a.w_hh[layer];
   const bool stash = a.stash[layer] != nullptr;
 
-  bf16x8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][PREC == PREC_BF16X3 ? KB : 1];
+  V8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][kWeightLo<PREC> ? KB : 1];
   float Bf[4][PREC == PREC_F32 ? KF : 1];
   if constexpr (PREC == PREC_F32) {
 #pragma unroll
@@ -674,16 +706,16 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          __bf16 hi, lo;
+          E hi, lo;
           split_bf16(w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
           Bhi[g][kb][e] = hi;
-          if constexpr (PREC == PREC_BF16X3) Blo[g][kb][e] = lo;
+          if constexpr (kWeightLo<PREC>) Blo[g][kb][e] = lo;
         }
   }
   if constexpr (PREC == PREC_F32) {
     for (int idx = threadIdx.x; idx < S * ROWF; idx += NW * 64) (&h_f[0][0][0])[idx] = 0.f;
   } else {
-    for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_hi[0][0][0])[idx] = (__bf16)0.f;
+    for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_hi[0][0][0])[idx] = (E)0.f;
     if constexpr (PREC == PREC_BF16X3)
       for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 64) (&h_lo[0][0][0])[idx] = (__bf16)0.f;
   }
@@ -734,22 +766,30 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     } else {
       // every A fragment first, then 4 independent MFMA chains (one per gate): per k-block [lo x hi, hi x lo,]
       // hi x hi
-      bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
+      V8 ahi[KB];
+      bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        ahi[kb] = *reinterpret_cast<const bf16x8*>(&h_hi[cur][j][32 * kb + 8 * q]);
+        ahi[kb] = *reinterpret_cast<const V8*>(&h_hi[cur][j][32 * kb + 8 * q]);
         if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&h_lo[cur][j][32 * kb + 8 * q]);
       }
       if (t > 0 && !MTA_DBG_NO_STAGE) stage(t - 1);
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
-        for (int sg = 0; sg < (PREC == PREC_BF16X3 ? 3 : 1); ++sg) {
+        for (int sg = 0; sg < kPasses<PREC>; ++sg) {
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            if (PREC == PREC_BF16X3 && sg == 0) acc[g] = mfma16x16x32(alo[kb], Bhi[g][kb], acc[g]);
-            else if (PREC == PREC_BF16X3 && sg == 1) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
-            else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            if constexpr (PREC == PREC_BF16X3) {
+              if (sg == 0) acc[g] = mfma16x16x32(alo[kb], Bhi[g][kb], acc[g]);
+              else if (sg == 1) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
+              else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            } else if constexpr (PREC == PREC_F16X2) {
+              if (sg == 0) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
+              else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            } else {
+              acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            }
           }
         }
       }
@@ -774,10 +814,14 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
       if constexpr (PREC == PREC_F32) {
         h_f[nb][s4][(u & 3) * KF + (u >> 2)] = h[i];
       } else {
-        __bf16 hi, lo;
-        split_bf16(h[i], hi, lo);
-        h_hi[nb][s4][u] = hi;
-        if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
+        if constexpr (PREC == PREC_F16X2) {
+          h_hi[nb][s4][u] = (_Float16)h[i];
+        } else {
+          __bf16 hi, lo;
+          split_bf16(h[i], hi, lo);
+          h_hi[nb][s4][u] = hi;
+          if constexpr (PREC == PREC_BF16X3) h_lo[nb][s4][u] = lo;
+        }
       }
     }
     SSTAMP(4)
@@ -1308,6 +1352,7 @@ template <int H>
 int dispatch_fwd(int prec, int fin, const StackFwdArgs& a, hipStream_t st) {
   if (prec == PREC_F32) return launch_fwd<H, PREC_F32>(fin, a, st);
   if (prec == PREC_BF16X3) return launch_fwd<H, PREC_BF16X3>(fin, a, st);
+  if (prec == PREC_F16X2) return launch_fwd<H, PREC_F16X2>(fin, a, st);
   return launch_fwd<H, PREC_BF16>(fin, a, st);
 }
 
@@ -1325,7 +1370,8 @@ int launch_bwd(const StackBwdArgs& a, size_t lds, hipStream_t st) {
 template <int H>
 int dispatch_bwd(int prec, const StackBwdArgs& a, size_t wg_lds, hipStream_t st) {
   if (prec == PREC_F32) return launch_bwd<H, PREC_F32>(a, wg_lds, st);
-  if (prec == PREC_BF16X3) return launch_bwd<H, PREC_BF16X3>(a, wg_lds, st);
+  // PREC_F16X2 is a forward mode: the backward products stay bf16x3 (gradients need bf16's exponent range)
+  if (prec == PREC_BF16X3 || prec == PREC_F16X2) return launch_bwd<H, PREC_BF16X3>(a, wg_lds, st);
   return launch_bwd<H, PREC_BF16>(a, wg_lds, st);
 }
 
@@ -1428,6 +1474,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   const uint32_t* const* mask, float* const* part, uint64_t* seeds, float drop_p,
                                   int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T + 8 >= (1 << MAX_EPOCH_SHIFT)) return -1;
+  if (prec == PREC_F16X2) prec = PREC_BF16X3;  // a forward mode: backward products in bf16x3
   StackBwdArgs a{};
   for (int l = 0; l < L; ++l) {
     a.stash[l] = stash[l];

@@ -22,12 +22,21 @@ from __future__ import annotations
 
 from typing import List, Sequence
 
+import os
+
 import torch
 from torch import Tensor
 
 from ._lib import lib, use_hip
 
-MATMUL_PRECISION = {"highest": 0, "high": 1, "medium": 2}
+# torch.set_float32_matmul_precision names -> csrc/common.h PREC_* codes.  "high" is PyTorch's TF32-class setting
+# (TF32, or bf16x2/x3 sums): here the LSTM forward's recurrent / input products run PREC_F16X2 (fp16 activations,
+# fp16 hi + lo weights: 2 MFMA passes, r4 probe fwd 87 -> 80 us at the headline shape, profiles/r4_lstm_f16x2_ab.txt)
+# and every backward product bf16x3.  "bf16x3" forces the r3 form (3 bf16 passes forward too); so does
+# MTA_LSTM_HIGH=bf16x3 for "high".
+MATMUL_PRECISION = {"highest": 0, "high": 3, "medium": 2, "bf16x3": 1, "f16x2": 3}
+if os.environ.get("MTA_LSTM_HIGH", "") == "bf16x3":
+    MATMUL_PRECISION["high"] = 1
 # deterministic mode (Trainer(deterministic=True)): the weight-gradient chunks write partials that are summed
 # in chunk order by one extra launch instead of f32 atomics, so two runs are bit-identical
 _DETERMINISTIC = [False]

@@ -43,10 +43,12 @@ def _ref_lstm(x, ws, L):
     return out[:, -1], x64, w64
 
 
-TOLS = {"highest": 2e-5, "high": 3e-4, "medium": 3e-2}
+# "high" = PyTorch's TF32-class setting: the pipelined forward runs fp16 activations x fp16 hi+lo weights (PREC_F16X2);
+# "bf16x3" = the ~fp32-accurate 3-pass form
+TOLS = {"highest": 2e-5, "high": 1e-3, "bf16x3": 3e-4, "medium": 3e-2}
 
 
-@pytest.mark.parametrize("prec", ["highest", "high", "medium"])
+@pytest.mark.parametrize("prec", ["highest", "high", "bf16x3", "medium"])
 @pytest.mark.parametrize("N,T,F,H,L", [(100, 60, 3, 64, 2), (37, 20, 5, 64, 1), (40, 15, 3, 32, 3),
                                        (33, 12, 64, 128, 2), (300, 60, 3, 64, 4)])
 def test_lstm_forward_backward(prec, N, T, F, H, L):

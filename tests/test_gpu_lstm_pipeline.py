@@ -7,7 +7,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-TOLS = {"highest": 2e-5, "high": 3e-4, "medium": 3e-2}
+# "high" = PyTorch's TF32-class setting: the pipelined forward runs fp16 activations x fp16 hi+lo weights (PREC_F16X2);
+# "bf16x3" = the ~fp32-accurate 3-pass form
+TOLS = {"highest": 2e-5, "high": 1e-3, "bf16x3": 3e-4, "medium": 3e-2}
 
 
 def _weights(F, H, L, seed=0):
@@ -63,7 +65,7 @@ def _ref(x, ws, L, masks=None):
     return inp[:, -1], ws64
 
 
-@pytest.mark.parametrize("prec", ["highest", "high", "medium"])
+@pytest.mark.parametrize("prec", ["highest", "high", "bf16x3", "medium"])
 @pytest.mark.parametrize("N,T,F,H,L", [(100, 60, 3, 64, 2), (37, 20, 5, 64, 3), (40, 15, 3, 32, 8),
                                        (300, 60, 3, 64, 4),
                                        # thesis grid (tex/diplomski_rad.tex:1106-1122): H in {16, 32}, L in {1, 2};
