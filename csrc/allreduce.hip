@@ -22,15 +22,17 @@
 //     all-gather    : copy the gather region of the bucket back into the gradient.
 // Double buffering by parity is enough: a rank only starts call e+2 of a channel after every peer signalled
 // phase 0 of e+1, i.e. after every peer finished call e.  Flags compare with a wrap-safe ">=".
-// Workgroups per launch stay <= XG_MAX_BLOCKS so the grid is co-resident beside a concurrent backward kernel (a
+// Workgroups per launch stay <= XG_BIG_BLOCKS so the grid is co-resident beside a concurrent backward kernel (a
 // workgroup waits for the arrival of its rank's others: a non-resident one would stall it until the bound).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 constexpr int XG_MAX = 8;
 constexpr int XG_TPB = 256;
-constexpr int XG_MAX_BLOCKS = 64;
+constexpr int XG_SMALL_BLOCKS = 32, XG_BIG_BLOCKS = 128;  // grid caps (<= 8 MB / larger buckets)
 constexpr int XG_FLAG_STRIDE = 32;  // words: one 128-byte line per flag
 constexpr int XG_MAX_CHANNELS = 64;
 // ctl (local device memory): per channel [epoch, arrive phase 0, arrive phase 1, pad] in one 128-byte line, then
@@ -150,7 +152,14 @@ extern "C" {
 
 // comm buffer of one rank: fine-grained device memory (coherent for peer access), zeroed
 int mta_xgmi_alloc(long bytes, void** out) {
-  if (hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess) return -1;
+  // MTA_XGMI_COARSE=1: coarse-grained comm buffer (A/B; the kernel's system-scope release / acquire fences make
+  // both forms correct)
+  static const bool coarse = getenv("MTA_XGMI_COARSE") && getenv("MTA_XGMI_COARSE")[0] == '1';
+  if (coarse) {
+    if (hipMalloc(out, (size_t)bytes) != hipSuccess) return -1;
+  } else if (hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+    return -1;
+  }
   if (hipMemset(*out, 0, (size_t)bytes) != hipSuccess) return -2;
   return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
@@ -204,8 +213,19 @@ int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int
   a.rank = rank;
   a.world = world;
   a.twoshot = twoshot ? 1 : 0;
+  // grid cap by bucket size (profiles/r4_xgmi_local.txt, 2 processes on one GPU): up to 8 MB the flag protocol
+  // dominates and fewer workgroups are faster (3.2 MB one-shot: 29 us at 32, 31 at 64, 35 at 128); a 52 MB bucket
+  // is bandwidth-bound (547 / 330 / 233 / 224 us at 32 / 64 / 128 / 256).  At most 256 (one per CU: every
+  // workgroup waits for its rank's others, so the grid must be co-resident beside a concurrent backward).
+  // MTA_XGMI_MAX_BLOCKS overrides (A/B).
+  static const long env_cap = [] {
+    const char* e = getenv("MTA_XGMI_MAX_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return v < 0 ? 0L : v > 256 ? 256L : v;
+  }();
+  const long max_blocks = env_cap ? env_cap : (n * 4L > (8L << 20) ? XG_BIG_BLOCKS : XG_SMALL_BLOCKS);
   long blocks = (a.n4 + XG_TPB * 8 - 1) / (XG_TPB * 8);
-  blocks = blocks < 1 ? 1 : blocks > XG_MAX_BLOCKS ? XG_MAX_BLOCKS : blocks;
+  blocks = blocks < 1 ? 1 : blocks > max_blocks ? max_blocks : blocks;
   xgmi_allreduce_kernel<<<(int)blocks, XG_TPB, 0, st>>>(a);
   return 0;
 }
