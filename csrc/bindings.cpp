@@ -25,6 +25,10 @@ int mta_lstm_wgrad(int prec, const float* dG, const float* hseq, const float* in
 long mta_lstm_wgrad_part_floats(int fused, int T, int H, int F);
 int mta_gemm_f32(int prec, const float* A, const float* B, const float* bias, const float* mask, float* C, int M,
                  int N, int K, int b_kn, hipStream_t st);
+int mta_gemm_f32x(int prec, const float* A, int a_km, int lda, const float* B, int b_kn, int ldb, float* C, int ldc,
+                  int n_store, int M, int N, int K, int flags, const float* bias, float* pre, hipStream_t st);
+void mta_colsum_f32(const float* A, int M, int N, int lda, float* out, hipStream_t st);
+void mta_seeds_advance(uint64_t* seeds, int n, hipStream_t st);
 void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
                    hipStream_t st);
 void mta_gather_batch(const float* const* src, float* const* dst, const long* row_floats, int ntensors,
@@ -71,7 +75,7 @@ int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* ro
                  const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds, hipStream_t st);
 int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps, const float* gamma,
              const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
-             float drop_p, const void* dy, int dy_bf16, const float* dres, const void* pre, void* dx_bf16,
+             float drop_p, const void* dy, int dy_bf16, const float* dres, const void* pre, int pre_f32, void* dx_bf16,
              float* dx_f32, float* dgamma, float* dbeta, hipStream_t st);
 int mta_tr_layer_fwd(int nseq, int T, int d, int dff, int heads, const float* xs, const void* wqkv, const void* wo,
                      const void* w1, const void* w2, const float* g1, const float* bqkv, const float* bo,
@@ -214,6 +218,33 @@ void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bo
                                 g_wih.data_ptr<float>(), g_whh.data_ptr<float>(), g_bih.data_ptr<float>(),
                                 g_bhh.data_ptr<float>(), opt_mut(part), cur_stream());
   TORCH_CHECK(rc == 0, "lstm_wgrad: unsupported configuration (H=", H, ", F=", F, ")");
+}
+
+// 32-true extras GEMM (csrc/gemm_f32.hip mta_gemm_f32x): C[:M, :n_store] (=|+=) op(A) . op(B)^T (+ bias, GELU with
+// its input saved to pre); A viewed [M][K] (lda) or stored [K][M] (a_km); B [N][K] or [K][N] (b_kn)
+void gemm_f32x(int64_t prec, at::Tensor A, bool a_km, int64_t lda, at::Tensor B, bool b_kn, int64_t ldb, at::Tensor C,
+               int64_t ldc, int64_t n_store, int64_t M, int64_t N, int64_t K, int64_t flags,
+               c10::optional<at::Tensor> bias, c10::optional<at::Tensor> pre) {
+  for (at::Tensor* t : {&A, &B, &C}) TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat, "gemm_f32x: fp32 GPU");
+  TORCH_CHECK(A.numel() >= (a_km ? (K - 1) * lda + M : (M - 1) * lda + K), "gemm_f32x: A too small");
+  TORCH_CHECK(B.numel() >= (b_kn ? (K - 1) * ldb + N : (N - 1) * ldb + K), "gemm_f32x: B too small");
+  TORCH_CHECK(C.numel() >= (M - 1) * ldc + n_store, "gemm_f32x: C too small");
+  if (bias.has_value()) TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() >= N, "bias");
+  if (pre.has_value()) TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->numel() >= (M - 1) * ldc + n_store, "pre");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  const int rc = mta_gemm_f32x((int)prec, A.data_ptr<float>(), a_km ? 1 : 0, (int)lda, B.data_ptr<float>(), b_kn ? 1 : 0,
+                               (int)ldb, C.data_ptr<float>(), (int)ldc, (int)n_store, (int)M, (int)N, (int)K, (int)flags,
+                               bias.has_value() ? bias->data_ptr<float>() : nullptr,
+                               pre.has_value() ? pre->data_ptr<float>() : nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "gemm_f32x: unsupported configuration (", rc, ")");
+}
+
+// out[:N] += column sums of A[:M][:N] (lda): bias gradients of the 32-true extras
+void colsum_f32(at::Tensor A, int64_t M, int64_t N, int64_t lda, at::Tensor out) {
+  TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kFloat && out.is_cuda() && out.scalar_type() == at::kFloat &&
+              out.numel() >= N && A.numel() >= (M - 1) * lda + N, "colsum_f32: fp32 GPU tensors");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
+  mta_colsum_f32(A.data_ptr<float>(), (int)M, (int)N, (int)lda, out.data_ptr<float>(), cur_stream());
 }
 
 // C = A . B^T (+ bias) (* mask); B is [N][K], or [K][N] with b_kn (csrc/gemm_f32.hip)
@@ -563,6 +594,7 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
               "x must be fp32 or bf16 GPU");
   const bool xb = x.scalar_type() == at::kBFloat16;
   const bool dyb = has(dy) && dy->scalar_type() == at::kBFloat16;
+  const bool pre_f = has(pre) && pre->scalar_type() == at::kFloat;  // fp32 GELU input (32-true extras)
   if (dyb) TORCH_CHECK(dy->is_cuda() && dy->is_contiguous(), "dy: contiguous GPU tensor");
   check_span(x, M, ldx, D, "x");
   MTA_CHECK_F32(rstd);
@@ -583,7 +615,10 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
                           reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
                           (float)drop_p, dyb ? dy->data_ptr() : (const void*)opt_typed<float>(dy, at::kFloat, "dy"),
                           dyb ? 1 : 0,
-                          opt_typed<float>(dres, at::kFloat, "dres"), opt_typed<void>(pre, at::kBFloat16, "pre"),
+                          opt_typed<float>(dres, at::kFloat, "dres"),
+                          pre_f ? (const void*)opt_typed<float>(pre, at::kFloat, "pre")
+                                : (const void*)opt_typed<void>(pre, at::kBFloat16, "pre"),
+                          pre_f ? 1 : 0,
                           opt_typed<void>(dx_bf16, at::kBFloat16, "dx_bf16"),
                           opt_typed<float>(dx_f32, at::kFloat, "dx_f32"), opt_typed<float>(dgamma, at::kFloat, "dgamma"),
                           opt_typed<float>(dbeta, at::kFloat, "dbeta"), cur_stream());
@@ -993,6 +1028,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
+  m.def("gemm_f32x", &gemm_f32x);
+  m.def("colsum_f32", &colsum_f32);
+  m.def("seeds_advance", [](at::Tensor seeds) {
+    TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() <= 64, "seeds: int64[<= 64] GPU");
+    c10::hip::HIPGuardMasqueradingAsCUDA guard(seeds.device());
+    mta_seeds_advance(reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (int)seeds.numel(), cur_stream());
+  });
   // contiguous tensor <- 0 by a zero-fill KERNEL on the current stream.  A captured hipMemsetAsync (memset graph
   // node) was not ordered against the neighbouring kernel nodes on replay when several processes shared the GPU
   // (4-rank graphed transformer NaN, profiles/r4_nan_root_cause.txt); MTA_ZERO_MEMSET=1 restores it for that A/B.

@@ -84,6 +84,7 @@ struct NormArgs {
   const __bf16* dyb;    // bf16 dy instead of dy (wide kernels)
   const float* dres;    // [M][ldx] residual-stream gradient added to dx (or null)
   const __bf16* pre;    // [M][D] GELU input: dx *= gelu'(pre) (or null)
+  const float* pre_f;   // the same in fp32 (32-true extras; narrow kernels only)
   __bf16* dx_bf16;      // [M][D]
   float* dx_f32;        // [M][ldx]
   float* dgamma;
@@ -520,7 +521,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
     const float mu = a.rms ? 0.f : a.mean[row];
     const float rs = a.rstd[row];
     float xh[VPL][4], g[VPL][4];
-    float4 rv[VPL];
+    float4 rv[VPL], pf[VPL];
     bf16x4 pv[VPL];
     float s1 = 0.f, s2 = 0.f;  // sum(g*gamma), sum(g*gamma*xhat)
 #pragma unroll
@@ -533,6 +534,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
         dv = *reinterpret_cast<const float4*>(dyr + c);
         if (a.dres) rv[i] = *reinterpret_cast<const float4*>(a.dres + (size_t)row * a.ldx + c);
         if (a.pre) pv[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
+        if (a.pre_f) pf[i] = *reinterpret_cast<const float4*>(a.pre_f + (size_t)row * a.D + c);
       }
       const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w};
       const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
@@ -565,6 +567,12 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
       if (a.pre) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] *= mta_gelu_grad((float)pv[i][j]);
+      }
+      if (a.pre_f) {
+        o[0] *= mta_gelu_grad(pf[i].x);
+        o[1] *= mta_gelu_grad(pf[i].y);
+        o[2] *= mta_gelu_grad(pf[i].z);
+        o[3] *= mta_gelu_grad(pf[i].w);
       }
       if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.dx_bf16) {
@@ -754,9 +762,11 @@ extern "C" void mta_norm_flush() {
 extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps,
                         const float* gamma, const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd,
                         const uint64_t* seed, float drop_p, const void* dy, int dy_bf16, const float* dres,
-                        const void* pre, void* dx_bf16, float* dx_f32, float* dgamma, float* dbeta, hipStream_t st) {
+                        const void* pre, int pre_f32, void* dx_bf16, float* dx_f32, float* dgamma, float* dbeta,
+                        hipStream_t st) {
   if (D % 4 || ldx % 4 || D > 2048) return 1;
-  const bool wide_ok = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr;
+  // fp32 GELU input (32-true extras): the one-wave-per-row kernels (the wide ones stage pre as bf16)
+  const bool wide_ok = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr && !(pre && pre_f32);
   if ((x_bf16 || dy_bf16) && !wide_ok) return 2;  // bf16 row inputs: wide kernels only
   NormArgs a{};
   a.x = x_bf16 ? nullptr : static_cast<const float*>(x);
@@ -777,13 +787,14 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   a.dy = dy_bf16 ? nullptr : static_cast<const float*>(dy);
   a.dyb = dy_bf16 ? static_cast<const __bf16*>(dy) : nullptr;
   a.dres = dres;
-  a.pre = static_cast<const __bf16*>(pre);
+  a.pre = pre_f32 ? nullptr : static_cast<const __bf16*>(pre);
+  a.pre_f = pre_f32 ? static_cast<const float*>(pre) : nullptr;
   a.dx_bf16 = static_cast<__bf16*>(dx_bf16);
   a.dx_f32 = dx_f32;
   a.dgamma = dgamma;
   a.dbeta = dbeta;
   const int vpl = (D + 255) / 256;
-  const bool wide = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr;
+  const bool wide = wide_ok;
   int rows_per_block = 1;
   int blocks = norm_blocks(M, bwd != 0);
   if (wide && bwd) {

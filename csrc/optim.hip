@@ -324,6 +324,15 @@ extern "C" void mta_zero_bytes(void* dst, long bytes, hipStream_t st) {
                                                  reinterpret_cast<unsigned char*>(dst) + n16 * 16, bytes - n16 * 16);
 }
 
+// dropout seeds += golden-ratio increment (one fresh counter-hash seed per site and step, graph-capturable): the
+// 32-true extras' forward has no cast_pad launch that would advance them
+__global__ void seeds_advance_kernel(uint64_t* seeds, int n) {
+  if ((int)threadIdx.x < n) seeds[threadIdx.x] += 0x9E3779B97F4A7C15ull;
+}
+extern "C" void mta_seeds_advance(uint64_t* seeds, int n, hipStream_t st) {
+  seeds_advance_kernel<<<1, 64, 0, st>>>(seeds, n);
+}
+
 extern "C" void mta_scale(float* x, long n, float s, hipStream_t st) {
   const long n4 = n / 4;
   scale_kernel<<<grid_for(n4), TPB, 0, st>>>(reinterpret_cast<float4*>(x), n4, s);

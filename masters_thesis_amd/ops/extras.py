@@ -230,16 +230,106 @@ class _MlpEncoderFn(torch.autograd.Function):
         return (None,) * (7 + len(params))
 
 
+# --------------------------------------------------------------------------------------------------
+# 32-true MLP encoder on HIP kernels: fp32 activations and gradients, every GEMM on csrc/gemm_f32.hip
+# (mta_gemm_f32x) at the matmul precision the trainer resolved -- "high": bf16x3 (hi*hi + hi*lo + lo*hi,
+# ~fp32-accurate), "highest": the exact-f32 MFMA -- LayerNorm / RMSNorm + dropout on csrc/norm.hip in fp32, the
+# GELU' of the backward fused into the norm backward (fp32 GELU input), bias gradients by an ordered column sum.
+# Reference math: mlp_reference (the same architecture in fp32 PyTorch).
+# --------------------------------------------------------------------------------------------------
+F32X_BIAS, F32X_GELU, F32X_ACCUM = 1, 2, 8
+_F32_PREC = {"highest": 0, "high": 1, "bf16x3": 1}
+
+
+class _MlpEncoderF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, seeds, num_layers, norm, dropout, training, need_grad, prec, *params):
+        dev = x.device
+        N = x.shape[0]
+        L = num_layers
+        per = 4 if norm == "layernorm" else 3
+        rms = norm != "layernorm"
+        drop = dropout > 0 and training
+        C = lib()
+        if drop:
+            C.seeds_advance(seeds)  # one fresh counter-hash mask per site and step (the bf16 path: in cast_pad)
+        z = x.reshape(N, -1)
+        Xs, pres, acts, means, rstds = [z], [], [], [], []
+        for i in range(L):
+            w, b = params[per * i], params[per * i + 1]
+            D, K = w.shape
+            pre = torch.empty((N, D), device=dev, dtype=torch.float32)
+            act = torch.empty((N, D), device=dev, dtype=torch.float32)
+            C.gemm_f32x(prec, z, False, K, w, False, K, act, D, D, N, D, K, F32X_BIAS | F32X_GELU, b, pre)
+            mean = None if rms else torch.empty(N, device=dev, dtype=torch.float32)
+            rstd = torch.empty(N, device=dev, dtype=torch.float32)
+            y = torch.empty((N, D), device=dev, dtype=torch.float32)
+            C.norm(False, act, D, N, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
+                   None if rms else params[per * i + 3], None, y, mean, rstd,
+                   seeds[i:i + 1] if (drop and i < L - 1) else None, float(dropout), None, None, None, None, None,
+                   None, None)
+            pres.append(pre)
+            acts.append(act)
+            means.append(mean)
+            rstds.append(rstd)
+            z = y
+            if i < L - 1:
+                Xs.append(y)
+        ctx.meta = (N, L, per, rms, drop, float(dropout), prec)
+        ctx.params = params
+        ctx.seeds = seeds
+        if need_grad:
+            ctx.save_for_backward(*Xs, *pres, *acts)
+            ctx.stats = (means, rstds)
+        return z
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh):
+        N, L, per, rms, drop, p, prec = ctx.meta
+        params = ctx.params
+        saved = ctx.saved_tensors
+        Xs, pres, acts = saved[:L], saved[L:2 * L], saved[2 * L:]
+        means, rstds = ctx.stats
+        C = lib()
+        dy = dh.contiguous().float()
+        for i in range(L - 1, -1, -1):
+            w, b = params[per * i], params[per * i + 1]
+            D, K = w.shape
+            dpre = torch.empty((N, D), device=dh.device, dtype=torch.float32)
+            dropped = drop and i < L - 1
+            C.norm(True, acts[i], D, N, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
+                   None if rms else params[per * i + 3], None, None, means[i], rstds[i],
+                   ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], None, dpre,
+                   _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]))
+            # dW_i += dPre^T X_i: dPre read as stored ([tokens][D] = A^T), X_i as [K = tokens][N = K_i]
+            C.gemm_f32x(prec, dpre, True, D, Xs[i], True, K, _grad_view(w), K, K, D, K, N, F32X_ACCUM, None, None)
+            C.colsum_f32(dpre, N, D, D, _grad_view(b))
+            if i > 0:
+                dy = torch.empty((N, K), device=dh.device, dtype=torch.float32)
+                C.gemm_f32x(prec, dpre, False, D, w, True, K, dy, K, K, N, K, D, 0, None, None)
+            grad_ready(w.grad, b.grad)
+        return (None,) * (8 + len(params))
+
+
 def mlp_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, norm: str,
                dropout: float, training: bool, precision: str = "medium") -> Tensor:
     """``precision`` = the matmul precision the trainer resolved (``Trainer._effective_matmul_precision``): "medium"
-    (``bf16-mixed``, or an explicit medium) runs the bf16 HIP kernels; "high" / "highest" (``32-true``) runs the
-    fp32 graph (fp32 GEMMs, norms and attention) -- the trainer's precision is honoured, never silently lowered."""
+    (``bf16-mixed``, or an explicit medium) runs the bf16 HIP kernels; "high" / "highest" (``32-true``) the fp32 HIP
+    path (:class:`_MlpEncoderF32Fn`: bf16x3 / exact-f32 MFMA GEMMs, fp32 norms) -- the trainer's precision is
+    honoured, never silently lowered.  ``MTA_EXTRAS_F32_TORCH=1`` keeps the fp32 PyTorch graph for 32-true."""
     if use_hip(x) and precision == "medium":
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _MlpEncoderFn.apply(x.contiguous(), seeds, num_layers, norm, float(dropout), bool(training),
                                    need_grad, *params)
+    if use_hip(x) and precision in _F32_PREC and not _F32_TORCH:
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        return _MlpEncoderF32Fn.apply(x.contiguous().float(), seeds, num_layers, norm, float(dropout), bool(training),
+                                      need_grad, _F32_PREC[precision], *params)
     return mlp_reference(x, params, num_layers, norm, dropout, training)
+
+
+_F32_TORCH = os.environ.get("MTA_EXTRAS_F32_TORCH", "0") == "1"
 
 
 # --------------------------------------------------------------------------------------------------

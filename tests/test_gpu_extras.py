@@ -507,3 +507,68 @@ def test_extras_honour_trainer_precision(arch):
         outs[prec] = (h.double() - ref).abs().max().item() / max(ref.abs().max().item(), 1.0)
     assert outs["32-true"] <= 1e-4, outs
     assert 1e-6 < outs["bf16-mixed"] <= 5e-2, outs
+
+
+@pytest.mark.parametrize("prec,tol", [("high", 1e-4), ("highest", 2e-5)])
+@pytest.mark.parametrize("norm", ["layernorm", "rmsnorm"])
+def test_mlp_32true_hip_path_matches_fp64(prec, tol, norm, monkeypatch):
+    """32-true MLP on HIP kernels (ops/extras.py _MlpEncoderF32Fn: csrc/gemm_f32.hip mta_gemm_f32x GEMMs at bf16x3 /
+    exact-f32 MFMA, fp32 norms, GELU' fused into the norm backward, ordered bias-gradient column sums) against the
+    same encoder in fp64 on the CPU: forward and every parameter gradient.  The HIP path must be the one taken."""
+    from masters_thesis_amd.models.extras import MLPEncoder
+    from masters_thesis_amd.ops import extras as X
+
+    calls = []
+    orig = X._MlpEncoderF32Fn.apply
+    monkeypatch.setattr(X._MlpEncoderF32Fn, "apply", lambda *a: calls.append(1) or orig(*a))
+    torch.manual_seed(0)
+    enc = MLPEncoder(3, 60, 256, 2, 0.0, norm).to(DEV)
+    enc.precision = prec
+    enc.train()
+    x = torch.randn(100, 60, 3, device=DEV)
+    R = torch.randn(100, 256, device=DEV)
+    out = enc(x)
+    (out * R).sum().backward()
+    torch.cuda.synchronize()
+    assert calls, "the 32-true HIP path was not taken"
+    params = enc.flat_params()
+    p64 = [p.detach().double().cpu().requires_grad_(True) for p in params]
+    ref = X.mlp_reference(x.double().cpu(), p64, 2, norm, 0.0, True)
+    (ref * R.double().cpu()).sum().backward()
+    err = (out.double().cpu() - ref.detach()).abs().max().item() / ref.abs().max().item()
+    assert err <= tol, f"forward rel err {err}"
+    for i, (p, r) in enumerate(zip(params, p64)):
+        e = (p.grad.double().cpu() - r.grad).abs().max().item() / max(r.grad.abs().max().item(), 1e-12)
+        assert e <= 10 * tol, f"grad {i} {tuple(p.shape)}: rel err {e}"
+
+
+def test_mlp_32true_dropout_masks_consistent():
+    """32-true MLP with dropout: the norm backward regenerates the forward's counter-hash mask (a step is
+    differentiated exactly: directional derivative check in fp32), and the seeds advance once per forward."""
+    from masters_thesis_amd.models.extras import MLPEncoder
+
+    torch.manual_seed(1)
+    enc = MLPEncoder(3, 60, 128, 3, 0.3, "layernorm").to(DEV)
+    enc.precision = "highest"
+    enc.train()
+    x = torch.randn(64, 60, 3, device=DEV)
+    s0 = enc.seeds.clone()
+    out = enc(x)
+    assert not torch.equal(enc.seeds, s0)
+    used = enc.seeds.clone()
+    R = torch.randn_like(out)
+    (out * R).sum().backward()
+    w = enc.layers[1].weight
+    g = w.grad.clone()
+    d = torch.randn_like(w) * 1e-3
+    vals = []
+    for sgn in (1.0, -1.0):
+        with torch.no_grad():
+            w.add_(sgn * d)
+            enc.seeds.copy_(used)
+            enc.seeds.sub_(0x9E3779B97F4A7C15 - (1 << 64))  # the forward advances them again: same mask
+            vals.append(float((enc(x) * R).sum()))
+            w.sub_(sgn * d)
+    fd = (vals[0] - vals[1]) / 2.0
+    an = float((g * d).sum())
+    assert abs(fd - an) <= 2e-2 * abs(an) + 1e-3, (fd, an)
