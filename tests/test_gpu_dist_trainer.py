@@ -32,7 +32,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, model, batch, steps, sync, q, extra_env):
+def _worker(rank, world, port, model, batch, steps, sync, q, extra_env, trainer="gpu_fast", spg=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), MTA_DIST_BACKEND="gloo")
     if sync == "xgmi":
@@ -54,16 +54,16 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env):
         dev = denv.device
         torch.manual_seed(0)
         cfg, _, _ = compose(os.path.join(REPO, "configs"), "config", [
-            f"model={model}", "loss=mse", "trainer=gpu_fast", f"datamodule.batch_size={batch}",
+            f"model={model}", "loss=mse", f"trainer={trainer}", f"datamodule.batch_size={batch}",
             "datamodule.n_samples=20000", "model.dropout=0"])
         dm = FinancialLstmDataModule.from_config(cfg.datamodule, cache=False, device=dev, rank=denv.rank,
                                                  world_size=denv.world_size)
         dm.setup("fit")
         mcls = get_model_class(cfg.loss.module_class, cfg.model.get("arch", "lstm"))
         net = mcls(**model_params_from_config(cfg))
-        tr = Trainer(max_epochs=1, gradient_clip_val=cfg.trainer.gradient_clip_val, precision="bf16-mixed",
+        tr = Trainer(max_epochs=1, gradient_clip_val=cfg.trainer.gradient_clip_val, precision=cfg.trainer.precision,
                      enable_progress_bar=False, enable_model_summary=False, logger=None, callbacks=[],
-                     use_hip_graphs=True, steps_per_graph=1)
+                     use_hip_graphs=True, steps_per_graph=spg)
         tr._setup_env()
         tr._setup_model(net)
         tr._configure_optimizers(net)
@@ -73,8 +73,12 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env):
         loader = dm.train_dataloader()
         step = tr.make_train_stepper(loader)
         launches = []
-        for _ in range(steps):
-            step()
+        info["grouped"] = tr._can_group(loader)
+        done = 0
+        while done < steps:
+            n = spg if (spg > 1 and steps - done >= spg) else 1
+            step(n)
+            done += n
             launches.append(tr.ddp._launches if world > 1 else 0)
         torch.cuda.synchronize()
         tr._check_device_health()
@@ -93,11 +97,12 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env):
         q.put((rank, None, None, traceback.format_exc()))
 
 
-def _run(world, model, batch, steps, sync, extra_env=None, timeout=280):
+def _run(world, model, batch, steps, sync, extra_env=None, timeout=280, trainer="gpu_fast", spg=1):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, model, batch, steps, sync, q, extra_env or {}))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, model, batch, steps, sync, q, extra_env or {}, trainer,
+                                               spg))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -186,3 +191,24 @@ def test_trainer_xgmi_four_ranks_two_shot_transformer():
         assert torch.isfinite(p).all(), rank
     for p in ps[1:]:
         assert torch.equal(ps[0], p), "replicas diverged"
+
+
+@pytest.mark.timeout(600)
+def test_trainer_xgmi_grouped_lstm_two_ranks():
+    """The headline model under the driver's multi-GPU configuration: LSTM small, 32-true, xGMI all-reduce inside
+    GROUPED step graphs (4 training steps per captured graph, each with its own all-reduce on the device-resident
+    channel epochs).  Replicas bit-identical; parameters vs one rank on the global batch."""
+    steps = 12
+    res = _run(2, "small", 1, steps, "xgmi", trainer="fast", spg=4)
+    (_, p0, info0, _), (_, p1, info1, _) = res
+    assert info0["backend"] == "xgmi" and info0["in_graph"] and info0["grouped"], info0
+    assert info0["nonfinite"] == 0 and info1["nonfinite"] == 0
+    assert torch.isfinite(p0).all()
+    assert torch.equal(p0, p1), "replicas diverged"
+    ((_, pref, info_ref, _),) = _run(1, "small", 2, steps, "none", trainer="fast", spg=4)
+    diff = (p0 - pref).abs()
+    frac = (diff > 2e-5 + 1e-4 * pref.abs()).float().mean().item()
+    stats = f"max {diff.max().item():.3g}, mean {diff.mean().item():.3g}, frac>tol {frac:.4g}"
+    print(f"[small LSTM] 2 ranks x B=1 vs 1 rank x B=2 after {steps} grouped steps: {stats}")
+    assert diff.max().item() <= 1.5 * steps * 1e-4, stats
+    assert frac < 0.02, stats
