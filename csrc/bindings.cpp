@@ -77,11 +77,12 @@ int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms,
              const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
              float drop_p, const void* dy, int dy_bf16, const float* dres, const void* pre, int pre_f32, void* dx_bf16,
              float* dx_f32, float* dgamma, float* dbeta, hipStream_t st);
-int mta_tr_layer_fwd(int nseq, int T, int d, int dff, int heads, const float* xs, const void* wqkv, const void* wo,
-                     const void* w1, const void* w2, const float* g1, const float* bqkv, const float* bo,
-                     const float* g2, const float* b1, const float* b2, float eps, void* xn, void* qkv, void* o,
-                     void* xn2, void* pre1, void* u, float* x1, float* x2, float* r1, float* r2, float* lse,
-                     const float* rope, const uint64_t* seed, float drop_p, hipStream_t st);
+int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, const void* w2, const float* b1,
+               const float* b2, const float* g2, const float* x1, const uint64_t* seed, float drop_p, void* xn2,
+               void* pre, void* u, float* r2, float* x2, const void* dxb, const float* dx, const float* r2in,
+               const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, hipStream_t st);
+int mta_tr_transpose_bf16(int n, const void* const* src, void* const* dst, const int* rows, const int* cols,
+                          hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
                   int D, int heads, float rope_base, const float* rope, hipStream_t st);
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
@@ -645,34 +646,77 @@ static const float* rope_table(const at::Device& dev, int64_t T, int64_t HD, dou
   return it->second.data_ptr<float>();
 }
 
-// one transformer block forward in one launch (csrc/transformer.hip); every saved activation written
-void tr_layer_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope_base, at::Tensor xs, at::Tensor wqkv,
-                  at::Tensor wo, at::Tensor w1, at::Tensor w2, at::Tensor g1, at::Tensor bqkv, at::Tensor bo,
-                  at::Tensor g2, at::Tensor b1, at::Tensor b2, at::Tensor xn, at::Tensor qkv, at::Tensor o,
-                  at::Tensor xn2, at::Tensor pre1, at::Tensor u, at::Tensor x1, at::Tensor x2, at::Tensor r1,
-                  at::Tensor r2, at::Tensor lse, const OptT& seed, double drop_p) {
-  const int64_t d = xs.size(-1), dff = w1.size(0), M = nseq * T;
-  for (auto* t : {&xs, &x1, &x2}) {
-    MTA_CHECK_F32(*t);
-    TORCH_CHECK(t->numel() >= M * d, "tr_layer_fwd: row tensor too small");
-  }
-  for (auto* t : {&wqkv, &wo, &w1, &w2, &xn, &qkv, &o, &xn2, &pre1, &u}) {
+// fused FFN half of a transformer block (csrc/tr_ffn.hip), forward: x1 -> xn2, r2, pre, u, x2
+void tr_ffn_fwd(at::Tensor x1, at::Tensor w1, at::Tensor w2, at::Tensor b1, at::Tensor b2, at::Tensor g2, double eps,
+                const OptT& seed, double drop_p, at::Tensor xn2, at::Tensor r2, at::Tensor pre, at::Tensor u,
+                at::Tensor x2) {
+  const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1.size(0);
+  MTA_CHECK_F32(x1);
+  MTA_CHECK_F32(x2);
+  MTA_CHECK_F32(r2);
+  for (auto* t : {&w1, &w2, &xn2, &pre, &u}) {
     MTA_CHECK_GPU(*t, at::kBFloat16);
   }
-  TORCH_CHECK(wqkv.size(0) == 3 * d && wqkv.size(1) == d && wo.size(0) == d && wo.size(1) == d && w1.size(1) == d &&
-                  w2.size(0) == d && w2.size(1) == dff, "tr_layer_fwd: weight shapes");
-  TORCH_CHECK(qkv.numel() >= M * 3 * d && pre1.numel() >= M * dff && u.numel() >= M * dff, "tr_layer_fwd: sizes");
-  TORCH_CHECK(lse.numel() >= nseq * heads * 64 && r1.numel() >= M && r2.numel() >= M, "tr_layer_fwd: stats");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(xs.device());
-  const int rc = mta_tr_layer_fwd(
-      (int)nseq, (int)T, (int)d, (int)dff, (int)heads, xs.data_ptr<float>(), wqkv.data_ptr(), wo.data_ptr(),
-      w1.data_ptr(), w2.data_ptr(), g1.data_ptr<float>(), bqkv.data_ptr<float>(), bo.data_ptr<float>(),
-      g2.data_ptr<float>(), b1.data_ptr<float>(), b2.data_ptr<float>(), (float)eps, xn.data_ptr(), qkv.data_ptr(),
-      o.data_ptr(), xn2.data_ptr(), pre1.data_ptr(), u.data_ptr(), x1.data_ptr<float>(), x2.data_ptr<float>(),
-      r1.data_ptr<float>(), r2.data_ptr<float>(), lse.data_ptr<float>(), rope_table(xs.device(), T, d / heads, rope_base),
-      reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")), (float)drop_p, cur_stream());
-  TORCH_CHECK(rc == 0, "tr_layer_fwd: unsupported configuration (d=", d, ", dff=", dff, ", heads=", heads, ", T=", T,
-              ", rc=", rc, ")");
+  TORCH_CHECK(w1.size(1) == d && w2.size(0) == d && w2.size(1) == dff, "tr_ffn_fwd: weight shapes");
+  TORCH_CHECK(x2.numel() >= M * d && xn2.numel() >= M * d && pre.numel() >= M * dff && u.numel() >= M * dff &&
+                  r2.numel() >= M && b1.numel() >= dff && b2.numel() >= d && g2.numel() >= d,
+              "tr_ffn_fwd: sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x1.device());
+  const int rc = mta_tr_ffn(0, (int)M, (int)d, (int)dff, (float)eps, w1.data_ptr(), w2.data_ptr(), b1.data_ptr<float>(),
+                            b2.data_ptr<float>(), g2.data_ptr<float>(), x1.data_ptr<float>(),
+                            reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
+                            (float)drop_p, xn2.data_ptr(), pre.data_ptr(), u.data_ptr(), r2.data_ptr<float>(),
+                            x2.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, cur_stream());
+  TORCH_CHECK(rc == 0, "tr_ffn_fwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
+}
+
+// backward (input gradients): dX (fp32 + its bf16 copy) -> dpre (bf16), dX1 (fp32 + bf16), dg2 +=
+// w1t = W1^T [d][dff], w2t = W2^T [dff][d]
+void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at::Tensor r2, at::Tensor pre,
+                const OptT& seed, double drop_p, at::Tensor dx, at::Tensor dxb, at::Tensor dpre, at::Tensor dx1,
+                at::Tensor dx1b, at::Tensor dg2) {
+  const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1t.size(1);
+  for (auto* t : {&x1, &r2, &dx, &dx1, &dg2}) {
+    MTA_CHECK_F32(*t);
+  }
+  for (auto* t : {&w1t, &w2t, &pre, &dxb, &dpre, &dx1b}) {
+    MTA_CHECK_GPU(*t, at::kBFloat16);
+  }
+  TORCH_CHECK(w1t.size(0) == d && w2t.size(0) == dff && w2t.size(1) == d, "tr_ffn_bwd: weight shapes");
+  TORCH_CHECK(dx.numel() >= M * d && dxb.numel() >= M * d && dx1.numel() >= M * d && dx1b.numel() >= M * d &&
+                  pre.numel() >= M * dff && dpre.numel() >= M * dff && r2.numel() >= M && dg2.numel() >= d,
+              "tr_ffn_bwd: sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x1.device());
+  const int rc = mta_tr_ffn(1, (int)M, (int)d, (int)dff, 0.f, w1t.data_ptr(), w2t.data_ptr(), nullptr, nullptr,
+                            g2.data_ptr<float>(), x1.data_ptr<float>(),
+                            reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
+                            (float)drop_p, nullptr, nullptr, nullptr, nullptr, nullptr, dxb.data_ptr(),
+                            dx.data_ptr<float>(), r2.data_ptr<float>(), pre.data_ptr(), dpre.data_ptr(),
+                            dx1.data_ptr<float>(), dx1b.data_ptr(), dg2.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "tr_ffn_bwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
+}
+
+// dst[i] = src[i]^T for bf16 matrices (one launch)
+void transpose_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
+  TORCH_CHECK(src.size() == dst.size() && !src.empty() && src.size() <= 32, "transpose_bf16: 1..32 matrices");
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<int> rows, cols;
+  for (size_t i = 0; i < src.size(); ++i) {
+    MTA_CHECK_GPU(src[i], at::kBFloat16);
+    MTA_CHECK_GPU(dst[i], at::kBFloat16);
+    TORCH_CHECK(src[i].dim() == 2 && dst[i].dim() == 2 && dst[i].size(0) == src[i].size(1) &&
+                    dst[i].size(1) == src[i].size(0) && src[i].is_contiguous() && dst[i].is_contiguous(),
+                "transpose_bf16: dst must be the contiguous [cols][rows] of src");
+    sp.push_back(src[i].data_ptr());
+    dp.push_back(dst[i].data_ptr());
+    rows.push_back((int)src[i].size(0));
+    cols.push_back((int)src[i].size(1));
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(src[0].device());
+  const int rc = mta_tr_transpose_bf16((int)sp.size(), sp.data(), dp.data(), rows.data(), cols.data(), cur_stream());
+  TORCH_CHECK(rc == 0, "transpose_bf16: rows/cols must be multiples of 8 (rc=", rc, ")");
 }
 
 void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
@@ -1049,7 +1093,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       mta_zero_bytes(t.data_ptr(), bytes, cur_stream());
     }
   });
-  m.def("tr_layer_fwd", &tr_layer_fwd);
+  m.def("tr_ffn_fwd", &tr_ffn_fwd);
+  m.def("tr_ffn_bwd", &tr_ffn_bwd);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("gemm_set_mid", [](int64_t on) { mta_gemm_set_mid((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });

@@ -79,6 +79,28 @@ union Bf8 {
   __bf16 e[8];
 };
 
+// GEMM epilogue store (probe builds: MTA_EPI_NT = nontemporal, MTA_EPI_NOSTORE = timing without the
+// stores; the flags bit 30 is never set, it only keeps the values live)
+template <typename T>
+__device__ __forceinline__ void epi_store(T* p, const T& v, int flags) {
+#if defined(MTA_EPI_NOSTORE)
+  if (flags & (1 << 30)) *p = v;
+#elif defined(MTA_EPI_NT)
+  (void)flags;
+  if constexpr (sizeof(T) == 2) {
+    __builtin_nontemporal_store(__builtin_bit_cast(unsigned short, v), reinterpret_cast<unsigned short*>(p));
+  } else if constexpr (sizeof(T) == 4) {
+    __builtin_nontemporal_store(__builtin_bit_cast(unsigned int, v), reinterpret_cast<unsigned int*>(p));
+  } else {
+    typedef unsigned int V __attribute__((ext_vector_type(sizeof(T) / 4)));
+    __builtin_nontemporal_store(__builtin_bit_cast(V, v), reinterpret_cast<V*>(p));
+  }
+#else
+  (void)flags;
+  *p = v;
+#endif
+}
+
 // Epilogue of one wave's MT x NT grid of 16x16 accumulator tiles whose top-left output element is (mbase, nbase):
 // tile (i, j), register r of lane l holds C[mbase + 16 i + 4 (l >> 4) + r][nbase + 16 j + (l & 15)].  Rows are done
 // IC tiles at a time; the operands the epilogue reads (residual stream, GELU input of a DGELU, the fp32 output of a
@@ -136,11 +158,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, const f32x4 (&a
           const size_t o = (size_t)m * g.ldc + n;
           if (g.flags & EPI_ACCUM) {
             if (split) atomicAdd(g.out_f32 + o, v);
-            else g.out_f32[o] = pre_in[i][j][r] + v;
+            else epi_store(g.out_f32 + o, pre_in[i][j][r] + v, g.flags);
             continue;
           }
           if (g.flags & EPI_BIAS) v += g.bias[n];
-          if (g.aux_pre) g.aux_pre[o] = (__bf16)v;
+          if (g.aux_pre) epi_store(g.aux_pre + o, (__bf16)v, g.flags);
           if (g.flags & EPI_GELU) v = mta_gelu(v);
           if (g.flags & EPI_DROPOUT) {
             const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
@@ -148,8 +170,8 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, const f32x4 (&a
           }
           if (g.flags & EPI_DGELU) v *= mta_gelu_grad(pre_in[i][j][r]);
           if (g.flags & EPI_RESID) v += pre_in[i][j][r];
-          if (g.out_f32) g.out_f32[o] = v;
-          if (g.out_bf16) g.out_bf16[o] = (__bf16)v;
+          if (g.out_f32) epi_store(g.out_f32 + o, v, g.flags);
+          if (g.out_bf16) epi_store(g.out_bf16 + o, (__bf16)v, g.flags);
         }
       }
     }
@@ -456,6 +478,7 @@ __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, in
 // diagnostic build (csrc/tools/gemm_probe.hip): s_memtime stamps of the main loop's segments, summed per wave
 #ifdef MTA_GEMM_STAMPS
 __device__ unsigned long long stamp_acc[8][8];  // [wave][segment]
+__device__ unsigned long long epi_stamp[8];  // probe extras (MTA_EPI_TWICE: epilogue first / second call)
 #define GSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define GACC(i, a, b) dsum[i] += (unsigned)((b) - (a))
 #else
@@ -528,6 +551,11 @@ __device__ __forceinline__ float stage_read1(const float* p) {
   return v;
 }
 
+// IN: the epilogue reads an operand per output (residual, GELU input of a DGELU, the fp32 output of a non-split
+// accumulate).  The IN = false form has no global load in its loops: with loads on any path hipcc waits vmcnt(0) --
+// every store issued so far -- ahead of the stores of each row (register reuse after a possibly outstanding load),
+// one store round trip per row, which was ~40 % of a 256 x 256 tile's time (r4 epilogue probe).
+template <bool IN>
 __device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* stage, const int mrow, const int n,
                                           const int lane, const bool vec, const bool split, const int bz,
                                           const float (&bias4)[4],
@@ -541,7 +569,7 @@ __device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* sta
     for (int q = 0; q < 16; ++q) {
       const int rr = 4 * q + (lane >> 4);
       const float4 t = stage_read4(stage + rr * EPI_ROW + cc);
-      if (mrow + rr < g.M && n + 3 < g.N) *reinterpret_cast<float4*>(slab + (size_t)(mrow + rr) * g.N + n) = t;
+      if (mrow + rr < g.M && n + 3 < g.N) epi_store(reinterpret_cast<float4*>(slab + (size_t)(mrow + rr) * g.N + n), t, g.flags);
     }
     return;
   }
@@ -564,7 +592,7 @@ __device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* sta
     const size_t o = (size_t)m * g.ldc + n;
     const bool wide = vec && n + 3 < g.n_store;
     float pin[4] = {0.f, 0.f, 0.f, 0.f};
-    if ((g.flags & (EPI_RESID | EPI_DGELU)) || accum) {
+    if (IN) {
       if (wide) {
         if (accum || (g.flags & EPI_RESID)) {
           const float4 x = *reinterpret_cast<const float4*>((accum ? g.out_f32 : g.resid) + o);
@@ -605,18 +633,18 @@ __device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* sta
       if (g.flags & EPI_RESID) v[e] += pin[e];
     }
     if (wide) {
-      if (g.out_f32) *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+      if (g.out_f32) epi_store(reinterpret_cast<float4*>(g.out_f32 + o), make_float4(v[0], v[1], v[2], v[3]), g.flags);
       if (!accum && g.out_bf16) {
         Bf8 b;
 #pragma unroll
         for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)v[e];
-        *reinterpret_cast<uint2*>(g.out_bf16 + o) = make_uint2(b.u.x, b.u.y);
+        epi_store(reinterpret_cast<uint2*>(g.out_bf16 + o), make_uint2(b.u.x, b.u.y), g.flags);
       }
       if (!accum && g.aux_pre) {
         Bf8 b;
 #pragma unroll
         for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)pre[e];
-        *reinterpret_cast<uint2*>(g.aux_pre + o) = make_uint2(b.u.x, b.u.y);
+        epi_store(reinterpret_cast<uint2*>(g.aux_pre + o), make_uint2(b.u.x, b.u.y), g.flags);
       }
     } else {
 #pragma unroll
@@ -650,7 +678,10 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias4[e] = n + e < g.N ? g.bias[n + e] : 0.f;
   }
-#pragma unroll
+  const bool in = (g.flags & (EPI_RESID | EPI_DGELU)) || (accum && !split);
+  // ROLLED over the two 64-row passes (the half of acc staged is a select, not an index): one copy of the row-out
+  // code, whose first run streams it into the instruction cache of every CU at once (~half the epilogue, r4 probe)
+#pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii)
@@ -658,24 +689,25 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          stage[(16 * ii + 4 * (lane >> 4) + r) * EPI_ROW + 16 * j + (lane & 15)] = g.alpha * acc[4 * pass + ii][j][r];
+          stage[(16 * ii + 4 * (lane >> 4) + r) * EPI_ROW + 16 * j + (lane & 15)] =
+              g.alpha * (pass ? acc[4 + ii][j][r] : acc[ii][j][r]);
     // the asm reads below are invisible to hipcc: order them behind the staging writes
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    big_rows_out(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
+    if (in) big_rows_out<true>(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
+    else big_rows_out<false>(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
   }
 }
 
+// One (tile, k-range) segment's main loop: acc = A[m0 .. +256][kbeg .. kbeg + 32 nk) B[n0 .. +256][same k]^T for this
+// wave's 128 x 64 slice; rowsum (want_rowsum) = row sums of this wave's A rows over the segment (bias gradients).
+// Ends with both wave rows aligned at a barrier, every DMA retired: the ring is free for the epilogue's staging.
 template <bool AT, bool BT>
-__device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
+__device__ __forceinline__ void mainloop(const GemmArgs& g, const int m0, const int n0, const int kbeg, const int nk,
+                                         const bool want_rowsum, char* lds, f32x4 (&acc)[8][4], float (&rowsum)[8]) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const bool row1 = wm == 1;
-  const int m0 = by * TM, n0 = bx * TN;
-  const int kbeg = bz * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = (kend - kbeg) / KT;
-  if (nk <= 0) return;
 
   const __bf16* sa[2];
   const __bf16* sb[2];
@@ -691,13 +723,10 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
     dma16(sb[1] + ob, slot + OP_BYTES + (wave + 8) * 1024);
   };
 
-  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
-  float rowsum[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) rowsum[i] = 0.f;
 
@@ -779,27 +808,61 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 #ifdef MTA_GEMM_STAMPS
   GSTAMP(tloop1);
   GACC(6, tloop0, tloop1);
-#endif
-
-  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
-               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
-  if (want_rowsum) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float s = rowsum[i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      const int m = m0 + wm * 128 + 16 * i + (lane & 15);
-      if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
-    }
-  }
-#ifdef MTA_GEMM_STAMPS
-  GSTAMP(tend);
-  GACC(7, tloop1, tend);  // epilogue
   if (lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
+    for (int i = 0; i < 7; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
 #endif
 }
+
+// bias gradient of the weight-gradient form: += this wave's row sums (f32 atomics, one per row and segment)
+__device__ __forceinline__ void flush_rowsum(const GemmArgs& g, const float (&rowsum)[8], const int mrow0,
+                                             const int lane) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float s = rowsum[i];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    const int m = mrow0 + 16 * i + (lane & 15);
+    if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
+  }
+}
+
+template <bool AT, bool BT>
+__device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int m0 = by * TM, n0 = bx * TN;
+  const int kbeg = bz * g.k_per_split;
+  const int kend = min(g.K, kbeg + g.k_per_split);
+  const int nk = (kend - kbeg) / KT;
+  if (nk <= 0) return;
+  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
+  f32x4 acc[8][4];
+  float rowsum[8];
+  mainloop<AT, BT>(g, m0, n0, kbeg, nk, want_rowsum, lds, acc, rowsum);
+#ifdef MTA_GEMM_STAMPS
+  GSTAMP(tepi0);
+#endif
+  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
+               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
+#ifdef MTA_EPI_TWICE
+  // probe: the same epilogue again with its code now in the instruction cache (epi_stamp[0] / [1]: first / second)
+  GSTAMP(tepi1);
+  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
+               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
+  GSTAMP(tepi2);
+  if (lane == 0 && wave == 0) {
+    atomicAdd(&epi_stamp[0], (unsigned long long)(tepi1 - tepi0));
+    atomicAdd(&epi_stamp[1], (unsigned long long)(tepi2 - tepi1));
+  }
+#endif
+  if (want_rowsum) flush_rowsum(g, rowsum, m0 + wm * 128, lane);
+#ifdef MTA_GEMM_STAMPS
+  GSTAMP(tend);
+  if (lane == 0) atomicAdd(&stamp_acc[wave][7], (unsigned long long)(unsigned)(tend - tepi0));  // epilogue
+#endif
+}
+
 // ---- 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each), same DMA images / swizzles / transposed reads as above ----
 // For the small weight-gradient products of the transformer (dY^T X: out <= 512 x 512, K = 6,272 tokens), which the
 // register-staged 128-tile path runs latency-bound (~2 us per 128-deep k-step: a transposing load -> LDS -> MFMA
@@ -1059,25 +1122,47 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const __bf16* __res
   }
 }
 
+// Per-(device, stream, slot) workspaces: 0 = weight-grad A^T, 1 = weight-grad B^T, 2 = input-grad B^T, 3 = split-K
+// slabs of the 256 x 256 kernel.  Keyed by stream, so GEMMs issued eagerly on concurrent streams never share a
+// buffer.  Grown outside graph capture only and never freed (a captured graph keeps pointing at the buffer it
+// recorded); a capture stream borrows the smallest fitting buffer of its device (its eager warm-up's).
 struct Workspace {
+  int dev = -1;
+  hipStream_t st = nullptr;
+  int slot = -1;
   void* p = nullptr;
   size_t cap = 0;
 };
-constexpr int WS_MAX_DEVICES = 16;
-Workspace g_ws[WS_MAX_DEVICES][4];  // per device: 0 = weight-grad A^T, 1 = weight-grad B^T, 2 = input-grad B^T,
-                                    // 3 = split-K slabs of the 256 x 256 kernel
+Workspace g_ws[128];
 
 __bf16* workspace(int slot, size_t bytes, hipStream_t st) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WS_MAX_DEVICES) return nullptr;
-  Workspace& w = g_ws[dev][slot];
-  if (bytes <= w.cap) return static_cast<__bf16*>(w.p);
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  Workspace* w = nullptr;
+  for (auto& e : g_ws)
+    if (e.dev == dev && e.st == st && e.slot == slot) { w = &e; break; }
+  if (w && bytes <= w->cap) return static_cast<__bf16*>(w->p);
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+    // no allocation inside a capture: a graph captured on its own stream (torch.cuda.graph) records the buffer its
+    // eager warm-up used -- graph replays and eager steps are ordered on the one compute stream
+    Workspace* best = nullptr;
+    for (auto& e : g_ws)
+      if (e.dev == dev && e.slot == slot && e.cap >= bytes && (!best || e.cap < best->cap)) best = &e;
+    return best ? static_cast<__bf16*>(best->p) : nullptr;
+  }
+  if (!w) {
+    for (auto& e : g_ws)
+      if (e.dev < 0) { w = &e; break; }
+    if (!w) return nullptr;
+  }
   void* p = nullptr;
   if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-  w.p = p;  // the previous buffer is intentionally leaked (graphs may reference it)
-  w.cap = bytes;
+  w->dev = dev;
+  w->st = st;
+  w->slot = slot;
+  w->p = p;  // the previous buffer is intentionally leaked (graphs may reference it)
+  w->cap = bytes;
   return static_cast<__bf16*>(p);
 }
 
@@ -1123,21 +1208,26 @@ inline int tile_config(const GemmArgs& g, int ksplit) {
   return tiles128 >= 256 ? (deep ? 0 : 1) : (deep ? 2 : 3);
 }
 
-template <int BM, int BN, int BKT, bool NN>
+// pair kinds: 0 = two k-contiguous (NN) problems, 1 = (weight gradient, input gradient), 2 = two weight gradients
+template <int BM, int BN, int BKT, int KIND>
 void launch_pair_cfg(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   PairGrid pg{(g1.N + BN - 1) / BN, (g1.M + BM - 1) / BM, k1, (g2.N + BN - 1) / BN, (g2.M + BM - 1) / BM, k2};
   const int blocks = pg.nx1 * pg.ny1 * pg.nz1 + pg.nx2 * pg.ny2 * pg.nz2;
-  if constexpr (NN) gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
-  else gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  if constexpr (KIND == 0)
+    gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  else if constexpr (KIND == 1)
+    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  else
+    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, true, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
 }
 
-template <bool NN>
-void launch_pair_nn(int c, const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
+template <int KIND>
+void launch_pair_kind(int c, const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   switch (c) {
-    case 0: launch_pair_cfg<128, 128, 64, NN>(g1, k1, g2, k2, st); break;
-    case 1: launch_pair_cfg<128, 128, 32, NN>(g1, k1, g2, k2, st); break;
-    case 2: launch_pair_cfg<64, 64, 128, NN>(g1, k1, g2, k2, st); break;
-    default: launch_pair_cfg<64, 64, 32, NN>(g1, k1, g2, k2, st); break;
+    case 0: launch_pair_cfg<128, 128, 64, KIND>(g1, k1, g2, k2, st); break;
+    case 1: launch_pair_cfg<128, 128, 32, KIND>(g1, k1, g2, k2, st); break;
+    case 2: launch_pair_cfg<64, 64, 128, KIND>(g1, k1, g2, k2, st); break;
+    default: launch_pair_cfg<64, 64, 32, KIND>(g1, k1, g2, k2, st); break;
   }
 }
 
@@ -1278,13 +1368,24 @@ bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, h
   const bool nn1 = to_nn(g1, 2, st);
   const bool nn2 = nn1 && to_nn(g2, 1, st);
   if (nn1 && nn2) {
-    launch_pair_nn<true>(c, g1, k1, g2, k2, st);
+    launch_pair_kind<0>(c, g1, k1, g2, k2, st);
   } else if (nn1) {  // workspace for the second operand unavailable (capture): launch the two separately
     dispatch_mode(0, g1, k1, st);
     dispatch_mode(1, g2_in, k2, st);
   } else {
-    launch_pair_nn<false>(c, g1, k1, g2, k2, st);
+    launch_pair_kind<1>(c, g1, k1, g2, k2, st);
   }
+  return true;
+}
+
+// two weight gradients (modes (2, 2), the transformer FFN's dW2 and dW1 after the fused input-gradient launch) in one
+// launch when neither takes the 256 x 256 / 128 x 128 DMA kernels and both have one tile configuration
+bool launch_pair_ww(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
+  if (big_eligible(g1, k1) || big_eligible(g2, k2) || mid_eligible(2, g1) || mid_eligible(2, g2)) return false;
+  if ((long)g1.M * g1.N * g1.K >= (1L << 31) || (long)g2.M * g2.N * g2.K >= (1L << 31)) return false;  // to_nn sizes
+  const int c = tile_config(g1, k1);
+  if (c != tile_config(g2, k2)) return false;
+  launch_pair_kind<2>(c, g1, k1, g2, k2, st);
   return true;
 }
 
@@ -1406,7 +1507,9 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   }
   if (pending.on) {
     pending.on = false;
-    if (!(mode == 1 && pending.st == st && launch_pair(pending.g, pending.ksplit, g, ksplit, st))) {
+    const bool paired = pending.st == st && ((mode == 1 && launch_pair(pending.g, pending.ksplit, g, ksplit, st)) ||
+                                             (mode == 2 && launch_pair_ww(pending.g, pending.ksplit, g, ksplit, st)));
+    if (!paired) {
       dispatch_mode(2, pending.g, pending.ksplit, pending.st);
       dispatch_mode(mode, g, ksplit, st);
     }

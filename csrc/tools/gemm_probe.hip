@@ -80,10 +80,20 @@ int main(int argc, char** argv) {
 #ifdef MTA_GEMM_STAMPS
   unsigned long long zero[8][8] = {};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(big::stamp_acc), zero, sizeof(zero)));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(big::epi_stamp), zero[0], sizeof(zero[0])));
   run();
   CK(hipDeviceSynchronize());
   unsigned long long acc[8][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(big::stamp_acc), sizeof(acc)));
+  unsigned long long ek[8];
+  CK(hipMemcpyFromSymbol(ek, HIP_SYMBOL(big::epi_stamp), sizeof(ek)));
+#ifdef MTA_EPI_TWICE
+  {
+    const int nb = ((M + 255) / 256) * ((N + 255) / 256) * ksplit;
+    printf("epilogue cycles per workgroup (wave 0): first call %.0f, second call %.0f\n", (double)ek[0] / nb,
+           (double)ek[1] / nb);
+  }
+#endif
   const char* mid = getenv("MTA_GEMM_MID");
   const int tile = mid && mid[0] == '1' ? 128 : 256;  // the mid kernel's stamps: [wait lgkm, mfma, wait vm, barrier, dma+reads]
   const int blocks = ((M + tile - 1) / tile) * ((N + tile - 1) / tile) * ksplit;

@@ -1,0 +1,535 @@
+// Fused feed-forward half of the transformer-encoder block (BASELINE.json north-star config 4: d = 128, dff = 512),
+// forward and input-gradient backward, one launch each (the weight gradients stay split-K GEMMs: they reduce over
+// all M tokens).
+//
+// The unfused chain was 3 launches forward (RMSNorm2, FFN-up GEMM + GELU + dropout, FFN-down GEMM + residual) and
+// 3 backward (two paired weight/input-gradient GEMMs, RMSNorm2 backward), each a ~6,000-row problem that is latency
+// bound at 5-19 us per launch (r3 transformer trace).  Here one 512-thread workgroup owns 32 token rows (rows are
+// independent in this half of the block), so M = 6,240 is 195 workgroups, and runs the whole chain with the
+// activations in LDS:
+//   forward : xn2 = RMSNorm(x1) g2 -> pre = xn2 W1^T + b1 -> u = dropout(GELU(pre)) -> x2 = x1 + u W2^T + b2
+//   backward: du = dX W2 -> dpre = du * keep * gelu'(pre) -> dxn2 = dpre W1 -> dX1 = dX + RMSNorm2'(dxn2)
+// Weight operands are streamed from L2 straight into MFMA B-fragment registers (16 B per lane, several k-steps in
+// flight; every wave owns a distinct slice of the output columns, so nothing is shared across waves and no LDS
+// round trip or barrier is needed for them).  Row activations are A fragments read from LDS images with 16-B
+// padded rows (conflict-free ds_read_b128).  Global traffic is staged through LDS into row-contiguous 16-B stores.
+// The backward takes the transposed bf16 weights (W2^T [512][128], W1^T [128][512], written by the forward's cast
+// launch) so that both of its products are k-contiguous too.
+// Dropout: the counter hash of the GEMM epilogues (gemm.hip gemm_pair_hash: pair of rows m >> 1, hidden unit j,
+// 16-bit halves), so the fused and unfused paths draw identical masks.
+// Reference semantics: models/extras.py transformer_reference (pre-norm block), ops/extras.py the unfused chain.
+#include <algorithm>
+
+#include "common.h"
+
+namespace {
+
+constexpr int FD = 128, FF = 512, FBM = 32, FT = 512;  // 8 waves per 32-row workgroup
+constexpr int XLD = FD + 8;    // bf16 row stride of [32][128] images (272 B)
+constexpr int ULD = FF + 8;    // bf16 row stride of [32][512] images (1040 B)
+constexpr int RLD = FD + 4;    // fp32 row stride of [32][128] row images (528 B)
+
+struct FfnFwdSmem {
+  __bf16 xn[FBM * XLD];   // xn2 (A of FFN-up)
+  __bf16 u[FBM * ULD];    // u   (A of FFN-down), then copied out
+  __bf16 pre[FBM * ULD];  // pre-activation, copied out
+  float x[FBM * RLD];     // x1 rows (residual), then x2 staging
+  float b1[FF], b2[FD], g2[FD];
+};
+
+struct FfnBwdSmem {
+  __bf16 dx[FBM * XLD];    // dX (bf16, A of du = dX W2)
+  __bf16 dpre[FBM * ULD];  // dpre (A of dxn2 = dpre W1), then copied out
+  float x[FBM * RLD];      // x1 rows
+  float g[FBM * RLD];      // dxn2 rows, then dX1 staging
+  float g2[FD];
+  float r[FBM];
+};
+
+struct FfnArgs {
+  int M;
+  float eps;
+  const __bf16* w1;   // [512][128]  (backward: W1^T [128][512])
+  const __bf16* w2;   // [128][512]  (backward: W2^T [512][128])
+  const float *b1, *b2, *g2;
+  const float* x1;    // [M][128] fp32
+  const uint64_t* seed;
+  float drop_p;
+  // forward outputs
+  __bf16 *xn2, *pre, *u;
+  float *r2, *x2;
+  // backward inputs / outputs
+  const __bf16* dxb;  // dX as bf16 [M][128] (the weight-gradient operand already made by the previous launch)
+  const float* dx;    // dX fp32 [M][128]
+  const float* r2in;  // [M]
+  const __bf16* prein;
+  __bf16* dpre;       // [M][512]
+  float* dx1;         // [M][128]
+  __bf16* dx1b;       // [M][128]
+  float* dg2;         // [128] += (f32 atomics, one per column and workgroup)
+};
+
+__device__ __forceinline__ uint32_t ffn_pair_hash(uint32_t s, uint32_t mpair, uint32_t n) {
+  const uint32_t b = n * 0x85EBCA77u;  // == gemm.hip gemm_pair_hash
+  uint32_t x = s ^ (mpair * 0x9E3779B1u) ^ ((b << 13) | (b >> 19));
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ bool ffn_keep(uint32_t dseed, uint32_t dthr, int m, int j) {
+  const uint32_t h = ffn_pair_hash(dseed, (uint32_t)m >> 1, (uint32_t)j);
+  const uint32_t u16 = (m & 1) ? (h >> 16) : (h & 0xFFFFu);
+  return u16 >= dthr;
+}
+
+// B fragment of 16 output columns starting at n0, k-chunk k0 .. k0 + 31, from a k-contiguous [N][ldk] bf16 matrix
+__device__ __forceinline__ bf16x8 bfrag(const __bf16* w, int ldk, int n0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + (size_t)(n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+}
+// A fragment of 16 rows starting at r0, k-chunk k0, from an LDS image with row stride ld
+__device__ __forceinline__ bf16x8 afrag(const __bf16* img, int ld, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));
+}
+
+// [32][width] bf16 LDS image -> global rows row0 .. (16-B pieces, row-contiguous)
+template <int WIDTH, int LD>
+__device__ __forceinline__ void copy_out_bf16(const __bf16* img, __bf16* dst, int row0, int M) {
+  constexpr int PER_ROW = WIDTH / 8;
+#pragma unroll
+  for (int i = 0; i < FBM * PER_ROW / FT; ++i) {
+    const int idx = threadIdx.x + FT * i, r = idx / PER_ROW, c = idx % PER_ROW;
+    if (row0 + r < M)
+      *reinterpret_cast<uint4*>(dst + (size_t)(row0 + r) * WIDTH + 8 * c) =
+          *reinterpret_cast<const uint4*>(img + r * LD + 8 * c);
+  }
+}
+// [32][128] fp32 LDS image -> global rows
+__device__ __forceinline__ void copy_out_f32(const float* img, float* dst, int row0, int M) {
+#pragma unroll
+  for (int i = 0; i < FBM * 32 / FT; ++i) {
+    const int idx = threadIdx.x + FT * i, r = idx >> 5, c = idx & 31;
+    if (row0 + r < M)
+      *reinterpret_cast<float4*>(dst + (size_t)(row0 + r) * FD + 4 * c) =
+          *reinterpret_cast<const float4*>(img + r * RLD + 4 * c);
+  }
+}
+
+__global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FfnFwdSmem& s = *reinterpret_cast<FfnFwdSmem*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * FBM;
+  const int rq = 4 * (lane >> 4), col = lane & 15;
+
+  // ---- every load first (one in-order vmcnt covers loads and stores on gfx950) ----
+  // FFN-up B fragments: this wave's 64 hidden units (4 tiles) x 4 k-steps
+  bf16x8 bw[4][4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+  // x1 rows: 16 threads per row, 8 columns each
+  const int xr = tid >> 4, xc = 8 * (tid & 15);
+  const bool rok = row0 + xr < a.M;
+  float4 xv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+  {
+    const float v0 = a.b1[tid];
+    const float v2 = tid < FD ? a.b2[tid] : 0.f, v3 = tid < FD ? a.g2[tid] : 0.f;
+    s.b1[tid] = v0;
+    if (tid < FD) {
+      s.b2[tid] = v2;
+      s.g2[tid] = v3;
+    }
+  }
+  // FFN-down B fragments: this wave's 16 output features x 16 k-steps
+  bf16x8 bd[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag(a.w2, FF, 16 * wave, 32 * ks, lane);
+  uint32_t dseed = 0, dthr = 0;
+  float dscale = 1.f;
+  if (a.seed) {
+    const uint64_t sd = *a.seed;
+    dseed = (uint32_t)(sd ^ (sd >> 32));
+    dthr = (uint32_t)(a.drop_p * 65536.f + 0.5f);
+    dscale = 1.0f / (1.0f - a.drop_p);
+  }
+  __syncthreads();  // g2 / biases in LDS
+
+  // ---- RMSNorm2 ----
+  {
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) q += xv[i].x * xv[i].x + xv[i].y * xv[i].y + xv[i].z * xv[i].z + xv[i].w * xv[i].w;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) q += __shfl_xor(q, off, 64);
+    const float rs = rsqrtf(q * (1.0f / FD) + a.eps);
+    __bf16 yb[8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float e[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) yb[4 * i + k] = (__bf16)(e[k] * rs * s.g2[xc + 4 * i + k]);
+      *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) = xv[i];
+    }
+    uint4 p0;
+    __builtin_memcpy(&p0, yb, 16);
+    *reinterpret_cast<uint4*>(&s.xn[xr * XLD + xc]) = p0;
+    if (rok) {
+      *reinterpret_cast<uint4*>(a.xn2 + (size_t)(row0 + xr) * FD + xc) = p0;
+      if ((tid & 15) == 0) a.r2[row0 + xr] = rs;
+    }
+  }
+  __syncthreads();  // xn2 image complete
+
+  // ---- FFN-up: 32 rows x this wave's 64 hidden units, K = 128 ----
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 a0 = afrag(s.xn, XLD, 0, 32 * ks, lane), a1 = afrag(s.xn, XLD, 16, 32 * ks, lane);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
+      acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
+    }
+  }
+  // bias, GELU, dropout (one hash per pair of rows) -> u and pre images
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int j = 64 * wave + 16 * nt + col;
+      const float bias = s.b1[j];
+      uint32_t hp[2] = {0u, 0u};
+      if (a.seed) {
+        const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
+        hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
+        hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = 16 * mt + rq + r;
+        const float v = acc[mt][nt][r] + bias;
+        float g = mta_gelu(v);
+        if (a.seed) {
+          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+          g *= u16 >= dthr ? dscale : 0.f;
+        }
+        s.pre[lr * ULD + j] = (__bf16)v;
+        s.u[lr * ULD + j] = (__bf16)g;
+      }
+    }
+  __syncthreads();  // u / pre complete
+  copy_out_bf16<FF, ULD>(s.pre, a.pre, row0, a.M);
+  copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M);
+
+  // ---- FFN-down: 32 rows x this wave's 16 output features, K = 512 ----
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const bf16x8 a0 = afrag(s.u, ULD, 0, 32 * ks, lane), a1 = afrag(s.u, ULD, 16, 32 * ks, lane);
+    o[0] = mfma16x16x32(a0, bd[ks], o[0]);
+    o[1] = mfma16x16x32(a1, bd[ks], o[1]);
+  }
+  // x2 = x1 + o + b2 into the x image (each wave its own 16 columns: no cross-wave hazard)
+  {
+    const int n = 16 * wave + col;
+    const float bias = s.b2[n];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = 16 * mt + rq + r;
+        s.x[lr * RLD + n] = (o[mt][r] + bias) + s.x[lr * RLD + n];
+      }
+  }
+  __syncthreads();
+  copy_out_f32(s.x, a.x2, row0, a.M);
+}
+
+__global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  FfnBwdSmem& s = *reinterpret_cast<FfnBwdSmem*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * FBM;
+  const int rq = 4 * (lane >> 4), col = lane & 15;
+
+  // ---- loads: du = dX W2 B fragments (W2^T [512][128]: this wave's 64 hidden units, 4 k-steps); dX (bf16) and
+  // the pre-activation tile into LDS (16-B pieces); x1 and dX rows (fp32, 16 threads per row); r2; g2 ----
+  bf16x8 bw[4][4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag(a.w2, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+  const int xr = tid >> 4, xc = 8 * (tid & 15);
+  const bool rok = row0 + xr < a.M;
+  {
+    const uint4 d0 = rok ? *reinterpret_cast<const uint4*>(a.dxb + (size_t)(row0 + xr) * FD + xc)
+                         : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&s.dx[xr * XLD + xc]) = d0;
+  }
+  // pre tile [32][512] -> the dpre image (the epilogue reads pre and writes dpre at the same element, same lane)
+#pragma unroll
+  for (int i = 0; i < FBM * (FF / 8) / FT; ++i) {
+    const int idx = tid + FT * i, r = idx / (FF / 8), c = idx % (FF / 8);
+    const uint4 v = row0 + r < a.M ? *reinterpret_cast<const uint4*>(a.prein + (size_t)(row0 + r) * FF + 8 * c)
+                                   : make_uint4(0u, 0u, 0u, 0u);
+    *reinterpret_cast<uint4*>(&s.dpre[r * ULD + 8 * c]) = v;
+  }
+  float4 xv[2], gv[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[i] = rok ? *reinterpret_cast<const float4*>(a.dx + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (tid < FD) s.g2[tid] = a.g2[tid];
+  if (tid < FBM) s.r[tid] = row0 + tid < a.M ? a.r2in[row0 + tid] : 0.f;
+  // dxn2 = dpre W1 B fragments (W1^T [128][512]: this wave's 16 features, 16 k-steps)
+  bf16x8 bd[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag(a.w1, FF, 16 * wave, 32 * ks, lane);
+  uint32_t dseed = 0, dthr = 0;
+  float dscale = 1.f;
+  if (a.seed) {
+    const uint64_t sd = *a.seed;
+    dseed = (uint32_t)(sd ^ (sd >> 32));
+    dthr = (uint32_t)(a.drop_p * 65536.f + 0.5f);
+    dscale = 1.0f / (1.0f - a.drop_p);
+  }
+  __syncthreads();  // dX image, pre tile, g2, r2
+
+  // ---- du = dX W2: 32 rows x this wave's 64 hidden units, K = 128 ----
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const bf16x8 a0 = afrag(s.dx, XLD, 0, 32 * ks, lane), a1 = afrag(s.dx, XLD, 16, 32 * ks, lane);
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
+      acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
+    }
+  }
+  // dpre = du * keep / (1 - p) * gelu'(pre), in place over the pre tile
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const int j = 64 * wave + 16 * nt + col;
+      uint32_t hp[2] = {0u, 0u};
+      if (a.seed) {
+        const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
+        hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
+        hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int lr = 16 * mt + rq + r;
+        float v = acc[mt][nt][r];
+        if (a.seed) {
+          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+          v *= u16 >= dthr ? dscale : 0.f;
+        }
+        v *= mta_gelu_grad((float)s.dpre[lr * ULD + j]);
+        s.dpre[lr * ULD + j] = (__bf16)v;
+      }
+    }
+  __syncthreads();  // dpre image complete
+  copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M);
+
+  // ---- dxn2 = dpre W1: 32 rows x this wave's 16 features, K = 512 ----
+  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    const bf16x8 a0 = afrag(s.dpre, ULD, 0, 32 * ks, lane), a1 = afrag(s.dpre, ULD, 16, 32 * ks, lane);
+    o[0] = mfma16x16x32(a0, bd[ks], o[0]);
+    o[1] = mfma16x16x32(a1, bd[ks], o[1]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s.g[(16 * mt + rq + r) * RLD + 16 * wave + col] = o[mt][r];
+  __syncthreads();  // dxn2 rows complete
+
+  // ---- RMSNorm2 backward + residual, 16 threads per row:
+  //   dx1 = dX + r (g2 dy) - x r^3 / d * sum(g2 dy x);  dg2 += dy x r ----
+  {
+    const float r = s.r[xr];
+    float dyv[8], xe[8];
+    float dot = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4 dy4 = *reinterpret_cast<const float4*>(&s.g[xr * RLD + xc + 4 * i]);
+      const float e[4] = {dy4.x, dy4.y, dy4.z, dy4.w};
+      const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        dyv[4 * i + k] = e[k];
+        xe[4 * i + k] = xx[k];
+        dot = fmaf(s.g2[xc + 4 * i + k] * e[k], xx[k], dot);
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
+    const float c = dot * r * r * r * (1.0f / FD);
+    float out[8];
+    __bf16 ob[8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float gd[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * i + k;
+        out[e] = gd[k] + (r * s.g2[xc + e] * dyv[e] - xe[e] * c);
+        ob[e] = (__bf16)out[e];
+      }
+    }
+    __syncthreads();  // every row's dy read before the image is reused for dX1
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<float4*>(&s.g[xr * RLD + xc + 4 * i]) =
+          make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+    if (rok) {
+      uint4 p0;
+      __builtin_memcpy(&p0, ob, 16);
+      *reinterpret_cast<uint4*>(a.dx1b + (size_t)(row0 + xr) * FD + xc) = p0;
+    }
+    // dg2: per-element dy x r into the x image (x is in registers), column sums after the barrier
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) =
+          make_float4(dyv[4 * i] * xe[4 * i] * r, dyv[4 * i + 1] * xe[4 * i + 1] * r,
+                      dyv[4 * i + 2] * xe[4 * i + 2] * r, dyv[4 * i + 3] * xe[4 * i + 3] * r);
+  }
+  __syncthreads();
+  copy_out_f32(s.g, a.dx1, row0, a.M);
+  if (tid < FD) {
+    float cs = 0.f;
+#pragma unroll 8
+    for (int rr = 0; rr < FBM; ++rr) cs += s.x[rr * RLD + tid];
+    atomicAdd(a.dg2 + tid, cs);
+  }
+}
+
+}  // namespace
+
+extern "C" int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, const void* w2,
+                          const float* b1, const float* b2, const float* g2, const float* x1, const uint64_t* seed,
+                          float drop_p, void* xn2, void* pre, void* u, float* r2, float* x2, const void* dxb,
+                          const float* dx, const float* r2in, const void* prein, void* dpre, float* dx1, void* dx1b,
+                          float* dg2, hipStream_t st) {
+  if (d != FD || dff != FF || M < 1) return 1;
+  FfnArgs a{};
+  a.M = M;
+  a.eps = eps;
+  a.w1 = static_cast<const __bf16*>(w1);
+  a.w2 = static_cast<const __bf16*>(w2);
+  a.b1 = b1;
+  a.b2 = b2;
+  a.g2 = g2;
+  a.x1 = x1;
+  a.seed = seed;
+  a.drop_p = drop_p;
+  a.xn2 = static_cast<__bf16*>(xn2);
+  a.pre = static_cast<__bf16*>(pre);
+  a.u = static_cast<__bf16*>(u);
+  a.r2 = r2;
+  a.x2 = x2;
+  a.dxb = static_cast<const __bf16*>(dxb);
+  a.dx = dx;
+  a.r2in = r2in;
+  a.prein = static_cast<const __bf16*>(prein);
+  a.dpre = static_cast<__bf16*>(dpre);
+  a.dx1 = dx1;
+  a.dx1b = static_cast<__bf16*>(dx1b);
+  a.dg2 = dg2;
+  const int grid = (M + FBM - 1) / FBM;
+  if (!backward) {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_ffn_fwd_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)sizeof(FfnFwdSmem)) == hipSuccess;
+    if (!attr) return 2;
+    tr_ffn_fwd_kernel<<<grid, FT, sizeof(FfnFwdSmem), st>>>(a);
+  } else {
+    static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_ffn_bwd_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)sizeof(FfnBwdSmem)) == hipSuccess;
+    if (!attr) return 2;
+    tr_ffn_bwd_kernel<<<grid, FT, sizeof(FfnBwdSmem), st>>>(a);
+  }
+  return 0;
+}
+
+// ---- bf16 weight transposes for the backward (W1^T, W2^T of every layer in one launch) ----
+namespace {
+constexpr int WT_MAX = 32;
+struct WtBatch {
+  const __bf16* src[WT_MAX];
+  __bf16* dst[WT_MAX];
+  int rows[WT_MAX], cols[WT_MAX];
+};
+// dst[c][r] = src[r][c]; blockIdx.y = matrix, blockIdx.x = 64 x 64 tile
+__global__ __launch_bounds__(256) void tr_wt_kernel(WtBatch b) {
+  __shared__ __attribute__((aligned(16))) __bf16 t[64][72];
+  const int mi = blockIdx.y, R = b.rows[mi], C = b.cols[mi];
+  const int tiles_c = (C + 63) / 64;
+  if ((int)blockIdx.x >= tiles_c * ((R + 63) / 64)) return;
+  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+  const __bf16* src = b.src[mi];
+  __bf16* dst = b.dst[mi];
+#pragma unroll
+  for (int q = threadIdx.x; q < 512; q += 256) {
+    const int r = q >> 3, ch = q & 7;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (r0 + r < R && c0 + 8 * ch < C) v = *reinterpret_cast<const uint4*>(src + (size_t)(r0 + r) * C + c0 + 8 * ch);
+    *reinterpret_cast<uint4*>(&t[r][8 * ch]) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = threadIdx.x; q < 512; q += 256) {
+    const int c = q >> 3, ch = q & 7;
+    if (c0 + c < C && r0 + 8 * ch < R) {
+      __bf16 o[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = t[8 * ch + i][c];
+      uint4 v;
+      __builtin_memcpy(&v, o, 16);
+      *reinterpret_cast<uint4*>(dst + (size_t)(c0 + c) * R + r0 + 8 * ch) = v;
+    }
+  }
+}
+}  // namespace
+
+// n matrices, src[i] bf16 [rows[i]][cols[i]] (rows, cols multiples of 8) -> dst[i] [cols[i]][rows[i]]
+extern "C" int mta_tr_transpose_bf16(int n, const void* const* src, void* const* dst, const int* rows, const int* cols,
+                                     hipStream_t st) {
+  if (n < 1 || n > WT_MAX) return 1;
+  WtBatch b{};
+  int tiles = 1;
+  for (int i = 0; i < n; ++i) {
+    if (rows[i] % 8 || cols[i] % 8) return 2;
+    b.src[i] = static_cast<const __bf16*>(src[i]);
+    b.dst[i] = static_cast<__bf16*>(dst[i]);
+    b.rows[i] = rows[i];
+    b.cols[i] = cols[i];
+    tiles = std::max(tiles, ((rows[i] + 63) / 64) * ((cols[i] + 63) / 64));
+  }
+  tr_wt_kernel<<<dim3(tiles, n), 256, 0, st>>>(b);
+  return 0;
+}

@@ -381,18 +381,18 @@ def transformer_reference(x: Tensor, params: Sequence[Tensor], num_layers: int, 
     return Fn.rms_norm(h[:, -1], (h.shape[-1],), gf, RMS_EPS)
 
 
-# fused block forward (csrc/transformer.hip) for the config it is built for: opt-in (MTA_TR_FUSED=1).  It replaces
-# 7 launches per block with one but measured 0.777 vs 0.719 ms per transformer B=1 step against the kernel chain
-# (70 us per block: the store-heavy epilogues with one wave per SIMD, profiles/r3_tr_fused_stamps.txt)
-_TR_FUSED = [os.environ.get("MTA_TR_FUSED", "0") == "1"]
+# fused FFN half of the block (csrc/tr_ffn.hip) for d = 128, dff = 512: RMSNorm2 + FFN-up + GELU + dropout + FFN-down +
+# residual in one launch forward, the input-gradient chain + RMSNorm2 backward in one launch backward (its gain gradient
+# through f32 atomics, so deterministic mode keeps the unfused chain).  MTA_TR_FFN=0 keeps the unfused chain (A/B).
+_TR_FFN = [os.environ.get("MTA_TR_FFN", "1") != "0"]
 
 
-def set_transformer_fused(on: bool) -> None:
-    _TR_FUSED[0] = bool(on)
+def set_transformer_ffn_fused(on: bool) -> None:
+    _TR_FFN[0] = bool(on)
 
 
-def _tr_fused_ok(d: int, dff: int, heads: int, T: int) -> bool:
-    return _TR_FUSED[0] and d == 128 and dff == 512 and heads == 4 and 1 <= T <= 64
+def _tr_ffn_ok(d: int, dff: int) -> bool:
+    return _TR_FFN[0] and not _DETERMINISTIC[0] and d == 128 and dff == 512
 
 
 class _TransformerEncoderFn(torch.autograd.Function):
@@ -421,33 +421,13 @@ class _TransformerEncoderFn(torch.autograd.Function):
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
-        fused = _tr_fused_ok(d, mats_b[3].shape[0] if L else 0, heads, T)
+        ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
         for l in range(L):
             base = 2 + nb * l
             g1, bqkv, bo, g2, b1, b2 = (params[base], params[base + 2], params[base + 4], params[base + 5],
                                         params[base + 7], params[base + 9])
             wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
             dff = w1_b.shape[0]
-            if fused:
-                # the whole block in one launch (csrc/transformer.hip), same saved tensors as the chain below
-                xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-                qkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
-                o = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-                xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-                pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
-                u = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
-                x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
-                x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
-                r1 = torch.empty(M, device=dev, dtype=torch.float32)
-                r2 = torch.empty(M, device=dev, dtype=torch.float32)
-                lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
-                C.tr_layer_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, wqkv_b, wo_b, w1_b, w2_b, g1, bqkv, bo, g2, b1,
-                               b2, xn, qkv, o, xn2, pre1, u, x1, x2, r1, r2, lse,
-                               seeds[l:l + 1] if drop else None, float(dropout))
-                saved += [xs, xn, qkv, o, x1, xn2, pre1, u]
-                stats += [r1, lse, r2]
-                xs = x2
-                continue
             xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             r1 = torch.empty(M, device=dev, dtype=torch.float32)
             C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
@@ -461,15 +441,19 @@ class _TransformerEncoderFn(torch.autograd.Function):
             gemm(0, o, wo_b, M, d, d, d, d, flags=EPI_BIAS | EPI_RESID, bias=bo, resid=xs, out_f32=x1)
             xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             r2 = torch.empty(M, device=dev, dtype=torch.float32)
-            C.norm(False, x1, d, M, d, True, RMS_EPS, g2, None, xn2, None, None, r2, None, 0.0, None, None, None,
-                   None, None, None, None)
             pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
             u = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
-            fl = EPI_BIAS | EPI_GELU | (EPI_DROPOUT if drop else 0)
-            gemm(0, xn2, w1_b, M, dff, d, d, d, flags=fl, bias=b1, seed=seeds[l:l + 1] if drop else None,
-                 drop_p=float(dropout), aux_pre=pre1, out_bf16=u)
             x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
-            gemm(0, u, w2_b, M, d, dff, dff, dff, flags=EPI_BIAS | EPI_RESID, bias=b2, resid=x1, out_f32=x2)
+            if ffn:
+                C.tr_ffn_fwd(x1, w1_b, w2_b, b1, b2, g2, RMS_EPS, seeds[l:l + 1] if drop else None, float(dropout),
+                             xn2, r2, pre1, u, x2)
+            else:
+                C.norm(False, x1, d, M, d, True, RMS_EPS, g2, None, xn2, None, None, r2, None, 0.0, None, None, None,
+                       None, None, None, None)
+                fl = EPI_BIAS | EPI_GELU | (EPI_DROPOUT if drop else 0)
+                gemm(0, xn2, w1_b, M, dff, d, d, d, flags=fl, bias=b1, seed=seeds[l:l + 1] if drop else None,
+                     drop_p=float(dropout), aux_pre=pre1, out_bf16=u)
+                gemm(0, u, w2_b, M, d, dff, dff, dff, flags=EPI_BIAS | EPI_RESID, bias=b2, resid=x1, out_f32=x2)
             saved += [xs, xn, qkv, o, x1, xn2, pre1, u]
             stats += [r1, lse, r2]
             xs = x2
@@ -480,7 +464,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                None, None, None, None, None, None, None)
         saved.append(xs)
         stats.append(rf)
-        ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout))
+        ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout), ffn)
         ctx.params, ctx.mats_b, ctx.seeds = params, mats_b, seeds
         if need_grad:
             ctx.save_for_backward(*saved)
@@ -490,7 +474,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, dh):
-        N, Np, T, F, Fp, d, L, heads, drop, p = ctx.meta
+        N, Np, T, F, Fp, d, L, heads, drop, p, ffn = ctx.meta
         params, mats_b = ctx.params, ctx.mats_b
         saved = ctx.saved_tensors
         stats = ctx.stats
@@ -511,6 +495,11 @@ class _TransformerEncoderFn(torch.autograd.Function):
                stats[-1], None, 0.0, dh, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
         dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
         cast_pad([dX], [dXb])
+        if ffn:
+            # W1^T, W2^T of every layer (k-contiguous operands of the fused FFN backward), one launch
+            src = [m for l in range(L) for m in mats_b[3 + 4 * l: 5 + 4 * l]]
+            wt = [torch.empty((m.shape[1], m.shape[0]), device=dev, dtype=torch.bfloat16) for m in src]
+            C.transpose_bf16(src, wt)
         for l in range(L - 1, -1, -1):
             base = 2 + nb * l
             g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
@@ -518,24 +507,34 @@ class _TransformerEncoderFn(torch.autograd.Function):
             dff = w1_b.shape[0]
             xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
             r1, lse, r2 = stats[3 * l: 3 * l + 3]
-            # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
-            gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                 ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)
             dpre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
-            fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
-            gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1, seed=ctx.seeds[l:l + 1] if drop else None,
-                 drop_p=p, out_bf16=dpre1)
-            # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
-            gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                 ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), defer=True)
-            dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
-            gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
-            # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
             dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-            C.norm_defer()  # dgamma: one batched reduction launch at the end of the backward
-            C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None, dX1b,
-                   dX1, _grad_view(g2), None)
+            if ffn:
+                # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
+                # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
+                C.tr_ffn_bwd(x1, wt[2 * l], wt[2 * l + 1], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None, p, dX,
+                             dXb, dpre1, dX1, dX1b, _grad_view(g2))
+                gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
+                gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+            else:
+                # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
+                gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)
+                fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
+                gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1,
+                     seed=ctx.seeds[l:l + 1] if drop else None, drop_p=p, out_bf16=dpre1)
+                # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
+                gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), defer=True)
+                dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
+                gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
+                # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
+                C.norm_defer()  # dgamma: one batched reduction launch at the end of the backward
+                C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None,
+                       dX1b, dX1, _grad_view(g2), None)
             # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
             gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
                  ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), defer=True)

@@ -80,6 +80,16 @@ def _ran_kernel(fn, name):
     return any(name in e.key for e in prof.key_averages())
 
 
+def _ran_big(fn):
+    """The 256 x 256 kernel ran."""
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return any("gemm_big_kernel" in e.key for e in prof.key_averages())
+
+
 # the 256 x 256 LDS-DMA kernel (csrc/gemm.hip, namespace big) in its three operand layouts, on ragged shapes (M, N not
 # multiples of 256, K a multiple of 32 but not of 64, re-split K for the accumulating weight gradient), against an fp32
 # PyTorch product and against the 128-tile path of the same call
@@ -102,7 +112,7 @@ def test_big_tile_gemm(mode, M, N, K):
             out = torch.empty(M, N, device=DEV)
             fn = lambda: X.gemm(0, A, B, M, N, K, K, K, flags=X.EPI_BIAS | X.EPI_GELU | X.EPI_RESID,  # noqa: E731
                                 bias=bias, resid=res, aux_pre=pre, out_f32=out)
-            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _ran_big(fn) == bool(big)
             assert _rel(pre.float(), ref_pre) < 5e-3
             assert _rel(out, Fn.gelu(ref_pre) + res) < 2e-3
             outs.append(out.clone())
@@ -116,7 +126,7 @@ def test_big_tile_gemm(mode, M, N, K):
             C.gemm_set_big(big)
             out = torch.empty(M, N, device=DEV)
             fn = lambda: X.gemm(1, A, B, M, N, K, K, N, flags=X.EPI_DGELU, aux_in=pre, out_f32=out)  # noqa: E731
-            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _ran_big(fn) == bool(big)
             assert _rel(out, ref) < 3e-3
             outs.append(out.clone())
     else:
@@ -129,7 +139,7 @@ def test_big_tile_gemm(mode, M, N, K):
             gb = torch.ones(M, device=DEV)
             fn = lambda: X.gemm(2, A, B, M, N, K, M, N, flags=X.EPI_ACCUM, out_f32=gw, ldc=N, n_store=N,  # noqa: E731
                                 ksplit=X.wgrad_split(M, N, K), bias_grad=gb)
-            assert _ran_kernel(fn, "gemm_big_kernel") == bool(big)
+            assert _ran_big(fn) == bool(big)
             assert _rel(gw - 1, ref) < 2e-3
             assert _rel(gb - 1, A.float().sum(0)) < 2e-3
             outs.append(gw.clone())
@@ -278,10 +288,11 @@ def test_transformer_encoder_matches_fp32_reference():
 
 
 @pytest.mark.parametrize("dropout,N", [(0.0, 100), (0.2, 37)])
-def test_fused_transformer_block_matches_unfused(dropout, N):
-    """csrc/transformer.hip (one launch per block) against the 7-launch kernel chain on the same inputs, seeds and
-    weights: encoder output and every parameter gradient (the backward consumes the fused forward's saved
-    tensors), plus the fp32 PyTorch reference without dropout."""
+def test_fused_transformer_ffn_matches_unfused(dropout, N):
+    """csrc/tr_ffn.hip (the FFN half of every block in one launch forward and one backward, plus split-K weight
+    gradients) against the unfused kernel chain on the same inputs, seeds and weights: encoder output and every
+    parameter gradient, plus the fp32 PyTorch reference without dropout.  N = 37: M = 40 x 60 rows, a partial
+    32-row workgroup at the end."""
     from masters_thesis_amd.models.extras import FinancialTransformerMse
     from masters_thesis_amd.ops import extras as X
 
@@ -292,9 +303,12 @@ def test_fused_transformer_block_matches_unfused(dropout, N):
     x = torch.randn(N, 60, 3, device=DEV)
     seeds0 = torch.randint(0, 2 ** 62, (8,), device=DEV, dtype=torch.int64)
     outs, grads = [], []
+    prev = X._TR_FFN[0]
     try:
         for fused in (True, False):
-            X.set_transformer_fused(fused)
+            X.set_transformer_ffn_fused(fused)
+            assert _ran_kernel(lambda: X.transformer_encode(x, params, seeds0.clone(), 2, 4, dropout, False),
+                               "tr_ffn_fwd_kernel") == fused
             for p in params:
                 p.grad = None
             seeds = seeds0.clone()
@@ -304,7 +318,7 @@ def test_fused_transformer_block_matches_unfused(dropout, N):
             outs.append(h.detach().clone())
             grads.append([p.grad.detach().clone() for p in params])
     finally:
-        X.set_transformer_fused(False)
+        X.set_transformer_ffn_fused(prev)
     assert _rel(outs[0], outs[1]) < 2e-3
     for a, b in zip(*grads):
         assert _rel(a, b) < 5e-3
