@@ -55,7 +55,10 @@ void mta_grad_sqnorm(const float* g, long n, float scale, float* partials, float
 int mta_adam_fused_partials();
 void mta_adam_fused(float* p, float* g, float* m, float* v, long n, float* partials, unsigned long long* ticket,
                     const float* lr, float* step, float beta1, float beta2, float eps, float wd, float max_norm,
-                    float scale, int adamw, int zero_grad, float* norm_out, float* nonfinite, hipStream_t st);
+                    float scale, int adamw, int zero_grad, float* norm_out, float* nonfinite, int n_cov,
+                    const long* cov_s, const long* cov_e, const float* ext, int n_ext, hipStream_t st);
+void mta_gemm_grad_producer(float* norm_parts, int overwrite);
+int mta_gemm_norm_parts();
 void mta_adam(float* p, float* g, float* m, float* v, long n, const float* partials, const float* lr,
               const float* step, float beta1, float beta2, float eps, float wd, float max_norm, float scale, int adamw,
               float* norm_out, float* nonfinite, hipStream_t st);
@@ -81,6 +84,9 @@ int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, c
                const float* b2, const float* g2, const float* x1, const uint64_t* seed, float drop_p, void* xn2,
                void* pre, void* u, float* r2, float* x2, const void* dxb, const float* dx, const float* r2in,
                const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, hipStream_t st);
+int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo, const float* g1,
+                    const float* bqkv, const float* bo, const float* rope, float eps, void* xn, float* r1, void* qkv,
+                    void* o, float* lse, float* x1, hipStream_t st);
 int mta_tr_transpose_bf16(int n, const void* const* src, void* const* dst, const int* rows, const int* cols,
                           hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
@@ -469,7 +475,8 @@ int64_t adam_fused_partials() { return mta_adam_fused_partials(); }
 // one launch: grad norm + clip + Adam/AdamW (+ grad zeroing); ticket is an int64[1] zero-initialised once
 void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor partials, at::Tensor ticket,
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd, double max_norm,
-                double scale, bool adamw, bool zero_grad, const OptT& norm_out, const OptT& nonfinite) {
+                double scale, bool adamw, bool zero_grad, const OptT& norm_out, const OptT& nonfinite,
+                std::vector<int64_t> cov_s, std::vector<int64_t> cov_e, const OptT& ext) {
   MTA_CHECK_F32(p);
   MTA_CHECK_F32(g);
   MTA_CHECK_F32(m);
@@ -482,12 +489,31 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
   TORCH_CHECK(!has(nonfinite) || nonfinite->numel() >= 2, "nonfinite needs 2 floats");
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "flat buffer size mismatch");
+  TORCH_CHECK(cov_s.size() == cov_e.size() && cov_s.size() <= 8, "adam_fused: at most 8 covered ranges");
+  for (size_t k = 0; k < cov_s.size(); ++k)
+    TORCH_CHECK(0 <= cov_s[k] && cov_s[k] <= cov_e[k] && cov_e[k] <= n / 4, "adam_fused: covered range out of bounds");
+  TORCH_CHECK(cov_s.empty() || has(ext), "adam_fused: covered ranges need their producer partials");
+  if (has(ext)) MTA_CHECK_F32(*ext);
+  std::vector<long> cs(cov_s.begin(), cov_s.end()), ce(cov_e.begin(), cov_e.end());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   mta_adam_fused(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (long)n,
                  partials.data_ptr<float>(), reinterpret_cast<unsigned long long*>(ticket.data_ptr<int64_t>()),
                  lr.data_ptr<float>(), step.data_ptr<float>(), (float)beta1, (float)beta2, (float)eps, (float)wd,
                  (float)max_norm, (float)scale, adamw ? 1 : 0, zero_grad ? 1 : 0, opt_mut(norm_out),
-                 opt_mut(nonfinite), cur_stream());
+                 opt_mut(nonfinite), (int)cs.size(), cs.data(), ce.data(),
+                 has(ext) ? ext->data_ptr<float>() : nullptr,
+                 has(ext) ? (int)std::min<int64_t>(ext->numel(), (int64_t)cs.size() * mta_gemm_norm_parts()) : 0,
+                 cur_stream());
+}
+
+// the next weight-gradient GEMM overwrites its output (no += onto a range the optimizer did not zero) and writes the
+// clip-norm partials of it into parts[0 .. gemm_norm_parts())
+void gemm_grad_producer(const OptT& parts, bool overwrite) {
+  if (has(parts)) {
+    MTA_CHECK_F32(*parts);
+    TORCH_CHECK(parts->numel() >= mta_gemm_norm_parts(), "gemm_grad_producer: parts too small");
+  }
+  mta_gemm_grad_producer(has(parts) ? parts->data_ptr<float>() : nullptr, overwrite ? 1 : 0);
 }
 
 void scale_(at::Tensor x, double s) {
@@ -695,6 +721,31 @@ void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at
                             dx.data_ptr<float>(), r2.data_ptr<float>(), pre.data_ptr(), dpre.data_ptr(),
                             dx1.data_ptr<float>(), dx1b.data_ptr(), dg2.data_ptr<float>(), cur_stream());
   TORCH_CHECK(rc == 0, "tr_ffn_bwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
+}
+
+// fused attention half of a transformer block forward (csrc/tr_attn.hip): x -> xn, r1, qkv, o, lse, x1
+void tr_attn_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope_base, at::Tensor x, at::Tensor wqkv,
+                 at::Tensor wo, at::Tensor g1, at::Tensor bqkv, at::Tensor bo, at::Tensor xn, at::Tensor r1,
+                 at::Tensor qkv, at::Tensor o, at::Tensor lse, at::Tensor x1) {
+  const int64_t d = x.size(-1), M = nseq * T;
+  for (auto* t : {&x, &r1, &lse, &x1, &g1, &bqkv, &bo}) {
+    MTA_CHECK_F32(*t);
+  }
+  for (auto* t : {&wqkv, &wo, &xn, &qkv, &o}) {
+    MTA_CHECK_GPU(*t, at::kBFloat16);
+  }
+  TORCH_CHECK(wqkv.size(0) == 3 * d && wqkv.size(1) == d && wo.size(0) == d && wo.size(1) == d,
+              "tr_attn_fwd: weight shapes");
+  TORCH_CHECK(x.numel() >= M * d && x1.numel() >= M * d && xn.numel() >= M * d && o.numel() >= M * d &&
+                  qkv.numel() >= M * 3 * d && r1.numel() >= M && lse.numel() >= nseq * heads * 64,
+              "tr_attn_fwd: sizes");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int rc = mta_tr_attn_fwd((int)nseq, (int)T, (int)d, (int)heads, x.data_ptr<float>(), wqkv.data_ptr(),
+                                 wo.data_ptr(), g1.data_ptr<float>(), bqkv.data_ptr<float>(), bo.data_ptr<float>(),
+                                 rope_table(x.device(), T, d / heads, rope_base), (float)eps, xn.data_ptr(),
+                                 r1.data_ptr<float>(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
+                                 x1.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "tr_attn_fwd: unsupported configuration (d=", d, ", heads=", heads, ", T=", T, ", rc=", rc, ")");
 }
 
 // dst[i] = src[i]^T for bf16 matrices (one launch)
@@ -1096,6 +1147,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tr_ffn_fwd", &tr_ffn_fwd);
   m.def("tr_ffn_bwd", &tr_ffn_bwd);
   m.def("transpose_bf16", &transpose_bf16);
+  m.def("tr_attn_fwd", &tr_attn_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("gemm_set_mid", [](int64_t on) { mta_gemm_set_mid((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
@@ -1132,6 +1184,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("heads_losses_train", &heads_losses_train);
   m.def("adam_fused_partials", &adam_fused_partials);
   m.def("adam_fused", &adam_fused);
+  m.def("gemm_grad_producer", &gemm_grad_producer);
+  m.def("gemm_norm_parts", []() { return (int64_t)mta_gemm_norm_parts(); });
   m.def("scale_", &scale_);
   m.attr("ARCH") = "gfx950";
 }

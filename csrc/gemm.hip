@@ -21,6 +21,8 @@
 
 #include <algorithm>
 
+extern "C" void mta_zero_bytes(void* dst, long bytes, hipStream_t st);  // optim.hip
+
 namespace {
 
 constexpr int GT = 256;  // threads per workgroup
@@ -50,7 +52,11 @@ struct GemmArgs {
   int k_per_split;          // multiple of BK
   float* bias_grad;         // AT mode: += row sums of A over K  ([M])
   float* slab;              // split-K partials of the 256 x 256 kernel: [split][M][N] fp32 (null: f32 atomics)
+  float* norm_parts;        // gradient producer: NORM_PARTS per-block sums of squares of the written output
+  int overwrite;            // gradient producer: output = product (not += ), the optimizer left the range dirty
 };
+// per-block partials a gradient-producing GEMM writes for the fused optimizer's clip norm (optim.hip ext_parts)
+constexpr int NORM_PARTS = 1024;
 
 
 __device__ __forceinline__ uint4 and_mask(uint4 v, bool keep) {
@@ -1000,12 +1006,17 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 }  // namespace big
 
 
-// out[m][n] += sum over the splits of slab[z][m][n] (n < n_store), 4 columns per thread
+// out[m][n] (+)= sum over the splits of slab[z][m][n] (n < n_store), 4 columns per thread.  overwrite: out = sum (a
+// gradient producer whose range the optimizer did not zero); norm_parts: every block's sum of squares of what it
+// wrote (grid = NORM_PARTS blocks then), the clip norm's share of this range without another pass over it
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ out, int ldc, int n_store, int M, int N,
-                                                            const float* __restrict__ slab, int splits) {
+                                                            const float* __restrict__ slab, int splits, int overwrite,
+                                                            float* __restrict__ norm_parts) {
+  __shared__ float scratch[4];
   const int n4 = N >> 2;
   const long total = (long)M * n4;
   const size_t plane = (size_t)M * N;
+  float sq = 0.f;
   for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
     const int m = (int)(e / n4), n = (int)(e - (long)m * n4) * 4;
     float4 s = *reinterpret_cast<const float4*>(slab + (size_t)m * N + n);
@@ -1020,8 +1031,26 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(float* __restrict__ 
     const float v[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (n + k < n_store) o[k] += v[k];
+      if (n + k < n_store) {
+        const float r = overwrite ? v[k] : o[k] + v[k];
+        o[k] = r;
+        sq = fmaf(r, r, sq);
+      }
   }
+  if (norm_parts) {
+    sq = block_sum(sq, scratch);
+    if (threadIdx.x == 0) norm_parts[blockIdx.x] = sq;
+  }
+}
+
+// norm partials of a contiguous fp32 range (gradient producers that did not take the slab path)
+__global__ __launch_bounds__(256) void sumsq_parts_kernel(const float* __restrict__ x, long n, float* __restrict__ parts) {
+  __shared__ float scratch[4];
+  float sq = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    sq = fmaf(x[i], x[i], sq);
+  sq = block_sum(sq, scratch);
+  if (threadIdx.x == 0) parts[blockIdx.x] = sq;
 }
 
 template <bool AT, bool BT>
@@ -1270,8 +1299,9 @@ void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
   gemm_big_kernel<AT, BT><<<nx * ny * ksplit, big::THREADS, big::LDS_BYTES, st>>>(ga, nx, ny, ksplit);
   if (ga.slab) {
     const long work = (long)g.M * (g.N / 4);
-    const int blocks = (int)std::min<long>(4096, (work + 255) / 256);
-    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(g.out_f32, g.ldc, g.n_store, g.M, g.N, ga.slab, ksplit);
+    const int blocks = g.norm_parts ? NORM_PARTS : (int)std::min<long>(4096, (work + 255) / 256);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(g.out_f32, g.ldc, g.n_store, g.M, g.N, ga.slab, ksplit, g.overwrite,
+                                                 g.norm_parts);
   }
 }
 
@@ -1456,6 +1486,23 @@ extern "C" void mta_gemm_flush() {
 
 namespace {
 
+// gradient-producer request for the NEXT weight-gradient call (mta_gemm_grad_producer): overwrite its output range
+// and / or write the clip-norm partials of it (the fused optimizer then neither zeroes nor re-reads that range)
+struct ProducerReq {
+  float* norm_parts = nullptr;
+  bool overwrite = false;
+} g_producer;
+
+// whether dispatch_mode(2, g, ksplit) runs the 256 x 256 kernel with fp32 slabs (whose reduce launch overwrites and
+// writes the partials itself)
+bool slab_path(const GemmArgs& g_in, int ksplit, hipStream_t st) {
+  if (!(g_in.flags & EPI_ACCUM) || !slabs_on()) return false;
+  GemmArgs g = g_in;
+  const int ks = big_split(g, ksplit);
+  if (ks <= 1) return false;
+  return workspace(3, (size_t)ks * g.M * g.N * sizeof(float), st) != nullptr;
+}
+
 // mode: 0 = NN-linear forward (AT=0,BT=0), 1 = input grad (AT=0,BT=1), 2 = weight grad (AT=1,BT=1)
 int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, int lda, int ldb,
                    float alpha, int flags, const float* bias, const float* resid, const void* aux_in,
@@ -1495,6 +1542,22 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   g.k_per_split = kps;
   g.bias_grad = bias_grad;
   if (mode < 0 || mode > 2) return 4;
+  const ProducerReq req = g_producer;
+  g_producer = ProducerReq{};
+  if (req.norm_parts || req.overwrite) {
+    if (mode != 2 || defer || ldc != n_store || !(flags & EPI_ACCUM)) return 10;
+    mta_gemm_flush();
+    if (slab_path(g, ksplit, st)) {
+      g.norm_parts = req.norm_parts;
+      g.overwrite = req.overwrite ? 1 : 0;
+      dispatch_mode(2, g, ksplit, st);
+    } else {
+      if (req.overwrite) mta_zero_bytes(out_f32, (long)M * ldc * (long)sizeof(float), st);
+      dispatch_mode(2, g, ksplit, st);
+      if (req.norm_parts) sumsq_parts_kernel<<<NORM_PARTS, 256, 0, st>>>(out_f32, (long)M * ldc, req.norm_parts);
+    }
+    return 0;
+  }
   if (defer) {
     // a weight-gradient GEMM held back for the next call (its input-gradient partner): one paired launch
     if (mode != 2) return 8;
@@ -1528,3 +1591,9 @@ extern "C" int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int 
   return gemm_bf16_impl(mode, A, B, M, N, K, lda, ldb, alpha, flags, bias, resid, aux_in, seed, drop_p, out_bf16,
                         out_f32, aux_pre, ldc, n_store, ksplit, bias_grad, defer, st);
 }
+
+extern "C" void mta_gemm_grad_producer(float* norm_parts, int overwrite) {
+  g_producer.norm_parts = norm_parts;
+  g_producer.overwrite = overwrite != 0;
+}
+extern "C" int mta_gemm_norm_parts() { return NORM_PARTS; }

@@ -112,6 +112,24 @@ inline unsigned fused_spin_limit() {
 // ~9 us launch for the 51K-parameter headline model)
 constexpr int REG_N = 4;
 
+// Gradient ranges whose producer (a weight-gradient GEMM's split-K reduce, gemm.hip mta_gemm_grad_producer) wrote
+// them by overwriting and left the clip-norm partials of them: phase 1 skips them (their squares come from ext, added
+// by workgroup b in a fixed order: deterministic), and with zero_grad they are not zeroed (the next step's producer
+// overwrites them again).  [s, e) in float4 units.
+constexpr int MAX_COVERED = 8;
+struct Covered {
+  int n;
+  long s[MAX_COVERED], e[MAX_COVERED];
+  const float* ext;  // producer partials
+  int n_ext;
+};
+__device__ __forceinline__ bool covered(const Covered& c, long i) {
+  bool in = false;
+#pragma unroll
+  for (int k = 0; k < MAX_COVERED; ++k) in |= (k < c.n) & (i >= c.s[k]) & (i < c.e[k]);
+  return in;
+}
+
 template <bool REG>
 __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v, long n4,
@@ -121,7 +139,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
                                                          float beta1, float beta2, float eps, float wd,
                                                          float max_norm, float scale, int adamw, int zero_grad,
                                                          float* __restrict__ norm_out, float* __restrict__ nonfinite,
-                                                         unsigned spin_limit) {
+                                                         unsigned spin_limit, Covered cov) {
   __shared__ float scratch[TPB / 64];
   __shared__ float s_norm;
   const long stride = (long)gridDim.x * TPB;
@@ -142,6 +160,8 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
 #pragma unroll
     for (int r = 0; r < REG_N; ++r) {
+      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      if (cov.n && covered(cov, i)) continue;
       acc = fmaf(rg[r].x, rg[r].x, acc);
       acc = fmaf(rg[r].y, rg[r].y, acc);
       acc = fmaf(rg[r].z, rg[r].z, acc);
@@ -149,6 +169,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
   } else {
     for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
+      if (cov.n && covered(cov, i)) continue;
       const float4 q = g[i];
       acc = fmaf(q.x, q.x, acc);
       acc = fmaf(q.y, q.y, acc);
@@ -156,6 +177,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
       acc = fmaf(q.w, q.w, acc);
     }
   }
+  for (int k = blockIdx.x * TPB + threadIdx.x; k < cov.n_ext; k += gridDim.x * TPB) acc += cov.ext[k];
   acc = block_sum(acc, scratch) * (scale * scale);
   // the step counter is read by every workgroup BEFORE it arrives (thread 0 loads it and its vmcnt(0) below
   // completes the load before the ticket add; the workgroup reads it from LDS); the last arriver advances it
@@ -228,7 +250,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
         pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
       }
       p[i] = pp;
-      g[i] = gg;
+      if (!(zero_grad && cov.n && covered(cov, i))) g[i] = gg;
       m[i] = mm;
       v[i] = vv;
     }
@@ -251,7 +273,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
       pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
     }
     p[i] = pp;
-    g[i] = gg;
+    if (!(zero_grad && cov.n && covered(cov, i))) g[i] = gg;
     m[i] = mm;
     v[i] = vv;
   }
@@ -342,20 +364,30 @@ extern "C" int mta_adam_fused_partials() { return FUSED_MAX_BLOCKS; }
 
 // ticket: one zero-initialised uint64 per optimizer (monotonic across launches); nonfinite: 2 floats
 // ([0] steps with a non-finite norm, [1] arrival waits that gave up)
+// covered: n_cov float4 ranges [cov_s[k], cov_e[k]) written by gradient producers, ext: their n_ext norm partials
 extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, float* partials,
                                unsigned long long* ticket, const float* lr, float* step, float beta1, float beta2,
                                float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
-                               float* norm_out, float* nonfinite, hipStream_t st) {
+                               float* norm_out, float* nonfinite, int n_cov, const long* cov_s, const long* cov_e,
+                               const float* ext, int n_ext, hipStream_t st) {
   const long n4 = n / 4;
   const unsigned spin = fused_spin_limit();
+  Covered cov{};
+  cov.n = (n_cov < 0 || n_cov > MAX_COVERED) ? 0 : n_cov;  // more ranges than fit: none skipped, ext unused
+  for (int k = 0; k < cov.n; ++k) {
+    cov.s[k] = cov_s[k];
+    cov.e[k] = cov_e[k];
+  }
+  cov.ext = ext;
+  cov.n_ext = cov.n ? n_ext : 0;
   if (fused_reg(n4))
     adam_fused_kernel<true><<<fused_grid_reg(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-        zero_grad, norm_out, nonfinite, spin);
+        zero_grad, norm_out, nonfinite, spin, cov);
   else
     adam_fused_kernel<false><<<fused_grid(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
-        zero_grad, norm_out, nonfinite, spin);
+        zero_grad, norm_out, nonfinite, spin, cov);
 }

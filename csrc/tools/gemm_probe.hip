@@ -9,6 +9,9 @@
 #include <cstdlib>
 #include <vector>
 
+// the extension links optim.hip's zero-fill; the probe never requests a gradient-producer overwrite
+extern "C" void mta_zero_bytes(void*, long, hipStream_t) {}
+
 #define CK(x)                                                                   \
   do {                                                                          \
     hipError_t e = (x);                                                         \

@@ -1,0 +1,288 @@
+// Fused attention half of the transformer-encoder block forward (BASELINE.json north-star config 4: d = 128, 4 heads
+// of 32, T <= 64 tokens per sequence), one launch per block:
+//   xn = RMSNorm1(x) g1 -> qkv = xn Wqkv^T + bqkv -> RoPE(q) / sqrt(32), RoPE(k) -> softmax(q k^T, keys >= T masked) v
+//   -> x1 = x + o Wo^T + bo
+// The unfused chain was 4 launches (RMSNorm, QKV GEMM, attention, projection GEMM + residual; 4.8 + 8.6 + 7.0 + 8.6 us
+// per block in the r4 trace).  One 512-thread workgroup owns one sequence (64 padded token rows) and keeps q, k, V^T,
+// P and o in LDS; the weights stream from L2 straight into MFMA B-fragment registers (every wave owns distinct output
+// columns: 48 of the 384 QKV features, 16 of the 128 projection features).  Attention: wave w runs head w / 2 for
+// query tiles 2 (w % 2) and 2 (w % 2) + 1 (its own P rows: no barrier between scores and P V).
+// Writes exactly what the unfused forward saves for the backward: xn, r1, qkv (UNROTATED, bias added, bf16), o, LSE,
+// x1 -- staged through LDS into row-contiguous 16-B stores.
+// Reference semantics: models/extras.py transformer_reference; ops/extras.py the unfused chain; csrc/attention.hip.
+#include "common.h"
+
+namespace {
+
+constexpr int AD = 128, AQ = 384, AHD = 32, AHEADS = 4, AT = 64, ATH = 512;
+constexpr int BLD = AD + 8;   // bf16 [64][128] images
+constexpr int QLD = AQ + 8;   // bf16 [64][384] staging
+constexpr int VLD = AT + 8;   // bf16 [.][64] images (V^T, P)
+constexpr int XLDF = AD + 4;  // fp32 [64][128] image
+
+struct AttnFwdSmem {
+  __bf16 xo[AT * BLD];          // xn (A of QKV), then o (A of the projection)
+  __bf16 q[AT * BLD], k[AT * BLD];
+  __bf16 vt[AD * VLD];
+  union {
+    __bf16 qkv[AT * QLD];       // qkv staging (copied out)
+    __bf16 p[8][32 * VLD];      // per-wave P rows
+    float x[AT * XLDF];         // x rows for the residual, then x1 staging
+  } u;
+  float2 rope[AT * (AHD / 2)];
+  float g1[AD], bqkv[AQ], bo[AD];
+};
+
+struct AttnFwdArgs {
+  const float* x;       // [M][128] block input (rows seq * T + t)
+  const __bf16* wqkv;   // [384][128]
+  const __bf16* wo;     // [128][128]
+  const float *g1, *bqkv, *bo;
+  const float* rope;    // [T][16] (cos, sin)
+  float eps;
+  int T;
+  __bf16 *xn, *qkv, *o;
+  float *r1, *lse, *x1;
+};
+
+__device__ __forceinline__ bf16x8 wfrag(const __bf16* w, int ldk, int n0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + (size_t)(n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+}
+__device__ __forceinline__ bf16x8 lfrag(const __bf16* img, int ld, int r0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));
+}
+
+__global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  AttnFwdSmem& s = *reinterpret_cast<AttnFwdSmem*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int seq = blockIdx.x, T = a.T;
+  const size_t grow0 = (size_t)seq * T;
+  const int rq = 4 * (lane >> 4), col = lane & 15;
+
+  // ---- loads: QKV B fragments (this wave's 48 features x 4 k-steps), projection B fragments (16 features), x rows
+  // (8 threads per row, 16 columns each), parameters and the RoPE table ----
+  bf16x8 bq[4][3], bp[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) bq[ks][nt] = wfrag(a.wqkv, AD, 48 * wave + 16 * nt, 32 * ks, lane);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) bp[ks] = wfrag(a.wo, AD, 16 * wave, 32 * ks, lane);
+  const int xr = tid >> 3, xc = 16 * (tid & 7);
+  const bool rok = xr < T;
+  float4 xv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x + (grow0 + xr) * AD + xc + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (tid < AD) {
+    s.g1[tid] = a.g1[tid];
+    s.bo[tid] = a.bo[tid];
+  }
+  if (tid < AQ) s.bqkv[tid] = a.bqkv[tid];
+#pragma unroll
+  for (int i = tid; i < AT * (AHD / 2); i += ATH) {
+    const int t = i / (AHD / 2);
+    s.rope[i] = t < T ? reinterpret_cast<const float2*>(a.rope)[i] : make_float2(1.f, 0.f);
+  }
+  __syncthreads();
+
+  // ---- RMSNorm1 -> xn image, xn / r1 out ----
+  {
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q += xv[i].x * xv[i].x + xv[i].y * xv[i].y + xv[i].z * xv[i].z + xv[i].w * xv[i].w;
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    q += __shfl_xor(q, 4, 64);
+    const float rs = rsqrtf(q * (1.0f / AD) + a.eps);
+    __bf16 yb[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) yb[4 * i + kk] = (__bf16)(e[kk] * rs * s.g1[xc + 4 * i + kk]);
+    }
+    uint4 p0, p1;
+    __builtin_memcpy(&p0, yb, 16);
+    __builtin_memcpy(&p1, yb + 8, 16);
+    *reinterpret_cast<uint4*>(&s.xo[xr * BLD + xc]) = p0;
+    *reinterpret_cast<uint4*>(&s.xo[xr * BLD + xc + 8]) = p1;
+    if (rok) {
+      *reinterpret_cast<uint4*>(a.xn + (grow0 + xr) * AD + xc) = p0;
+      *reinterpret_cast<uint4*>(a.xn + (grow0 + xr) * AD + xc + 8) = p1;
+      if ((tid & 7) == 0) a.r1[grow0 + xr] = rs;
+    }
+  }
+  __syncthreads();
+
+  // ---- QKV: 64 rows x this wave's 48 features, K = 128 ----
+  f32x4 acc[4][3];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bf16x8 af[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) af[mt] = lfrag(s.xo, BLD, 16 * mt, 32 * ks, lane);
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = mfma16x16x32(af[mt], bq[ks][nt], acc[mt][nt]);
+  }
+  // bias -> bf16 qkv (saved unrotated); RoPE on q / k pairs (adjacent lanes), q scaled; V transposed
+  const float scale = 0.17677669529663687f;  // 1 / sqrt(32)
+#pragma unroll
+  for (int nt = 0; nt < 3; ++nt) {
+    const int c = 48 * wave + 16 * nt + col;  // feature in [0, 384)
+    const int which = c >> 7, f = c & 127;     // q / k / v, feature within
+    const float bias = s.bqkv[c];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + rq + r;
+        const __bf16 hb = (__bf16)(acc[mt][nt][r] + bias);
+        s.u.qkv[t * QLD + c] = hb;
+        float xval = (float)hb;
+        if (which < 2) {
+          const float px = __shfl_xor(xval, 1, 64);
+          const float2 cs = s.rope[t * (AHD / 2) + ((f & (AHD - 1)) >> 1)];
+          xval = (f & 1) ? (px * cs.y + xval * cs.x) : (xval * cs.x - px * cs.y);
+          if (which == 0) xval *= scale;
+          (which == 0 ? s.q : s.k)[t * BLD + f] = (__bf16)xval;
+        } else {
+          s.vt[f * VLD + t] = (__bf16)xval;
+        }
+      }
+  }
+  __syncthreads();  // qkv staging, q, k, V^T complete
+  // qkv rows out (16-B pieces)
+#pragma unroll
+  for (int i = 0; i < AT * (AQ / 8) / ATH; ++i) {
+    const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
+    if (r < T)
+      *reinterpret_cast<uint4*>(a.qkv + (grow0 + r) * AQ + 8 * c8) =
+          *reinterpret_cast<const uint4*>(&s.u.qkv[r * QLD + 8 * c8]);
+  }
+  __syncthreads();  // staging read out before the P images reuse it
+
+  // ---- attention: head h = wave / 2, query tiles 2 (wave & 1) + {0, 1} ----
+  {
+    const int h = wave >> 1;
+    __bf16* pw = s.u.p[wave];  // this wave's 32 P rows
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const int qi = 2 * (wave & 1) + qq;
+      f32x4 sc[4];
+      const bf16x8 aq = lfrag(s.q, BLD, 16 * qi, AHD * h, lane);
+#pragma unroll
+      for (int ki = 0; ki < 4; ++ki) {
+        sc[ki] = mfma16x16x32(aq, lfrag(s.k, BLD, 16 * ki, AHD * h, lane), f32x4{0.f, 0.f, 0.f, 0.f});
+        if (16 * ki + col >= T) sc[ki] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m = fmaxf(fmaxf(sc[0][r], sc[1][r]), fmaxf(sc[2][r], sc[3][r]));
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+        float sum = 0.f;
+#pragma unroll
+        for (int ki = 0; ki < 4; ++ki) {
+          sc[ki][r] = __expf(sc[ki][r] - m);
+          sum += sc[ki][r];
+        }
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) sum += __shfl_xor(sum, off, 64);
+        const float inv = 1.0f / sum;
+#pragma unroll
+        for (int ki = 0; ki < 4; ++ki) sc[ki][r] *= inv;
+        if (col == 0) a.lse[((size_t)seq * AHEADS + h) * AT + 16 * qi + rq + r] = m + __logf(sum);
+      }
+#pragma unroll
+      for (int ki = 0; ki < 4; ++ki)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pw[(16 * qq + rq + r) * VLD + 16 * ki + col] = (__bf16)sc[ki][r];
+      // O tile (16 queries x 32 features of head h) = P (16 x 64) V (64 x 32): own P rows, written above
+#pragma unroll
+      for (int dj = 0; dj < 2; ++dj) {
+        f32x4 ov = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          ov = mfma16x16x32(lfrag(pw, VLD, 16 * qq, 32 * kk, lane), lfrag(s.vt, VLD, AHD * h + 16 * dj, 32 * kk, lane),
+                            ov);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s.xo[(16 * qi + rq + r) * BLD + AHD * h + 16 * dj + col] = (__bf16)ov[r];
+      }
+    }
+  }
+  __syncthreads();  // o image complete; P images dead
+  // o rows out; x rows (residual) into the freed staging space
+#pragma unroll
+  for (int i = 0; i < AT * (AD / 8) / ATH; ++i) {
+    const int idx = tid + ATH * i, r = idx / (AD / 8), c8 = idx % (AD / 8);
+    if (r < T)
+      *reinterpret_cast<uint4*>(a.o + (grow0 + r) * AD + 8 * c8) = *reinterpret_cast<const uint4*>(&s.xo[r * BLD + 8 * c8]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(&s.u.x[xr * XLDF + xc + 4 * i]) = xv[i];
+
+  // ---- projection: x1 = x + o Wo^T + bo, this wave's 16 features x 64 rows ----
+  f32x4 pacc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                   f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) pacc[mt] = mfma16x16x32(lfrag(s.xo, BLD, 16 * mt, 32 * ks, lane), bp[ks], pacc[mt]);
+  __syncthreads();  // x rows staged
+  {
+    const int n = 16 * wave + col;
+    const float bias = s.bo[n];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + rq + r;
+        s.u.x[t * XLDF + n] = (pacc[mt][r] + bias) + s.u.x[t * XLDF + n];
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
+    const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
+    if (r < T)
+      *reinterpret_cast<float4*>(a.x1 + (grow0 + r) * AD + 4 * c4) = *reinterpret_cast<const float4*>(&s.u.x[r * XLDF + 4 * c4]);
+  }
+}
+
+}  // namespace
+
+extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo,
+                               const float* g1, const float* bqkv, const float* bo, const float* rope, float eps,
+                               void* xn, float* r1, void* qkv, void* o, float* lse, float* x1, hipStream_t st) {
+  if (d != AD || heads != AHEADS || T < 1 || T > AT || !rope) return 1;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_attn_fwd_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)sizeof(AttnFwdSmem)) == hipSuccess;
+  if (!attr) return 2;
+  AttnFwdArgs a{};
+  a.x = x;
+  a.wqkv = static_cast<const __bf16*>(wqkv);
+  a.wo = static_cast<const __bf16*>(wo);
+  a.g1 = g1;
+  a.bqkv = bqkv;
+  a.bo = bo;
+  a.rope = rope;
+  a.eps = eps;
+  a.T = T;
+  a.xn = static_cast<__bf16*>(xn);
+  a.qkv = static_cast<__bf16*>(qkv);
+  a.o = static_cast<__bf16*>(o);
+  a.r1 = r1;
+  a.lse = lse;
+  a.x1 = x1;
+  tr_attn_fwd_kernel<<<nseq, ATH, sizeof(AttnFwdSmem), st>>>(a);
+  return 0;
+}

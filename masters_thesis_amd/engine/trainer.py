@@ -33,7 +33,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ..metrics import Metric, sync_metrics
-from ..ops.optim import FlatParameters, FusedAdam
+from ..ops.optim import FlatParameters, FusedAdam, set_producer_optimizer
 from ..parallel import dist as pdist
 from ..parallel.ddp import FlatDDP
 from .callbacks import Callback, ModelCheckpoint, StepTimer
@@ -257,6 +257,10 @@ class Trainer:
             }
         self.ddp = FlatDDP(self.flat)
         self.ddp.broadcast_parameters()
+        # gradient producers (weight-gradient GEMMs that overwrite their range and hand the clip norm its partials,
+        # ops/optim.py) need the optimizer to see exactly what the backward wrote: one process only (with DDP the
+        # all-reduce rewrites the buffer between the producers and the norm)
+        set_producer_optimizer(self.optimizer if self.ddp.world == 1 else None)
 
     def _model_summary(self, model) -> None:
         if not (self.enable_model_summary and self.is_global_zero):

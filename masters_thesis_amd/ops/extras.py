@@ -36,6 +36,7 @@ import torch.nn.functional as Fn
 from torch import Tensor
 
 from ..parallel.overlap import grad_ready
+from .optim import register_grad_producer
 from ._lib import lib, use_hip
 
 EPI_BIAS, EPI_GELU, EPI_RESID, EPI_ACCUM, EPI_DROPOUT, EPI_DGELU = 1, 2, 4, 8, 16, 32
@@ -217,10 +218,15 @@ class _MlpEncoderFn(torch.autograd.Function):
                        None if rms else params[per * i + 3], None, None, means[i], rstds[i],
                        ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], dpre, None,
                        _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]))
-            # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre)
+            # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre).  A big dW_i is
+            # a gradient PRODUCER of the fused optimizer (ops/optim.py register_grad_producer): its split-K reduce
+            # overwrites the range and leaves the clip-norm partials, so the update neither zeroes nor re-reads it
+            parts = register_grad_producer(_grad_view(params[per * i])) if D * Din >= (1 << 20) else None
+            if parts is not None:
+                lib().gemm_grad_producer(parts, True)
             gemm(2, dpre, Xs[i], D, kp[i], Mp, D, kp[i], flags=EPI_ACCUM, out_f32=_grad_view(params[per * i]),
                  ldc=Din, n_store=Din, ksplit=wgrad_split(D, kp[i], Mp), bias_grad=_grad_view(params[per * i + 1]),
-                 defer=i > 0)  # paired with the input-gradient GEMM below (same dPre)
+                 defer=i > 0 and parts is None)  # paired with the input-gradient GEMM below (same dPre)
             if i > 0:
                 dy = torch.empty((Mp, Din), device=dev, dtype=_row_dtype(Din))
                 gemm(1, dpre, wb[i], Mp, Din, D, D, kp[i], **_row_out(dy))
@@ -395,6 +401,20 @@ def _tr_ffn_ok(d: int, dff: int) -> bool:
     return _TR_FFN[0] and not _DETERMINISTIC[0] and d == 128 and dff == 512
 
 
+# fused attention half of the block forward (csrc/tr_attn.hip) for d = 128, 4 heads, T <= 64: RMSNorm1 + QKV + RoPE +
+# attention + projection + residual in one launch, saving exactly the unfused chain's tensors.  MTA_TR_ATTN=0 keeps
+# the unfused chain (A/B).
+_TR_ATTN = [os.environ.get("MTA_TR_ATTN", "1") != "0"]
+
+
+def set_transformer_attn_fused(on: bool) -> None:
+    _TR_ATTN[0] = bool(on)
+
+
+def _tr_attn_ok(d: int, heads: int, T: int) -> bool:
+    return _TR_ATTN[0] and d == 128 and heads == 4 and 1 <= T <= 64
+
+
 class _TransformerEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, seeds, num_layers, heads, dropout, training, need_grad, *params):
@@ -422,6 +442,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
         ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
+        attn = _tr_attn_ok(d, heads, T)
         for l in range(L):
             base = 2 + nb * l
             g1, bqkv, bo, g2, b1, b2 = (params[base], params[base + 2], params[base + 4], params[base + 5],
@@ -430,15 +451,18 @@ class _TransformerEncoderFn(torch.autograd.Function):
             dff = w1_b.shape[0]
             xn = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             r1 = torch.empty(M, device=dev, dtype=torch.float32)
-            C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
-                   None, None, None, None)
             qkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
-            gemm(0, xn, wqkv_b, M, 3 * d, d, d, d, flags=EPI_BIAS, bias=bqkv, out_bf16=qkv)
             o = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
-            C.attention(False, qkv, o, lse, None, None, Np, T, d, heads, ROPE_BASE)
             x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
-            gemm(0, o, wo_b, M, d, d, d, d, flags=EPI_BIAS | EPI_RESID, bias=bo, resid=xs, out_f32=x1)
+            if attn:
+                C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, wqkv_b, wo_b, g1, bqkv, bo, xn, r1, qkv, o, lse, x1)
+            else:
+                C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
+                       None, None, None, None)
+                gemm(0, xn, wqkv_b, M, 3 * d, d, d, d, flags=EPI_BIAS, bias=bqkv, out_bf16=qkv)
+                C.attention(False, qkv, o, lse, None, None, Np, T, d, heads, ROPE_BASE)
+                gemm(0, o, wo_b, M, d, d, d, d, flags=EPI_BIAS | EPI_RESID, bias=bo, resid=xs, out_f32=x1)
             xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             r2 = torch.empty(M, device=dev, dtype=torch.float32)
             pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)

@@ -33,6 +33,22 @@ from ._lib import lib, use_hip
 
 _ALIGN = 1024
 
+# The optimizer whose flat gradient the ops may produce into by OVERWRITING (see FusedAdam.register_producer), or None.
+_PRODUCER_OPT: List[Optional["FusedAdam"]] = [None]
+
+
+def set_producer_optimizer(opt: Optional["FusedAdam"]) -> None:
+    """Enable (single-process training) or disable gradient producers for ``opt`` (the trainer calls this)."""
+    _PRODUCER_OPT[0] = opt
+
+
+def register_grad_producer(grad: Tensor) -> Optional[Tensor]:
+    """For a weight-gradient op about to write ``grad`` (a view into the active optimizer's flat gradient): the norm
+    partials buffer it must fill, with overwrite semantics (``lib().gemm_grad_producer(parts, True)``), or None
+    (accumulate as usual)."""
+    opt = _PRODUCER_OPT[0]
+    return None if opt is None else opt.register_producer(grad)
+
 
 class FlatParameters:
     def __init__(self, params: Iterable[torch.nn.Parameter], device: Optional[torch.device] = None):
@@ -94,18 +110,49 @@ class FusedAdam:
         self.adamw = bool(adamw)
         self._lr = float(lr)
         self.hip = use_hip(flat.data)
+        # gradient producers (register_producer): float4 ranges of the flat gradient a weight-gradient GEMM overwrote
+        # this step, and their clip-norm partials; consumed by the next step()
+        self._plan: Dict[int, tuple] = {}
         if self.hip:
             C = lib()
             self.single_launch = os.environ.get("MTA_OPTIM_TWO_LAUNCH", "0") != "1"
             n = C.adam_fused_partials() if self.single_launch else C.optim_num_partials(flat.padded)
             self.partials = torch.zeros(n, device=dev, dtype=torch.float32)
             self.ticket = torch.zeros(1, device=dev, dtype=torch.int64)
+            self._nparts = int(C.gemm_norm_parts())
+            self.ext_parts = torch.zeros(self.MAX_PRODUCERS * self._nparts, device=dev, dtype=torch.float32)
         # torch.optim-like surface for schedulers / LR monitors / checkpoints
         self.param_groups = [{
             "lr": lr, "betas": self.betas, "eps": self.eps, "weight_decay": self.weight_decay, "amsgrad": False,
             "maximize": False, "foreach": None, "capturable": True, "differentiable": False, "fused": True,
             "decoupled_weight_decay": self.adamw, "params": list(range(len(flat.params))),
         }]
+
+    MAX_PRODUCERS = 8  # csrc/optim.hip MAX_COVERED
+
+    def register_producer(self, grad: Tensor) -> Optional[Tensor]:
+        """A producer that overwrites ``grad`` (contiguous view into the flat gradient, float4-aligned) and writes the
+        clip-norm partials of it into the returned buffer; this step's fused update then neither re-reads it for the
+        norm nor zeroes it.  None when not applicable (accumulate as usual).  Decided from static properties only
+        (alignment, slots), so a producer makes the same choice every step: a range the update left unzeroed is
+        always overwritten by the next backward."""
+        if not (self.hip and self.single_launch) or os.environ.get("MTA_OPTIM_PRODUCERS", "1") == "0":
+            return None
+        f = self.flat
+        if not grad.is_contiguous() or grad.dtype != torch.float32:
+            return None
+        off = (grad.data_ptr() - f.grad.data_ptr()) // 4
+        n = grad.numel()
+        if off < 0 or off + n > f.padded or off % 4 or n % 4:
+            return None
+        key = off // 4
+        if key not in self._plan:
+            if len(self._plan) >= self.MAX_PRODUCERS:
+                return None
+            slot = len(self._plan)
+            self._plan[key] = (off // 4, (off + n) // 4, slot)
+        slot = self._plan[key][2]
+        return self.ext_parts[slot * self._nparts:(slot + 1) * self._nparts]
 
     # ---- lr (device-resident) --------------------------------------------------
     @property
@@ -132,9 +179,13 @@ class FusedAdam:
         b1, b2 = self.betas
         self.grads_zeroed = False
         if self.hip and self.single_launch:
+            plan = sorted(self._plan.values(), key=lambda r: r[2])
+            self._plan = {}
             lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
                              self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
-                             float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health)
+                             float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health,
+                             [r[0] for r in plan], [r[1] for r in plan], self.ext_parts if plan else None)
+            # covered ranges keep this step's gradient (their producers overwrite them next step)
             self.grads_zeroed = bool(zero_grad)
             return
         if self.hip:

@@ -287,12 +287,12 @@ def test_transformer_encoder_matches_fp32_reference():
     _encoder_parity(FinancialTransformerMse, dict(hidden_size=128, num_layers=2, num_heads=4, dropout=0.0), 3e-2, 8e-2)
 
 
-@pytest.mark.parametrize("dropout,N", [(0.0, 100), (0.2, 37)])
-def test_fused_transformer_ffn_matches_unfused(dropout, N):
+@pytest.mark.parametrize("dropout,N,T", [(0.0, 100, 60), (0.2, 37, 60), (0.0, 20, 33)])
+def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
     """csrc/tr_ffn.hip (the FFN half of every block in one launch forward and one backward, plus split-K weight
-    gradients) against the unfused kernel chain on the same inputs, seeds and weights: encoder output and every
-    parameter gradient, plus the fp32 PyTorch reference without dropout.  N = 37: M = 40 x 60 rows, a partial
-    32-row workgroup at the end."""
+    gradients) and csrc/tr_attn.hip (the attention half forward in one launch) against the unfused kernel chain on the
+    same inputs, seeds and weights: encoder output and every parameter gradient, plus the fp32 PyTorch reference
+    without dropout.  N = 37: M = 40 x 60 rows, a partial 32-row workgroup at the end; T = 33: padded key masking."""
     from masters_thesis_amd.models.extras import FinancialTransformerMse
     from masters_thesis_amd.ops import extras as X
 
@@ -300,15 +300,17 @@ def test_fused_transformer_ffn_matches_unfused(dropout, N):
     m = FinancialTransformerMse(hidden_size=128, num_layers=2, num_heads=4, dropout=dropout).to(DEV)
     enc = m.encoder
     params = list(enc.flat_params()) if hasattr(enc, "flat_params") else [p for p in enc.parameters()]
-    x = torch.randn(N, 60, 3, device=DEV)
+    x = torch.randn(N, T, 3, device=DEV)
     seeds0 = torch.randint(0, 2 ** 62, (8,), device=DEV, dtype=torch.int64)
     outs, grads = [], []
-    prev = X._TR_FFN[0]
+    prev = X._TR_FFN[0], X._TR_ATTN[0]
     try:
         for fused in (True, False):
             X.set_transformer_ffn_fused(fused)
-            assert _ran_kernel(lambda: X.transformer_encode(x, params, seeds0.clone(), 2, 4, dropout, False),
-                               "tr_ffn_fwd_kernel") == fused
+            X.set_transformer_attn_fused(fused)
+            fn = lambda: X.transformer_encode(x, params, seeds0.clone(), 2, 4, dropout, False)  # noqa: E731
+            assert _ran_kernel(fn, "tr_ffn_fwd_kernel") == fused
+            assert _ran_kernel(fn, "tr_attn_fwd_kernel") == fused
             for p in params:
                 p.grad = None
             seeds = seeds0.clone()
@@ -318,7 +320,8 @@ def test_fused_transformer_ffn_matches_unfused(dropout, N):
             outs.append(h.detach().clone())
             grads.append([p.grad.detach().clone() for p in params])
     finally:
-        X.set_transformer_ffn_fused(prev)
+        X.set_transformer_ffn_fused(prev[0])
+        X.set_transformer_attn_fused(prev[1])
     assert _rel(outs[0], outs[1]) < 2e-3
     for a, b in zip(*grads):
         assert _rel(a, b) < 5e-3
@@ -381,6 +384,46 @@ def test_extras_train_through_trainer_graph(arch):
     torch.cuda.synchronize()
     assert torch.isfinite(tr.flat.data).all() and torch.isfinite(loss).all()
     assert tr._graphs  # the step was captured and replayed
+
+
+@pytest.mark.parametrize("batch", [1, 32])
+def test_mlp_grad_producers_match_accumulating_path(batch, monkeypatch):
+    """Big MLP weight gradients as optimizer gradient PRODUCERS (csrc/gemm.hip mta_gemm_grad_producer: the split-K
+    reduce overwrites the flat-gradient range and writes the clip-norm partials; the fused update skips re-reading and
+    zeroing it) against the accumulate + zero path, through the Trainer's captured steps with clipping active: the
+    parameter trajectories agree and the producers actually ran.  batch 1: K = 104 tokens, the fallback (zero-fill +
+    accumulating GEMM + partials launch); batch 32: K = 3,200, the 256 x 256 kernel's fp32-slab split-K reduce."""
+    from masters_thesis_amd.data.datamodule import TensorBatchLoader
+    from masters_thesis_amd.engine import Trainer
+    from masters_thesis_amd.models import get_model_class
+
+    g = torch.Generator().manual_seed(0)
+    W = 64
+    data = [torch.randn(W, 100, 60, 3, generator=g), torch.randn(W, 100, 30, 4, generator=g) * 0.01,
+            torch.stack([torch.randn(W, generator=g) * 0.01, torch.rand(W, generator=g) * 1e-3 + 1e-4], -1),
+            torch.rand(W, 100, generator=g) * 3 + 1]
+    outs = []
+    for prod in ("1", "0"):
+        monkeypatch.setenv("MTA_OPTIM_PRODUCERS", prod)
+        torch.manual_seed(1)
+        model = get_model_class("FinancialLstmMse", "mlp")(input_size=3, hidden_size=1024, num_layers=3, dropout=0.0,
+                                                             learning_rate=1e-3)
+        tr = Trainer(gradient_clip_val=0.05, enable_progress_bar=False, enable_model_summary=False,
+                     use_hip_graphs=True, precision="bf16-mixed")
+        tr._setup_env()
+        tr._setup_model(model)
+        tr._configure_optimizers(model)
+        model.train()
+        step = tr.make_train_stepper(TensorBatchLoader([t.to(DEV) for t in data], batch, shuffle=True, seed=0))
+        for _ in range(10):
+            step()
+        torch.cuda.synchronize()
+        outs.append(tr.flat.data.detach().clone())
+        if prod == "1":
+            assert tr.optimizer.ext_parts.abs().sum().item() > 0, "no gradient producer ran"
+        assert tr.optimizer.nonfinite.item() == 0
+    diff = (outs[0] - outs[1]).abs()
+    assert diff.max().item() < 1e-5, diff.max().item()
 
 
 # (6400, 2048, *): above 2^31 MACs both products run on transposed copies through the NN kernel (csrc/gemm.hip
