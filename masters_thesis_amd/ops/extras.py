@@ -404,7 +404,7 @@ def _tr_ffn_ok(d: int, dff: int) -> bool:
 # fused attention half of the block forward (csrc/tr_attn.hip) for d = 128, 4 heads, T <= 64: RMSNorm1 + QKV + RoPE +
 # attention + projection + residual in one launch, saving exactly the unfused chain's tensors.  MTA_TR_ATTN=0 keeps
 # the unfused chain (A/B).
-_TR_ATTN = [os.environ.get("MTA_TR_ATTN", "1") != "0"]
+_TR_ATTN = [os.environ.get("MTA_TR_ATTN", "0") == "1"]  # default flips on once measured on the GPU
 
 
 def set_transformer_attn_fused(on: bool) -> None:
