@@ -142,10 +142,13 @@ namespace {
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
+// one statement (do / while): an unbraced `if (x) MTA_CHECK_F32(*x);` must not run the later checks on an empty x
 #define MTA_CHECK_F32(t)                                                                            \
-  TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor");                                           \
-  TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32");                              \
-  TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+  do {                                                                                              \
+    TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor");                                         \
+    TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32");                            \
+    TORCH_CHECK((t).is_contiguous(), #t " must be contiguous");                                     \
+  } while (0)
 
 using OptT = c10::optional<at::Tensor>;
 
@@ -493,7 +496,9 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
   for (size_t k = 0; k < cov_s.size(); ++k)
     TORCH_CHECK(0 <= cov_s[k] && cov_s[k] <= cov_e[k] && cov_e[k] <= n / 4, "adam_fused: covered range out of bounds");
   TORCH_CHECK(cov_s.empty() || has(ext), "adam_fused: covered ranges need their producer partials");
-  if (has(ext)) MTA_CHECK_F32(*ext);
+  if (has(ext)) {
+    MTA_CHECK_F32(*ext);
+  }
   std::vector<long> cs(cov_s.begin(), cov_s.end()), ce(cov_e.begin(), cov_e.end());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   mta_adam_fused(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), (long)n,
@@ -528,8 +533,10 @@ void scale_(at::Tensor x, double s) {
 
 // ------------------------------------------------------------------------------- MLP / transformer extras
 #define MTA_CHECK_GPU(t, dt)                                                                        \
-  TORCH_CHECK((t).is_cuda() && (t).scalar_type() == (dt), #t " must be a GPU tensor of " #dt);     \
-  TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+  do {                                                                                              \
+    TORCH_CHECK((t).is_cuda() && (t).scalar_type() == (dt), #t " must be a GPU tensor of " #dt);   \
+    TORCH_CHECK((t).is_contiguous(), #t " must be contiguous");                                     \
+  } while (0)
 
 template <class T>
 T* opt_typed(const OptT& t, at::ScalarType dt, const char* name) {
