@@ -1,0 +1,64 @@
+"""Gradient-producer bookkeeping of the fused optimizer (ops/optim.py FusedAdam.register_producer), on CPU tensors:
+which flat-gradient ranges may be overwritten by a producer, the float4 ranges and partial slots handed to the fused
+update, the static-decision rules (alignment, slot limit, env switch).  The GPU side is tests/test_gpu_extras.py::
+test_mlp_grad_producers_match_accumulating_path."""
+import torch
+
+from masters_thesis_amd.ops import optim as O
+
+
+def _opt(shapes, monkeypatch):
+    params = [torch.nn.Parameter(torch.zeros(*s)) for s in shapes]
+    flat = O.FlatParameters(params)
+    opt = O.FusedAdam(flat, lr=1e-3)
+    # pretend the single-launch HIP path is available (the bookkeeping is host-side only)
+    opt.hip = True
+    opt.single_launch = True
+    opt._nparts = 16
+    opt.ext_parts = torch.zeros(opt.MAX_PRODUCERS * opt._nparts)
+    monkeypatch.setenv("MTA_OPTIM_PRODUCERS", "1")
+    return opt, params
+
+
+def test_register_ranges_and_slots(monkeypatch):
+    opt, params = _opt([(8, 4), (3,), (4, 4)], monkeypatch)  # flat offsets 0, 32, 35
+    f = opt.flat
+    offs = f.offsets
+    a = opt.register_producer(params[0].grad)
+    assert a is not None and a.numel() == 16 and a.data_ptr() == opt.ext_parts.data_ptr()
+    # the same range again in one step: same slot
+    assert opt.register_producer(params[0].grad).data_ptr() == a.data_ptr()
+    # a 3-float bias is not float4-granular: refused (accumulates as usual)
+    assert opt.register_producer(params[1].grad) is None
+    # the third tensor starts at 35: not float4-aligned, refused
+    assert offs[2] % 4 != 0 and opt.register_producer(params[2].grad) is None
+    assert list(opt._plan.values()) == [(0, 8, 0)]
+
+
+def test_slot_limit_and_switch(monkeypatch):
+    opt, params = _opt([(4,)] * 12, monkeypatch)
+    got = [opt.register_producer(p.grad) for p in params]
+    assert sum(g is not None for g in got) == opt.MAX_PRODUCERS
+    assert all(g is None for g in got[opt.MAX_PRODUCERS:])
+    slots = sorted(v[2] for v in opt._plan.values())
+    assert slots == list(range(opt.MAX_PRODUCERS))
+    opt._plan = {}
+    monkeypatch.setenv("MTA_OPTIM_PRODUCERS", "0")
+    assert opt.register_producer(params[0].grad) is None
+
+
+def test_foreign_gradient_refused(monkeypatch):
+    opt, _ = _opt([(8,)], monkeypatch)
+    other = torch.zeros(64)
+    assert opt.register_producer(other[:8]) is None
+
+
+def test_active_optimizer_hook(monkeypatch):
+    opt, params = _opt([(8,)], monkeypatch)
+    O.set_producer_optimizer(None)
+    assert O.register_grad_producer(params[0].grad) is None
+    O.set_producer_optimizer(opt)
+    try:
+        assert O.register_grad_producer(params[0].grad) is not None
+    finally:
+        O.set_producer_optimizer(None)
