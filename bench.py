@@ -299,10 +299,23 @@ def main(argv=None):
                 "hip_graphs": not args.no_graphs,
                 "steps_per_graph": S,
                 "residency": args.residency,
+                # optional fused paths in force (env switches, ops/extras.py / ops/optim.py)
+                "fused_paths": _fused_paths(cfg),
             },
         }
         print(json.dumps(rec), flush=True)
     pdist.destroy()
+
+
+def _fused_paths(cfg) -> dict:
+    arch = cfg.model.get("arch", "lstm")
+    if arch == "transformer":
+        from masters_thesis_amd.ops import extras as X
+
+        return {"transformer_ffn": bool(X._TR_FFN[0]), "transformer_attn": bool(X._TR_ATTN[0])}
+    if arch == "mlp":
+        return {"optimizer_grad_producers": os.environ.get("MTA_OPTIM_PRODUCERS", "0") == "1"}
+    return {}
 
 
 if __name__ == "__main__":
