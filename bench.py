@@ -312,7 +312,8 @@ def _fused_paths(cfg) -> dict:
     if arch == "transformer":
         from masters_thesis_amd.ops import extras as X
 
-        return {"transformer_ffn": bool(X._TR_FFN[0]), "transformer_attn": bool(X._TR_ATTN[0])}
+        return {"transformer_ffn": bool(X._TR_FFN[0]), "transformer_attn": bool(X._TR_ATTN[0]),
+                "transformer_wgrad_nn": bool(X._TR_FFN[0] and X._TR_WGRAD_NN[0])}
     if arch == "mlp":
         return {"optimizer_grad_producers": os.environ.get("MTA_OPTIM_PRODUCERS", "0") == "1"}
     return {}

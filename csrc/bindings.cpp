@@ -83,7 +83,8 @@ int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms,
 int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, const void* w2, const float* b1,
                const float* b2, const float* g2, const float* x1, const uint64_t* seed, float drop_p, void* xn2,
                void* pre, void* u, float* r2, float* x2, const void* dxb, const float* dx, const float* r2in,
-               const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, hipStream_t st);
+               const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, void* uT, void* xn2T, void* dpreT,
+               void* dxT, hipStream_t st);
 int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo, const float* g1,
                     const float* bqkv, const float* bo, const float* rope, float eps, void* xn, float* r1, void* qkv,
                     void* o, float* lse, float* x1, hipStream_t st);
@@ -679,54 +680,65 @@ static const float* rope_table(const at::Device& dev, int64_t T, int64_t HD, dou
   return it->second.data_ptr<float>();
 }
 
-// fused FFN half of a transformer block (csrc/tr_ffn.hip), forward: x1 -> xn2, r2, pre, u, x2
+// optional bf16 [rows][cols] operand of the fused FFN (nullptr when absent)
+void* opt_bf16(const OptT& t, int64_t numel, const char* name) {
+  if (!has(t)) return nullptr;
+  MTA_CHECK_GPU(*t, at::kBFloat16);
+  TORCH_CHECK(t->numel() >= numel, name, ": too small");
+  return t->data_ptr();
+}
+
+// fused FFN half of a transformer block (csrc/tr_ffn.hip), forward: x1 -> xn2, r2, pre, u, x2.
+// xn2 / u (row-major) and xn2T / uT ([features][M], the k-contiguous weight-gradient operands) are each optional.
 void tr_ffn_fwd(at::Tensor x1, at::Tensor w1, at::Tensor w2, at::Tensor b1, at::Tensor b2, at::Tensor g2, double eps,
-                const OptT& seed, double drop_p, at::Tensor xn2, at::Tensor r2, at::Tensor pre, at::Tensor u,
-                at::Tensor x2) {
+                const OptT& seed, double drop_p, const OptT& xn2, at::Tensor r2, at::Tensor pre, const OptT& u,
+                at::Tensor x2, const OptT& xn2T, const OptT& uT) {
   const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1.size(0);
   MTA_CHECK_F32(x1);
   MTA_CHECK_F32(x2);
   MTA_CHECK_F32(r2);
-  for (auto* t : {&w1, &w2, &xn2, &pre, &u}) {
+  for (auto* t : {&w1, &w2, &pre}) {
     MTA_CHECK_GPU(*t, at::kBFloat16);
   }
   TORCH_CHECK(w1.size(1) == d && w2.size(0) == d && w2.size(1) == dff, "tr_ffn_fwd: weight shapes");
-  TORCH_CHECK(x2.numel() >= M * d && xn2.numel() >= M * d && pre.numel() >= M * dff && u.numel() >= M * dff &&
-                  r2.numel() >= M && b1.numel() >= dff && b2.numel() >= d && g2.numel() >= d,
+  TORCH_CHECK(x2.numel() >= M * d && pre.numel() >= M * dff && r2.numel() >= M && b1.numel() >= dff &&
+                  b2.numel() >= d && g2.numel() >= d,
               "tr_ffn_fwd: sizes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x1.device());
   const int rc = mta_tr_ffn(0, (int)M, (int)d, (int)dff, (float)eps, w1.data_ptr(), w2.data_ptr(), b1.data_ptr<float>(),
                             b2.data_ptr<float>(), g2.data_ptr<float>(), x1.data_ptr<float>(),
                             reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
-                            (float)drop_p, xn2.data_ptr(), pre.data_ptr(), u.data_ptr(), r2.data_ptr<float>(),
-                            x2.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                            nullptr, cur_stream());
+                            (float)drop_p, opt_bf16(xn2, M * d, "xn2"), pre.data_ptr(), opt_bf16(u, M * dff, "u"),
+                            r2.data_ptr<float>(), x2.data_ptr<float>(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                            nullptr, nullptr, nullptr, opt_bf16(uT, M * dff, "uT"), opt_bf16(xn2T, M * d, "xn2T"),
+                            nullptr, nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "tr_ffn_fwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
 }
 
 // backward (input gradients): dX (fp32 + its bf16 copy) -> dpre (bf16), dX1 (fp32 + bf16), dg2 +=
-// w1t = W1^T [d][dff], w2t = W2^T [dff][d]
+// w1t = W1^T [d][dff], w2t = W2^T [dff][d]; dpre row-major and dpreT / dxT ([features][M]) are each optional
 void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at::Tensor r2, at::Tensor pre,
-                const OptT& seed, double drop_p, at::Tensor dx, at::Tensor dxb, at::Tensor dpre, at::Tensor dx1,
-                at::Tensor dx1b, at::Tensor dg2) {
+                const OptT& seed, double drop_p, at::Tensor dx, at::Tensor dxb, const OptT& dpre, at::Tensor dx1,
+                at::Tensor dx1b, at::Tensor dg2, const OptT& dpreT, const OptT& dxT) {
   const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1t.size(1);
   for (auto* t : {&x1, &r2, &dx, &dx1, &dg2}) {
     MTA_CHECK_F32(*t);
   }
-  for (auto* t : {&w1t, &w2t, &pre, &dxb, &dpre, &dx1b}) {
+  for (auto* t : {&w1t, &w2t, &pre, &dxb, &dx1b}) {
     MTA_CHECK_GPU(*t, at::kBFloat16);
   }
   TORCH_CHECK(w1t.size(0) == d && w2t.size(0) == dff && w2t.size(1) == d, "tr_ffn_bwd: weight shapes");
   TORCH_CHECK(dx.numel() >= M * d && dxb.numel() >= M * d && dx1.numel() >= M * d && dx1b.numel() >= M * d &&
-                  pre.numel() >= M * dff && dpre.numel() >= M * dff && r2.numel() >= M && dg2.numel() >= d,
+                  pre.numel() >= M * dff && r2.numel() >= M && dg2.numel() >= d,
               "tr_ffn_bwd: sizes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x1.device());
   const int rc = mta_tr_ffn(1, (int)M, (int)d, (int)dff, 0.f, w1t.data_ptr(), w2t.data_ptr(), nullptr, nullptr,
                             g2.data_ptr<float>(), x1.data_ptr<float>(),
                             reinterpret_cast<const uint64_t*>(opt_typed<int64_t>(seed, at::kLong, "seed")),
                             (float)drop_p, nullptr, nullptr, nullptr, nullptr, nullptr, dxb.data_ptr(),
-                            dx.data_ptr<float>(), r2.data_ptr<float>(), pre.data_ptr(), dpre.data_ptr(),
-                            dx1.data_ptr<float>(), dx1b.data_ptr(), dg2.data_ptr<float>(), cur_stream());
+                            dx.data_ptr<float>(), r2.data_ptr<float>(), pre.data_ptr(), opt_bf16(dpre, M * dff, "dpre"),
+                            dx1.data_ptr<float>(), dx1b.data_ptr(), dg2.data_ptr<float>(), nullptr, nullptr,
+                            opt_bf16(dpreT, M * dff, "dpreT"), opt_bf16(dxT, M * d, "dxT"), cur_stream());
   TORCH_CHECK(rc == 0, "tr_ffn_bwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
 }
 

@@ -1419,6 +1419,16 @@ bool launch_pair_ww(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipS
   return true;
 }
 
+// two accumulating products on k-contiguous operands (weight gradients from transposed activations, the transformer
+// FFN's dW2 / dW1 with MTA_TR_WGRAD_NN=1) in one launch, same conditions as launch_pair_ww
+bool launch_pair_nn_acc(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
+  if (big_eligible(g1, k1) || big_eligible(g2, k2)) return false;
+  const int c = tile_config(g1, k1);
+  if (c != tile_config(g2, k2)) return false;
+  launch_pair_kind<0>(c, g1, k1, g2, k2, st);
+  return true;
+}
+
 template <bool AT, bool BT>
 void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   // 128x128 tiles once they already fill the chip; 64x64 otherwise (these encoders' GEMMs are small).
@@ -1466,6 +1476,7 @@ void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
 // one deferred weight-gradient GEMM waiting for its input-gradient partner (stream-ordered, single-threaded use)
 struct Pending {
   bool on = false;
+  int mode = 2;  // 2: weight gradient dY^T X; 0: the same product on transposed (k-contiguous) operands
   GemmArgs g{};
   int ksplit;
   hipStream_t st;
@@ -1480,7 +1491,7 @@ extern "C" void mta_gemm_set_mid(int on) { g_mid_override = on; }
 extern "C" void mta_gemm_flush() {
   if (pending.on) {
     pending.on = false;
-    dispatch_mode(2, pending.g, pending.ksplit, pending.st);
+    dispatch_mode(pending.mode, pending.g, pending.ksplit, pending.st);
   }
 }
 
@@ -1512,7 +1523,8 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   if (M % 8 || N % 8 || K % 8 || lda % 8 || ldb % 8 || ldc < n_store) return 1;
   if ((flags & EPI_ACCUM) == 0 && ksplit > 1) return 2;
   if ((flags & EPI_RESID) && (flags & EPI_DGELU)) return 7;  // one prefetched epilogue operand
-  if (bias_grad && mode != 2) return 3;
+  // bias gradient = row sums of A over K: the weight-gradient forms (mode 2, or mode 0 on transposed operands)
+  if (bias_grad && !(mode == 2 || (mode == 0 && (flags & EPI_ACCUM)))) return 3;
   GemmArgs g{};
   g.A = static_cast<const __bf16*>(A);
   g.B = static_cast<const __bf16*>(B);
@@ -1560,9 +1572,10 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   }
   if (defer) {
     // a weight-gradient GEMM held back for the next call (its input-gradient partner): one paired launch
-    if (mode != 2) return 8;
+    if (!(mode == 2 || (mode == 0 && (flags & EPI_ACCUM)))) return 8;
     mta_gemm_flush();
     pending.on = true;
+    pending.mode = mode;
     pending.g = g;
     pending.ksplit = ksplit;
     pending.st = st;
@@ -1570,10 +1583,14 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   }
   if (pending.on) {
     pending.on = false;
-    const bool paired = pending.st == st && ((mode == 1 && launch_pair(pending.g, pending.ksplit, g, ksplit, st)) ||
-                                             (mode == 2 && launch_pair_ww(pending.g, pending.ksplit, g, ksplit, st)));
+    const bool same = pending.st == st;
+    const bool paired =
+        same && ((pending.mode == 2 && mode == 1 && launch_pair(pending.g, pending.ksplit, g, ksplit, st)) ||
+                 (pending.mode == 2 && mode == 2 && launch_pair_ww(pending.g, pending.ksplit, g, ksplit, st)) ||
+                 (pending.mode == 0 && mode == 0 && (flags & EPI_ACCUM) &&
+                  launch_pair_nn_acc(pending.g, pending.ksplit, g, ksplit, st)));
     if (!paired) {
-      dispatch_mode(2, pending.g, pending.ksplit, pending.st);
+      dispatch_mode(pending.mode, pending.g, pending.ksplit, pending.st);
       dispatch_mode(mode, g, ksplit, st);
     }
     return 0;

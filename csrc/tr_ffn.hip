@@ -28,12 +28,15 @@ constexpr int FD = 128, FF = 512, FBM = 32, FT = 512;  // 8 waves per 32-row wor
 constexpr int XLD = FD + 8;    // bf16 row stride of [32][128] images (272 B)
 constexpr int ULD = FF + 8;    // bf16 row stride of [32][512] images (1040 B)
 constexpr int RLD = FD + 4;    // fp32 row stride of [32][128] row images (528 B)
+constexpr int TLD = FBM + 8;   // bf16 row stride of transposed [features][32 tokens] images (80 B)
 
 struct FfnFwdSmem {
   __bf16 xn[FBM * XLD];   // xn2 (A of FFN-up)
   __bf16 u[FBM * ULD];    // u   (A of FFN-down), then copied out
   __bf16 pre[FBM * ULD];  // pre-activation, copied out
   float x[FBM * RLD];     // x1 rows (residual), then x2 staging
+  __bf16 uT[FF * TLD];    // u^T, xn2^T: the transposed (k-contiguous) weight-gradient operands
+  __bf16 xnT[FD * TLD];
   float b1[FF], b2[FD], g2[FD];
 };
 
@@ -42,6 +45,8 @@ struct FfnBwdSmem {
   __bf16 dpre[FBM * ULD];  // dpre (A of dxn2 = dpre W1), then copied out
   float x[FBM * RLD];      // x1 rows
   float g[FBM * RLD];      // dxn2 rows, then dX1 staging
+  __bf16 dpreT[FF * TLD];  // dpre^T, dX^T: the transposed weight-gradient operands
+  __bf16 dxT[FD * TLD];
   float g2[FD];
   float r[FBM];
 };
@@ -67,7 +72,22 @@ struct FfnArgs {
   float* dx1;         // [M][128]
   __bf16* dx1b;       // [M][128]
   float* dg2;         // [128] += (f32 atomics, one per column and workgroup)
+  // transposed weight-gradient operands [features][ldT] (token-contiguous; null: not written).  Forward: u^T, xn2^T;
+  // backward: dpre^T, dX^T -- dW2 = dX^T u and dW1 = dpre^T xn2 then run as k-contiguous (NN) GEMMs
+  __bf16 *uT, *xn2T, *dpreT, *dxT;
+  int ldT;
 };
+
+// [features][32] transposed LDS image -> global [features][ldT] at token row0 (16-B pieces; M % 8 == 0)
+template <int NF>
+__device__ __forceinline__ void copy_out_t(const __bf16* img, __bf16* dst, int ldT, int row0, int M) {
+#pragma unroll
+  for (int i = 0; i < (NF * 4 + FT - 1) / FT; ++i) {
+    const int idx = threadIdx.x + FT * i, f = idx >> 2, c = idx & 3;
+    if (f < NF && row0 + 8 * c < M)
+      *reinterpret_cast<uint4*>(dst + (size_t)f * ldT + row0 + 8 * c) = *reinterpret_cast<const uint4*>(img + f * TLD + 8 * c);
+  }
+}
 
 __device__ __forceinline__ uint32_t ffn_pair_hash(uint32_t s, uint32_t mpair, uint32_t n) {
   const uint32_t b = n * 0x85EBCA77u;  // == gemm.hip gemm_pair_hash
@@ -182,12 +202,17 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     uint4 p0;
     __builtin_memcpy(&p0, yb, 16);
     *reinterpret_cast<uint4*>(&s.xn[xr * XLD + xc]) = p0;
+    if (a.xn2T) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s.xnT[(xc + k) * TLD + xr] = yb[k];
+    }
     if (rok) {
-      *reinterpret_cast<uint4*>(a.xn2 + (size_t)(row0 + xr) * FD + xc) = p0;
+      if (a.xn2) *reinterpret_cast<uint4*>(a.xn2 + (size_t)(row0 + xr) * FD + xc) = p0;
       if ((tid & 15) == 0) a.r2[row0 + xr] = rs;
     }
   }
   __syncthreads();  // xn2 image complete
+  if (a.xn2T) copy_out_t<FD>(s.xnT, a.xn2T, a.ldT, row0, a.M);
 
   // ---- FFN-up: 32 rows x this wave's 64 hidden units, K = 128 ----
   f32x4 acc[2][4];
@@ -217,6 +242,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
         hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
         hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
       }
+      bf16x4 ut;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int lr = 16 * mt + rq + r;
@@ -228,11 +254,15 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
         }
         s.pre[lr * ULD + j] = (__bf16)v;
         s.u[lr * ULD + j] = (__bf16)g;
+        ut[r] = (__bf16)g;
       }
+      // four consecutive token rows of hidden unit j: one 8-byte write of the transposed image
+      if (a.uT) *reinterpret_cast<bf16x4*>(&s.uT[j * TLD + 16 * mt + rq]) = ut;
     }
   __syncthreads();  // u / pre complete
   copy_out_bf16<FF, ULD>(s.pre, a.pre, row0, a.M);
-  copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M);
+  if (a.u) copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M);
+  if (a.uT) copy_out_t<FF>(s.uT, a.uT, a.ldT, row0, a.M);
 
   // ---- FFN-down: 32 rows x this wave's 16 output features, K = 512 ----
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -278,6 +308,12 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
     const uint4 d0 = rok ? *reinterpret_cast<const uint4*>(a.dxb + (size_t)(row0 + xr) * FD + xc)
                          : make_uint4(0u, 0u, 0u, 0u);
     *reinterpret_cast<uint4*>(&s.dx[xr * XLD + xc]) = d0;
+    if (a.dxT) {
+      __bf16 e8[8];
+      __builtin_memcpy(e8, &d0, 16);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s.dxT[(xc + k) * TLD + xr] = e8[k];
+    }
   }
   // pre tile [32][512] -> the dpre image (the epilogue reads pre and writes dpre at the same element, same lane)
 #pragma unroll
@@ -338,6 +374,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
         hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
         hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
       }
+      bf16x4 dt;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int lr = 16 * mt + rq + r;
@@ -348,10 +385,14 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
         }
         v *= mta_gelu_grad((float)s.dpre[lr * ULD + j]);
         s.dpre[lr * ULD + j] = (__bf16)v;
+        dt[r] = (__bf16)v;
       }
+      if (a.dpreT) *reinterpret_cast<bf16x4*>(&s.dpreT[j * TLD + 16 * mt + rq]) = dt;
     }
   __syncthreads();  // dpre image complete
-  copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M);
+  if (a.dpre) copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M);
+  if (a.dpreT) copy_out_t<FF>(s.dpreT, a.dpreT, a.ldT, row0, a.M);
+  if (a.dxT) copy_out_t<FD>(s.dxT, a.dxT, a.ldT, row0, a.M);
 
   // ---- dxn2 = dpre W1: 32 rows x this wave's 16 features, K = 512 ----
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
@@ -433,8 +474,9 @@ extern "C" int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const 
                           const float* b1, const float* b2, const float* g2, const float* x1, const uint64_t* seed,
                           float drop_p, void* xn2, void* pre, void* u, float* r2, float* x2, const void* dxb,
                           const float* dx, const float* r2in, const void* prein, void* dpre, float* dx1, void* dx1b,
-                          float* dg2, hipStream_t st) {
+                          float* dg2, void* uT, void* xn2T, void* dpreT, void* dxT, hipStream_t st) {
   if (d != FD || dff != FF || M < 1) return 1;
+  if ((uT || xn2T || dpreT || dxT) && M % 8) return 3;
   FfnArgs a{};
   a.M = M;
   a.eps = eps;
@@ -459,6 +501,11 @@ extern "C" int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const 
   a.dx1 = dx1;
   a.dx1b = static_cast<__bf16*>(dx1b);
   a.dg2 = dg2;
+  a.uT = static_cast<__bf16*>(uT);
+  a.xn2T = static_cast<__bf16*>(xn2T);
+  a.dpreT = static_cast<__bf16*>(dpreT);
+  a.dxT = static_cast<__bf16*>(dxT);
+  a.ldT = M;
   const int grid = (M + FBM - 1) / FBM;
   if (!backward) {
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_ffn_fwd_kernel),

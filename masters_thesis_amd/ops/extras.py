@@ -411,6 +411,16 @@ def set_transformer_attn_fused(on: bool) -> None:
     _TR_ATTN[0] = bool(on)
 
 
+# FFN weight gradients as k-contiguous (NN) products: the fused FFN kernels also write u^T, xn2^T (forward) and
+# dpre^T, dX^T (backward) as [features][tokens] images, so dW2 += dX^T u and dW1 += dpre^T xn2 read both operands
+# along K instead of through the transposed (AT/BT) loaders.  Opt-in until measured (MTA_TR_WGRAD_NN=1).
+_TR_WGRAD_NN = [os.environ.get("MTA_TR_WGRAD_NN", "0") == "1"]
+
+
+def set_transformer_wgrad_nn(on: bool) -> None:
+    _TR_WGRAD_NN[0] = bool(on)
+
+
 def _tr_attn_ok(d: int, heads: int, T: int) -> bool:
     return _TR_ATTN[0] and d == 128 and heads == 4 and 1 <= T <= 64
 
@@ -442,6 +452,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
         ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
+        nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
         attn = _tr_attn_ok(d, heads, T)
         for l in range(L):
             base = 2 + nb * l
@@ -463,14 +474,15 @@ class _TransformerEncoderFn(torch.autograd.Function):
                 gemm(0, xn, wqkv_b, M, 3 * d, d, d, d, flags=EPI_BIAS, bias=bqkv, out_bf16=qkv)
                 C.attention(False, qkv, o, lse, None, None, Np, T, d, heads, ROPE_BASE)
                 gemm(0, o, wo_b, M, d, d, d, d, flags=EPI_BIAS | EPI_RESID, bias=bo, resid=xs, out_f32=x1)
-            xn2 = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+            xn2 = torch.empty((d, M) if nn else (M, d), device=dev, dtype=torch.bfloat16)
             r2 = torch.empty(M, device=dev, dtype=torch.float32)
             pre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
-            u = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+            u = torch.empty((dff, M) if nn else (M, dff), device=dev, dtype=torch.bfloat16)
             x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
             if ffn:
                 C.tr_ffn_fwd(x1, w1_b, w2_b, b1, b2, g2, RMS_EPS, seeds[l:l + 1] if drop else None, float(dropout),
-                             xn2, r2, pre1, u, x2)
+                             None if nn else xn2, r2, pre1, None if nn else u, x2, xn2 if nn else None,
+                             u if nn else None)
             else:
                 C.norm(False, x1, d, M, d, True, RMS_EPS, g2, None, xn2, None, None, r2, None, 0.0, None, None, None,
                        None, None, None, None)
@@ -488,7 +500,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                None, None, None, None, None, None, None)
         saved.append(xs)
         stats.append(rf)
-        ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout), ffn)
+        ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout), ffn, nn)
         ctx.params, ctx.mats_b, ctx.seeds = params, mats_b, seeds
         if need_grad:
             ctx.save_for_backward(*saved)
@@ -498,7 +510,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
     @staticmethod
     @torch.autograd.function.once_differentiable
     def backward(ctx, dh):
-        N, Np, T, F, Fp, d, L, heads, drop, p, ffn = ctx.meta
+        N, Np, T, F, Fp, d, L, heads, drop, p, ffn, nn = ctx.meta
         params, mats_b = ctx.params, ctx.mats_b
         saved = ctx.saved_tensors
         stats = ctx.stats
@@ -531,14 +543,23 @@ class _TransformerEncoderFn(torch.autograd.Function):
             dff = w1_b.shape[0]
             xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
             r1, lse, r2 = stats[3 * l: 3 * l + 3]
-            dpre1 = torch.empty((M, dff), device=dev, dtype=torch.bfloat16)
+            dpre1 = torch.empty((dff, M) if nn else (M, dff), device=dev, dtype=torch.bfloat16)
             dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-            if ffn:
+            if nn:
+                # same chain; the weight gradients then run on the transposed images as NN products (one paired launch)
+                dXt = torch.empty((d, M), device=dev, dtype=torch.bfloat16)
+                C.tr_ffn_bwd(x1, wt[2 * l], wt[2 * l + 1], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None, p, dX,
+                             dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
+                gemm(0, dXt, u, d, dff, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
+                gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+            elif ffn:
                 # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
                 # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
                 C.tr_ffn_bwd(x1, wt[2 * l], wt[2 * l + 1], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None, p, dX,
-                             dXb, dpre1, dX1, dX1b, _grad_view(g2))
+                             dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
                 gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
                      ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,

@@ -303,11 +303,13 @@ def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
     x = torch.randn(N, T, 3, device=DEV)
     seeds0 = torch.randint(0, 2 ** 62, (8,), device=DEV, dtype=torch.int64)
     outs, grads = [], []
-    prev = X._TR_FFN[0], X._TR_ATTN[0]
+    prev = X._TR_FFN[0], X._TR_ATTN[0], X._TR_WGRAD_NN[0]
     try:
-        for fused in (True, False):
+        # fused with the FFN weight gradients on transposed (NN) operands, fused, unfused
+        for fused, nn in ((True, True), (True, False), (False, False)):
             X.set_transformer_ffn_fused(fused)
             X.set_transformer_attn_fused(fused)
+            X.set_transformer_wgrad_nn(nn)
             fn = lambda: X.transformer_encode(x, params, seeds0.clone(), 2, 4, dropout, False)  # noqa: E731
             assert _ran_kernel(fn, "tr_ffn_fwd_kernel") == fused
             assert _ran_kernel(fn, "tr_attn_fwd_kernel") == fused
@@ -322,9 +324,11 @@ def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
     finally:
         X.set_transformer_ffn_fused(prev[0])
         X.set_transformer_attn_fused(prev[1])
-    assert _rel(outs[0], outs[1]) < 2e-3
-    for a, b in zip(*grads):
-        assert _rel(a, b) < 5e-3
+        X.set_transformer_wgrad_nn(prev[2])
+    for i in (0, 1):
+        assert _rel(outs[i], outs[2]) < 2e-3
+        for a, b in zip(grads[i], grads[2]):
+            assert _rel(a, b) < 5e-3
     if dropout == 0.0:
         with torch.no_grad():
             ref = X.transformer_reference(x.double(), [p.double() for p in params], 2, 4, 0.0, False)
