@@ -403,8 +403,8 @@ def _tr_ffn_ok(d: int, dff: int) -> bool:
 
 # fused attention half of the block forward (csrc/tr_attn.hip) for d = 128, 4 heads, T <= 64: RMSNorm1 + QKV + RoPE +
 # attention + projection + residual in one launch, saving exactly the unfused chain's tensors.  MTA_TR_ATTN=0 keeps
-# the unfused chain (A/B).
-_TR_ATTN = [os.environ.get("MTA_TR_ATTN", "0") == "1"]  # default flips on once measured on the GPU
+# the unfused chain (A/B: transformer_encoder B=1 0.647 -> 0.6175 ms, profiles/r4_transformer_fused_ab.jsonl).
+_TR_ATTN = [os.environ.get("MTA_TR_ATTN", "1") != "0"]
 
 
 def set_transformer_attn_fused(on: bool) -> None:
@@ -413,8 +413,8 @@ def set_transformer_attn_fused(on: bool) -> None:
 
 # FFN weight gradients as k-contiguous (NN) products: the fused FFN kernels also write u^T, xn2^T (forward) and
 # dpre^T, dX^T (backward) as [features][tokens] images, so dW2 += dX^T u and dW1 += dpre^T xn2 read both operands
-# along K instead of through the transposed (AT/BT) loaders.  Opt-in until measured (MTA_TR_WGRAD_NN=1).
-_TR_WGRAD_NN = [os.environ.get("MTA_TR_WGRAD_NN", "0") == "1"]
+# along K instead of through the transposed (AT/BT) loaders (0.6175 -> 0.6145 ms; MTA_TR_WGRAD_NN=0 for the A/B).
+_TR_WGRAD_NN = [os.environ.get("MTA_TR_WGRAD_NN", "1") != "0"]
 
 
 def set_transformer_wgrad_nn(on: bool) -> None:

@@ -60,7 +60,9 @@ class FlatParameters:
         off = 0
         for p in self.params:
             self.offsets.append(off)
-            off += p.numel()
+            # every parameter starts on a 16-byte boundary: its range is whole float4s (the vectorised kernels and
+            # the gradient producers' covered ranges); the gaps stay zero in every buffer
+            off += -(-p.numel() // 4) * 4
         self.numel = off
         self.padded = -(-off // _ALIGN) * _ALIGN
         self.data = torch.zeros(self.padded, device=dev, dtype=torch.float32)

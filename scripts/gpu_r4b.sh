@@ -5,7 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r4b
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_extras.py tests/test_gpu_kernels.py > $O/pytest.log 2>&1 || exit $?
+timeout -k 10 200 python -u scripts/debug_producers.py > $O/debug_producers.log 2>&1 || exit $?
+timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_extras.py tests/test_gpu_kernels.py -k "not grad_producers" > $O/pytest.log 2>&1 || exit $?
 # (ffn, attn, wgrad-nn): all fused, no NN wgrads, FFN only, unfused
 for v in 111 110 100 000; do
   MTA_TR_FFN=${v:0:1} MTA_TR_ATTN=${v:1:1} MTA_TR_WGRAD_NN=${v:2:1} timeout -k 10 300 python bench.py --model transformer_encoder --trainer gpu_fast --steps 200 --warmup 20 >> $O/bench_tr.jsonl 2>> $O/bench.err || exit $?

@@ -21,7 +21,7 @@ def _opt(shapes, monkeypatch):
 
 
 def test_register_ranges_and_slots(monkeypatch):
-    opt, params = _opt([(8, 4), (3,), (4, 4)], monkeypatch)  # flat offsets 0, 32, 35
+    opt, params = _opt([(8, 4), (3,), (4, 4)], monkeypatch)  # flat offsets 0, 32, 36 (float4-aligned starts)
     f = opt.flat
     offs = f.offsets
     a = opt.register_producer(params[0].grad)
@@ -30,9 +30,12 @@ def test_register_ranges_and_slots(monkeypatch):
     assert opt.register_producer(params[0].grad).data_ptr() == a.data_ptr()
     # a 3-float bias is not float4-granular: refused (accumulates as usual)
     assert opt.register_producer(params[1].grad) is None
-    # the third tensor starts at 35: not float4-aligned, refused
-    assert offs[2] % 4 != 0 and opt.register_producer(params[2].grad) is None
-    assert list(opt._plan.values()) == [(0, 8, 0)]
+    # every parameter starts on a float4 boundary (the 3-float bias is followed by a zero gap): the third is a producer
+    assert offs == [0, 32, 36] and f.padded % 4 == 0
+    assert opt.register_producer(params[2].grad) is not None
+    # a range that does not start on a float4 boundary is refused
+    assert opt.register_producer(f.grad[33:37]) is None
+    assert sorted(opt._plan.values()) == [(0, 8, 0), (9, 13, 1)]
 
 
 def test_slot_limit_and_switch(monkeypatch):
