@@ -315,7 +315,7 @@ def _fused_paths(cfg) -> dict:
         return {"transformer_ffn": bool(X._TR_FFN[0]), "transformer_attn": bool(X._TR_ATTN[0]),
                 "transformer_wgrad_nn": bool(X._TR_FFN[0] and X._TR_WGRAD_NN[0])}
     if arch == "mlp":
-        return {"optimizer_grad_producers": os.environ.get("MTA_OPTIM_PRODUCERS", "0") == "1"}
+        return {"optimizer_grad_producers": os.environ.get("MTA_OPTIM_PRODUCERS", "1") != "0"}
     return {}
 
 

@@ -24,6 +24,36 @@
 
 namespace {
 
+#ifndef MTA_FFN_STAMPS
+#define MTA_FFN_STAMPS 0
+#endif
+// probe experiments only (csrc/tools/ffn_probe.hip; results are garbage): 1 = no global weight-fragment loads,
+// 2 = no x1 row loads
+#ifndef MTA_FFN_EXP
+#define MTA_FFN_EXP 0
+#endif
+#if MTA_FFN_STAMPS
+// probe build only (csrc/tools/ffn_probe.hip): s_memtime at the phase boundaries of every workgroup's wave 0
+// ([direction][block][phase]), the per-phase split of one workgroup's critical path
+__device__ unsigned long long mta_ffn_stamp[2][256][12];
+#define FSTAMP(dir, k)                                                                                   \
+  do {                                                                                                   \
+    if ((threadIdx.x & 511) == 0 && blockIdx.x < 256) mta_ffn_stamp[(dir)][blockIdx.x][(k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// launch fill / drain in the globally consistent 100 MHz clock (the per-XCD shader clocks are not aligned)
+#define FSTAMP_RT(dir, k)                                                                                \
+  do {                                                                                                   \
+    if ((threadIdx.x & 511) == 0 && blockIdx.x < 256) mta_ffn_stamp[(dir)][blockIdx.x][(k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define FSTAMP(dir, k) \
+  do {                 \
+  } while (0)
+#define FSTAMP_RT(dir, k) \
+  do {                    \
+  } while (0)
+#endif
+
 constexpr int FD = 128, FF = 512, FBM = 32, FT = 512;  // 8 waves per 32-row workgroup
 constexpr int XLD = FD + 8;    // bf16 row stride of [32][128] images (272 B)
 constexpr int ULD = FF + 8;    // bf16 row stride of [32][512] images (1040 B)
@@ -144,6 +174,8 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * FBM;
   const int rq = 4 * (lane >> 4), col = lane & 15;
+  FSTAMP_RT(0, 10);
+  FSTAMP(0, 0);
 
   // ---- every load first (one in-order vmcnt covers loads and stores on gfx950) ----
   // FFN-up B fragments: this wave's 64 hidden units (4 tiles) x 4 k-steps
@@ -151,15 +183,16 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+    for (int nt = 0; nt < 4; ++nt)
+      bw[ks][nt] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
   // x1 rows: 16 threads per row, 8 columns each
   const int xr = tid >> 4, xc = 8 * (tid & 15);
   const bool rok = row0 + xr < a.M;
   float4 xv[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
-    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
+    xv[i] = (rok && MTA_FFN_EXP != 2) ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                                      : make_float4(1.f, 1.f, 1.f, 1.f);
   {
     const float v0 = a.b1[tid];
     const float v2 = tid < FD ? a.b2[tid] : 0.f, v3 = tid < FD ? a.g2[tid] : 0.f;
@@ -172,7 +205,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   // FFN-down B fragments: this wave's 16 output features x 16 k-steps
   bf16x8 bd[16];
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag(a.w2, FF, 16 * wave, 32 * ks, lane);
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag(a.w2, FF, 16 * wave, 32 * ks, lane);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 1.f;
   if (a.seed) {
@@ -182,6 +215,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     dscale = 1.0f / (1.0f - a.drop_p);
   }
   __syncthreads();  // g2 / biases in LDS
+  FSTAMP(0, 1);
 
   // ---- RMSNorm2 ----
   {
@@ -212,6 +246,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     }
   }
   __syncthreads();  // xn2 image complete
+  FSTAMP(0, 2);
   if (a.xn2T) copy_out_t<FD>(s.xnT, a.xn2T, a.ldT, row0, a.M);
 
   // ---- FFN-up: 32 rows x this wave's 64 hidden units, K = 128 ----
@@ -229,6 +264,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
       acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
     }
   }
+  FSTAMP(0, 3);
   // bias, GELU, dropout (one hash per pair of rows) -> u and pre images
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -260,10 +296,12 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
       if (a.uT) *reinterpret_cast<bf16x4*>(&s.uT[j * TLD + 16 * mt + rq]) = ut;
     }
   __syncthreads();  // u / pre complete
+  FSTAMP(0, 4);
   copy_out_bf16<FF, ULD>(s.pre, a.pre, row0, a.M);
   if (a.u) copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M);
   if (a.uT) copy_out_t<FF>(s.uT, a.uT, a.ldT, row0, a.M);
 
+  FSTAMP(0, 5);
   // ---- FFN-down: 32 rows x this wave's 16 output features, K = 512 ----
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -272,6 +310,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     o[0] = mfma16x16x32(a0, bd[ks], o[0]);
     o[1] = mfma16x16x32(a1, bd[ks], o[1]);
   }
+  FSTAMP(0, 6);
   // x2 = x1 + o + b2 into the x image (each wave its own 16 columns: no cross-wave hazard)
   {
     const int n = 16 * wave + col;
@@ -285,7 +324,10 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
       }
   }
   __syncthreads();
+  FSTAMP(0, 7);
   copy_out_f32(s.x, a.x2, row0, a.M);
+  FSTAMP(0, 8);
+  FSTAMP_RT(0, 11);
 }
 
 __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
@@ -294,6 +336,8 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * FBM;
   const int rq = 4 * (lane >> 4), col = lane & 15;
+  FSTAMP_RT(1, 10);
+  FSTAMP(1, 0);
 
   // ---- loads: du = dX W2 B fragments (W2^T [512][128]: this wave's 64 hidden units, 4 k-steps); dX (bf16) and
   // the pre-activation tile into LDS (16-B pieces); x1 and dX rows (fp32, 16 threads per row); r2; g2 ----
@@ -346,6 +390,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
     dscale = 1.0f / (1.0f - a.drop_p);
   }
   __syncthreads();  // dX image, pre tile, g2, r2
+  FSTAMP(1, 1);
 
   // ---- du = dX W2: 32 rows x this wave's 64 hidden units, K = 128 ----
   f32x4 acc[2][4];
@@ -362,6 +407,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
       acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
     }
   }
+  FSTAMP(1, 2);
   // dpre = du * keep / (1 - p) * gelu'(pre), in place over the pre tile
 #pragma unroll
   for (int mt = 0; mt < 2; ++mt)
@@ -390,10 +436,12 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
       if (a.dpreT) *reinterpret_cast<bf16x4*>(&s.dpreT[j * TLD + 16 * mt + rq]) = dt;
     }
   __syncthreads();  // dpre image complete
+  FSTAMP(1, 3);
   if (a.dpre) copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M);
   if (a.dpreT) copy_out_t<FF>(s.dpreT, a.dpreT, a.ldT, row0, a.M);
   if (a.dxT) copy_out_t<FD>(s.dxT, a.dxT, a.ldT, row0, a.M);
 
+  FSTAMP(1, 4);
   // ---- dxn2 = dpre W1: 32 rows x this wave's 16 features, K = 512 ----
   f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
@@ -407,6 +455,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) s.g[(16 * mt + rq + r) * RLD + 16 * wave + col] = o[mt][r];
   __syncthreads();  // dxn2 rows complete
+  FSTAMP(1, 5);
 
   // ---- RMSNorm2 backward + residual, 16 threads per row:
   //   dx1 = dX + r (g2 dy) - x r^3 / d * sum(g2 dy x);  dg2 += dy x r ----
@@ -459,6 +508,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
                       dyv[4 * i + 2] * xe[4 * i + 2] * r, dyv[4 * i + 3] * xe[4 * i + 3] * r);
   }
   __syncthreads();
+  FSTAMP(1, 6);
   copy_out_f32(s.g, a.dx1, row0, a.M);
   if (tid < FD) {
     float cs = 0.f;
@@ -466,6 +516,8 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
     for (int rr = 0; rr < FBM; ++rr) cs += s.x[rr * RLD + tid];
     atomicAdd(a.dg2 + tid, cs);
   }
+  FSTAMP(1, 7);
+  FSTAMP_RT(1, 11);
 }
 
 }  // namespace

@@ -138,7 +138,7 @@ class FusedAdam:
         norm nor zeroes it.  None when not applicable (accumulate as usual).  Decided from static properties only
         (alignment, slots), so a producer makes the same choice every step: a range the update left unzeroed is
         always overwritten by the next backward."""
-        if not (self.hip and self.single_launch) or os.environ.get("MTA_OPTIM_PRODUCERS", "0") != "1":
+        if not (self.hip and self.single_launch) or os.environ.get("MTA_OPTIM_PRODUCERS", "1") == "0":
             return None
         f = self.flat
         if not grad.is_contiguous() or grad.dtype != torch.float32:

@@ -4,6 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r4c
 mkdir -p $O
+timeout -k 10 200 python -u scripts/wgrad_split_sweep.py > $O/wgrad_split.log 2>&1 || exit $?
 timeout -k 10 200 python -u scripts/debug_producers.py > $O/debug_producers.log 2>&1 || exit $?
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || exit $?
 for f in 1 0 1 0; do
