@@ -111,6 +111,7 @@ inline unsigned fused_spin_limit() {
 // wait, so phase 2 is compute + stores only (the post-barrier HBM round trip of the re-reads was ~1.5 us of a
 // ~9 us launch for the 51K-parameter headline model)
 constexpr int REG_N = 4;
+constexpr int U1 = 8, U2 = 4;  // streaming form: float4 loads in flight per thread (phase 1 / phase 2)
 
 // Gradient ranges whose producer (a weight-gradient GEMM's split-K reduce, gemm.hip mta_gemm_grad_producer) wrote
 // them by overwriting and left the clip-norm partials of them: phase 1 skips them (their squares come from ext, added
@@ -168,13 +169,22 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
       acc = fmaf(rg[r].w, rg[r].w, acc);
     }
   } else {
-    for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
-      if (cov.n && covered(cov, i)) continue;
-      const float4 q = g[i];
-      acc = fmaf(q.x, q.x, acc);
-      acc = fmaf(q.y, q.y, acc);
-      acc = fmaf(q.z, q.z, acc);
-      acc = fmaf(q.w, q.w, acc);
+    // U1 independent float4 loads in flight per thread: one workgroup per CU (the arrival wait needs them all
+    // co-resident) holds too few bytes in flight for HBM with one load per iteration (Little's law)
+    for (long i0 = (long)blockIdx.x * TPB + threadIdx.x; i0 < n4; i0 += stride * U1) {
+      float4 q[U1];
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const long i = i0 + u * stride;
+        q[u] = (i < n4 && !(cov.n && covered(cov, i))) ? g[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        acc = fmaf(q[u].x, q[u].x, acc);
+        acc = fmaf(q[u].y, q[u].y, acc);
+        acc = fmaf(q[u].z, q[u].z, acc);
+        acc = fmaf(q[u].w, q[u].w, acc);
+      }
     }
   }
   for (int k = blockIdx.x * TPB + threadIdx.x; k < cov.n_ext; k += gridDim.x * TPB) acc += cov.ext[k];
@@ -256,26 +266,42 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
     return;
   }
-  for (long i = (long)blockIdx.x * TPB + threadIdx.x; i < n4; i += stride) {
-    float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
-    float* pf = reinterpret_cast<float*>(&pp);
-    float* gf = reinterpret_cast<float*>(&gg);
-    float* mf = reinterpret_cast<float*>(&mm);
-    float* vf = reinterpret_cast<float*>(&vv);
+  // U2 elements' four streams in flight per thread (same reason as phase 1)
+  for (long i0 = (long)blockIdx.x * TPB + threadIdx.x; i0 < n4; i0 += stride * U2) {
+    float4 pp[U2], gg[U2], mm[U2], vv[U2];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = gf[k] * gs;
-      gf[k] = zero_grad ? 0.0f : gk;
-      gk = fmaf(l2, pf[k], gk);
-      mf[k] = fmaf(1.0f - beta1, gk - mf[k], mf[k]);
-      vf[k] = fmaf(beta2, vf[k], (1.0f - beta2) * gk * gk);
-      const float denom = sqrtf(vf[k]) / bc2_sqrt + eps;
-      pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
+    for (int u = 0; u < U2; ++u) {
+      const long i = i0 + u * stride;
+      if (i < n4) {
+        pp[u] = p[i];
+        gg[u] = g[i];
+        mm[u] = m[i];
+        vv[u] = v[i];
+      }
     }
-    p[i] = pp;
-    if (!(zero_grad && cov.n && covered(cov, i))) g[i] = gg;
-    m[i] = mm;
-    v[i] = vv;
+#pragma unroll
+    for (int u = 0; u < U2; ++u) {
+      const long i = i0 + u * stride;
+      if (i >= n4) continue;
+      float* pf = reinterpret_cast<float*>(&pp[u]);
+      float* gf = reinterpret_cast<float*>(&gg[u]);
+      float* mf = reinterpret_cast<float*>(&mm[u]);
+      float* vf = reinterpret_cast<float*>(&vv[u]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float gk = gf[k] * gs;
+        gf[k] = zero_grad ? 0.0f : gk;
+        gk = fmaf(l2, pf[k], gk);
+        mf[k] = fmaf(1.0f - beta1, gk - mf[k], mf[k]);
+        vf[k] = fmaf(beta2, vf[k], (1.0f - beta2) * gk * gk);
+        const float denom = sqrtf(vf[k]) / bc2_sqrt + eps;
+        pf[k] = pf[k] * decay - step_size * (mf[k] / denom);
+      }
+      p[i] = pp[u];
+      if (!(zero_grad && cov.n && covered(cov, i))) g[i] = gg[u];
+      m[i] = mm[u];
+      v[i] = vv[u];
+    }
   }
 }
 

@@ -53,7 +53,7 @@ LAUNCHER_PRESETS: Dict[str, Dict[str, Any]] = {
     "basic": {"_target_": "basic"},
     "joblib": {"_target_": "joblib", "n_jobs": -1, "backend": None, "prefer": "processes", "verbose": 0,
                "max_retries": 0, "heartbeat_timeout_s": 0},
-    "gpu_pool": {"_target_": "gpu_pool", "devices": None, "jobs_per_device": 1, "n_jobs": None, "max_retries": 0,
+    "gpu_pool": {"_target_": "gpu_pool", "devices": None, "jobs_per_device": 1, "max_jobs_per_device": 4, "n_jobs": None, "max_retries": 0,
                  "heartbeat_timeout_s": 0},
 }
 

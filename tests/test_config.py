@@ -97,3 +97,15 @@ def test_launcher_override_and_hydra_node():
     _, hy, _ = compose(CFG, "config", ["hydra/launcher=gpu_pool", "hydra.launcher.jobs_per_device=3"])
     assert hy.launcher["_target_"] == "gpu_pool" and hy.launcher.jobs_per_device == 3
     assert str(hy.sweep.subdir) == "0"
+
+
+def test_jobs_per_device_capped_at_measured_optimum():
+    """Trial packing beyond 4 per GPU measured slower in aggregate (profiles/r4_pack_sweep.jsonl): capped unless
+    max_jobs_per_device is raised."""
+    from masters_thesis_amd.config.app import MAX_JOBS_PER_DEVICE, jobs_per_device
+
+    _, hy, _ = compose(CFG, "config", ["hydra/launcher=gpu_pool", "hydra.launcher.jobs_per_device=8"])
+    assert hy.launcher.max_jobs_per_device == MAX_JOBS_PER_DEVICE == 4
+    assert jobs_per_device(hy.launcher) == 4
+    assert jobs_per_device({"jobs_per_device": 3}) == 3
+    assert jobs_per_device({"jobs_per_device": 8, "max_jobs_per_device": 8}) == 8
