@@ -140,6 +140,13 @@ __device__ __forceinline__ bool ffn_keep(uint32_t dseed, uint32_t dthr, int m, i
 __device__ __forceinline__ bf16x8 bfrag(const __bf16* w, int ldk, int n0, int k0, int lane) {
   return *reinterpret_cast<const bf16x8*>(w + (size_t)(n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
 }
+// The same fragment from a FRAGMENT-MAJOR image of a [N][K] matrix (ffn_frag_kernel below): 16 x 32 blocks of 1 KB in
+// (n / 16, k / 32) order, lane l's 8 elements at l * 8 -- one wave's fragment is 1 KB contiguous (8 full cache lines)
+// instead of 16 rows x 64 B (16 half-used lines): the fused kernels' weight loads were ~14k of their ~34k cycles per
+// workgroup (profiles/r4_ffn_probe_stamps.txt, EXP 1)
+__device__ __forceinline__ bf16x8 bfrag_fm(const __bf16* w, int K, int n0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + ((size_t)((n0 >> 4) * (K >> 5) + (k0 >> 5)) << 9) + 8 * lane);
+}
 // A fragment of 16 rows starting at r0, k-chunk k0, from an LDS image with row stride ld
 __device__ __forceinline__ bf16x8 afrag(const __bf16* img, int ld, int r0, int k0, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));
@@ -184,7 +191,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
-      bw[ks][nt] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+      bw[ks][nt] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag_fm(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
   // x1 rows: 16 threads per row, 8 columns each
   const int xr = tid >> 4, xc = 8 * (tid & 15);
   const bool rok = row0 + xr < a.M;
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   // FFN-down B fragments: this wave's 16 output features x 16 k-steps
   bf16x8 bd[16];
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bd[ks] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag(a.w2, FF, 16 * wave, 32 * ks, lane);
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag_fm(a.w2, FF, 16 * wave, 32 * ks, lane);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 1.f;
   if (a.seed) {
@@ -345,7 +352,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag(a.w2, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag_fm(a.w2, FD, 64 * wave + 16 * nt, 32 * ks, lane);
   const int xr = tid >> 4, xc = 8 * (tid & 15);
   const bool rok = row0 + xr < a.M;
   {
@@ -380,7 +387,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
   // dxn2 = dpre W1 B fragments (W1^T [128][512]: this wave's 16 features, 16 k-steps)
   bf16x8 bd[16];
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag(a.w1, FF, 16 * wave, 32 * ks, lane);
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag_fm(a.w1, FF, 16 * wave, 32 * ks, lane);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 1.f;
   if (a.seed) {
@@ -630,5 +637,58 @@ extern "C" int mta_tr_transpose_bf16(int n, const void* const* src, void* const*
     tiles = std::max(tiles, ((rows[i] + 63) / 64) * ((cols[i] + 63) / 64));
   }
   tr_wt_kernel<<<dim3(tiles, n), 256, 0, st>>>(b);
+  return 0;
+}
+
+// ---- fp32 FFN weights -> the four bf16 fragment-major images the fused kernels read (every layer, one launch) ----
+// per layer: W1 [dff][d] as (N = dff, K = d) for FFN-up, W2 [d][dff] as (N = d, K = dff) for FFN-down, and the
+// backward's W2^T (N = dff, K = d) and W1^T (N = d, K = dff); each image FD * FF elements
+namespace {
+constexpr int FRAG_MAX = 16;
+struct FragBatch {
+  const float* w1[FRAG_MAX];
+  const float* w2[FRAG_MAX];
+  __bf16* out;  // [layers][4][FD * FF]
+  int layers;
+};
+__global__ __launch_bounds__(256) void ffn_frag_kernel(FragBatch b) {
+  constexpr int CHUNKS = FD * FF / 8;  // 16-B pieces per image
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int img = blockIdx.y, layer = img >> 2, which = img & 3;
+  if (c >= CHUNKS || layer >= b.layers) return;
+  // image geometry: (N, K), source, transposed
+  const int N = (which == 0 || which == 2) ? FF : FD, K = (which == 0 || which == 2) ? FD : FF;
+  const float* src = (which == 0 || which == 3) ? b.w1[layer] : b.w2[layer];
+  const bool tr = which >= 2;
+  const int blk = c >> 6, lane = c & 63;
+  const int n = 16 * (blk / (K >> 5)) + (lane & 15), k0 = 32 * (blk % (K >> 5)) + 8 * (lane >> 4);
+  __bf16 e[8];
+  if (!tr) {
+    const float4 x0 = *reinterpret_cast<const float4*>(src + (size_t)n * K + k0);
+    const float4 x1 = *reinterpret_cast<const float4*>(src + (size_t)n * K + k0 + 4);
+    e[0] = (__bf16)x0.x; e[1] = (__bf16)x0.y; e[2] = (__bf16)x0.z; e[3] = (__bf16)x0.w;
+    e[4] = (__bf16)x1.x; e[5] = (__bf16)x1.y; e[6] = (__bf16)x1.z; e[7] = (__bf16)x1.w;
+  } else {
+    // image(n, k) = W[k][n]: W is [K][N] row-major
+#pragma unroll
+    for (int i = 0; i < 8; ++i) e[i] = (__bf16)src[(size_t)(k0 + i) * N + n];
+  }
+  uint4 v;
+  __builtin_memcpy(&v, e, 16);
+  *reinterpret_cast<uint4*>(b.out + ((size_t)img * FD * FF) + 8 * (size_t)c) = v;
+}
+}  // namespace
+
+extern "C" int mta_ffn_frag(int layers, int d, int dff, const float* const* w1, const float* const* w2, void* out,
+                            hipStream_t st) {
+  if (d != FD || dff != FF || layers < 1 || layers > FRAG_MAX) return 1;
+  FragBatch b{};
+  for (int l = 0; l < layers; ++l) {
+    b.w1[l] = w1[l];
+    b.w2[l] = w2[l];
+  }
+  b.out = static_cast<__bf16*>(out);
+  b.layers = layers;
+  ffn_frag_kernel<<<dim3(FD * FF / 8 / 256, 4 * layers), 256, 0, st>>>(b);
   return 0;
 }

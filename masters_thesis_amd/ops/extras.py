@@ -445,13 +445,22 @@ class _TransformerEncoderFn(torch.autograd.Function):
             base = 2 + nb * l
             mats += [params[base + 1], params[base + 3], params[base + 6], params[base + 8]]
         mats_b = [_padded_bf16(w, _r8(w.shape[1])) for w in mats]
+        ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
+        # fused FFN: its weights go to fragment-major images instead (W1, W2 for the forward, W2^T, W1^T for the
+        # backward; csrc/tr_ffn.hip ffn_frag), so the cast skips them
+        cast = [i for i in range(len(mats)) if not (ffn and i > 0 and (i - 1) % 4 >= 2)]
         # rows of the padded sequences (Np > N) are zero-filled by the cast itself
-        cast_pad([x.reshape(N * T, F)] + mats, [Xin] + mats_b, seeds if drop else None)
+        cast_pad([x.reshape(N * T, F)] + [mats[i] for i in cast], [Xin] + [mats_b[i] for i in cast],
+                 seeds if drop else None)
+        frag = None
+        if ffn:
+            dff0 = mats[3].shape[0]
+            frag = torch.empty((L, 4, dff0, d), device=dev, dtype=torch.bfloat16)
+            C.ffn_frag([params[2 + nb * l + 6] for l in range(L)], [params[2 + nb * l + 8] for l in range(L)], frag)
         xs = torch.empty((M, d), device=dev, dtype=torch.float32)
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
-        ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
         nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
         attn = _tr_attn_ok(d, heads, T)
         for l in range(L):
@@ -480,7 +489,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
             u = torch.empty((dff, M) if nn else (M, dff), device=dev, dtype=torch.bfloat16)
             x2 = torch.empty((M, d), device=dev, dtype=torch.float32)
             if ffn:
-                C.tr_ffn_fwd(x1, w1_b, w2_b, b1, b2, g2, RMS_EPS, seeds[l:l + 1] if drop else None, float(dropout),
+                C.tr_ffn_fwd(x1, frag[l, 0], frag[l, 1].view(d, dff), b1, b2, g2, RMS_EPS, seeds[l:l + 1] if drop else None, float(dropout),
                              None if nn else xn2, r2, pre1, None if nn else u, x2, xn2 if nn else None,
                              u if nn else None)
             else:
@@ -501,7 +510,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
         saved.append(xs)
         stats.append(rf)
         ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout), ffn, nn)
-        ctx.params, ctx.mats_b, ctx.seeds = params, mats_b, seeds
+        ctx.params, ctx.mats_b, ctx.seeds, ctx.frag = params, mats_b, seeds, frag
         if need_grad:
             ctx.save_for_backward(*saved)
             ctx.stats = stats
@@ -531,11 +540,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                stats[-1], None, 0.0, dh, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
         dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
         cast_pad([dX], [dXb])
-        if ffn:
-            # W1^T, W2^T of every layer (k-contiguous operands of the fused FFN backward), one launch
-            src = [m for l in range(L) for m in mats_b[3 + 4 * l: 5 + 4 * l]]
-            wt = [torch.empty((m.shape[1], m.shape[0]), device=dev, dtype=torch.bfloat16) for m in src]
-            C.transpose_bf16(src, wt)
+        frag = ctx.frag  # fused FFN: W2^T / W1^T fragment-major images, written by the forward's packing launch
         for l in range(L - 1, -1, -1):
             base = 2 + nb * l
             g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
@@ -549,8 +554,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
             if nn:
                 # same chain; the weight gradients then run on the transposed images as NN products (one paired launch)
                 dXt = torch.empty((d, M), device=dev, dtype=torch.bfloat16)
-                C.tr_ffn_bwd(x1, wt[2 * l], wt[2 * l + 1], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None, p, dX,
-                             dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
+                C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
+                             p, dX, dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
                 gemm(0, dXt, u, d, dff, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
                      ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
                 gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
@@ -558,8 +563,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
             elif ffn:
                 # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
                 # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
-                C.tr_ffn_bwd(x1, wt[2 * l], wt[2 * l + 1], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None, p, dX,
-                             dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
+                C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
+                             p, dX, dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
                 gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
                      ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,

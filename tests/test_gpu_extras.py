@@ -638,3 +638,23 @@ def test_mlp_32true_dropout_masks_consistent():
     fd = (vals[0] - vals[1]) / 2.0
     an = float((g * d).sum())
     assert abs(fd - an) <= 2e-2 * abs(an) + 1e-3, (fd, an)
+
+
+def test_ffn_fragment_major_packing():
+    """csrc/tr_ffn.hip ffn_frag: the four bf16 fragment-major images (W1, W2, W2^T, W1^T) hold exactly the bf16 of
+    the fp32 weights at offset ((n / 16) (K / 32) + k / 32) 512 + ((n % 16) + 16 ((k % 32) / 8)) 8 + k % 8."""
+    from masters_thesis_amd.ops._lib import lib
+
+    torch.manual_seed(0)
+    w1s = [torch.randn(512, 128, device=DEV) for _ in range(2)]
+    w2s = [torch.randn(128, 512, device=DEV) for _ in range(2)]
+    out = torch.empty((2, 4, 512, 128), device=DEV, dtype=torch.bfloat16)
+    lib().ffn_frag(w1s, w2s, out)
+    for l in range(2):
+        for which, src in enumerate((w1s[l], w2s[l], w2s[l].t(), w1s[l].t())):
+            N, K = src.shape
+            n = torch.arange(N, device=DEV).view(N, 1)
+            k = torch.arange(K, device=DEV).view(1, K)
+            off = ((n // 16) * (K // 32) + k // 32) * 512 + ((n % 16) + 16 * ((k % 32) // 8)) * 8 + k % 8
+            got = out[l, which].reshape(-1)[off.reshape(-1)].view(N, K)
+            assert torch.equal(got, src.bfloat16()), (l, which)
