@@ -85,7 +85,8 @@ int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, c
                void* pre, void* u, float* r2, float* x2, const void* dxb, const float* dx, const float* r2in,
                const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, void* uT, void* xn2T, void* dpreT,
                void* dxT, hipStream_t st);
-int mta_ffn_frag(int layers, int d, int dff, const float* const* w1, const float* const* w2, void* out, hipStream_t st);
+int mta_frag_pack(int count, const float* const* src, void* const* dst, const int* n, const int* k, const int* tr,
+                  hipStream_t st);
 int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo, const float* g1,
                     const float* bqkv, const float* bo, const float* rope, float eps, void* xn, float* r1, void* qkv,
                     void* o, float* lse, float* x1, hipStream_t st);
@@ -743,26 +744,27 @@ void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at
   TORCH_CHECK(rc == 0, "tr_ffn_bwd: unsupported configuration (d=", d, ", dff=", dff, ", rc=", rc, ")");
 }
 
-// fp32 FFN weights of every layer -> out [layers][4][d * dff] bf16 fragment-major images (csrc/tr_ffn.hip):
-// W1 and W2 for the fused forward, W2^T and W1^T for the fused backward
-void ffn_frag(std::vector<at::Tensor> w1, std::vector<at::Tensor> w2, at::Tensor out) {
-  TORCH_CHECK(!w1.empty() && w1.size() == w2.size() && w1.size() <= 16, "ffn_frag: 1..16 layers");
-  const int64_t dff = w1[0].size(0), d = w1[0].size(1);
-  std::vector<const float*> p1, p2;
-  for (size_t l = 0; l < w1.size(); ++l) {
-    MTA_CHECK_F32(w1[l]);
-    MTA_CHECK_F32(w2[l]);
-    TORCH_CHECK(w1[l].dim() == 2 && w1[l].size(0) == dff && w1[l].size(1) == d && w2[l].dim() == 2 &&
-                    w2[l].size(0) == d && w2[l].size(1) == dff,
-                "ffn_frag: W1 [dff][d], W2 [d][dff]");
-    p1.push_back(w1[l].data_ptr<float>());
-    p2.push_back(w2[l].data_ptr<float>());
+// fp32 matrices -> bf16 fragment-major [N][K] images (csrc/tr_ffn.hip): src [N][K], or with transposed[i] src [K][N]
+// and image(n, k) = src[k][n] -- the fused transformer halves' weights, every layer in one launch
+void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::vector<bool> transposed) {
+  TORCH_CHECK(!src.empty() && src.size() == dst.size() && src.size() == transposed.size() && src.size() <= 32,
+              "frag_pack: 1..32 matrices");
+  std::vector<const float*> sp;
+  std::vector<void*> dp;
+  std::vector<int> n, k, tr;
+  for (size_t i = 0; i < src.size(); ++i) {
+    MTA_CHECK_F32(src[i]);
+    MTA_CHECK_GPU(dst[i], at::kBFloat16);
+    TORCH_CHECK(src[i].dim() == 2 && dst[i].numel() == src[i].numel(), "frag_pack: shapes");
+    sp.push_back(src[i].data_ptr<float>());
+    dp.push_back(dst[i].data_ptr());
+    n.push_back((int)src[i].size(transposed[i] ? 1 : 0));
+    k.push_back((int)src[i].size(transposed[i] ? 0 : 1));
+    tr.push_back(transposed[i] ? 1 : 0);
   }
-  MTA_CHECK_GPU(out, at::kBFloat16);
-  TORCH_CHECK(out.numel() >= (int64_t)w1.size() * 4 * d * dff, "ffn_frag: out too small");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
-  const int rc = mta_ffn_frag((int)w1.size(), (int)d, (int)dff, p1.data(), p2.data(), out.data_ptr(), cur_stream());
-  TORCH_CHECK(rc == 0, "ffn_frag: unsupported configuration (d=", d, ", dff=", dff, ")");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dst[0].device());
+  const int rc = mta_frag_pack((int)sp.size(), sp.data(), dp.data(), n.data(), k.data(), tr.data(), cur_stream());
+  TORCH_CHECK(rc == 0, "frag_pack: N must be a multiple of 16 and K of 32 (rc=", rc, ")");
 }
 
 // fused attention half of a transformer block forward (csrc/tr_attn.hip): x -> xn, r1, qkv, o, lse, x1
@@ -1187,7 +1189,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     }
   });
   m.def("tr_ffn_fwd", &tr_ffn_fwd);
-  m.def("ffn_frag", &ffn_frag);
+  m.def("frag_pack", &frag_pack);
   m.def("tr_ffn_bwd", &tr_ffn_bwd);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("tr_attn_fwd", &tr_attn_fwd);

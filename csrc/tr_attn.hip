@@ -35,8 +35,8 @@ struct AttnFwdSmem {
 
 struct AttnFwdArgs {
   const float* x;       // [M][128] block input (rows seq * T + t)
-  const __bf16* wqkv;   // [384][128]
-  const __bf16* wo;     // [128][128]
+  const __bf16* wqkv;   // [384][128] fragment-major
+  const __bf16* wo;     // [128][128] fragment-major
   const float *g1, *bqkv, *bo;
   const float* rope;    // [T][16] (cos, sin)
   float eps;
@@ -45,8 +45,10 @@ struct AttnFwdArgs {
   float *r1, *lse, *x1;
 };
 
-__device__ __forceinline__ bf16x8 wfrag(const __bf16* w, int ldk, int n0, int k0, int lane) {
-  return *reinterpret_cast<const bf16x8*>(w + (size_t)(n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
+// B fragment from a fragment-major weight image (csrc/tr_ffn.hip frag_pack: 16 x 32 blocks of 1 KB, lane l's 8
+// elements at l * 8): one wave's fragment is 1 KB contiguous instead of 16 rows x 64 B
+__device__ __forceinline__ bf16x8 wfrag(const __bf16* w, int K, int n0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + ((size_t)((n0 >> 4) * (K >> 5) + (k0 >> 5)) << 9) + 8 * lane);
 }
 __device__ __forceinline__ bf16x8 lfrag(const __bf16* img, int ld, int r0, int k0, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + (r0 + (lane & 15)) * ld + k0 + 8 * (lane >> 4));

@@ -140,7 +140,7 @@ __device__ __forceinline__ bool ffn_keep(uint32_t dseed, uint32_t dthr, int m, i
 __device__ __forceinline__ bf16x8 bfrag(const __bf16* w, int ldk, int n0, int k0, int lane) {
   return *reinterpret_cast<const bf16x8*>(w + (size_t)(n0 + (lane & 15)) * ldk + k0 + 8 * (lane >> 4));
 }
-// The same fragment from a FRAGMENT-MAJOR image of a [N][K] matrix (ffn_frag_kernel below): 16 x 32 blocks of 1 KB in
+// The same fragment from a FRAGMENT-MAJOR image of a [N][K] matrix (frag_pack_kernel below): 16 x 32 blocks of 1 KB in
 // (n / 16, k / 32) order, lane l's 8 elements at l * 8 -- one wave's fragment is 1 KB contiguous (8 full cache lines)
 // instead of 16 rows x 64 B (16 half-used lines): the fused kernels' weight loads were ~14k of their ~34k cycles per
 // workgroup (profiles/r4_ffn_probe_stamps.txt, EXP 1)
@@ -640,55 +640,52 @@ extern "C" int mta_tr_transpose_bf16(int n, const void* const* src, void* const*
   return 0;
 }
 
-// ---- fp32 FFN weights -> the four bf16 fragment-major images the fused kernels read (every layer, one launch) ----
-// per layer: W1 [dff][d] as (N = dff, K = d) for FFN-up, W2 [d][dff] as (N = d, K = dff) for FFN-down, and the
-// backward's W2^T (N = dff, K = d) and W1^T (N = d, K = dff); each image FD * FF elements
+// ---- fp32 weights -> bf16 fragment-major [N][K] images (N % 16 == 0, K % 32 == 0), every one of a step in one
+// launch: the fused FFN's W1, W2 (forward) and W2^T, W1^T (backward, tr: image(n, k) = src[k][n] of a [K][N] source),
+// the fused attention half's W_qkv, W_o ----
 namespace {
-constexpr int FRAG_MAX = 16;
-struct FragBatch {
-  const float* w1[FRAG_MAX];
-  const float* w2[FRAG_MAX];
-  __bf16* out;  // [layers][4][FD * FF]
-  int layers;
+constexpr int FP_MAX = 32;
+struct FragPackBatch {
+  const float* src[FP_MAX];
+  __bf16* dst[FP_MAX];
+  int n[FP_MAX], k[FP_MAX], tr[FP_MAX];
 };
-__global__ __launch_bounds__(256) void ffn_frag_kernel(FragBatch b) {
-  constexpr int CHUNKS = FD * FF / 8;  // 16-B pieces per image
+__global__ __launch_bounds__(256) void frag_pack_kernel(FragPackBatch b) {
+  const int mi = blockIdx.y, N = b.n[mi], K = b.k[mi];
   const int c = blockIdx.x * 256 + threadIdx.x;
-  const int img = blockIdx.y, layer = img >> 2, which = img & 3;
-  if (c >= CHUNKS || layer >= b.layers) return;
-  // image geometry: (N, K), source, transposed
-  const int N = (which == 0 || which == 2) ? FF : FD, K = (which == 0 || which == 2) ? FD : FF;
-  const float* src = (which == 0 || which == 3) ? b.w1[layer] : b.w2[layer];
-  const bool tr = which >= 2;
+  if (c >= N * K / 8) return;
   const int blk = c >> 6, lane = c & 63;
   const int n = 16 * (blk / (K >> 5)) + (lane & 15), k0 = 32 * (blk % (K >> 5)) + 8 * (lane >> 4);
   __bf16 e[8];
-  if (!tr) {
-    const float4 x0 = *reinterpret_cast<const float4*>(src + (size_t)n * K + k0);
-    const float4 x1 = *reinterpret_cast<const float4*>(src + (size_t)n * K + k0 + 4);
+  if (!b.tr[mi]) {
+    const float* s = b.src[mi] + (size_t)n * K + k0;
+    const float4 x0 = *reinterpret_cast<const float4*>(s), x1 = *reinterpret_cast<const float4*>(s + 4);
     e[0] = (__bf16)x0.x; e[1] = (__bf16)x0.y; e[2] = (__bf16)x0.z; e[3] = (__bf16)x0.w;
     e[4] = (__bf16)x1.x; e[5] = (__bf16)x1.y; e[6] = (__bf16)x1.z; e[7] = (__bf16)x1.w;
   } else {
-    // image(n, k) = W[k][n]: W is [K][N] row-major
 #pragma unroll
-    for (int i = 0; i < 8; ++i) e[i] = (__bf16)src[(size_t)(k0 + i) * N + n];
+    for (int i = 0; i < 8; ++i) e[i] = (__bf16)b.src[mi][(size_t)(k0 + i) * N + n];
   }
   uint4 v;
   __builtin_memcpy(&v, e, 16);
-  *reinterpret_cast<uint4*>(b.out + ((size_t)img * FD * FF) + 8 * (size_t)c) = v;
+  *reinterpret_cast<uint4*>(b.dst[mi] + 8 * (size_t)c) = v;
 }
 }  // namespace
 
-extern "C" int mta_ffn_frag(int layers, int d, int dff, const float* const* w1, const float* const* w2, void* out,
-                            hipStream_t st) {
-  if (d != FD || dff != FF || layers < 1 || layers > FRAG_MAX) return 1;
-  FragBatch b{};
-  for (int l = 0; l < layers; ++l) {
-    b.w1[l] = w1[l];
-    b.w2[l] = w2[l];
+extern "C" int mta_frag_pack(int count, const float* const* src, void* const* dst, const int* n, const int* k,
+                             const int* tr, hipStream_t st) {
+  if (count < 1 || count > FP_MAX) return 1;
+  FragPackBatch b{};
+  int chunks = 1;
+  for (int i = 0; i < count; ++i) {
+    if (n[i] < 16 || n[i] % 16 || k[i] < 32 || k[i] % 32) return 2;
+    b.src[i] = src[i];
+    b.dst[i] = static_cast<__bf16*>(dst[i]);
+    b.n[i] = n[i];
+    b.k[i] = k[i];
+    b.tr[i] = tr[i];
+    chunks = std::max(chunks, n[i] * k[i] / 8);
   }
-  b.out = static_cast<__bf16*>(out);
-  b.layers = layers;
-  ffn_frag_kernel<<<dim3(FD * FF / 8 / 256, 4 * layers), 256, 0, st>>>(b);
+  frag_pack_kernel<<<dim3((chunks + 255) / 256, count), 256, 0, st>>>(b);
   return 0;
 }

@@ -447,22 +447,54 @@ class _TransformerEncoderFn(torch.autograd.Function):
         mats_b = [_padded_bf16(w, _r8(w.shape[1])) for w in mats]
         ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
         # fused FFN: its weights go to fragment-major images instead (W1, W2 for the forward, W2^T, W1^T for the
-        # backward; csrc/tr_ffn.hip ffn_frag), so the cast skips them
+        # backward; csrc/tr_ffn.hip frag_pack), so the cast skips them
         cast = [i for i in range(len(mats)) if not (ffn and i > 0 and (i - 1) % 4 >= 2)]
         # rows of the padded sequences (Np > N) are zero-filled by the cast itself
         cast_pad([x.reshape(N * T, F)] + [mats[i] for i in cast], [Xin] + [mats_b[i] for i in cast],
                  seeds if drop else None)
-        frag = None
+        attn = _tr_attn_ok(d, heads, T)
+        # fragment-major weight images of the fused halves, one packing launch: per layer the FFN's W1, W2 (forward)
+        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (its unfused backward keeps the casts)
+        frag, afrag = None, None
+        srcs, dsts, trs = [], [], []
         if ffn:
-            dff0 = mats[3].shape[0]
-            frag = torch.empty((L, 4, dff0, d), device=dev, dtype=torch.bfloat16)
-            C.ffn_frag([params[2 + nb * l + 6] for l in range(L)], [params[2 + nb * l + 8] for l in range(L)], frag)
+            frag = torch.empty((L, 4, mats[3].shape[0], d), device=dev, dtype=torch.bfloat16)
+            for l in range(L):
+                w1, w2 = mats[3 + 4 * l], mats[4 + 4 * l]
+                srcs += [w1, w2, w2, w1]
+                dsts += [frag[l, 0], frag[l, 1], frag[l, 2], frag[l, 3]]
+                trs += [False, False, True, True]
+        if attn:
+            afrag = [torch.empty_like(mats_b[1 + 4 * l + j]) for l in range(L) for j in (0, 1)]
+            srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1)]
+            dsts += afrag
+            trs += [False] * len(afrag)
+        for i in range(0, len(srcs), 32):
+            C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32])
         xs = torch.empty((M, d), device=dev, dtype=torch.float32)
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]
         stats: List[Tensor] = []
-        nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
         attn = _tr_attn_ok(d, heads, T)
+        # fragment-major weight images of the fused halves, one packing launch: per layer the FFN's W1, W2 (forward)
+        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (its unfused backward keeps the casts)
+        frag, afrag = None, None
+        srcs, dsts, trs = [], [], []
+        if ffn:
+            frag = torch.empty((L, 4, mats[3].shape[0], d), device=dev, dtype=torch.bfloat16)
+            for l in range(L):
+                w1, w2 = mats[3 + 4 * l], mats[4 + 4 * l]
+                srcs += [w1, w2, w2, w1]
+                dsts += [frag[l, 0], frag[l, 1], frag[l, 2], frag[l, 3]]
+                trs += [False, False, True, True]
+        if attn:
+            afrag = [torch.empty_like(mats_b[1 + 4 * l + j]) for l in range(L) for j in (0, 1)]
+            srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1)]
+            dsts += afrag
+            trs += [False] * len(afrag)
+        for i in range(0, len(srcs), 32):
+            C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32])
+        nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
         for l in range(L):
             base = 2 + nb * l
             g1, bqkv, bo, g2, b1, b2 = (params[base], params[base + 2], params[base + 4], params[base + 5],
@@ -476,7 +508,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
             lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
             x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             if attn:
-                C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, wqkv_b, wo_b, g1, bqkv, bo, xn, r1, qkv, o, lse, x1)
+                C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, afrag[2 * l], afrag[2 * l + 1], g1, bqkv, bo, xn, r1, qkv, o, lse, x1)
             else:
                 C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
                        None, None, None, None)

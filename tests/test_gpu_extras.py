@@ -641,15 +641,16 @@ def test_mlp_32true_dropout_masks_consistent():
 
 
 def test_ffn_fragment_major_packing():
-    """csrc/tr_ffn.hip ffn_frag: the four bf16 fragment-major images (W1, W2, W2^T, W1^T) hold exactly the bf16 of
-    the fp32 weights at offset ((n / 16) (K / 32) + k / 32) 512 + ((n % 16) + 16 ((k % 32) / 8)) 8 + k % 8."""
+    """csrc/tr_ffn.hip frag_pack: the fused FFN's four bf16 fragment-major images (W1, W2, W2^T, W1^T) hold exactly
+    the bf16 of the fp32 weights at offset ((n / 16) (K / 32) + k / 32) 512 + ((n % 16) + 16 ((k % 32) / 8)) 8 + k % 8."""
     from masters_thesis_amd.ops._lib import lib
 
     torch.manual_seed(0)
     w1s = [torch.randn(512, 128, device=DEV) for _ in range(2)]
     w2s = [torch.randn(128, 512, device=DEV) for _ in range(2)]
     out = torch.empty((2, 4, 512, 128), device=DEV, dtype=torch.bfloat16)
-    lib().ffn_frag(w1s, w2s, out)
+    lib().frag_pack([w for l in range(2) for w in (w1s[l], w2s[l], w2s[l], w1s[l])],
+                    [out[l, i] for l in range(2) for i in range(4)], [False, False, True, True] * 2)
     for l in range(2):
         for which, src in enumerate((w1s[l], w2s[l], w2s[l].t(), w1s[l].t())):
             N, K = src.shape
