@@ -1105,10 +1105,27 @@ inline bool pipe_on() {
   return on;
 }
 
+// the same two-stage loop for the 64 x 64 x 128 k-contiguous tiles (the transformer's long-K weight gradients on
+// transposed activations and its K = 128 products).  Opt-in (MTA_GEMM_PIPE64=1): measured no faster, 0-10 % slower
+// on the wgrad shapes even with one workgroup streaming K = 6,240 alone (profiles/r4_gemm_pipe64_negative.txt)
+inline bool pipe64_on() {
+  static const bool on = [] {
+    const char* e = getenv("MTA_GEMM_PIPE64");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
   const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
   const int blocks = nx * ny * ksplit;
+  if constexpr (BM == 64 && BKT == 128 && !AT && !BT) {
+    if (pipe64_on()) {
+      gemm_bf16_kernel<BM, BN, BKT, AT, BT, true><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
+      return;
+    }
+  }
   if constexpr (BM == 128 && !AT && !BT) {
     if (pipe_on()) {
       gemm_bf16_kernel<BM, BN, BKT, AT, BT, true><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
@@ -1242,8 +1259,15 @@ template <int BM, int BN, int BKT, int KIND>
 void launch_pair_cfg(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   PairGrid pg{(g1.N + BN - 1) / BN, (g1.M + BM - 1) / BM, k1, (g2.N + BN - 1) / BN, (g2.M + BM - 1) / BM, k2};
   const int blocks = pg.nx1 * pg.ny1 * pg.nz1 + pg.nx2 * pg.ny2 * pg.nz2;
-  if constexpr (KIND == 0)
+  if constexpr (KIND == 0) {
+    if constexpr (BM == 64 && BKT == 128) {
+      if (pipe64_on()) {
+        gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
+        return;
+      }
+    }
     gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+  }
   else if constexpr (KIND == 1)
     gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
   else
