@@ -10,6 +10,8 @@
 // Writes exactly what the unfused forward saves for the backward: xn, r1, qkv (UNROTATED, bias added, bf16), o, LSE,
 // x1 -- staged through LDS into row-contiguous 16-B stores.
 // Reference semantics: models/extras.py transformer_reference; ops/extras.py the unfused chain; csrc/attention.hip.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -43,6 +45,7 @@ struct AttnFwdArgs {
   int T;
   __bf16 *xn, *qkv, *o;
   float *r1, *lse, *x1;
+  int split;  // 1: two workgroups per sequence, one per 32-query half (each recomputes the shared xn / k / v)
 };
 
 // B fragment from a fragment-major weight image (csrc/tr_ffn.hip frag_pack: 16 x 32 blocks of 1 KB, lane l's 8
@@ -58,7 +61,10 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   AttnFwdSmem& s = *reinterpret_cast<AttnFwdSmem*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int seq = blockIdx.x, T = a.T;
+  const bool split = a.split != 0;
+  const int seq = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, T = a.T;
+  const int qh = split ? (int)(blockIdx.x & 1) : 0;  // query half (split): rows 32 qh .. 32 qh + 31 are this WG's
+  auto own = [&](int r) { return !split || (r >> 5) == qh; };
   const size_t grow0 = (size_t)seq * T;
   const int rq = 4 * (lane >> 4), col = lane & 15;
 
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
     __builtin_memcpy(&p1, yb + 8, 16);
     *reinterpret_cast<uint4*>(&s.xo[xr * BLD + xc]) = p0;
     *reinterpret_cast<uint4*>(&s.xo[xr * BLD + xc + 8]) = p1;
-    if (rok) {
+    if (rok && own(xr)) {
       *reinterpret_cast<uint4*>(a.xn + (grow0 + xr) * AD + xc) = p0;
       *reinterpret_cast<uint4*>(a.xn + (grow0 + xr) * AD + xc + 8) = p1;
       if ((tid & 7) == 0) a.r1[grow0 + xr] = rs;
@@ -165,7 +171,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < AT * (AQ / 8) / ATH; ++i) {
     const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
-    if (r < T)
+    if (r < T && own(r))
       *reinterpret_cast<uint4*>(a.qkv + (grow0 + r) * AQ + 8 * c8) =
           *reinterpret_cast<const uint4*>(&s.u.qkv[r * QLD + 8 * c8]);
   }
@@ -177,7 +183,8 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
     __bf16* pw = s.u.p[wave];  // this wave's 32 P rows
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
-      const int qi = 2 * (wave & 1) + qq;
+      if (split && qq > 0) break;  // split: one query tile per wave (this half's tiles 2 qh, 2 qh + 1)
+      const int qi = split ? 2 * qh + (wave & 1) : 2 * (wave & 1) + qq;
       f32x4 sc[4];
       const bf16x8 aq = lfrag(s.q, BLD, 16 * qi, AHD * h, lane);
 #pragma unroll
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < AT * (AD / 8) / ATH; ++i) {
     const int idx = tid + ATH * i, r = idx / (AD / 8), c8 = idx % (AD / 8);
-    if (r < T)
+    if (r < T && own(r))
       *reinterpret_cast<uint4*>(a.o + (grow0 + r) * AD + 8 * c8) = *reinterpret_cast<const uint4*>(&s.xo[r * BLD + 8 * c8]);
   }
 #pragma unroll
@@ -237,7 +244,8 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) pacc[mt] = mfma16x16x32(lfrag(s.xo, BLD, 16 * mt, 32 * ks, lane), bp[ks], pacc[mt]);
+    for (int mt = 0; mt < 4; ++mt)
+      if (!split || (mt >> 1) == qh) pacc[mt] = mfma16x16x32(lfrag(s.xo, BLD, 16 * mt, 32 * ks, lane), bp[ks], pacc[mt]);
   __syncthreads();  // x rows staged
   {
     const int n = 16 * wave + col;
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
     const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
-    if (r < T)
+    if (r < T && own(r))
       *reinterpret_cast<float4*>(a.x1 + (grow0 + r) * AD + 4 * c4) = *reinterpret_cast<const float4*>(&s.u.x[r * XLDF + 4 * c4]);
   }
 }
@@ -285,6 +293,13 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   a.r1 = r1;
   a.lse = lse;
   a.x1 = x1;
-  tr_attn_fwd_kernel<<<nseq, ATH, sizeof(AttnFwdSmem), st>>>(a);
+  // two workgroups per sequence (query halves) with MTA_TR_ATTN_SPLIT=1: 2 x 104 sequences still fit one wave of
+  // workgroups on the 256 CUs, and each recomputes only the shared norm / K / V
+  static const bool split_on = [] {
+    const char* e = getenv("MTA_TR_ATTN_SPLIT");
+    return e && e[0] == '1';
+  }();
+  a.split = split_on && T > 32 ? 1 : 0;
+  tr_attn_fwd_kernel<<<nseq * (a.split ? 2 : 1), ATH, sizeof(AttnFwdSmem), st>>>(a);
   return 0;
 }
