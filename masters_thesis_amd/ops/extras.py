@@ -80,12 +80,18 @@ def set_deterministic(flag: bool) -> None:
     _DETERMINISTIC[0] = bool(flag)
 
 
+# workgroup target of a split-K weight gradient (MTA_WGRAD_WGS for the A/B): 128, so that a (weight-gradient,
+# input-gradient) pair of the transformer (~128 + ~196 workgroups) runs as one wave of workgroups and the fp32 atomics
+# halve -- transformer B=1 0.565 -> 0.528 ms; 64: 0.586, 256: 0.565, 512: 0.638 (profiles/r4_wgrad_wgs_sweep.txt)
+_WGRAD_WGS = int(os.environ.get("MTA_WGRAD_WGS", "128"))
+
+
 def wgrad_split(M: int, N: int, K: int) -> int:
-    """Split-K count for a weight-gradient GEMM: ~256 workgroups, >= 4 k-slices of 32 each."""
+    """Split-K count for a weight-gradient GEMM: ~_WGRAD_WGS workgroups, >= 4 k-slices of 32 each."""
     if _DETERMINISTIC[0]:
         return 1
     tiles = -(-M // 64) * -(-N // 64)
-    return max(1, min(256 // max(tiles, 1), K // 128))
+    return max(1, min(_WGRAD_WGS // max(tiles, 1), K // 128))
 
 
 def cast_pad(srcs: Sequence[Tensor], dsts: Sequence[Tensor], seeds: Optional[Tensor] = None) -> None:
