@@ -1332,11 +1332,22 @@ void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
 // Eligible for the 256 x 256 kernel: 32-deep k-tiles and enough macro-tiles to fill at least half the CUs; the
 // split-K accumulating form is re-split towards one wave of 256 workgroups (>= 8 k-tiles per split).  Returns the
 // split it runs with (g.k_per_split updated), 0 = not eligible.
+// workgroup target of the split accumulating form (MTA_BIG_WGS for the A/B; default one per CU: 128 / 192 / 384 / 512
+// measured slower on mlp_large, profiles/r4_big_wgs_sweep.txt)
+inline long big_wgs() {
+  static const long v = [] {
+    const char* e = getenv("MTA_BIG_WGS");
+    const long x = e ? atol(e) : 256;
+    return x >= 64 && x <= 2048 ? x : 256L;
+  }();
+  return v;
+}
+
 int big_split(GemmArgs& g, int ksplit) {
   if (!big_on() || g.K % big::KT || g.M < 64 || g.N < 64) return 0;
   const long tiles = (long)((g.M + big::TM - 1) / big::TM) * ((g.N + big::TN - 1) / big::TN);
-  if ((g.flags & EPI_ACCUM) && tiles * ksplit < 256) {
-    int ks = (int)std::max(1L, 256 / tiles);
+  if ((g.flags & EPI_ACCUM) && tiles * ksplit < big_wgs()) {
+    int ks = (int)std::max(1L, big_wgs() / tiles);
     ks = std::min(ks, std::max(1, g.K / 256));
     if (ks > ksplit) {
       int kps = (g.K + ks - 1) / ks;
