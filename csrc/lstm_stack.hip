@@ -51,8 +51,10 @@ __device__ unsigned long long mta_stack_tl[2][64][4];
 #ifndef MTA_STACK_GX_DELAY
 #define MTA_STACK_GX_DELAY 0
 #endif
+// DX: 4 (the backward gradient waves yield the SIMD to the recurrent waves' MFMA chain for ~256 cycles after each step
+// barrier): bwd 98.0 -> 94.5 us at the headline shape; 2: 96, 6: 95.2, 8: 98.2, 12: 104 (profiles/r4_lstm_knobs.txt)
 #ifndef MTA_STACK_DX_DELAY
-#define MTA_STACK_DX_DELAY 0
+#define MTA_STACK_DX_DELAY 4
 #endif
 // timing-only debug switches (results are garbage): input / store waves only run their barriers, recurrent waves
 // skip the staging writes
@@ -77,9 +79,10 @@ __device__ unsigned long long mta_stack_tl[2][64][4];
 #ifndef MTA_STACK_DG_MODE
 #define MTA_STACK_DG_MODE 0
 #endif
-// static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD
+// static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD: on
+// (fwd 80.0 -> 79.5 us, with DX_DELAY 4 bwd 94.1 us; profiles/r4_lstm_knobs.txt)
 #ifndef MTA_STACK_PRIO
-#define MTA_STACK_PRIO 0
+#define MTA_STACK_PRIO 1
 #endif
 #if MTA_STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
