@@ -21,6 +21,8 @@ import torch
 from torch import Tensor
 
 from ..ops import extras as xops
+from ..ops._lib import use_hip
+from ..ops.losses import heads_losses_train, train_decoder_fits
 from . import register_model_class
 from .lstm import FinancialLstmCombined, FinancialLstmMse, FinancialLstmNll
 
@@ -166,8 +168,39 @@ def _make(base, arch: str):
         self.encoder.precision = self.matmul_precision
         return self.encoder(x)
 
-    cls = type(name, (base,), {"__init__": __init__, "encode": encode, "__doc__": f"{base.__name__} with the {arch} "
-                                                                                   f"encoder (north-star extra)."})
+    def fused_step_supported(self, batch) -> bool:
+        """The training step as [encoder forward (HIP autograd Function), the one-launch decoder (losses, metrics,
+        dh, head grads: ops.losses.heads_losses_train), encoder backward from dh]: two decoder launches (the
+        heads/losses forward and its backward) become one.  HIP path, decoder small enough for one workgroup."""
+        x, y = batch[0], batch[1]
+        if self.backend == "torch" or not use_hip(x) or not self.training:
+            return False
+        if any(p.grad is None for p in self.parameters()):
+            return False
+        return train_decoder_fits(int(x.shape[0]) * int(x.shape[1]), int(y.shape[2]),
+                                  int(self.alpha_head.weight.shape[1]))
+
+    def fused_training_step(self, batch, batch_idx):
+        """``training_step`` + ``loss.backward()`` with the decoder in one launch (same math and metric bookkeeping
+        as the autograd path: tests/test_gpu_extras.py)."""
+        if getattr(batch, "pending", False):
+            batch.materialize()
+        context, target, factor, inv_psi, B = self._unpack(batch)
+        h = self.encode(context)
+        c_nll, c_mse = self.loss_coefficients
+        grads = (self.alpha_head.weight.grad, self.alpha_head.bias.grad, self.beta_head.weight.grad,
+                 self.beta_head.bias.grad)
+        out, dh = heads_losses_train(h.detach(), self.alpha_head.weight, self.alpha_head.bias,
+                                     self.beta_head.weight, self.beta_head.bias, target, factor, inv_psi,
+                                     batch_windows=B, want_nll=self.want_nll, nll_mode=self.nll_mode, c_nll=c_nll,
+                                     c_mse=c_mse, acc=self.train_acc.acc, grads=grads)
+        h.backward(dh)
+        self._log_stage("train", self.train_acc, self.train_log_names)
+        return out[3]
+
+    cls = type(name, (base,), {"__init__": __init__, "encode": encode, "fused_step_supported": fused_step_supported,
+                               "fused_training_step": fused_training_step,
+                               "__doc__": f"{base.__name__} with the {arch} encoder (north-star extra)."})
     return cls
 
 

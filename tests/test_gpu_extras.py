@@ -659,3 +659,38 @@ def test_ffn_fragment_major_packing():
             off = ((n // 16) * (K // 32) + k // 32) * 512 + ((n % 16) + 16 * ((k % 32) // 8)) * 8 + k % 8
             got = out[l, which].reshape(-1)[off.reshape(-1)].view(N, K)
             assert torch.equal(got, src.bfloat16()), (l, which)
+
+
+@pytest.mark.parametrize("arch", ["mlp", "transformer"])
+def test_extras_fused_training_step_matches_autograd(arch):
+    """models/extras.py fused_training_step (encoder forward, the one-launch decoder ops.losses.heads_losses_train,
+    encoder backward from its dh) against training_step + loss.backward(): same loss, metrics and every gradient."""
+    from masters_thesis_amd.models import get_model_class
+
+    g = torch.Generator().manual_seed(0)
+    batch = [torch.randn(1, 100, 60, 3, generator=g).to(DEV), (torch.randn(1, 100, 30, 4, generator=g) * 0.01).to(DEV),
+             torch.stack([torch.randn(1, generator=g) * 0.01, torch.rand(1, generator=g) * 1e-3 + 1e-4], -1).to(DEV),
+             (torch.rand(1, 100, generator=g) * 3 + 1).to(DEV)]
+    torch.manual_seed(1)
+    kw = dict(hidden_size=128, num_layers=2, dropout=0.0) if arch == "transformer" else dict(hidden_size=256,
+                                                                                            num_layers=2, dropout=0.0)
+    model = get_model_class("FinancialLstmCombined", arch)(input_size=3, **kw).to(DEV)
+    model.train()
+    res = []
+    for fused in (False, True):
+        for p in model.parameters():
+            p.grad = torch.zeros_like(p)
+        model.train_acc.reset()
+        if fused:
+            assert model.fused_step_supported(batch)
+            loss = model.fused_training_step(batch, 0)
+        else:
+            loss = model.training_step(batch, 0)
+            loss.backward()
+        torch.cuda.synchronize()
+        res.append((loss.detach().clone(), [p.grad.detach().clone() for p in model.parameters()],
+                    model.train_acc.acc.detach().clone()))
+    assert _rel(res[0][0], res[1][0]) < 1e-5
+    assert _rel(res[0][2], res[1][2]) < 1e-5
+    for a, b in zip(res[0][1], res[1][1]):
+        assert _rel(a, b) < 1e-4
