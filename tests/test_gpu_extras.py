@@ -358,8 +358,8 @@ def test_extras_dropout_train_vs_eval_and_finite_grads():
 
 @pytest.mark.parametrize("arch", ["mlp", "transformer"])
 def test_extras_train_through_trainer_graph(arch):
-    """The extras encoders through the Trainer's captured training step (graph warm-up, capture, replays):
-    the fused-LSTM step must not be taken for them, and training must stay finite."""
+    """The extras encoders through the Trainer's captured training step (graph warm-up, capture, replays) with their
+    fused step (one-launch decoder, models/extras.py fused_training_step): captured and replayed, training finite."""
     from masters_thesis_amd.data.datamodule import TensorBatchLoader
     from masters_thesis_amd.engine import Trainer
     from masters_thesis_amd.models import get_model_class
@@ -381,7 +381,7 @@ def test_extras_train_through_trainer_graph(arch):
     tr._setup_model(model)
     tr._configure_optimizers(model)
     model.train()
-    assert not model.fused_step_supported([t.to(DEV) for t in data])
+    assert model.fused_step_supported([t.to(DEV) for t in data])
     step = tr.make_train_stepper(TensorBatchLoader([t.to(DEV) for t in data], 1, shuffle=True, seed=0))
     for _ in range(8):
         loss = step()
