@@ -40,7 +40,7 @@ int mta_heads_losses_train(const float* h, int H, const float* wa, const float* 
                            const float* y, const float* factor, const float* inv_psi, int N, int n, int C, int windows,
                            int kwin, int factor_stride, int want_nll, float c_nll, float c_mse, float batch_weight,
                            float* out, double* acc, float* dh, float* g_wa, float* g_ba, float* g_wb, float* g_bb,
-                           hipStream_t st);
+                           int dh_rows, hipStream_t st);
 void mta_heads_losses(const float* h, int H, const float* wa, const float* ba, const float* wb, const float* bb,
                       float* ab_out, const float* y, const float* factor, const float* inv_psi, int N, int n, int C,
                       int windows, int kwin, int factor_stride, int want_nll, float c_nll, float c_mse,
@@ -400,7 +400,8 @@ bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor w
   TORCH_CHECK(h.dim() == 2, "h must be (N, H)");
   const int64_t N = h.size(0), H = h.size(1);
   TORCH_CHECK(wa.numel() == H && wb.numel() == H && ba.numel() == 1 && bb.numel() == 1, "bad head shapes");
-  TORCH_CHECK(dh.numel() == N * H && g_wa.numel() == H && g_wb.numel() == H && g_ba.numel() == 1 &&
+  // dh may hold padded rows beyond N (the MLP encoder's 16-row padding): the launch zero-fills them
+  TORCH_CHECK(dh.numel() >= N * H && dh.numel() % H == 0 && g_wa.numel() == H && g_wb.numel() == H && g_ba.numel() == 1 &&
                   g_bb.numel() == 1, "dh / head gradient shapes");
   TORCH_CHECK(y.is_cuda() && y.scalar_type() == at::kFloat && y.is_contiguous() && y.dim() == 3 && y.size(0) == N &&
                   y.size(2) >= 2, "y must be (N, n, C >= 2) fp32");
@@ -416,7 +417,8 @@ bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor w
       bb.data_ptr<float>(), y.data_ptr<float>(), factor.data_ptr<float>(), inv_psi.data_ptr<float>(), (int)N,
       (int)y.size(1), (int)y.size(2), (int)windows, (int)kwin, (int)factor_stride, want_nll ? 1 : 0, (float)c_nll,
       (float)c_mse, (float)batch_weight, out.data_ptr<float>(), opt_acc(acc), dh.data_ptr<float>(),
-      g_wa.data_ptr<float>(), g_ba.data_ptr<float>(), g_wb.data_ptr<float>(), g_bb.data_ptr<float>(), cur_stream());
+      g_wa.data_ptr<float>(), g_ba.data_ptr<float>(), g_wb.data_ptr<float>(), g_bb.data_ptr<float>(),
+      (int)(dh.numel() / H), cur_stream());
   return rc == 0;
 }
 

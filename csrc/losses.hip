@@ -48,7 +48,13 @@ struct LossArgs {
   float* gmse;           // (N, 2) d mse / d (alpha, beta)
   float* gnll;           // (N, 2) d nll / d (alpha, beta)
   double* acc;           // optional metric accumulator (8 doubles) or nullptr
+  int dh_rows;           // training decoders: dh rows [N, dh_rows) are zero-filled (the encoder's padded rows)
 };
+
+// the encoder's padded rows of dh (their sequences do not exist): zeros, written by the decoder launch itself
+__device__ __forceinline__ void zero_dh_pad(float* dh, int N, int H, int rows) {
+  for (long i = (long)N * H + threadIdx.x; i < (long)rows * H; i += blockDim.x) dh[i] = 0.f;
+}
 
 // Work split: one wave per sequence, lanes over the n target days (looping when n > 64);
 // every per-sequence sum is a wave reduction, u_t accumulates with LDS atomics whose
@@ -284,6 +290,7 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
     const float* __restrict__ h, int H, const float* __restrict__ wa, const float* __restrict__ ba,
     const float* __restrict__ wb, const float* __restrict__ bb, LossArgs A, float* __restrict__ dh,
     float* __restrict__ g_wa, float* __restrict__ g_ba, float* __restrict__ g_wb, float* __restrict__ g_bb) {
+  zero_dh_pad(dh, A.N, H, A.dh_rows);
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int N = A.N, n = A.n;
   const int N2 = 2 * ((N + 1) & ~1);
@@ -369,6 +376,7 @@ __global__ __launch_bounds__(TPB) void decoder_train_reg_kernel(
     const float* __restrict__ wb, const float* __restrict__ bb, LossArgs A, float* __restrict__ dh,
     float* __restrict__ g_wa, float* __restrict__ g_ba, float* __restrict__ g_wb, float* __restrict__ g_bb) {
   constexpr int H = 4 * G, SPP = TPB / G;  // sequences per h pass
+  zero_dh_pad(dh, A.N, H, A.dh_rows);
   __shared__ float2 ab[RD_MAXN], dab[RD_MAXN];
   __shared__ float cpart[RD_MAXN * 33];    // w_i b_i D_it, row i (stride 33); later the head-gradient partials
   __shared__ float upart[RD_MAXW][32][33];  // u_t partials: [window][sequence residue q][t]
@@ -1014,9 +1022,10 @@ extern "C" int mta_heads_losses_train(const float* h, int H, const float* wa, co
                                       const float* bb, const float* y, const float* factor, const float* inv_psi,
                                       int N, int n, int C, int windows, int kwin, int factor_stride, int want_nll,
                                       float c_nll, float c_mse, float batch_weight, float* out, double* acc, float* dh,
-                                      float* g_wa, float* g_ba, float* g_wb, float* g_bb, hipStream_t st) {
+                                      float* g_wa, float* g_ba, float* g_wb, float* g_bb, int dh_rows,
+                                      hipStream_t st) {
   LossArgs A{y, factor, inv_psi, N, n, C, windows, kwin, factor_stride, want_nll, c_nll, c_mse, batch_weight,
-             out, nullptr, nullptr, acc};
+             out, nullptr, nullptr, acc, dh_rows < N ? N : dh_rows};
   if (decoder_reg_fits(h, y, dh, wa, wb, H, N, n, C, windows, kwin, want_nll)) {
     switch (H) {
       case 16: launch_decoder_reg<4>(h, wa, ba, wb, bb, A, dh, g_wa, g_ba, g_wb, g_bb, st); break;

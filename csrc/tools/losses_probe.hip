@@ -56,7 +56,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     CK(hipEventRecord(a));
     mta_heads_losses_train(h, H, wa, ba, wb, bb, y, fac, ip, N, n, C, 1, N, 0, want_nll, 1.f, 1.f, 1.f, out, acc, dh,
-                           g, g + H, g + H + 1, g + 2 * H + 1, 0);
+                           g, g + H, g + H + 1, g + 2 * H + 1, N, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float m;
@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
   // one fresh call for the values (the head gradients accumulate)
   CK(hipMemset(g, 0, (2 * H + 2) * 4));
   mta_heads_losses_train(h, H, wa, ba, wb, bb, y, fac, ip, N, n, C, 1, N, 0, want_nll, 1.f, 1.f, 1.f, out, acc, dh,
-                         g, g + H, g + H + 1, g + 2 * H + 1, 0);
+                         g, g + H, g + H + 1, g + 2 * H + 1, N, 0);
   CK(hipDeviceSynchronize());
   std::vector<float> ho(4), hdh((size_t)N * H), hg(2 * H + 2);
   CK(hipMemcpy(ho.data(), out, 16, hipMemcpyDeviceToHost));

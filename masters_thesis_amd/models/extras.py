@@ -190,11 +190,18 @@ def _make(base, arch: str):
         c_nll, c_mse = self.loss_coefficients
         grads = (self.alpha_head.weight.grad, self.alpha_head.bias.grad, self.beta_head.weight.grad,
                  self.beta_head.bias.grad)
+        N, H = h.shape
+        dh_buf = None
+        if arch == "mlp" and N % 16:
+            # the MLP encoder runs 16-row padded: the decoder writes dh into that padded shape with zero pad rows,
+            # so the encoder backward reads it in place (no zero-fill + copy launches)
+            dh_buf = torch.empty(((N + 15) // 16 * 16, H), device=h.device, dtype=torch.float32)
+            dh_buf._mta_zero_pad = True
         out, dh = heads_losses_train(h.detach(), self.alpha_head.weight, self.alpha_head.bias,
                                      self.beta_head.weight, self.beta_head.bias, target, factor, inv_psi,
                                      batch_windows=B, want_nll=self.want_nll, nll_mode=self.nll_mode, c_nll=c_nll,
-                                     c_mse=c_mse, acc=self.train_acc.acc, grads=grads)
-        h.backward(dh)
+                                     c_mse=c_mse, acc=self.train_acc.acc, grads=grads, dh=dh_buf)
+        h.backward(dh if dh_buf is None else dh_buf[:N])
         self._log_stage("train", self.train_acc, self.train_log_names)
         return out[3]
 

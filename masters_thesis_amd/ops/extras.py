@@ -210,8 +210,12 @@ class _MlpEncoderFn(torch.autograd.Function):
         Xs, pres, acts = saved[:L], saved[L:2 * L], saved[2 * L:]
         means, rstds = ctx.stats
         dev = dh.device
+        base = dh._base
         if Mp == N and dh.dtype == torch.float32 and dh.is_contiguous():
             dy = dh  # read-only below: no zero-fill + copy of the output gradient
+        elif (getattr(base, "_mta_zero_pad", False) and base.shape == (Mp, dims[-1]) and base.is_contiguous()
+              and dh.data_ptr() == base.data_ptr() and dh.shape[0] == N):
+            dy = base  # the fused step's decoder wrote dh into a padded buffer with zero pad rows
         else:
             dy = torch.empty((Mp, dims[-1]), device=dev, dtype=torch.float32)
             dy[:N].copy_(dh)
