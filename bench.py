@@ -14,6 +14,11 @@ exactly as ``train.py`` runs it.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model M] [--trainer T] [--concurrent k]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+``--gpus N`` without a torchrun environment starts the N ranks itself (parallel/launch.py: ranks 1..N-1 are fresh
+child processes re-running this command, this process is rank 0; one rank per GPU, ranks share GPUs only when
+fewer are visible).  The record reports the process group's world size, the visible device count and the
+gradient all-reduce that ran.
+
 Weak scaling: ``--batch`` windows per GPU per step (global batch = B * N).
 Prints exactly one JSON line (rank 0) on stdout.
 """
@@ -156,11 +161,16 @@ def main(argv=None):
     from masters_thesis_amd.engine import Trainer
     from masters_thesis_amd.models import get_model_class, model_params_from_config
     from masters_thesis_amd.parallel import dist as pdist
+    from masters_thesis_amd.parallel import launch
 
+    if args.gpus > 1 and not launch.in_launched_job():
+        launch.launch_script_ranks(args.gpus)  # before anything touches the GPU
     denv = pdist.init_distributed()
     world = denv.world_size
-    if args.gpus != world and world > 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    pg_world = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+    if not (world == pg_world == args.gpus):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the job has WORLD_SIZE={world} (process group "
+                         f"{pg_world}): refusing to report a different world than asked for")
     dev = denv.device
     torch.manual_seed(1234 + denv.rank)
 
@@ -256,6 +266,9 @@ def main(argv=None):
             "value": round(value, 3),
             "unit": "samples/s",
             "n_gpus": world,
+            "world_size": pg_world,
+            "visible_devices": torch.cuda.device_count() if dev.type == "cuda" else 0,
+            "process_group": denv.backend or "none",
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),

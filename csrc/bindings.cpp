@@ -1150,6 +1150,34 @@ class HostPrefetcher {
   void* h_ = nullptr;
 };
 
+// Node census of a captured HIP graph (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()): the type of every
+// node, child graphs walked recursively.  The trainer's step graphs must hold kernel nodes only (a captured memset
+// node was the root of the r3 multi-process NaN, profiles/r4_nan_root_cause.txt); tests assert it.
+static void graph_node_types_rec(hipGraph_t g, std::vector<int64_t>& out, int depth) {
+  size_t n = 0;
+  TORCH_CHECK(hipGraphGetNodes(g, nullptr, &n) == hipSuccess, "hipGraphGetNodes (count) failed");
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n) TORCH_CHECK(hipGraphGetNodes(g, nodes.data(), &n) == hipSuccess, "hipGraphGetNodes failed");
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    TORCH_CHECK(hipGraphNodeGetType(nodes[i], &t) == hipSuccess, "hipGraphNodeGetType failed");
+    if (t == hipGraphNodeTypeGraph && depth < 8) {
+      hipGraph_t child;
+      TORCH_CHECK(hipGraphChildGraphNodeGetGraph(nodes[i], &child) == hipSuccess, "child graph lookup failed");
+      graph_node_types_rec(child, out, depth + 1);
+    } else {
+      out.push_back((int64_t)t);
+    }
+  }
+}
+
+static std::vector<int64_t> graph_node_types(int64_t graph) {
+  TORCH_CHECK(graph != 0, "graph_node_types: null graph (capture with keep_graph=True)");
+  std::vector<int64_t> out;
+  graph_node_types_rec(reinterpret_cast<hipGraph_t>(graph), out, 0);
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   py::class_<HostPrefetcher>(m, "HostPrefetcher")
       .def(py::init<std::vector<at::Tensor>, std::vector<at::Tensor>, int64_t, int64_t, int64_t>())
@@ -1161,6 +1189,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("close", &HostPrefetcher::close);
   m.doc() = "masters_thesis_amd CDNA4 (gfx950) HIP kernels";
   m.def("dgp", &dgp);
+  m.def("graph_node_types", &graph_node_types);
+  m.attr("GRAPH_NODE_KERNEL") = (int64_t)hipGraphNodeTypeKernel;
+  m.attr("GRAPH_NODE_MEMCPY") = (int64_t)hipGraphNodeTypeMemcpy;
+  m.attr("GRAPH_NODE_MEMSET") = (int64_t)hipGraphNodeTypeMemset;
   m.def("ols_features", &ols_features);
   m.def("lstm_stack_fwd", &lstm_stack_fwd);
   m.def("lstm_stack_fwd_gather", &lstm_stack_fwd_gather);

@@ -39,6 +39,7 @@ from .nodes import DictConfig, OmegaConf
 log = logging.getLogger("masters_thesis_amd.config")
 
 _ENV_CHILD = "MTA_SWEEP_CHILD"
+_ENV_RUN_DIR = "MTA_HYDRA_RUN_DIR"
 
 
 def _parse_argv(argv: Sequence[str]):
@@ -91,9 +92,16 @@ def _run_job(task_fn, config_dir, config_name, overrides: List[Override], job_nu
         hydra_cfg["mode"] = "MULTIRUN"
     else:
         run_dir = Path(str(hydra_cfg["run"]["dir"]))
+    # ranks 1..N-1 started by the trainer's own launcher (parallel/launch.py) re-run this script a moment later:
+    # they share rank 0's run directory (exported below) and leave its .hydra files and job log to rank 0
+    child_rank = int(os.environ.get("RANK", "0")) > 0 and os.environ.get(_ENV_RUN_DIR)
+    if child_rank:
+        run_dir = Path(os.environ[_ENV_RUN_DIR])
     hydra_cfg["runtime"]["output_dir"] = str(run_dir.resolve())
-    _write_hydra_dir(run_dir, job_cfg, hydra_cfg, overrides)
-    _attach_job_log(run_dir / f"{hydra_cfg['job']['name']}.log")
+    os.environ[_ENV_RUN_DIR] = str(run_dir.resolve())
+    if not child_rank:
+        _write_hydra_dir(run_dir, job_cfg, hydra_cfg, overrides)
+        _attach_job_log(run_dir / f"{hydra_cfg['job']['name']}.log")
     if hydra_cfg["job"].get("chdir", False):
         os.chdir(run_dir)
     return task_fn(job_cfg)
@@ -266,9 +274,13 @@ def run(task_fn: Callable[[DictConfig], object], config_path: str, config_name: 
             raise SystemExit(f"{sum(1 for c in codes if c)} of {len(jobs)} jobs failed")
         return codes
     results = []
-    for num, ovs in enumerate(jobs):
-        print(f"\t#{num} : {' '.join(o.text() for o in ovs)}")
-        results.append(_run_job(task_fn, config_dir, config_name, ovs, num, "sweep", sweep_dir=sweep_dir))
+    os.environ["MTA_MULTIRUN_INPROC"] = "1"  # the trainer keeps in-process sweep jobs on one device each
+    try:
+        for num, ovs in enumerate(jobs):
+            print(f"\t#{num} : {' '.join(o.text() for o in ovs)}")
+            results.append(_run_job(task_fn, config_dir, config_name, ovs, num, "sweep", sweep_dir=sweep_dir))
+    finally:
+        os.environ.pop("MTA_MULTIRUN_INPROC", None)
     return results
 
 

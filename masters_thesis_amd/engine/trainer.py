@@ -81,7 +81,7 @@ class Trainer:
     def __init__(self, max_epochs: int = 1000, gradient_clip_val: Optional[float] = None,
                  precision: str = "32-true", enable_progress_bar: bool = True, enable_model_summary: bool = True,
                  logger=None, callbacks: Optional[List[Callback]] = None, check_val_every_n_epoch: int = 1,
-                 num_sanity_val_steps: int = 2, accelerator: str = "auto", devices: Any = "auto",
+                 num_sanity_val_steps: int = 2, accelerator: str = "auto", devices: Any = 1,
                  use_hip_graphs: bool = True, graph_warmup_steps: int = 2, matmul_precision: str = "high",
                  limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
                  limit_test_batches: Optional[int] = None, default_root_dir: str = ".",
@@ -100,6 +100,10 @@ class Trainer:
         self.check_val_every_n_epoch = int(check_val_every_n_epoch or 1)
         self.num_sanity_val_steps = int(num_sanity_val_steps)
         self.accelerator = accelerator
+        # ranks of this job (parallel/launch.py): "auto"/-1 = every visible GPU, an int = that many.  The configs'
+        # trainer.devices is "auto" like Lightning's default; a programmatic Trainer defaults to 1 so that library
+        # use (tests, notebooks) never re-runs its host script
+        self.devices = devices
         self.use_hip_graphs = use_hip_graphs
         self.graph_warmup_steps = max(1, int(graph_warmup_steps))
         # consecutive training steps captured into ONE graph (device-resident loaders only): one graph launch per
@@ -173,6 +177,8 @@ class Trainer:
         self.phase_timer: Optional[PhaseTimer] = None
         self._torch_prof = None
         self._in_graph = False
+        # keep the captured (un-instantiated) graphs for graph_census(): which node types each step graph holds
+        self.keep_graphs = os.environ.get("MTA_KEEP_GRAPHS", "0") == "1"
         # MTA_DEBUG_FINITE=1: after every training step synchronise and name the first parameter whose local
         # (pre-sync) gradient or updated value is non-finite, with rank and step (localises a bad kernel / race)
         self.debug_finite = os.environ.get("MTA_DEBUG_FINITE", "0") == "1"
@@ -200,7 +206,26 @@ class Trainer:
             print(*a, **k, flush=True)
 
     # ------------------------------------------------------------------ setup
+    def _launch_ranks(self) -> None:
+        """Lightning's subprocess-script launch (`/root/reference/train.py:169-180` gets DDP from it implicitly):
+        with ``devices`` > 1 and no rank environment yet, start ranks 1..N-1 re-running this script and become rank
+        0 -- before anything touches the GPU (parallel/launch.py)."""
+        from ..parallel import launch
+
+        if launch.in_launched_job() or pdist._ENV is not None:
+            return
+        n = launch.resolve_devices(self.devices, self.accelerator)
+        if n <= 1:
+            return
+        if os.environ.get("MTA_MULTIRUN_INPROC") == "1":
+            if self.devices in ("auto", -1, "-1", None):
+                return  # an in-process sequential sweep: one device per job (use hydra/launcher=gpu_pool for more)
+            raise RuntimeError(f"trainer.devices={self.devices}: multi-process jobs cannot run inside an in-process "
+                               "multirun; use hydra/launcher=gpu_pool (one GPU per trial) or a single run")
+        launch.launch_script_ranks(n)
+
     def _setup_env(self) -> None:
+        self._launch_ranks()
         want_cpu = self.accelerator == "cpu" or not torch.cuda.is_available()
         self.denv = pdist.init_distributed(device="cpu" if want_cpu else None)
         self.device = self.denv.device
@@ -390,7 +415,7 @@ class Trainer:
                 torch.cuda.current_stream().wait_stream(side)
                 return out
             torch.cuda.synchronize()
-            graph = torch.cuda.CUDAGraph()
+            graph = torch.cuda.CUDAGraph(keep_graph=self.keep_graphs) if self.keep_graphs else torch.cuda.CUDAGraph()
             if static:
                 self._in_graph = True
                 try:
@@ -416,6 +441,22 @@ class Trainer:
         if g.static_in is None:
             return g.replay()
         return g.replay(provider())
+
+    def graph_census(self) -> Dict[Tuple, Dict[str, int]]:
+        """Node types of every captured step graph (needs ``keep_graphs``): {graph key: {"kernel": n, "memset": n,
+        "memcpy": n, "other": n}}.  The step graphs are meant to hold kernel nodes only (tests/test_gpu_graphs.py)."""
+        from ..ops._lib import lib
+
+        C = lib()
+        names = {int(C.GRAPH_NODE_KERNEL): "kernel", int(C.GRAPH_NODE_MEMSET): "memset",
+                 int(C.GRAPH_NODE_MEMCPY): "memcpy"}
+        out = {}
+        for key, g in self._graphs.items():
+            counts = {"kernel": 0, "memset": 0, "memcpy": 0, "other": 0}
+            for t in C.graph_node_types(int(g.graph.raw_cuda_graph())):
+                counts[names.get(int(t), "other")] += 1
+            out[key] = counts
+        return out
 
     def _static_hooks(self, loader):
         """Streaming loaders stage batch ``s`` (H2D on their copy stream) before and fence after a step."""
@@ -744,6 +785,14 @@ class Trainer:
 
     def fit(self, model, datamodule=None, ckpt_path: Optional[str] = None, train_dataloaders=None,
             val_dataloaders=None) -> None:
+        try:
+            self._fit(model, datamodule, ckpt_path, train_dataloaders, val_dataloaders)
+        finally:
+            # the gradient producers' overwrite semantics belong to this fit's optimizer only: a later manual
+            # backward on the model (gradient checks, accumulation) must accumulate as usual
+            set_producer_optimizer(None)
+
+    def _fit(self, model, datamodule, ckpt_path, train_dataloaders, val_dataloaders) -> None:
         self._setup_env()
         self._print_devices()
         dm = datamodule

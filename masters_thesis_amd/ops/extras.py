@@ -462,25 +462,6 @@ class _TransformerEncoderFn(torch.autograd.Function):
         # rows of the padded sequences (Np > N) are zero-filled by the cast itself
         cast_pad([x.reshape(N * T, F)] + [mats[i] for i in cast], [Xin] + [mats_b[i] for i in cast],
                  seeds if drop else None)
-        attn = _tr_attn_ok(d, heads, T)
-        # fragment-major weight images of the fused halves, one packing launch: per layer the FFN's W1, W2 (forward)
-        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (its unfused backward keeps the casts)
-        frag, afrag = None, None
-        srcs, dsts, trs = [], [], []
-        if ffn:
-            frag = torch.empty((L, 4, mats[3].shape[0], d), device=dev, dtype=torch.bfloat16)
-            for l in range(L):
-                w1, w2 = mats[3 + 4 * l], mats[4 + 4 * l]
-                srcs += [w1, w2, w2, w1]
-                dsts += [frag[l, 0], frag[l, 1], frag[l, 2], frag[l, 3]]
-                trs += [False, False, True, True]
-        if attn:
-            afrag = [torch.empty_like(mats_b[1 + 4 * l + j]) for l in range(L) for j in (0, 1)]
-            srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1)]
-            dsts += afrag
-            trs += [False] * len(afrag)
-        for i in range(0, len(srcs), 32):
-            C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32])
         xs = torch.empty((M, d), device=dev, dtype=torch.float32)
         gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
         saved: List[Tensor] = [Xin]

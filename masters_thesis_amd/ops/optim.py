@@ -114,7 +114,8 @@ class FusedAdam:
         self.hip = use_hip(flat.data)
         # gradient producers (register_producer): float4 ranges of the flat gradient a weight-gradient GEMM overwrote
         # this step, and their clip-norm partials; consumed by the next step()
-        self._plan: Dict[int, tuple] = {}
+        self._plan: Dict[tuple, tuple] = {}
+        self._dropped: set = set()  # ranges produced twice this step: accumulated, not covered
         if self.hip:
             C = lib()
             self.single_launch = os.environ.get("MTA_OPTIM_TWO_LAUNCH", "0") != "1"
@@ -147,13 +148,26 @@ class FusedAdam:
         n = grad.numel()
         if off < 0 or off + n > f.padded or off % 4 or n % 4:
             return None
-        key = off // 4
-        if key not in self._plan:
-            if len(self._plan) >= self.MAX_PRODUCERS:
-                return None
-            slot = len(self._plan)
-            self._plan[key] = (off // 4, (off + n) // 4, slot)
-        slot = self._plan[key][2]
+        key = (off // 4, (off + n) // 4)
+        clash = [k for k in self._plan if k[0] < key[1] and key[0] < k[1]]
+        if clash:
+            # a second producer of the same range before step() (a weight used twice, two backward calls): the
+            # first one overwrote the range, this one must ADD to it, and the range's norm partials would be stale
+            # -- drop the range from this step's covered plan (the update re-reads it for the norm and zeroes it)
+            # and let this GEMM accumulate
+            for k in clash:
+                del self._plan[k]
+                self._dropped.add(k)
+            self._dropped.add(key)
+            return None
+        if any(k[0] < key[1] and key[0] < k[1] for k in self._dropped):
+            return None
+        used = {s for _, _, s in self._plan.values()}
+        free = [s for s in range(self.MAX_PRODUCERS) if s not in used]
+        if not free:
+            return None
+        self._plan[key] = (key[0], key[1], free[0])
+        slot = free[0]
         return self.ext_parts[slot * self._nparts:(slot + 1) * self._nparts]
 
     # ---- lr (device-resident) --------------------------------------------------
@@ -183,6 +197,7 @@ class FusedAdam:
         if self.hip and self.single_launch:
             plan = sorted(self._plan.values(), key=lambda r: r[2])
             self._plan = {}
+            self._dropped = set()
             lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
                              self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
                              float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health,

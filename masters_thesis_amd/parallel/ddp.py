@@ -42,8 +42,9 @@ class FlatDDP:
         self._gloo_cpu = self.world > 1 and dist.get_backend(group) == "gloo" and flat.grad.is_cuda
         # one-shot xGMI all-reduce (csrc/allreduce.hip) for single-node GPU groups; None -> the group's all-reduce
         self.xgmi = None
-        if self.world > 1 and flat.grad.is_cuda and (dist.get_backend(group) == "nccl"
-                                                     or os.environ.get("MTA_ALLREDUCE", "") == "xgmi"):
+        # GPU gradients: the xGMI kernel whatever the host process group is (RCCL, or gloo when ranks share a GPU);
+        # XgmiAllReduce.create returns None (-> the group's all-reduce) under MTA_ALLREDUCE=rccl or a failed check
+        if self.world > 1 and flat.grad.is_cuda:
             from .xgmi import XgmiAllReduce
 
             self.xgmi = XgmiAllReduce.create(flat.padded, flat.grad.device, group)

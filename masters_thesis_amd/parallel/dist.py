@@ -61,7 +61,10 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0, de
         dev = torch.device("cpu")
     be = None
     if world > 1:
-        be = backend or os.environ.get("MTA_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
+        # RCCL needs one GPU per rank: ranks sharing a GPU (a rehearsal on fewer GPUs than ranks) take gloo for the
+        # host collectives; their gradient sync is still the xGMI/IPC kernel (parallel/ddp.py)
+        shared = use_gpu and int(os.environ.get("LOCAL_WORLD_SIZE", world)) > torch.cuda.device_count()
+        be = backend or os.environ.get("MTA_DIST_BACKEND") or ("nccl" if use_gpu and not shared else "gloo")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         if not dist.is_initialized():
             kw = {}

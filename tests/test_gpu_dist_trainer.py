@@ -64,12 +64,28 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env, trainer=
         tr = Trainer(max_epochs=1, gradient_clip_val=cfg.trainer.gradient_clip_val, precision=cfg.trainer.precision,
                      enable_progress_bar=False, enable_model_summary=False, logger=None, callbacks=[],
                      use_hip_graphs=True, steps_per_graph=spg)
+        tr.keep_graphs = True  # graph_census() below: node types of every captured step graph
         tr._setup_env()
         tr._setup_model(net)
         tr._configure_optimizers(net)
         net.train()
         info = {"backend": tr.ddp.backend_name, "in_graph": tr._allreduce_in_graph(),
                 "overlap": bool(getattr(tr.ddp, "overlap", False))}
+        # the gradient the optimizer sees at step 1 (summed over ranks, times the 1/world it applies) and the clip
+        # norm it computes from it: the first step is an eager warm-up step, so the wrapper sees it
+        snap = {}
+        opt_step = tr.optimizer.step
+
+        def step_and_snapshot(max_norm=0.0, grad_scale=1.0, zero_grad=False):
+            first = "grad" not in snap
+            if first:
+                torch.cuda.synchronize()
+                snap["grad"] = (tr.flat.grad.detach().double() * grad_scale).cpu().numpy().copy()
+            opt_step(max_norm, grad_scale, zero_grad)
+            if first:
+                snap["norm"] = float(tr.optimizer.grad_norm.item())
+
+        tr.optimizer.step = step_and_snapshot
         loader = dm.train_dataloader()
         step = tr.make_train_stepper(loader)
         launches = []
@@ -85,6 +101,8 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env, trainer=
         info["nonfinite"] = float(tr.optimizer.nonfinite.item())
         info["launches"] = launches
         info["graphed"] = bool(tr._graphs)
+        info["grad1"], info["norm1"] = snap.get("grad"), snap.get("norm")
+        info["census"] = [(str(k), c) for k, c in tr.graph_census().items()] if tr._graphs else []
         # numpy (pickled by value): a torch CPU tensor would travel as a shared-memory fd the exiting worker closes
         q.put((rank, tr.flat.data.detach().cpu().numpy().copy(), info, None))
         pdist.barrier()
@@ -115,6 +133,32 @@ def _run(world, model, batch, steps, sync, extra_env=None, timeout=280, trainer=
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("model,trainer,tol", [("small", "fast", 1e-5), ("mlp_small", "gpu_fast", 2e-3),
+                                               ("transformer_encoder", "gpu_fast", 2e-3)])
+def test_step1_summed_gradient_matches_global_batch(model, trainer, tol):
+    """The all-reduce checked where it can be checked sharply: the gradient the optimizer receives at step 1 (sum over
+    2 ranks x B=1 through the xGMI kernel, times 1/world) against ONE rank on the same 2 windows (B=2), and the clip
+    norm computed from it -- before Adam, which turns near-zero gradients' rounding noise into lr-sized steps.
+
+    Tolerances: fp32 LSTM (32-true) 1e-5 relative (norm of the difference over the norm of the gradient; the two runs
+    differ only in the order the kernels sum per-sequence weight-gradient contributions and the loss mean over two
+    windows); bf16 extras 2e-3 (bf16 GEMM tiles of a 100- vs 200-row batch round their inputs identically but split
+    K differently: fp32 partial sums in another order, relative to bf16-rounded products)."""
+    dist_res = _run(2, model, 1, 1, "xgmi", trainer=trainer)
+    (_, _, i0, _), (_, _, i1, _) = dist_res
+    assert i0["backend"] == "xgmi", i0["backend"]
+    ((_, _, iref, _),) = _run(1, model, 2, 1, "none", trainer=trainer)
+    g0, g1, gref = (torch.from_numpy(i["grad1"]) for i in (i0, i1, iref))
+    assert torch.equal(g0, g1), "ranks received different summed gradients"
+    rel = ((g0 - gref).norm() / gref.norm()).item()
+    nrel = abs(i0["norm1"] - iref["norm1"]) / iref["norm1"]
+    print(f"[{model}] step-1 gradient 2 ranks x B=1 vs 1 rank x B=2: rel {rel:.3g}, clip-norm rel {nrel:.3g}")
+    assert gref.norm().item() > 0
+    assert rel <= tol, rel
+    assert nrel <= tol, (i0["norm1"], iref["norm1"])
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("model", ["mlp_small", "transformer_encoder"])
 def test_trainer_xgmi_in_graph_two_ranks(model):
     steps = 6
@@ -124,6 +168,7 @@ def test_trainer_xgmi_in_graph_two_ranks(model):
     (_, p0, info0, _), (_, p1, info1, _) = dist_res
     assert info0["backend"] == "xgmi" and info0["in_graph"] and info0["overlap"], info0
     assert info0["graphed"], info0
+    _assert_kernel_only(info0["census"])
     # the backward reported ranges during the backward (side-stream launches) besides the final sync
     assert min(info0["launches"]) >= 2, info0
     assert info0["nonfinite"] == 0 and info1["nonfinite"] == 0
@@ -143,6 +188,14 @@ def test_trainer_xgmi_in_graph_two_ranks(model):
     assert moved > 1e-4, "parameters did not move: " + stats
     assert diff.max().item() <= 1.5 * steps * 1e-4, stats
     assert frac < 0.02, stats
+
+
+def _assert_kernel_only(census):
+    """The world-2 step graphs (xGMI all-reduce inside) hold kernel nodes only (tests/test_gpu_graphs.py)."""
+    assert census, "no graph captured"
+    for key, c in census:
+        print(f"census {key}: {c}")
+        assert c["kernel"] > 0 and c["memset"] == 0 and c["memcpy"] == 0 and c["other"] == 0, (key, c)
 
 
 _INIT = {}
@@ -202,6 +255,7 @@ def test_trainer_xgmi_grouped_lstm_two_ranks():
     res = _run(2, "small", 1, steps, "xgmi", trainer="fast", spg=4)
     (_, p0, info0, _), (_, p1, info1, _) = res
     assert info0["backend"] == "xgmi" and info0["in_graph"] and info0["grouped"], info0
+    _assert_kernel_only(info0["census"])
     assert info0["nonfinite"] == 0 and info1["nonfinite"] == 0
     assert torch.isfinite(p0).all()
     assert torch.equal(p0, p1), "replicas diverged"

@@ -26,8 +26,6 @@ def test_register_ranges_and_slots(monkeypatch):
     offs = f.offsets
     a = opt.register_producer(params[0].grad)
     assert a is not None and a.numel() == 16 and a.data_ptr() == opt.ext_parts.data_ptr()
-    # the same range again in one step: same slot
-    assert opt.register_producer(params[0].grad).data_ptr() == a.data_ptr()
     # a 3-float bias is not float4-granular: refused (accumulates as usual)
     assert opt.register_producer(params[1].grad) is None
     # every parameter starts on a float4 boundary (the 3-float bias is followed by a zero gap): the third is a producer
@@ -36,6 +34,27 @@ def test_register_ranges_and_slots(monkeypatch):
     # a range that does not start on a float4 boundary is refused
     assert opt.register_producer(f.grad[33:37]) is None
     assert sorted(opt._plan.values()) == [(0, 8, 0), (9, 13, 1)]
+
+
+def test_double_registration_falls_back_to_accumulation(monkeypatch):
+    """a weight whose gradient GEMM runs twice before one step() (a weight used twice, two backward
+    calls) must not be overwritten by the second producer: the second registration returns None (accumulate), the
+    range leaves this step's covered plan (the update re-reads it for the norm and zeroes it), its slot is freed,
+    and the next step covers it again."""
+    opt, params = _opt([(8, 4), (4, 4), (4,)], monkeypatch)
+    assert opt.register_producer(params[0].grad) is not None
+    assert opt.register_producer(params[1].grad) is not None
+    assert opt.register_producer(params[0].grad) is None  # second producer of the same range: accumulate
+    assert opt.register_producer(params[0].grad) is None  # and any further one this step
+    assert sorted(opt._plan.values()) == [(8, 12, 1)]
+    # an overlapping sub-range of a covered range is a double producer too
+    assert opt.register_producer(opt.flat.grad[32:36]) is None and opt._plan == {}
+    # the freed slots are reused by a new range
+    assert opt.register_producer(params[2].grad) is not None
+    assert sorted(v[2] for v in opt._plan.values()) == [0]
+    # next step: everything starts fresh
+    opt._plan, opt._dropped = {}, set()
+    assert opt.register_producer(params[0].grad) is not None
 
 
 def test_slot_limit_and_switch(monkeypatch):

@@ -6,7 +6,9 @@
     python train.py datamodule=real model=large loss=combined trainer=slow
     python train.py -m loss=mse,nll,combined model=small,medium,large
     python train.py -m loss=combined loss.mse_weight=0.3,0.5,0.7
-    torchrun --nproc-per-node 8 train.py ...          # DDP, one process per MI355X (RCCL/xGMI)
+    python train.py trainer.devices=8                 # DDP, one process per MI355X (RCCL/xGMI), own launcher
+                                                      # (trainer.devices=auto, the default: every visible GPU)
+    torchrun --nproc-per-node 8 train.py ...          # the same under an external launcher
 
 MI355X additions (all optional): ``resume=<ckpt>|auto`` (full state; ``auto`` = this run's own
 last.ckpt if present, used by the launcher's retries), ``init_from=<ckpt>``
@@ -52,7 +54,7 @@ def build_trainer(cfg, logger, callbacks):
     for k in ("use_hip_graphs", "matmul_precision", "limit_train_batches", "limit_val_batches",
               "limit_test_batches", "accelerator", "num_sanity_val_steps", "max_steps", "graph_warmup_steps",
               "steps_per_graph", "deterministic", "log_every_n_steps", "profiler", "profile_steps",
-              "debug_serialize"):
+              "debug_serialize", "devices"):
         if k in t:
             kw[k] = t[k]
     return Trainer(**kw)
