@@ -99,11 +99,11 @@ int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const 
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                          float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
                          const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
-                         const MtaBatchGather* gather, hipStream_t st);
+                         const MtaBatchGather* gather, float* gx_ws, hipStream_t st);
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
-                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
+                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, float* gx_ws, hipStream_t st);
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
@@ -111,6 +111,7 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
                        hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
+long mta_lstm_stack_gx_floats(int L, int Np, int T, int H);
 int mta_lstm_stack_epoch_shift(int T);
 // allreduce.hip (one-shot / two-shot all-reduce over xGMI peer memory, one channel per bucket)
 int mta_xgmi_alloc(long bytes, void** out);
@@ -886,11 +887,15 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
   for (int64_t l = 0; l < L; ++l)
     if (xdrop[l].numel()) mk[l] = reinterpret_cast<uint32_t*>(masks[l].data_ptr<uint8_t>());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  // the projection workgroups' gx (layers >= 1): launch-private scratch from the caching allocator (stream-ordered
+  // reuse; inside a captured graph it comes from the graph's pool)
+  const long gxn = mta_lstm_stack_gx_floats((int)L, (int)Np, (int)T, (int)H);
+  at::Tensor gx_ws = gxn ? at::empty({gxn}, x.options()) : at::Tensor();
   const int rc = mta_lstm_stack_fwd_g((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(),
                                       cwh.data(), cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
                                       reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
                                       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
-                                      gather, cur_stream());
+                                      gather, gxn ? gx_ws.data_ptr<float>() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
 }
 
@@ -1210,17 +1215,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   // contiguous tensor <- 0 by a zero-fill KERNEL on the current stream.  A captured hipMemsetAsync (memset graph
   // node) was not ordered against the neighbouring kernel nodes on replay when several processes shared the GPU
-  // (4-rank graphed transformer NaN, profiles/r4_nan_root_cause.txt); MTA_ZERO_MEMSET=1 restores it for that A/B.
+  // (4-rank graphed transformer NaN, profiles/r4_nan_root_cause.txt): step graphs hold kernel nodes only
+  // (tests/test_gpu_graphs.py)
   m.def("zero_", [](at::Tensor t) {
     TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
     c10::hip::HIPGuardMasqueradingAsCUDA guard(t.device());
-    static const bool memset_node = getenv("MTA_ZERO_MEMSET") && getenv("MTA_ZERO_MEMSET")[0] == '1';
-    const long bytes = (long)(t.numel() * t.element_size());
-    if (memset_node) {
-      TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, bytes, cur_stream()) == hipSuccess, "zero_: hipMemsetAsync failed");
-    } else {
-      mta_zero_bytes(t.data_ptr(), bytes, cur_stream());
-    }
+    mta_zero_bytes(t.data_ptr(), (long)(t.numel() * t.element_size()), cur_stream());
   });
   m.def("tr_ffn_fwd", &tr_ffn_fwd);
   m.def("frag_pack", &frag_pack);

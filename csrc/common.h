@@ -13,6 +13,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// LDS destination of global_load_lds (LDS-DMA: 16 B per lane at the wave-uniform base + 16 lane, no VGPR round trip)
+typedef __attribute__((address_space(3))) void lds_void;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Matmul precision for fp32 recurrences, mirroring torch.set_float32_matmul_precision:

@@ -307,18 +307,10 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
 
 // register-resident form: one float4 per thread while that fills <= 256 workgroups, at most REG_N
 inline bool fused_reg(long n4) { return n4 <= (long)FUSED_MAX_BLOCKS * TPB * REG_N; }
-// float4 per thread the register-resident form starts from (MTA_ADAM_REG_PER = 1..REG_N for the A/B: fewer,
-// fuller workgroups -> a cheaper grid-wide arrival wait): measured no gain, profiles/r4_adam_reg_per_negative.txt
-inline long adam_reg_per() {
-  static const long v = [] {
-    const char* e = getenv("MTA_ADAM_REG_PER");
-    const long x = e ? atol(e) : 1;
-    return x >= 1 && x <= REG_N ? x : 1L;
-  }();
-  return v;
-}
 inline int fused_grid_reg(long n4) {
-  long blocks = (n4 + TPB * adam_reg_per() - 1) / (TPB * adam_reg_per());
+  // one float4 per thread while that fills the grid (fewer, fuller workgroups measured no gain:
+  // profiles/r4_adam_reg_per_negative.txt)
+  long blocks = (n4 + TPB - 1) / TPB;
   if (blocks < 1) blocks = 1;
   if (blocks > FUSED_MAX_BLOCKS) blocks = FUSED_MAX_BLOCKS;
   return (int)blocks;

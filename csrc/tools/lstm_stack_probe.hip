@@ -84,6 +84,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
   unsigned* flags;
   const long nflags = mta_lstm_stack_flag_words(Np);
+  float* gx_ws = L > 1 ? dev_zero((size_t)mta_lstm_stack_gx_floats(L, Np, T, H)) : nullptr;
   CK(hipMalloc(&flags, nflags * 4));
   CK(hipMemset(flags, 0, nflags * 4));
 
@@ -92,7 +93,7 @@ int main(int argc, char** argv) {
   // and the top layer's first tile in the backward (block 0: its gradient waves run the dx MFMAs)
   const int ntiles = Np / 16, tr8 = (ntiles + 7) / 8 * 8;
   const int which = argc > 6 ? atoi(argv[6]) : L - 1;
-  int sb[2] = {which * tr8, 0};
+  int sb[2] = {3 * which * tr8, 0};  // [rec(0) | proj(1) x NPP=2 | rec(1) | ...] forward block layout
   CK(hipMemcpyToSymbol(HIP_SYMBOL(mta_stack_stamp_block), sb, sizeof(sb)));
   printf("stamping forward layer %d (block %d), backward block 0 (top layer)\n", which, sb[0]);
 #endif
@@ -105,7 +106,7 @@ int main(int argc, char** argv) {
     float m;
     CK(hipEventRecord(a));
     int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
+                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gx_ws, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -155,7 +156,7 @@ int main(int argc, char** argv) {
     for (int pass = 0; pass < 2; ++pass) {
       CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
       int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
+                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gx_ws, 0);
       CK(hipDeviceSynchronize());
       if (rc) return 1;
       for (int l = 0; l < L; ++l) {
@@ -201,13 +202,13 @@ int main(int argc, char** argv) {
   const char* seg[2][3][8] = {
       {{"", "gx_lds_read", "mfma_chain", "activations", "lds_write", "barrier", "", ""},
        {"", "vmcnt_drain+flag", "store_step", "barrier", "", "", "", ""},
-       {"", "write_x(load_wait)", "compute_gx", "poll+load_issue", "barrier", "", "", ""}},
-      {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
-        "mfma_dh"},
-       {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""},
+       {"", "l0:compute_gx|l>0:wait+copy_gx", "l0:load|l>0:poll+load_gx", "l0:-|l>0:barrier", "l0:barrier", "", "",
+        ""}},
+      {{"", "lds_reads(dh+stash)", "vmcnt_wait", "elementwise+lds", "dG_store_issue", "barrier", "mfma_dh", ""},
+       {"", "stash_dma_issue", "dma_wait", "barrier", "", "", "", ""},
        {"", "", "", "", "", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
-  const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "gradient", ""}};
+  const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "dma-helper", ""}};
   for (int d = 0; d < 2; ++d)
     for (int r = 0; r < 3; ++r) {
       if (!role[d][r][0]) continue;

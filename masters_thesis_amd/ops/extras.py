@@ -109,13 +109,10 @@ def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
 
 
 def _row_dtype(D: int) -> torch.dtype:
-    """Storage of a GEMM -> norm row tensor (activation or its gradient).  fp32: the bf16 form (MTA_BF16_ROWS=1, wide
-    norms only) measured slower end to end -- mlp_large B=64 1.277 -> 1.327 ms, the wide norm backward 50 -> 62 us
-    per call on 8-byte row loads, no gain in the GEMM epilogues (r3 trace, profiles/r3_bf16_rows_negative.txt)."""
-    return torch.bfloat16 if (_BF16_ROWS and D >= 1024) else torch.float32
-
-
-_BF16_ROWS = os.environ.get("MTA_BF16_ROWS", "0") == "1"
+    """Storage of a GEMM -> norm row tensor (activation or its gradient): fp32.  The bf16 form measured slower end to
+    end -- mlp_large B=64 1.277 -> 1.327 ms, the wide norm backward 50 -> 62 us per call on 8-byte row loads, no gain
+    in the GEMM epilogues (profiles/r3_bf16_rows_negative.txt) -- and was removed."""
+    return torch.float32
 
 
 def _row_out(t: Tensor) -> dict:
@@ -171,8 +168,7 @@ class _MlpEncoderFn(torch.autograd.Function):
             D = dims[i + 1]
             assert D % 8 == 0, "MLP hidden size must be a multiple of 8"
             pre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
-            # the GELU output rows are fp32 by default; bf16 only with MTA_BF16_ROWS=1 for wide layers (measured
-            # slower end to end, see _row_dtype)
+            # the GELU output rows are fp32 (_row_dtype)
             act = torch.empty((Mp, D), device=dev, dtype=_row_dtype(D))
             gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU, bias=params[per * i + 1],
                  aux_pre=pre, **_row_out(act))

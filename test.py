@@ -29,6 +29,7 @@ def init_test_results():
     res = {k: {"model": [], "ols": []} for k in _KINDS}
     res["alpha"] = {"model": [], "ols": [], "true": []}
     res["beta"] = {"model": [], "ols": [], "true": []}
+    res["recon"] = {"model": [], "ols": [], "true": []}
     return res
 
 
@@ -52,6 +53,9 @@ def test_step(model, test_results, batch):
     tr["recon_residuals"]["ols"].append((r_target - r_pred_ols).detach())
     tr["alpha_residuals"]["ols"].append((alpha_target - alpha_ols).detach())
     tr["beta_residuals"]["ols"].append((beta_target - beta_ols).detach())
+    tr["recon"]["model"].append(r_pred_model.detach().flatten())
+    tr["recon"]["ols"].append(r_pred_ols.detach().flatten())
+    tr["recon"]["true"].append(r_target.detach().flatten())
     for k, m, o, t in (("alpha", alpha_model, alpha_ols, alpha_target), ("beta", beta_model, beta_ols, beta_target)):
         tr[k]["model"].append(m.detach())
         tr[k]["ols"].append(o.detach())
@@ -63,12 +67,30 @@ def transform_test_results(tr):
         tr["recon_residuals"][src] = torch.stack(tr["recon_residuals"][src]).mean(dim=-1).cpu()
         tr["alpha_residuals"][src] = torch.stack(tr["alpha_residuals"][src]).cpu()
         tr["beta_residuals"][src] = torch.stack(tr["beta_residuals"][src]).cpu()
-    for k in ("alpha", "beta"):
+    for k in ("alpha", "beta", "recon"):
         for src in ("model", "ols", "true"):
             tr[k][src] = torch.stack(tr[k][src]).cpu()
 
 
+def _corr(a, b) -> float:
+    return float(torch.corrcoef(torch.stack([a.flatten().double(), b.flatten().double()]))[0, 1])
+
+
+def summary(tr) -> dict:
+    """The thesis' estimation correlations (`tex/diplomski_rad.tex:1193-1212`): alpha / beta estimates and the
+    return reconstruction of the model and of OLS-on-lookback against the truth, and model vs OLS."""
+    out = {}
+    for k in ("alpha", "beta", "recon"):
+        m, o, t = tr[k]["model"], tr[k]["ols"], tr[k]["true"]
+        out[f"{k}_corr_model"] = _corr(m, t)
+        out[f"{k}_corr_ols"] = _corr(o, t)
+        out[f"{k}_corr_model_vs_ols"] = _corr(m, o)
+    out["n_test_windows"] = int(tr["alpha"]["model"].shape[0])
+    return out
+
+
 def plot(tb_logger, tr):
+    tr = {k: v for k, v in tr.items() if k != "recon"}
     tb = tb_logger.experiment
     tb.add_figure("scatter/recon_residuals", scatter_plot(tr["recon_residuals"]["model"], tr["recon_residuals"]["ols"],
                                                           title="Model vs OLS Reconstruction Residuals"))
@@ -137,6 +159,9 @@ def main(cfg):
     transform_test_results(results)
     plot(tb_logger, results)
     tb_logger.close()
+    import json
+
+    print("[test-summary] " + json.dumps(summary(results)), flush=True)
 
     print("\n" + "=" * 50)
     print("Testing and plotting Complete!")
