@@ -60,7 +60,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("MTA_BENCH_BATCH", "1")),
+    ap.add_argument("--batch", type=int, default=1,
                     help="windows per GPU per step (reference datamodule default: 1)")
     ap.add_argument("--model", default="small")
     ap.add_argument("--loss", default="mse")

@@ -152,14 +152,7 @@ extern "C" {
 
 // comm buffer of one rank: fine-grained device memory (coherent for peer access), zeroed
 int mta_xgmi_alloc(long bytes, void** out) {
-  // MTA_XGMI_COARSE=1: coarse-grained comm buffer (A/B; the kernel's system-scope release / acquire fences make
-  // both forms correct)
-  static const bool coarse = getenv("MTA_XGMI_COARSE") && getenv("MTA_XGMI_COARSE")[0] == '1';
-  if (coarse) {
-    if (hipMalloc(out, (size_t)bytes) != hipSuccess) return -1;
-  } else if (hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-    return -1;
-  }
+  if (hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess) return -1;
   if (hipMemset(*out, 0, (size_t)bytes) != hipSuccess) return -2;
   return hipDeviceSynchronize() == hipSuccess ? 0 : -3;
 }
@@ -217,13 +210,7 @@ int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int
   // dominates and fewer workgroups are faster (3.2 MB one-shot: 29 us at 32, 31 at 64, 35 at 128); a 52 MB bucket
   // is bandwidth-bound (547 / 330 / 233 / 224 us at 32 / 64 / 128 / 256).  At most 256 (one per CU: every
   // workgroup waits for its rank's others, so the grid must be co-resident beside a concurrent backward).
-  // MTA_XGMI_MAX_BLOCKS overrides (A/B).
-  static const long env_cap = [] {
-    const char* e = getenv("MTA_XGMI_MAX_BLOCKS");
-    const long v = e ? atol(e) : 0;
-    return v < 0 ? 0L : v > 256 ? 256L : v;
-  }();
-  const long max_blocks = env_cap ? env_cap : (n * 4L > (8L << 20) ? XG_BIG_BLOCKS : XG_SMALL_BLOCKS);
+  const long max_blocks = n * 4L > (8L << 20) ? XG_BIG_BLOCKS : XG_SMALL_BLOCKS;
   long blocks = (a.n4 + XG_TPB * 8 - 1) / (XG_TPB * 8);
   blocks = blocks < 1 ? 1 : blocks > max_blocks ? max_blocks : blocks;
   xgmi_allreduce_kernel<<<(int)blocks, XG_TPB, 0, st>>>(a);

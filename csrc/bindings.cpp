@@ -26,8 +26,10 @@ long mta_lstm_wgrad_part_floats(int fused, int T, int H, int F);
 int mta_gemm_f32(int prec, const float* A, const float* B, const float* bias, const float* mask, float* C, int M,
                  int N, int K, int b_kn, hipStream_t st);
 int mta_gemm_f32x(int prec, const float* A, int a_km, int lda, const float* B, int b_kn, int ldb, float* C, int ldc,
-                  int n_store, int M, int N, int K, int flags, const float* bias, float* pre, hipStream_t st);
+                  int n_store, int M, int N, int K, int flags, const float* bias, float* pre, const float* mask, const float* resid, const uint64_t* seed, float drop_p, hipStream_t st);
 void mta_colsum_f32(const float* A, int M, int N, int lda, float* out, hipStream_t st);
+int mta_attention_f32(int bwd, const float* qkv, const float* out, const float* dout, float* o, float* lse, float* dqkv,
+                      int nseq, int T, int D, int heads, const float* rope, hipStream_t st);
 void mta_seeds_advance(uint64_t* seeds, int n, hipStream_t st);
 void mta_lstm_prep(const float* w_ih, const float* b_ih, const float* b_hh, int H, int F, float* w_um, float* b_um,
                    hipStream_t st);
@@ -71,7 +73,6 @@ int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, i
                   float* bias_grad, int defer, hipStream_t st);
 void mta_gemm_flush();
 void mta_gemm_set_big(int on);
-void mta_gemm_set_mid(int on);
 void mta_norm_flush();
 void mta_norm_defer();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
@@ -99,11 +100,11 @@ int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const 
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                          float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
                          const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
-                         const MtaBatchGather* gather, float* gx_ws, hipStream_t st);
+                         const MtaBatchGather* gather, hipStream_t st);
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
-                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, float* gx_ws, hipStream_t st);
+                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
@@ -111,7 +112,6 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
                        hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
-long mta_lstm_stack_gx_floats(int L, int Np, int T, int H);
 int mta_lstm_stack_epoch_shift(int T);
 // allreduce.hip (one-shot / two-shot all-reduce over xGMI peer memory, one channel per bucket)
 int mta_xgmi_alloc(long bytes, void** out);
@@ -146,8 +146,8 @@ namespace {
 
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 
-// one statement (do / while): an unbraced `if (x) MTA_CHECK_F32(*x);` must not run the later checks on an empty x
-#define MTA_CHECK_F32(t)                                                                            \
+// one statement (do / while): an unbraced `if (x) CHECK_F32(*x);` must not run the later checks on an empty x
+#define CHECK_F32(t)                                                                            \
   do {                                                                                              \
     TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor");                                         \
     TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32");                            \
@@ -160,7 +160,7 @@ bool has(const OptT& t) { return t.has_value() && t->defined(); }
 
 const float* opt_ptr(const OptT& t) {
   if (!has(t)) return nullptr;
-  MTA_CHECK_F32(*t);
+  CHECK_F32(*t);
   return t->data_ptr<float>();
 }
 
@@ -170,8 +170,8 @@ float* opt_mut(const OptT& t) { return const_cast<float*>(opt_ptr(t)); }
 void lstm_fwd_layer(int64_t H, int64_t prec, const OptT& x, const OptT& w_ih, const OptT& b_ih, const OptT& b_hh,
                     const OptT& gx, const OptT& stash, at::Tensor w_hh, at::Tensor hseq, int64_t N, int64_t Np,
                     int64_t T) {
-  MTA_CHECK_F32(w_hh);
-  MTA_CHECK_F32(hseq);
+  CHECK_F32(w_hh);
+  CHECK_F32(hseq);
   TORCH_CHECK(Np % 16 == 0 && N <= Np && N >= 1, "Np must be a multiple of 16 and >= N");
   TORCH_CHECK(hseq.numel() == T * Np * H, "hseq must be (T, Np, H)");
   TORCH_CHECK(w_hh.numel() == 4 * H * H, "w_hh must be (4H, H)");
@@ -195,9 +195,9 @@ void lstm_fwd_layer(int64_t H, int64_t prec, const OptT& x, const OptT& w_ih, co
 
 void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor stash, at::Tensor w_hh, const OptT& dH, const OptT& dh_last,
                     at::Tensor dG, int64_t N, int64_t Np, int64_t T) {
-  MTA_CHECK_F32(stash);
-  MTA_CHECK_F32(w_hh);
-  MTA_CHECK_F32(dG);
+  CHECK_F32(stash);
+  CHECK_F32(w_hh);
+  CHECK_F32(dG);
   TORCH_CHECK(stash.numel() == T * Np * 5 * H && dG.numel() == T * Np * 4 * H, "bad stash/dG shape");
   const bool has_dh = has(dH);
   if (has_dh) {
@@ -215,13 +215,13 @@ void lstm_bwd_layer(int64_t H, int64_t prec, at::Tensor stash, at::Tensor w_hh, 
 void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bool inp_batch_first, int64_t N, int64_t Np,
                 int64_t T, int64_t H, at::Tensor g_wih, at::Tensor g_whh, at::Tensor g_bih, at::Tensor g_bhh,
                 const OptT& part) {
-  MTA_CHECK_F32(dG);
-  MTA_CHECK_F32(hseq);
-  MTA_CHECK_F32(inp);
-  MTA_CHECK_F32(g_wih);
-  MTA_CHECK_F32(g_whh);
-  MTA_CHECK_F32(g_bih);
-  MTA_CHECK_F32(g_bhh);
+  CHECK_F32(dG);
+  CHECK_F32(hseq);
+  CHECK_F32(inp);
+  CHECK_F32(g_wih);
+  CHECK_F32(g_whh);
+  CHECK_F32(g_bih);
+  CHECK_F32(g_bhh);
   const int64_t F = g_wih.numel() / (4 * H);
   TORCH_CHECK(dG.numel() == T * Np * 4 * H && hseq.numel() == T * Np * H, "bad dG/hseq shape");
   TORCH_CHECK(inp.numel() == (inp_batch_first ? N * T * F : T * Np * F), "bad layer-input shape");
@@ -238,18 +238,27 @@ void lstm_wgrad(int64_t prec, at::Tensor dG, at::Tensor hseq, at::Tensor inp, bo
 // its input saved to pre); A viewed [M][K] (lda) or stored [K][M] (a_km); B [N][K] or [K][N] (b_kn)
 void gemm_f32x(int64_t prec, at::Tensor A, bool a_km, int64_t lda, at::Tensor B, bool b_kn, int64_t ldb, at::Tensor C,
                int64_t ldc, int64_t n_store, int64_t M, int64_t N, int64_t K, int64_t flags,
-               c10::optional<at::Tensor> bias, c10::optional<at::Tensor> pre) {
+               c10::optional<at::Tensor> bias, c10::optional<at::Tensor> pre, c10::optional<at::Tensor> mask,
+               c10::optional<at::Tensor> resid, c10::optional<at::Tensor> seed, double drop_p) {
   for (at::Tensor* t : {&A, &B, &C}) TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat, "gemm_f32x: fp32 GPU");
   TORCH_CHECK(A.numel() >= (a_km ? (K - 1) * lda + M : (M - 1) * lda + K), "gemm_f32x: A too small");
   TORCH_CHECK(B.numel() >= (b_kn ? (K - 1) * ldb + N : (N - 1) * ldb + K), "gemm_f32x: B too small");
   TORCH_CHECK(C.numel() >= (M - 1) * ldc + n_store, "gemm_f32x: C too small");
   if (bias.has_value()) TORCH_CHECK(bias->is_cuda() && bias->scalar_type() == at::kFloat && bias->numel() >= N, "bias");
   if (pre.has_value()) TORCH_CHECK(pre->is_cuda() && pre->scalar_type() == at::kFloat && pre->numel() >= (M - 1) * ldc + n_store, "pre");
+  if (mask.has_value()) TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kFloat && mask->numel() >= M * N, "mask");
+  if (resid.has_value())
+    TORCH_CHECK(resid->is_cuda() && resid->scalar_type() == at::kFloat && resid->numel() >= (M - 1) * ldc + n_store, "resid");
+  if (seed.has_value()) TORCH_CHECK(seed->is_cuda() && seed->scalar_type() == at::kLong && seed->numel() >= 1, "seed");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(A.device());
   const int rc = mta_gemm_f32x((int)prec, A.data_ptr<float>(), a_km ? 1 : 0, (int)lda, B.data_ptr<float>(), b_kn ? 1 : 0,
                                (int)ldb, C.data_ptr<float>(), (int)ldc, (int)n_store, (int)M, (int)N, (int)K, (int)flags,
                                bias.has_value() ? bias->data_ptr<float>() : nullptr,
-                               pre.has_value() ? pre->data_ptr<float>() : nullptr, cur_stream());
+                               pre.has_value() ? pre->data_ptr<float>() : nullptr,
+                               mask.has_value() ? mask->data_ptr<float>() : nullptr,
+                               resid.has_value() ? resid->data_ptr<float>() : nullptr,
+                               seed.has_value() ? reinterpret_cast<const uint64_t*>(seed->data_ptr<int64_t>()) : nullptr,
+                               (float)drop_p, cur_stream());
   TORCH_CHECK(rc == 0, "gemm_f32x: unsupported configuration (", rc, ")");
 }
 
@@ -264,21 +273,21 @@ void colsum_f32(at::Tensor A, int64_t M, int64_t N, int64_t lda, at::Tensor out)
 // C = A . B^T (+ bias) (* mask); B is [N][K], or [K][N] with b_kn (csrc/gemm_f32.hip)
 void gemm_f32(int64_t prec, at::Tensor A, at::Tensor B, at::Tensor C, c10::optional<at::Tensor> bias,
               c10::optional<at::Tensor> mask, bool b_kn) {
-  MTA_CHECK_F32(A);
-  MTA_CHECK_F32(B);
-  MTA_CHECK_F32(C);
+  CHECK_F32(A);
+  CHECK_F32(B);
+  CHECK_F32(C);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f32: 2-D operands");
   const int64_t M = A.size(0), K = A.size(1), N = b_kn ? B.size(1) : B.size(0);
   TORCH_CHECK((b_kn ? B.size(0) : B.size(1)) == K && C.size(0) == M && C.size(1) == N, "gemm_f32: shape mismatch");
   const float* pb = nullptr;
   const float* pm = nullptr;
   if (bias && bias->defined()) {
-    MTA_CHECK_F32((*bias));
+    CHECK_F32((*bias));
     TORCH_CHECK(bias->numel() == N, "gemm_f32: bias[N]");
     pb = bias->data_ptr<float>();
   }
   if (mask && mask->defined()) {
-    MTA_CHECK_F32((*mask));
+    CHECK_F32((*mask));
     TORCH_CHECK(mask->numel() == M * N, "gemm_f32: mask[M][N]");
     pm = mask->data_ptr<float>();
   }
@@ -289,11 +298,11 @@ void gemm_f32(int64_t prec, at::Tensor A, at::Tensor B, at::Tensor C, c10::optio
 }
 
 void lstm_prep(at::Tensor w_ih, at::Tensor b_ih, at::Tensor b_hh, int64_t H, at::Tensor w_um, at::Tensor b_um) {
-  MTA_CHECK_F32(w_ih);
-  MTA_CHECK_F32(b_ih);
-  MTA_CHECK_F32(b_hh);
-  MTA_CHECK_F32(w_um);
-  MTA_CHECK_F32(b_um);
+  CHECK_F32(w_ih);
+  CHECK_F32(b_ih);
+  CHECK_F32(b_hh);
+  CHECK_F32(w_um);
+  CHECK_F32(b_um);
   const int64_t F = w_ih.numel() / (4 * H);
   TORCH_CHECK(w_um.numel() == w_ih.numel() && b_um.numel() == 4 * H, "bad prep shapes");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(w_ih.device());
@@ -311,8 +320,8 @@ void gather_batch(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::
   float* d[4];
   long rf[4];
   for (size_t k = 0; k < src.size(); ++k) {
-    MTA_CHECK_F32(src[k]);
-    MTA_CHECK_F32(dst[k]);
+    CHECK_F32(src[k]);
+    CHECK_F32(dst[k]);
     rf[k] = (long)(src[k].numel() / src[k].size(0));
     TORCH_CHECK(dst[k].numel() == B * rf[k], "dst ", k, " must hold B rows");
     s[k] = src[k].data_ptr<float>();
@@ -334,12 +343,12 @@ double* opt_acc(const OptT& acc) {
 void check_loss_inputs(int64_t N, const at::Tensor& y, const at::Tensor& factor, const at::Tensor& inv_psi,
                        int64_t windows, int64_t kwin, int64_t factor_stride, const at::Tensor& out,
                        const at::Tensor& gmse, const at::Tensor& gnll) {
-  MTA_CHECK_F32(y);
-  MTA_CHECK_F32(factor);
-  MTA_CHECK_F32(inv_psi);
-  MTA_CHECK_F32(out);
-  MTA_CHECK_F32(gmse);
-  MTA_CHECK_F32(gnll);
+  CHECK_F32(y);
+  CHECK_F32(factor);
+  CHECK_F32(inv_psi);
+  CHECK_F32(out);
+  CHECK_F32(gmse);
+  CHECK_F32(gnll);
   TORCH_CHECK(y.dim() == 3 && y.size(0) == N && y.size(2) >= 2, "y must be (N, n, C>=2)");
   TORCH_CHECK(inv_psi.numel() == N, "inv_psi must be (N,)");
   TORCH_CHECK(windows * kwin == N, "windows * kwin must equal N");
@@ -350,7 +359,7 @@ void check_loss_inputs(int64_t N, const at::Tensor& y, const at::Tensor& factor,
 void decoder_losses(at::Tensor ab, at::Tensor y, at::Tensor factor, at::Tensor inv_psi, int64_t windows, int64_t kwin,
                     int64_t factor_stride, bool want_nll, double c_nll, double c_mse, double batch_weight,
                     at::Tensor out, at::Tensor gmse, at::Tensor gnll, const OptT& acc) {
-  MTA_CHECK_F32(ab);
+  CHECK_F32(ab);
   const int64_t N = ab.size(0);
   TORCH_CHECK(ab.dim() == 2 && ab.size(1) == 2, "ab must be (N, 2)");
   check_loss_inputs(N, y, factor, inv_psi, windows, kwin, factor_stride, out, gmse, gnll);
@@ -365,12 +374,12 @@ void heads_losses(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor wb, at:
                   at::Tensor y, at::Tensor factor, at::Tensor inv_psi, int64_t windows, int64_t kwin,
                   int64_t factor_stride, bool want_nll, double c_nll, double c_mse, double batch_weight,
                   at::Tensor out, at::Tensor gmse, at::Tensor gnll, const OptT& acc) {
-  MTA_CHECK_F32(h);
-  MTA_CHECK_F32(wa);
-  MTA_CHECK_F32(ba);
-  MTA_CHECK_F32(wb);
-  MTA_CHECK_F32(bb);
-  MTA_CHECK_F32(ab_out);
+  CHECK_F32(h);
+  CHECK_F32(wa);
+  CHECK_F32(ba);
+  CHECK_F32(wb);
+  CHECK_F32(bb);
+  CHECK_F32(ab_out);
   TORCH_CHECK(h.dim() == 2, "h must be (N, H)");
   const int64_t N = h.size(0), H = h.size(1);
   TORCH_CHECK(wa.numel() == H && wb.numel() == H && ba.numel() == 1 && bb.numel() == 1, "bad head shapes");
@@ -392,12 +401,12 @@ bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor w
                         bool want_nll, double c_nll, double c_mse, double batch_weight, at::Tensor out,
                         const OptT& acc, at::Tensor dh, at::Tensor g_wa, at::Tensor g_ba, at::Tensor g_wb,
                         at::Tensor g_bb) {
-  MTA_CHECK_F32(h);
-  MTA_CHECK_F32(dh);
-  MTA_CHECK_F32(g_wa);
-  MTA_CHECK_F32(g_ba);
-  MTA_CHECK_F32(g_wb);
-  MTA_CHECK_F32(g_bb);
+  CHECK_F32(h);
+  CHECK_F32(dh);
+  CHECK_F32(g_wa);
+  CHECK_F32(g_ba);
+  CHECK_F32(g_wb);
+  CHECK_F32(g_bb);
   TORCH_CHECK(h.dim() == 2, "h must be (N, H)");
   const int64_t N = h.size(0), H = h.size(1);
   TORCH_CHECK(wa.numel() == H && wb.numel() == H && ba.numel() == 1 && bb.numel() == 1, "bad head shapes");
@@ -408,8 +417,8 @@ bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor w
                   y.size(2) >= 2, "y must be (N, n, C >= 2) fp32");
   TORCH_CHECK(out.is_cuda() && out.numel() >= 4, "out: float[4]");
   TORCH_CHECK(windows * kwin == N, "windows * kwin must equal N");
-  MTA_CHECK_F32(factor);
-  MTA_CHECK_F32(inv_psi);
+  CHECK_F32(factor);
+  CHECK_F32(inv_psi);
   TORCH_CHECK(inv_psi.numel() == N, "inv_psi must be (N,)");
   TORCH_CHECK(factor.numel() >= 2 + (windows - 1) * factor_stride, "factor too small");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(h.device());
@@ -426,8 +435,8 @@ bool heads_losses_train(at::Tensor h, at::Tensor wa, at::Tensor ba, at::Tensor w
 void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total, double c_nll, double c_mse,
                       at::Tensor gmse, at::Tensor gnll, bool has_nll, const OptT& h, const OptT& wa, const OptT& wb, const OptT& dh, const OptT& dab,
                       const OptT& g_wa, const OptT& g_ba, const OptT& g_wb, const OptT& g_bb) {
-  MTA_CHECK_F32(gmse);
-  MTA_CHECK_F32(gnll);
+  CHECK_F32(gmse);
+  CHECK_F32(gnll);
   const int64_t N = gmse.numel() / 2;
   int64_t H = 0;
   if (has(h)) {
@@ -451,8 +460,8 @@ void heads_losses_bwd(const OptT& g_mse, const OptT& g_nll, const OptT& g_total,
 int64_t optim_num_partials(int64_t n) { return mta_optim_num_partials((long)n); }
 
 void grad_sqnorm(at::Tensor g, double scale, at::Tensor partials, const OptT& step) {
-  MTA_CHECK_F32(g);
-  MTA_CHECK_F32(partials);
+  CHECK_F32(g);
+  CHECK_F32(partials);
   TORCH_CHECK(g.numel() % 4 == 0, "flat buffers must be padded to a multiple of 4");
   TORCH_CHECK(partials.numel() >= mta_optim_num_partials((long)g.numel()), "partials too small");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
@@ -463,13 +472,13 @@ void grad_sqnorm(at::Tensor g, double scale, at::Tensor partials, const OptT& st
 void adam(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor partials, at::Tensor lr, at::Tensor step,
           double beta1, double beta2, double eps, double wd, double max_norm, double scale, bool adamw,
           const OptT& norm_out, const OptT& nonfinite) {
-  MTA_CHECK_F32(p);
-  MTA_CHECK_F32(g);
-  MTA_CHECK_F32(m);
-  MTA_CHECK_F32(v);
-  MTA_CHECK_F32(partials);
-  MTA_CHECK_F32(lr);
-  MTA_CHECK_F32(step);
+  CHECK_F32(p);
+  CHECK_F32(g);
+  CHECK_F32(m);
+  CHECK_F32(v);
+  CHECK_F32(partials);
+  CHECK_F32(lr);
+  CHECK_F32(step);
   const int64_t n = p.numel();
   TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n && n % 4 == 0, "flat buffer size mismatch");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
@@ -486,13 +495,13 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd, double max_norm,
                 double scale, bool adamw, bool zero_grad, const OptT& norm_out, const OptT& nonfinite,
                 std::vector<int64_t> cov_s, std::vector<int64_t> cov_e, const OptT& ext) {
-  MTA_CHECK_F32(p);
-  MTA_CHECK_F32(g);
-  MTA_CHECK_F32(m);
-  MTA_CHECK_F32(v);
-  MTA_CHECK_F32(partials);
-  MTA_CHECK_F32(lr);
-  MTA_CHECK_F32(step);
+  CHECK_F32(p);
+  CHECK_F32(g);
+  CHECK_F32(m);
+  CHECK_F32(v);
+  CHECK_F32(partials);
+  CHECK_F32(lr);
+  CHECK_F32(step);
   TORCH_CHECK(ticket.is_cuda() && ticket.scalar_type() == at::kLong && ticket.numel() >= 1, "ticket: int64[1]");
   TORCH_CHECK(partials.numel() >= mta_adam_fused_partials(), "partials too small");
   TORCH_CHECK(!has(nonfinite) || nonfinite->numel() >= 2, "nonfinite needs 2 floats");
@@ -503,7 +512,7 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
     TORCH_CHECK(0 <= cov_s[k] && cov_s[k] <= cov_e[k] && cov_e[k] <= n / 4, "adam_fused: covered range out of bounds");
   TORCH_CHECK(cov_s.empty() || has(ext), "adam_fused: covered ranges need their producer partials");
   if (has(ext)) {
-    MTA_CHECK_F32(*ext);
+    CHECK_F32(*ext);
   }
   std::vector<long> cs(cov_s.begin(), cov_s.end()), ce(cov_e.begin(), cov_e.end());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
@@ -521,14 +530,14 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
 // clip-norm partials of it into parts[0 .. gemm_norm_parts())
 void gemm_grad_producer(const OptT& parts, bool overwrite) {
   if (has(parts)) {
-    MTA_CHECK_F32(*parts);
+    CHECK_F32(*parts);
     TORCH_CHECK(parts->numel() >= mta_gemm_norm_parts(), "gemm_grad_producer: parts too small");
   }
   mta_gemm_grad_producer(has(parts) ? parts->data_ptr<float>() : nullptr, overwrite ? 1 : 0);
 }
 
 void scale_(at::Tensor x, double s) {
-  MTA_CHECK_F32(x);
+  CHECK_F32(x);
   TORCH_CHECK(x.numel() % 4 == 0, "flat buffers must be padded to a multiple of 4");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   mta_scale(x.data_ptr<float>(), (long)x.numel(), (float)s, cur_stream());
@@ -538,7 +547,7 @@ void scale_(at::Tensor x, double s) {
 
 
 // ------------------------------------------------------------------------------- MLP / transformer extras
-#define MTA_CHECK_GPU(t, dt)                                                                        \
+#define CHECK_GPU(t, dt)                                                                        \
   do {                                                                                              \
     TORCH_CHECK((t).is_cuda() && (t).scalar_type() == (dt), #t " must be a GPU tensor of " #dt);   \
     TORCH_CHECK((t).is_contiguous(), #t " must be contiguous");                                     \
@@ -561,8 +570,8 @@ void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, i
                double drop_p, const OptT& out_bf16, const OptT& out_f32, const OptT& aux_pre, int64_t ldc,
                int64_t n_store, int64_t ksplit, const OptT& bias_grad, bool defer) {
   const int64_t NS = (n_store <= 0 || n_store > N) ? N : n_store;
-  MTA_CHECK_GPU(A, at::kBFloat16);
-  MTA_CHECK_GPU(B, at::kBFloat16);
+  CHECK_GPU(A, at::kBFloat16);
+  CHECK_GPU(B, at::kBFloat16);
   if (mode == 0) {
     check_span(A, M, lda, K, "A");
     check_span(B, N, ldb, K, "B");
@@ -604,7 +613,7 @@ void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, const Op
     auto d2 = dst[i].dim() == 1 ? dst[i].view({1, -1}) : dst[i];
     TORCH_CHECK(s2.dim() == 2 && d2.dim() == 2, "cast_pad: 1-D or 2-D tensors");
     TORCH_CHECK(s2.is_cuda() && s2.scalar_type() == at::kFloat && s2.stride(1) == 1, "cast_pad: src fp32 rows");
-    MTA_CHECK_GPU(d2, at::kBFloat16);
+    CHECK_GPU(d2, at::kBFloat16);
     TORCH_CHECK(d2.size(0) >= s2.size(0) && d2.size(1) >= s2.size(1), "cast_pad: dst smaller than src");
     sp.push_back(s2.data_ptr<float>());
     dp.push_back(d2.data_ptr());
@@ -618,7 +627,7 @@ void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, const Op
   uint64_t* sd = nullptr;
   int ns = 0;
   if (seeds.has_value() && seeds->defined()) {
-    MTA_CHECK_GPU(*seeds, at::kLong);
+    CHECK_GPU(*seeds, at::kLong);
     sd = reinterpret_cast<uint64_t*>(seeds->data_ptr<int64_t>());
     ns = (int)seeds->numel();
   }
@@ -637,7 +646,7 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
   const bool pre_f = has(pre) && pre->scalar_type() == at::kFloat;  // fp32 GELU input (32-true extras)
   if (dyb) TORCH_CHECK(dy->is_cuda() && dy->is_contiguous(), "dy: contiguous GPU tensor");
   check_span(x, M, ldx, D, "x");
-  MTA_CHECK_F32(rstd);
+  CHECK_F32(rstd);
   TORCH_CHECK(rstd.numel() >= M, "rstd too small");
   if (!rms) TORCH_CHECK(has(mean) && mean->numel() >= M, "LayerNorm needs mean");
   if (bwd) TORCH_CHECK(has(dy), "norm backward needs dy");
@@ -688,7 +697,7 @@ static const float* rope_table(const at::Device& dev, int64_t T, int64_t HD, dou
 // optional bf16 [rows][cols] operand of the fused FFN (nullptr when absent)
 void* opt_bf16(const OptT& t, int64_t numel, const char* name) {
   if (!has(t)) return nullptr;
-  MTA_CHECK_GPU(*t, at::kBFloat16);
+  CHECK_GPU(*t, at::kBFloat16);
   TORCH_CHECK(t->numel() >= numel, name, ": too small");
   return t->data_ptr();
 }
@@ -699,11 +708,11 @@ void tr_ffn_fwd(at::Tensor x1, at::Tensor w1, at::Tensor w2, at::Tensor b1, at::
                 const OptT& seed, double drop_p, const OptT& xn2, at::Tensor r2, at::Tensor pre, const OptT& u,
                 at::Tensor x2, const OptT& xn2T, const OptT& uT) {
   const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1.size(0);
-  MTA_CHECK_F32(x1);
-  MTA_CHECK_F32(x2);
-  MTA_CHECK_F32(r2);
+  CHECK_F32(x1);
+  CHECK_F32(x2);
+  CHECK_F32(r2);
   for (auto* t : {&w1, &w2, &pre}) {
-    MTA_CHECK_GPU(*t, at::kBFloat16);
+    CHECK_GPU(*t, at::kBFloat16);
   }
   TORCH_CHECK(w1.size(1) == d && w2.size(0) == d && w2.size(1) == dff, "tr_ffn_fwd: weight shapes");
   TORCH_CHECK(x2.numel() >= M * d && pre.numel() >= M * dff && r2.numel() >= M && b1.numel() >= dff &&
@@ -727,10 +736,10 @@ void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at
                 at::Tensor dx1b, at::Tensor dg2, const OptT& dpreT, const OptT& dxT) {
   const int64_t d = x1.size(-1), M = x1.numel() / d, dff = w1t.size(1);
   for (auto* t : {&x1, &r2, &dx, &dx1, &dg2}) {
-    MTA_CHECK_F32(*t);
+    CHECK_F32(*t);
   }
   for (auto* t : {&w1t, &w2t, &pre, &dxb, &dx1b}) {
-    MTA_CHECK_GPU(*t, at::kBFloat16);
+    CHECK_GPU(*t, at::kBFloat16);
   }
   TORCH_CHECK(w1t.size(0) == d && w2t.size(0) == dff && w2t.size(1) == d, "tr_ffn_bwd: weight shapes");
   TORCH_CHECK(dx.numel() >= M * d && dxb.numel() >= M * d && dx1.numel() >= M * d && dx1b.numel() >= M * d &&
@@ -756,8 +765,8 @@ void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::ve
   std::vector<void*> dp;
   std::vector<int> n, k, tr;
   for (size_t i = 0; i < src.size(); ++i) {
-    MTA_CHECK_F32(src[i]);
-    MTA_CHECK_GPU(dst[i], at::kBFloat16);
+    CHECK_F32(src[i]);
+    CHECK_GPU(dst[i], at::kBFloat16);
     TORCH_CHECK(src[i].dim() == 2 && dst[i].numel() == src[i].numel(), "frag_pack: shapes");
     sp.push_back(src[i].data_ptr<float>());
     dp.push_back(dst[i].data_ptr());
@@ -776,10 +785,10 @@ void tr_attn_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope
                  at::Tensor qkv, at::Tensor o, at::Tensor lse, at::Tensor x1) {
   const int64_t d = x.size(-1), M = nseq * T;
   for (auto* t : {&x, &r1, &lse, &x1, &g1, &bqkv, &bo}) {
-    MTA_CHECK_F32(*t);
+    CHECK_F32(*t);
   }
   for (auto* t : {&wqkv, &wo, &xn, &qkv, &o}) {
-    MTA_CHECK_GPU(*t, at::kBFloat16);
+    CHECK_GPU(*t, at::kBFloat16);
   }
   TORCH_CHECK(wqkv.size(0) == 3 * d && wqkv.size(1) == d && wo.size(0) == d && wo.size(1) == d,
               "tr_attn_fwd: weight shapes");
@@ -802,8 +811,8 @@ void transpose_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
   std::vector<void*> dp;
   std::vector<int> rows, cols;
   for (size_t i = 0; i < src.size(); ++i) {
-    MTA_CHECK_GPU(src[i], at::kBFloat16);
-    MTA_CHECK_GPU(dst[i], at::kBFloat16);
+    CHECK_GPU(src[i], at::kBFloat16);
+    CHECK_GPU(dst[i], at::kBFloat16);
     TORCH_CHECK(src[i].dim() == 2 && dst[i].dim() == 2 && dst[i].size(0) == src[i].size(1) &&
                     dst[i].size(1) == src[i].size(0) && src[i].is_contiguous() && dst[i].is_contiguous(),
                 "transpose_bf16: dst must be the contiguous [cols][rows] of src");
@@ -819,9 +828,9 @@ void transpose_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
 
 void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
                int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base) {
-  MTA_CHECK_GPU(qkv, at::kBFloat16);
-  MTA_CHECK_GPU(out, at::kBFloat16);
-  MTA_CHECK_F32(lse);
+  CHECK_GPU(qkv, at::kBFloat16);
+  CHECK_GPU(out, at::kBFloat16);
+  CHECK_F32(lse);
   TORCH_CHECK(qkv.numel() >= nseq * T * 3 * D && out.numel() >= nseq * T * D, "attention: qkv/out too small");
   TORCH_CHECK(lse.numel() >= nseq * heads * 64, "attention: lse must hold nseq*heads*64");
   if (bwd) {
@@ -836,6 +845,30 @@ void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const O
   TORCH_CHECK(rc == 0, "attention: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc, ")");
 }
 
+
+// fp32 RoPE attention of the 32-true transformer (csrc/attention_f32.hip): forward o, lse <- qkv; backward dqkv <-
+// (qkv, o, dout, lse)
+void attention_f32(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
+                   int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base) {
+  CHECK_F32(qkv);
+  CHECK_F32(out);
+  CHECK_F32(lse);
+  TORCH_CHECK(qkv.numel() >= nseq * T * 3 * D && out.numel() >= nseq * T * D, "attention_f32: qkv/out too small");
+  TORCH_CHECK(lse.numel() >= nseq * heads * 64, "attention_f32: lse must hold nseq*heads*64");
+  if (bwd) {
+    TORCH_CHECK(has(dout) && has(dqkv), "attention_f32 backward needs dout and dqkv");
+    CHECK_F32(*dout);
+    CHECK_F32(*dqkv);
+    TORCH_CHECK(dout->numel() >= nseq * T * D && dqkv->numel() >= nseq * T * 3 * D, "attention_f32: grads too small");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  const int rc = mta_attention_f32(bwd ? 1 : 0, qkv.data_ptr<float>(), bwd ? out.data_ptr<float>() : nullptr,
+                                   bwd ? dout->data_ptr<float>() : nullptr, bwd ? nullptr : out.data_ptr<float>(),
+                                   lse.data_ptr<float>(), bwd ? dqkv->data_ptr<float>() : nullptr, (int)nseq, (int)T,
+                                   (int)D, (int)heads, rope_table(qkv.device(), T, D / heads, rope_base), cur_stream());
+  TORCH_CHECK(rc == 0, "attention_f32: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc,
+              ")");
+}
 
 // ------------------------------------------------------------------------------- pipelined LSTM stack
 // list entries with numel() == 0 stand for "no tensor"
@@ -861,7 +894,7 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
                                 std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags,
                                 int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather) {
   const int64_t L = (int64_t)w_hh.size();
-  MTA_CHECK_F32(x);
+  CHECK_F32(x);
   TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
   TORCH_CHECK(w_ih.size() == (size_t)L && b_ih.size() == (size_t)L && b_hh.size() == (size_t)L &&
               hseq.size() == (size_t)L && xdrop.size() == (size_t)L && stash.size() == (size_t)L, "per-layer lists");
@@ -887,15 +920,11 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
   for (int64_t l = 0; l < L; ++l)
     if (xdrop[l].numel()) mk[l] = reinterpret_cast<uint32_t*>(masks[l].data_ptr<uint8_t>());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  // the projection workgroups' gx (layers >= 1): launch-private scratch from the caching allocator (stream-ordered
-  // reuse; inside a captured graph it comes from the graph's pool)
-  const long gxn = mta_lstm_stack_gx_floats((int)L, (int)Np, (int)T, (int)H);
-  at::Tensor gx_ws = gxn ? at::empty({gxn}, x.options()) : at::Tensor();
   const int rc = mta_lstm_stack_fwd_g((int)H, (int)prec, (int)L, (int)fin, x.data_ptr<float>(), cwi.data(),
                                       cwh.data(), cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
                                       reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
                                       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
-                                      gather, gxn ? gx_ws.data_ptr<float>() : nullptr, cur_stream());
+                                      gather, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
 }
 
@@ -923,8 +952,8 @@ void lstm_stack_fwd_gather(int64_t H, int64_t prec, int64_t fin, at::Tensor x, s
   TORCH_CHECK(dst[0].data_ptr() == x.data_ptr(), "x must be the static batch buffer dst[0]");
   MtaBatchGather g{};
   for (size_t k = 0; k < src.size(); ++k) {
-    MTA_CHECK_F32(src[k]);
-    MTA_CHECK_F32(dst[k]);
+    CHECK_F32(src[k]);
+    CHECK_F32(dst[k]);
     g.row[k] = (long)(src[k].numel() / src[k].size(0));
     TORCH_CHECK(dst[k].numel() == B * g.row[k], "dst ", k, " must hold B rows");
     g.src[k] = src[k].data_ptr<float>();
@@ -947,7 +976,7 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
                     std::vector<at::Tensor> parts, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
                     int64_t N, int64_t Np, int64_t T) {
   const int64_t L = (int64_t)w_hh.size();
-  MTA_CHECK_F32(dh_last);
+  CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
   TORCH_CHECK(stash.size() == (size_t)L && w_ih.size() == (size_t)L && dG.size() == (size_t)L &&
               dX.size() == (size_t)L, "per-layer lists");
@@ -997,7 +1026,7 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
   if (!parts.empty()) {
     TORCH_CHECK(fused && parts.size() == (size_t)L, "parts: one buffer per layer (fused weight gradients)");
     for (int64_t l = 0; l < L; ++l) {
-      MTA_CHECK_F32(parts[l]);
+      CHECK_F32(parts[l]);
       TORCH_CHECK(parts[l].numel() >= mta_lstm_wgrad_part_floats(1, (int)T, (int)H, l == 0 ? (int)fin : (int)H),
                   "parts buffer too small");
       pt.push_back(parts[l].data_ptr<float>());
@@ -1050,7 +1079,7 @@ void xgmi_ipc_close(int64_t p) { mta_xgmi_ipc_close(reinterpret_cast<void*>(p));
 // (per-channel epoch and arrival counters, the shared timeout count)
 void xgmi_allreduce(at::Tensor grad, int64_t off, int64_t cap, int64_t channel, int64_t channels, bool twoshot,
                     std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl) {
-  MTA_CHECK_F32(grad);
+  CHECK_F32(grad);
   TORCH_CHECK(ctl.is_cuda() && ctl.scalar_type() == at::kInt && ctl.numel() >= mta_xgmi_ctl_words(), "ctl words");
   std::vector<void*> b;
   for (auto v : bufs) b.push_back(reinterpret_cast<void*>(v));
@@ -1065,10 +1094,10 @@ void xgmi_allreduce(at::Tensor grad, int64_t off, int64_t cap, int64_t channel, 
 void dgp(int64_t seed, int64_t mkt_df, double mkt_loc, double mkt_scale, int64_t idio_df, double idio_loc,
          double idio_scale, double a_loc, double a_scale, double b_loc, double b_scale, at::Tensor r_market,
          at::Tensor r_stocks, at::Tensor alphas, at::Tensor betas) {
-  MTA_CHECK_F32(r_market);
-  MTA_CHECK_F32(r_stocks);
-  MTA_CHECK_F32(alphas);
-  MTA_CHECK_F32(betas);
+  CHECK_F32(r_market);
+  CHECK_F32(r_stocks);
+  CHECK_F32(alphas);
+  CHECK_F32(betas);
   const int64_t K = r_stocks.size(0), S = r_market.numel();
   TORCH_CHECK(r_stocks.dim() == 2 && r_stocks.size(1) == S && alphas.numel() == K && betas.numel() == K,
               "dgp: shapes");
@@ -1081,14 +1110,14 @@ void dgp(int64_t seed, int64_t mkt_df, double mkt_loc, double mkt_scale, int64_t
 }
 
 void ols_features(at::Tensor target, at::Tensor alphas, at::Tensor betas, at::Tensor factor, at::Tensor inv_psi) {
-  MTA_CHECK_F32(target);
+  CHECK_F32(target);
   TORCH_CHECK(target.dim() == 4 && target.size(3) >= 2 && target.size(2) >= 2, "target must be (W, K, n, C>=2)");
   const int64_t W = target.size(0), K = target.size(1);
   for (auto* t : {&alphas, &betas, &inv_psi}) {
-    MTA_CHECK_F32(*t);
+    CHECK_F32(*t);
     TORCH_CHECK(t->numel() == W * K, "per-(window, stock) output shape");
   }
-  MTA_CHECK_F32(factor);
+  CHECK_F32(factor);
   TORCH_CHECK(factor.numel() == W * 2, "factor must be (W, 2)");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(target.device());
   mta_ols_features(target.data_ptr<float>(), (int)W, (int)K, (int)target.size(2), (int)target.size(3),
@@ -1206,7 +1235,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_stack_epoch_shift", [](int64_t T) { return (int64_t)mta_lstm_stack_epoch_shift((int)T); });
   m.def("gemm_bf16", &gemm_bf16);
   m.def("gemm_flush", []() { mta_gemm_flush(); });
-  m.def("gemm_f32x", &gemm_f32x);
+  m.def("gemm_f32x", &gemm_f32x, py::arg("prec"), py::arg("A"), py::arg("a_km"), py::arg("lda"), py::arg("B"),
+        py::arg("b_kn"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("n_store"), py::arg("M"), py::arg("N"),
+        py::arg("K"), py::arg("flags"), py::arg("bias"), py::arg("pre"), py::arg("mask") = py::none(),
+        py::arg("resid") = py::none(), py::arg("seed") = py::none(), py::arg("drop_p") = 0.0);
+  m.def("attention_f32", &attention_f32);
   m.def("colsum_f32", &colsum_f32);
   m.def("seeds_advance", [](at::Tensor seeds) {
     TORCH_CHECK(seeds.is_cuda() && seeds.scalar_type() == at::kLong && seeds.numel() <= 64, "seeds: int64[<= 64] GPU");
@@ -1228,7 +1261,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_bf16", &transpose_bf16);
   m.def("tr_attn_fwd", &tr_attn_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
-  m.def("gemm_set_mid", [](int64_t on) { mta_gemm_set_mid((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());

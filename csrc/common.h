@@ -29,8 +29,6 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 //                           reference by default (cudnn.allow_tf32), with the weights more exact than TF32's
 enum { PREC_F32 = 0, PREC_BF16X3 = 1, PREC_BF16 = 2, PREC_F16X2 = 3 };
 
-#define MTA_WAVE 64
-
 // Activations on the transcendental unit: v_exp_f32 + v_rcp_f32 (1 ulp) instead of the ~10-instruction
 // IEEE division sequence a plain '1.0f / x' compiles to.
 __device__ __forceinline__ float mta_rcp(float x) { return __builtin_amdgcn_rcpf(x); }

@@ -85,26 +85,11 @@ union Bf8 {
   __bf16 e[8];
 };
 
-// GEMM epilogue store (probe builds: MTA_EPI_NT = nontemporal, MTA_EPI_NOSTORE = timing without the
-// stores; the flags bit 30 is never set, it only keeps the values live)
+// GEMM epilogue store (nontemporal stores and store-less timing builds measured no gain: r3 probe, git history)
 template <typename T>
 __device__ __forceinline__ void epi_store(T* p, const T& v, int flags) {
-#if defined(MTA_EPI_NOSTORE)
-  if (flags & (1 << 30)) *p = v;
-#elif defined(MTA_EPI_NT)
-  (void)flags;
-  if constexpr (sizeof(T) == 2) {
-    __builtin_nontemporal_store(__builtin_bit_cast(unsigned short, v), reinterpret_cast<unsigned short*>(p));
-  } else if constexpr (sizeof(T) == 4) {
-    __builtin_nontemporal_store(__builtin_bit_cast(unsigned int, v), reinterpret_cast<unsigned int*>(p));
-  } else {
-    typedef unsigned int V __attribute__((ext_vector_type(sizeof(T) / 4)));
-    __builtin_nontemporal_store(__builtin_bit_cast(V, v), reinterpret_cast<V*>(p));
-  }
-#else
   (void)flags;
   *p = v;
-#endif
 }
 
 // Epilogue of one wave's MT x NT grid of 16x16 accumulator tiles whose top-left output element is (mbase, nbase):
@@ -184,7 +169,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmArgs& g, const f32x4 (&a
   }
 }
 
-template <int BM, int BN, int BKT, bool AT, bool BT, bool PIPE = false>
+template <int BM, int BN, int BKT, bool AT, bool BT>
 __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const int by, const int bz, const int gz,
                                           __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
   constexpr int RST = BKT + 8;  // LDS row stride (bf16): BKT + 8 pad (16 B): conflict-free b128 rows
@@ -206,9 +191,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
 
   typedef uint4 RegA[A_PER][A_REGS];
   typedef uint4 RegB[B_PER][B_REGS];
-  RegA ra[PIPE ? 2 : 1];
-  RegB rb[PIPE ? 2 : 1];
-  uint32_t ma[PIPE ? 2 : 1][A_PER], mb[PIPE ? 2 : 1][B_PER];  // validity bits (one per 16-B load)
+  RegA ra[1];
+  RegB rb[1];
+  uint32_t ma[1][A_PER], mb[1][B_PER];  // validity bits (one per 16-B load)
 
   // ---- global -> registers (raw values + masks; masks applied at LDS-store time) ----
   auto load = [&](RegA& ra, RegB& rb, uint32_t (&ma)[A_PER], uint32_t (&mb)[B_PER], int k0)
@@ -340,41 +325,15 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g, const int bx, const
     }
   };
 
-  if constexpr (!PIPE) {
-    load(ra[0], rb[0], ma[0], mb[0], kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BKT) {
-      __syncthreads();
-      store(ra[0], rb[0], ma[0], mb[0], As, Bs);
-      __syncthreads();
-      if (k0 + BKT < kend) load(ra[0], rb[0], ma[0], mb[0], k0 + BKT);
-      compute(As, Bs);
-    }
-  } else {
-    // Two LDS stages and two register sets: the k-slice stored at step t was loaded at step t - 2 (two slices of
-    // MFMA work between a load's issue and its use, instead of one), one barrier per k-step.
-    __bf16* const As1 = As + (BM + BN) * RST;
-    __bf16* const Bs1 = Bs + (BM + BN) * RST;
-    const int nk = (kend - kbeg + BKT - 1) / BKT;
-    load(ra[0], rb[0], ma[0], mb[0], kbeg);
-    if (nk > 1) load(ra[1], rb[1], ma[1], mb[1], kbeg + BKT);
-    store(ra[0], rb[0], ma[0], mb[0], As, Bs);
-    if (nk > 2) load(ra[0], rb[0], ma[0], mb[0], kbeg + 2 * BKT);
+  // single-stage loop: a two-stage form (two LDS images, loads two k-slices ahead) measured equal on mlp_large and
+  // 0-10 % slower on the transformer's wgrad shapes (profiles/r4_gemm_pipe64_negative.txt) and was removed
+  load(ra[0], rb[0], ma[0], mb[0], kbeg);
+  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
     __syncthreads();
-    for (int t = 0; t < nk; t += 2) {
-      compute(As, Bs);
-      if (t + 1 < nk) {
-        store(ra[1], rb[1], ma[1], mb[1], As1, Bs1);
-        if (t + 3 < nk) load(ra[1], rb[1], ma[1], mb[1], kbeg + (t + 3) * BKT);
-      }
-      __syncthreads();
-      if (t + 1 >= nk) break;
-      compute(As1, Bs1);
-      if (t + 2 < nk) {
-        store(ra[0], rb[0], ma[0], mb[0], As, Bs);
-        if (t + 4 < nk) load(ra[0], rb[0], ma[0], mb[0], kbeg + (t + 4) * BKT);
-      }
-      __syncthreads();
-    }
+    store(ra[0], rb[0], ma[0], mb[0], As, Bs);
+    __syncthreads();
+    if (k0 + BKT < kend) load(ra[0], rb[0], ma[0], mb[0], k0 + BKT);
+    compute(As, Bs);
   }
 
   gemm_epilogue<MT, NT, MT>(g, acc, m0 + wm * WM, n0 + wn * WN, gz > 1, lane);
@@ -398,14 +357,14 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return b < nb8 ? (b & 7) * (nb8 >> 3) + (b >> 3) : b;
 }
 
-template <int BM, int BN, int BKT, bool PIPE>
-constexpr int gemm_lds_elems() { return (PIPE ? 2 : 1) * (BM + BN) * (BKT + 8); }
+template <int BM, int BN, int BKT>
+constexpr int gemm_lds_elems() { return (BM + BN) * (BKT + 8); }
 
-template <int BM, int BN, int BKT, bool AT, bool BT, bool PIPE>
+template <int BM, int BN, int BKT, bool AT, bool BT>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_bf16_kernel(GemmArgs g, int nx, int ny, int nz) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT, PIPE>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT>()];
   const int b = xcd_remap(blockIdx.x, nx * ny * nz);
-  gemm_body<BM, BN, BKT, AT, BT, PIPE>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, smem, smem + BM * (BKT + 8));
+  gemm_body<BM, BN, BKT, AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, smem, smem + BM * (BKT + 8));
 }
 
 // ---- 256 x 256 macro-tile GEMM: LDS-DMA ring, staggered wave groups, in-kernel transposed operands ----
@@ -428,8 +387,7 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
 //     ds_read_b64_tr_b16 (two per fragment), conflict-free: no transpose kernels, no transposing register staging.
 // Ring hazards (j = k-tile; segments R = reads, M = DMA issue + MFMAs; row 0: R0 M0 R1 M1 ..., row 1: -- R0 M0 R1 ...):
 //   WAR: tile j+AHEAD is issued during R_j into slot (j+AHEAD) % (AHEAD+2) = the slot of tile j-2; both rows retired
-//        their reads of it (lgkmcnt(0) ahead of their MFMAs of M_{j-2}) before a barrier that precedes R_j (with the
-//        MTA_GEMM_DMA_IN_READS=0 form: issued at the head of M_j into the slot of tile j-1, AHEAD+1 slots);
+//        their reads of it (lgkmcnt(0) ahead of their MFMAs of M_{j-2}) before a barrier that precedes R_j;
 //   RAW: row 0 first reads tile j+1 right after the barrier that closes its M_j, so at that barrier every wave has
 //        waited for all but the tiles it issued after tile j+1 (row 0 at the end of M_j, row 1 at the end of R_j).
 // Rows / columns beyond M, N are clamped on load (their outputs are not stored); K per split is a multiple of 32.
@@ -438,25 +396,18 @@ constexpr int TM = 256, TN = 256, KT = 32, THREADS = 512;
 // DMA issued in the read segment, 3 k-tiles ahead, 5 slots (160 KB): r3 probe A/B against issuing it at the head of
 // the MFMA segment (4 ahead, 5 slots): main loop 1832 -> 1555 cycles per k-tile, 4096^3 858 -> 892..1038 TF,
 // mlp_large forward 545 -> 590 TF, input gradient 665 -> 707 TF (profiles/r3_gemm_variants.txt)
-#ifndef MTA_GEMM_BIG_AHEAD
-#define MTA_GEMM_BIG_AHEAD 3
-#endif
-#ifndef MTA_GEMM_DMA_IN_READS
-#define MTA_GEMM_DMA_IN_READS 1  // 0: issue the DMA at the head of the MFMA segment (one ring slot fewer)
-#endif
-constexpr int AHEAD = MTA_GEMM_BIG_AHEAD;                      // k-tiles in flight beyond the one multiplied
-constexpr int SLOTS = AHEAD + 1 + MTA_GEMM_DMA_IN_READS;
+constexpr int AHEAD = 3;              // k-tiles in flight beyond the one multiplied
+constexpr int SLOTS = AHEAD + 2;      // + the slot being read + the one whose reads retire during the issue
 constexpr int OP_BYTES = 256 * KT * 2;     // one operand's k-tile image: 16 KB
 constexpr int SLOT_BYTES = 2 * OP_BYTES;  // A | B
 constexpr int EPI_ROW = 68;                                   // staged row: 64 f32 + 4 pad (conflict-free writes)
 constexpr int EPI_WAVE_BYTES = 64 * EPI_ROW * 4;               // 64 rows of one wave's 128 x 64 tile per pass
 constexpr int LDS_BYTES = SLOTS * SLOT_BYTES > 8 * EPI_WAVE_BYTES ? SLOTS * SLOT_BYTES : 8 * EPI_WAVE_BYTES;
 
-typedef __attribute__((address_space(3))) void lds_void;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 // per-lane source of the two DMA instructions this wave issues for one operand of one k-tile
-// (TW = image width in rows/columns: 256 for the macro-tile kernel, 128 for the mid kernel; WAVES issuing)
+// (TW = image width in rows/columns; WAVES issuing)
 template <bool T, int TW = 256, int WAVES = 8>
 __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, int r0, int kbeg, int wave, int lane,
                                         const __bf16* (&src)[2]) {
@@ -482,9 +433,8 @@ __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, in
 }
 
 // diagnostic build (csrc/tools/gemm_probe.hip): s_memtime stamps of the main loop's segments, summed per wave
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
 __device__ unsigned long long stamp_acc[8][8];  // [wave][segment]
-__device__ unsigned long long epi_stamp[8];  // probe extras (MTA_EPI_TWICE: epilogue first / second call)
 #define GSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define GACC(i, a, b) dsum[i] += (unsigned)((b) - (a))
 #else
@@ -742,11 +692,8 @@ __device__ __forceinline__ void mainloop(const GemmArgs& g, const int m0, const 
   wait_tiles(pro - 1);
   barrier();
   if (row1) barrier();  // the second wave row runs one barrier behind
-#ifdef MTA_GEMM_STATIC_PRIO
-  if (row1) __builtin_amdgcn_s_setprio(1);  // the younger half: no per-cluster flips (guide T5, static form)
-#endif
   int rd = 0, wr = AHEAD % SLOTS;  // ring slots of tile j and of tile j + AHEAD
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
   unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   GSTAMP(tloop0);
 #endif
@@ -759,23 +706,14 @@ __device__ __forceinline__ void mainloop(const GemmArgs& g, const int m0, const 
     for (int i = 0; i < 8; ++i) af[i] = frag<AT>(slot, wm * 128 + 16 * i, lane);
 #pragma unroll
     for (int n = 0; n < 4; ++n) bfr[n] = frag<BT>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
-#if MTA_GEMM_DMA_IN_READS
     if (j + AHEAD < nk) stage(j + AHEAD, wr);
     GSTAMP(t1);
     if (row1) wait_tiles(min(nk - 1, j + AHEAD) - (j + 1));
-#else
-    GSTAMP(t1);
-    // row 1 ends its read segment at the barrier before row 0 reads tile j + 1: everything up to it landed
-    if (row1) wait_tiles(min(nk - 1, j - 1 + AHEAD) - (j + 1));
-#endif
     GSTAMP(t2);
     barrier();
     GSTAMP(t3);
-    // [MFMA] tile j, with the DMA of tile j + AHEAD issued up front into the slot tile j - 1 used (both rows
-    // retired their reads of it: lgkmcnt(0) at their previous MFMA segments, and a barrier since)
-#if !MTA_GEMM_DMA_IN_READS
-    if (j + AHEAD < nk) stage(j + AHEAD, wr);
-#endif
+    // [MFMA] tile j (priority raised over the other wave row's reads: no-priority and static-priority builds
+    // measured slower, profiles/r3_gemm_variants.txt)
     if (want_rowsum) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)
@@ -786,16 +724,12 @@ __device__ __forceinline__ void mainloop(const GemmArgs& g, const int m0, const 
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
-#if !defined(MTA_GEMM_NO_PRIO) && !defined(MTA_GEMM_STATIC_PRIO)
     __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(af[i], bfr[n], acc[i][n]);
-#if !defined(MTA_GEMM_NO_PRIO) && !defined(MTA_GEMM_STATIC_PRIO)
     __builtin_amdgcn_s_setprio(0);
-#endif
     GSTAMP(t4);
     if (!row1) wait_tiles(min(nk - 1, j + AHEAD) - (j + 1));
     GSTAMP(t5);
@@ -811,7 +745,7 @@ __device__ __forceinline__ void mainloop(const GemmArgs& g, const int m0, const 
     wr = wr + 1 == SLOTS ? 0 : wr + 1;
   }
   if (!row1) barrier();
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
   GSTAMP(tloop1);
   GACC(6, tloop0, tloop1);
   if (lane == 0)
@@ -846,163 +780,18 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
   f32x4 acc[8][4];
   float rowsum[8];
   mainloop<AT, BT>(g, m0, n0, kbeg, nk, want_rowsum, lds, acc, rowsum);
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
   GSTAMP(tepi0);
 #endif
   big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
                reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
-#ifdef MTA_EPI_TWICE
-  // probe: the same epilogue again with its code now in the instruction cache (epi_stamp[0] / [1]: first / second)
-  GSTAMP(tepi1);
-  big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
-               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
-  GSTAMP(tepi2);
-  if (lane == 0 && wave == 0) {
-    atomicAdd(&epi_stamp[0], (unsigned long long)(tepi1 - tepi0));
-    atomicAdd(&epi_stamp[1], (unsigned long long)(tepi2 - tepi1));
-  }
-#endif
   if (want_rowsum) flush_rowsum(g, rowsum, m0 + wm * 128, lane);
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
   GSTAMP(tend);
   if (lane == 0) atomicAdd(&stamp_acc[wave][7], (unsigned long long)(unsigned)(tend - tepi0));  // epilogue
 #endif
 }
 
-// ---- 128 x 128 tile, 4 waves (2 x 2, 64 x 64 each), same DMA images / swizzles / transposed reads as above ----
-// For the small weight-gradient products of the transformer (dY^T X: out <= 512 x 512, K = 6,272 tokens), which the
-// register-staged 128-tile path runs latency-bound (~2 us per 128-deep k-step: a transposing load -> LDS -> MFMA
-// round trip per step, r3 split-K A/B).  One barrier per 32-deep k-tile, the DMA AHEAD tiles in flight, several
-// workgroups per CU (32 KB LDS each) instead of ping-pong; split-K through the fp32 atomic epilogue (small outputs).
-namespace mid {
-// r3 stamps (csrc/tools/gemm_probe.hip, MTA_GEMM_MID=1, 512 x 128 x 6272): ~1380 cycles per k-tile whatever the
-// split (1, 8, 32) and the ring depth (AHEAD 4 or 8): DMA issue + fragment reads ~590, DMA wait ~460, MFMAs ~45 --
-// the per-CU load path of the [K][rows] operands (256-B row pieces) runs at ~12 B/clk here, so a deeper ring or
-// fewer, longer workgroups do not help (profiles/r3_gemm_mid_negative.txt)
-constexpr int TM = 128, TN = 128, THREADS = 256, AHEAD = 4, SLOTS = AHEAD + 1;  // 80 KB: two workgroups per CU
-constexpr int OP_BYTES = 128 * KT * 2, SLOT_BYTES = 2 * OP_BYTES, LDS_BYTES = SLOTS * SLOT_BYTES;
-
-__device__ __forceinline__ void wait_tiles(int n) {  // 4 DMA instructions per wave per k-tile
-  switch (n < 0 ? 0 : n > 7 ? 7 : n) {
-    case 7: asm volatile("s_waitcnt vmcnt(28)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(24)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <bool AT, bool BT>
-__device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, int gz, char* lds) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = by * TM, n0 = bx * TN;
-  const int kbeg = bz * g.k_per_split;
-  const int kend = min(g.K, kbeg + g.k_per_split);
-  const int nk = (kend - kbeg) / KT;
-  if (nk <= 0) return;
-  const __bf16* sa[2];
-  const __bf16* sb[2];
-  dma_src<AT, 128, 4>(g.A, g.lda, g.M, m0, kbeg, wave, lane, sa);
-  dma_src<BT, 128, 4>(g.B, g.ldb, g.N, n0, kbeg, wave, lane, sb);
-  const size_t stepA = AT ? (size_t)KT * g.lda : KT, stepB = BT ? (size_t)KT * g.ldb : KT;
-  auto stage = [&](int j) __attribute__((always_inline)) {
-    char* slot = lds + (j % SLOTS) * SLOT_BYTES;
-    const size_t oa = (size_t)j * stepA, ob = (size_t)j * stepB;
-    dma16(sa[0] + oa, slot + wave * 1024);
-    dma16(sa[1] + oa, slot + (wave + 4) * 1024);
-    dma16(sb[0] + ob, slot + OP_BYTES + wave * 1024);
-    dma16(sb[1] + ob, slot + OP_BYTES + (wave + 4) * 1024);
-  };
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bool want_rowsum = g.bias_grad != nullptr && bx == 0 && wn == 0;
-  float rowsum[4] = {0.f, 0.f, 0.f, 0.f};
-  // fragments double-buffered in registers: the reads of k-tile j + 1 are issued right behind the MFMAs of tile j
-  // (issued asynchronously), so the LDS latency overlaps the matrix core instead of preceding every k-tile
-  bf16x8 fa0[4], fb0[4], fa1[4], fb1[4];
-  auto read_frags = [&](int j, bf16x8 (&fa)[4], bf16x8 (&fb)[4]) __attribute__((always_inline)) {
-    const char* slot = lds + (j % SLOTS) * SLOT_BYTES;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag<AT, 128>(slot, wm * 64 + 16 * i, lane);
-#pragma unroll
-    for (int n = 0; n < 4; ++n) fb[n] = frag<BT, 128>(slot + OP_BYTES, wn * 64 + 16 * n, lane);
-  };
-#ifdef MTA_GEMM_STAMPS
-  unsigned dsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  auto step = [&](int j, bf16x8 (&fa)[4], bf16x8 (&fb)[4], bf16x8 (&na)[4], bf16x8 (&nb)[4])
-      __attribute__((always_inline)) {
-    GSTAMP(t0);
-    if constexpr (AT || BT) {  // the transposed reads are inline asm: hipcc does not track them
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    GSTAMP(t1);
-    if (want_rowsum) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) rowsum[i] += (float)fa[i][e];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int n = 0; n < 4; ++n) acc[i][n] = mfma16x16x32(fa[i], fb[n], acc[i][n]);
-    GSTAMP(t2);
-    if (j + 1 < nk) {
-      wait_tiles(min(nk - 1, j - 1 + AHEAD) - (j + 1));  // tile j + 1 landed (this wave's part)
-      GSTAMP(t3);
-      barrier();  // ... every wave's part; every wave's reads of tile j done (waited before its MFMAs)
-      GSTAMP(t4);
-      if (j + AHEAD < nk) stage(j + AHEAD);  // into the slot of tile j - 1
-      read_frags(j + 1, na, nb);
-      GSTAMP(t5);
-      GACC(2, t2, t3);
-      GACC(3, t3, t4);
-      GACC(4, t4, t5);
-    }
-    GACC(0, t0, t1);
-    GACC(1, t1, t2);
-  };
-  const int pro = min(nk, AHEAD);
-  for (int t = 0; t < pro; ++t) stage(t);
-  wait_tiles(pro - 1);
-  barrier();
-  read_frags(0, fa0, fb0);
-  GSTAMP(tloop0);
-  for (int j = 0; j < nk; j += 2) {
-    step(j, fa0, fb0, fa1, fb1);
-    if (j + 1 < nk) step(j + 1, fa1, fb1, fa0, fb0);
-  }
-  GSTAMP(tloop1);
-  gemm_epilogue<4, 4, 4>(g, acc, m0 + wm * 64, n0 + wn * 64, gz > 1, lane);
-#ifdef MTA_GEMM_STAMPS
-  GACC(6, tloop0, tloop1);
-  GSTAMP(tend);
-  GACC(7, tloop1, tend);
-  if (lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&stamp_acc[wave][i], (unsigned long long)dsum[i]);
-#endif
-  if (want_rowsum) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float s = rowsum[i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      const int m = m0 + wm * 64 + 16 * i + (lane & 15);
-      if (lane < 16 && m < g.M) atomicAdd(g.bias_grad + m, s);
-    }
-  }
-}
-}  // namespace mid
 }  // namespace big
 
 
@@ -1060,22 +849,15 @@ __global__ __launch_bounds__(big::THREADS) __attribute__((amdgpu_waves_per_eu(2,
   big::body<AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, big_lds);
 }
 
-template <bool AT, bool BT>
-__global__ __launch_bounds__(big::mid::THREADS) void gemm_mid_kernel(GemmArgs g, int nx, int ny, int nz) {
-  extern __shared__ __attribute__((aligned(16))) char mid_lds[];
-  const int b = xcd_remap(blockIdx.x, nx * ny * nz);
-  big::mid::body<AT, BT>(g, b % nx, (b / nx) % ny, b / (nx * ny), nz, mid_lds);
-}
-
 // Two independent GEMMs of one tile configuration in ONE launch (the backward's weight gradient and input
 // gradient of a Linear read the same dY): one launch gap instead of two, and both grids fill the chip together.
 // Blocks [0, n1) are problem 1 (x fastest, as a 3-D grid would be dispatched), [n1, n1 + n2) problem 2.
 struct PairGrid {
   int nx1, ny1, nz1, nx2, ny2, nz2;
 };
-template <int BM, int BN, int BKT, bool AT1, bool BT1, bool AT2, bool BT2, bool PIPE>
+template <int BM, int BN, int BKT, bool AT1, bool BT1, bool AT2, bool BT2>
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_bf16_pair_kernel(GemmArgs g1, GemmArgs g2, PairGrid pg) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT, PIPE>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT>()];
   __bf16* const As = smem;
   __bf16* const Bs = smem + BM * (BKT + 8);
   // XCD remap within each problem (a remap over the joint range deals the long weight-gradient tiles to the first
@@ -1084,55 +866,20 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
   int b = blockIdx.x;
   b = b < n1 ? xcd_remap(b, n1) : ((n1 & 7) == 0 ? n1 + xcd_remap(b - n1, pg.nx2 * pg.ny2 * pg.nz2) : b);
   if (b < n1) {
-    gemm_body<BM, BN, BKT, AT1, BT1, PIPE>(g1, b % pg.nx1, (b / pg.nx1) % pg.ny1, b / (pg.nx1 * pg.ny1), pg.nz1, As,
+    gemm_body<BM, BN, BKT, AT1, BT1>(g1, b % pg.nx1, (b / pg.nx1) % pg.ny1, b / (pg.nx1 * pg.ny1), pg.nz1, As,
                                            Bs);
   } else {
     b -= n1;
-    gemm_body<BM, BN, BKT, AT2, BT2, PIPE>(g2, b % pg.nx2, (b / pg.nx2) % pg.ny2, b / (pg.nx2 * pg.ny2), pg.nz2, As,
+    gemm_body<BM, BN, BKT, AT2, BT2>(g2, b % pg.nx2, (b / pg.nx2) % pg.ny2, b / (pg.nx2 * pg.ny2), pg.nz2, As,
                                            Bs);
   }
-}
-
-// the two-stage pipelined main loop where it fits: 128x128 tiles (enough k-steps to pipeline) whose register
-// staging is one 16-B load per item (k-contiguous operands; the transposing staging holds 8 loads per item, and
-// a second register set of those would spill).  Opt-in (MTA_GEMM_PIPE=1): measured equal to the single-stage loop
-// (mlp_large forward 117.4 vs 117.0 us, 6400x2048x2048) at one more 73.7 KB LDS image per workgroup.
-inline bool pipe_on() {
-  static const bool on = [] {
-    const char* e = getenv("MTA_GEMM_PIPE");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// the same two-stage loop for the 64 x 64 x 128 k-contiguous tiles (the transformer's long-K weight gradients on
-// transposed activations and its K = 128 products).  Opt-in (MTA_GEMM_PIPE64=1): measured no faster, 0-10 % slower
-// on the wgrad shapes even with one workgroup streaming K = 6,240 alone (profiles/r4_gemm_pipe64_negative.txt)
-inline bool pipe64_on() {
-  static const bool on = [] {
-    const char* e = getenv("MTA_GEMM_PIPE64");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
   const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
   const int blocks = nx * ny * ksplit;
-  if constexpr (BM == 64 && BKT == 128 && !AT && !BT) {
-    if (pipe64_on()) {
-      gemm_bf16_kernel<BM, BN, BKT, AT, BT, true><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
-      return;
-    }
-  }
-  if constexpr (BM == 128 && !AT && !BT) {
-    if (pipe_on()) {
-      gemm_bf16_kernel<BM, BN, BKT, AT, BT, true><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
-      return;
-    }
-  }
-  gemm_bf16_kernel<BM, BN, BKT, AT, BT, false><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
+  gemm_bf16_kernel<BM, BN, BKT, AT, BT><<<blocks, GT, 0, st>>>(g, nx, ny, ksplit);
 }
 
 // ---- big transposed-operand problems -> k-contiguous copies + the NN kernel ----
@@ -1212,14 +959,6 @@ __bf16* workspace(int slot, size_t bytes, hipStream_t st) {
   return static_cast<__bf16*>(p);
 }
 
-inline bool transpose_on() {
-  static const bool on = [] {
-    const char* e = getenv("MTA_GEMM_TRANSPOSE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // out[c][r] = in[r][c] for an R x C bf16 matrix (R, C multiples of 8)
 void transpose(const __bf16* in, int R, int C, int ld_in, __bf16* out, hipStream_t st) {
   transpose_bf16_kernel<<<dim3((C + 63) / 64, (R + 63) / 64), 256, 0, st>>>(in, R, C, ld_in, out, R);
@@ -1227,7 +966,7 @@ void transpose(const __bf16* in, int R, int C, int ld_in, __bf16* out, hipStream
 
 // rewrite a mode-1/2 problem as a mode-0 one over transposed copies; false = keep the transposing kernel
 bool to_nn(GemmArgs& g, int mode, hipStream_t st) {
-  if (mode == 0 || !transpose_on() || (long)g.M * g.N * g.K < (1L << 31)) return false;
+  if (mode == 0 || (long)g.M * g.N * g.K < (1L << 31)) return false;
   if (mode == 2) {
     __bf16* at = workspace(0, (size_t)g.M * g.K * sizeof(__bf16), st);
     __bf16* bt = workspace(1, (size_t)g.N * g.K * sizeof(__bf16), st);
@@ -1259,19 +998,12 @@ template <int BM, int BN, int BKT, int KIND>
 void launch_pair_cfg(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
   PairGrid pg{(g1.N + BN - 1) / BN, (g1.M + BM - 1) / BM, k1, (g2.N + BN - 1) / BN, (g2.M + BM - 1) / BM, k2};
   const int blocks = pg.nx1 * pg.ny1 * pg.nz1 + pg.nx2 * pg.ny2 * pg.nz2;
-  if constexpr (KIND == 0) {
-    if constexpr (BM == 64 && BKT == 128) {
-      if (pipe64_on()) {
-        gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
-        return;
-      }
-    }
-    gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
-  }
+  if constexpr (KIND == 0)
+    gemm_bf16_pair_kernel<BM, BN, BKT, false, false, false, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
   else if constexpr (KIND == 1)
-    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, false, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
   else
-    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, true, true, false><<<blocks, GT, 0, st>>>(g1, g2, pg);
+    gemm_bf16_pair_kernel<BM, BN, BKT, true, true, true, true><<<blocks, GT, 0, st>>>(g1, g2, pg);
 }
 
 template <int KIND>
@@ -1287,15 +1019,9 @@ void launch_pair_kind(int c, const GemmArgs& g1, int k1, const GemmArgs& g2, int
 void dispatch_mode(int mode, const GemmArgs& g, int ksplit, hipStream_t st);
 
 // ---- routing to the 256 x 256 kernel ----
-// MTA_GEMM_BIG=0 disables it; mta_gemm_set_big(0/1) overrides at run time (tests compare the two paths in one process)
+// mta_gemm_set_big(0/1) turns it off / on at run time (tests compare the two paths in one process)
 int g_big_override = -1;
-inline bool big_on() {
-  static const bool env_on = [] {
-    const char* e = getenv("MTA_GEMM_BIG");
-    return !(e && e[0] == '0');
-  }();
-  return g_big_override >= 0 ? g_big_override == 1 : env_on;
-}
+inline bool big_on() { return g_big_override != 0; }
 
 // split-K of the 256 x 256 kernel through fp32 slabs + one reduce launch (default) instead of fp32 atomics, which
 // run at ~1 TB/s of added bytes chip-wide (mlp_large weight gradient: 64 MB of atomics = ~110k cycles per tile on
@@ -1332,22 +1058,15 @@ void launch_big_t(const GemmArgs& g, int ksplit, hipStream_t st) {
 // Eligible for the 256 x 256 kernel: 32-deep k-tiles and enough macro-tiles to fill at least half the CUs; the
 // split-K accumulating form is re-split towards one wave of 256 workgroups (>= 8 k-tiles per split).  Returns the
 // split it runs with (g.k_per_split updated), 0 = not eligible.
-// workgroup target of the split accumulating form (MTA_BIG_WGS for the A/B; default one per CU: 128 / 192 / 384 / 512
-// measured slower on mlp_large, profiles/r4_big_wgs_sweep.txt)
-inline long big_wgs() {
-  static const long v = [] {
-    const char* e = getenv("MTA_BIG_WGS");
-    const long x = e ? atol(e) : 256;
-    return x >= 64 && x <= 2048 ? x : 256L;
-  }();
-  return v;
-}
+// workgroup target of the split accumulating form: one per CU (128 / 192 / 384 / 512 measured slower on mlp_large,
+// profiles/r4_big_wgs_sweep.txt)
+constexpr long BIG_WGS = 256;
 
 int big_split(GemmArgs& g, int ksplit) {
   if (!big_on() || g.K % big::KT || g.M < 64 || g.N < 64) return 0;
   const long tiles = (long)((g.M + big::TM - 1) / big::TM) * ((g.N + big::TN - 1) / big::TN);
-  if ((g.flags & EPI_ACCUM) && tiles * ksplit < big_wgs()) {
-    int ks = (int)std::max(1L, big_wgs() / tiles);
+  if ((g.flags & EPI_ACCUM) && tiles * ksplit < BIG_WGS) {
+    int ks = (int)std::max(1L, BIG_WGS / tiles);
     ks = std::min(ks, std::max(1, g.K / 256));
     if (ks > ksplit) {
       int kps = (g.K + ks - 1) / ks;
@@ -1374,44 +1093,6 @@ bool try_big(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
   return true;
 }
 
-// ---- the 128 x 128 LDS-DMA kernel for weight gradients too small for the macro tiles ----
-// Opt-in (MTA_GEMM_MID=1): measured slower than the register-staged path on the transformer's weight gradients
-// (512 x 128 x 6272: 19.0 vs 16.9 us at the best split, with fragment double buffering and an 8-deep ring tried;
-// the stamps put ~1050 of its ~1380 cycles per k-tile in the DMA issue / wait: load-path bound, not latency bound;
-// profiles/r3_gemm_mid_negative.txt).
-int g_mid_override = -1;
-inline bool mid_on() {
-  static const bool env_on = [] {
-    const char* e = getenv("MTA_GEMM_MID");
-    return e && e[0] == '1';
-  }();
-  return g_mid_override >= 0 ? g_mid_override == 1 : env_on;
-}
-
-bool mid_eligible(int mode, const GemmArgs& g) {
-  return mid_on() && mode == 2 && (g.flags & EPI_ACCUM) && g.K % big::KT == 0 && g.M >= 64 && g.N >= 64;
-}
-
-// split towards ~256 workgroups with >= 4 k-tiles each (fp32 atomic epilogue: the outputs are small); a caller that
-// asked for no split (deterministic mode) gets none: the atomics' order would vary
-bool try_mid(int mode, const GemmArgs& g_in, int ksplit_in, hipStream_t st) {
-  if (!mid_eligible(mode, g_in)) return false;
-  GemmArgs g = g_in;
-  const int nx = (g.N + big::mid::TN - 1) / big::mid::TN, ny = (g.M + big::mid::TM - 1) / big::mid::TM;
-  int ks = std::max(1, std::min(ksplit_in, 256 / (nx * ny)));
-  ks = std::min(ks, std::max(1, g.K / (4 * big::KT)));
-  int kps = (g.K + ks - 1) / ks;
-  kps = (kps + big::KT - 1) / big::KT * big::KT;
-  ks = (g.K + kps - 1) / kps;
-  g.k_per_split = kps;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_mid_kernel<true, true>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               big::mid::LDS_BYTES) == hipSuccess;
-  (void)attr;
-  gemm_mid_kernel<true, true><<<nx * ny * ks, big::mid::THREADS, big::mid::LDS_BYTES, st>>>(g, nx, ny, ks);
-  return true;
-}
-
 // (weight-gradient, input-gradient) pair: modes (2, 1) with one tile configuration; false -> launch separately.
 // Big pairs run on transposed copies (both NN) when both problems qualify.
 bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, hipStream_t st) {
@@ -1419,12 +1100,6 @@ bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, h
   if (big_eligible(g1_in, k1) && big_eligible(g2_in, k2)) {
     try_big(2, g1_in, k1, st);
     try_big(1, g2_in, k2, st);
-    return true;
-  }
-  // small weight gradient on the 128 x 128 LDS-DMA kernel, its input-gradient partner on its own path
-  if (!big_eligible(g1_in, k1) && mid_eligible(2, g1_in)) {
-    try_mid(2, g1_in, k1, st);
-    dispatch_mode(1, g2_in, k2, st);
     return true;
   }
   const int c = tile_config(g1_in, k1);
@@ -1444,9 +1119,9 @@ bool launch_pair(const GemmArgs& g1_in, int k1, const GemmArgs& g2_in, int k2, h
 }
 
 // two weight gradients (modes (2, 2), the transformer FFN's dW2 and dW1 after the fused input-gradient launch) in one
-// launch when neither takes the 256 x 256 / 128 x 128 DMA kernels and both have one tile configuration
+// launch when neither takes the 256 x 256 DMA kernel and both have one tile configuration
 bool launch_pair_ww(const GemmArgs& g1, int k1, const GemmArgs& g2, int k2, hipStream_t st) {
-  if (big_eligible(g1, k1) || big_eligible(g2, k2) || mid_eligible(2, g1) || mid_eligible(2, g2)) return false;
+  if (big_eligible(g1, k1) || big_eligible(g2, k2)) return false;
   if ((long)g1.M * g1.N * g1.K >= (1L << 31) || (long)g2.M * g2.N * g2.K >= (1L << 31)) return false;  // to_nn sizes
   const int c = tile_config(g1, k1);
   if (c != tile_config(g2, k2)) return false;
@@ -1475,18 +1150,13 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
   // busiest CUs run 4 while the mean is 3.1 (78 %); 1,600 tiles of 128x64 = 6.25 per CU (89 %).  128x64 tiles cost
   // ~10 % per FLOP at equal balance (4096^3: 251 vs 226 us), so they are taken when 0.9 x their balance beats the
   // 128x128 balance: mlp_large forward 118 -> 108 us, step 1.69 -> 1.59 ms (profiles/r2_gemm_bn64_ab.txt).
-  // MTA_GEMM_BN64=0/1 forces the choice.
-  static const int bn64_env = [] {
-    const char* e = getenv("MTA_GEMM_BN64");
-    return e ? (e[0] == '1' ? 1 : 0) : -1;
-  }();
   bool bn64 = false;
   if (deep && !AT && !BT) {
     constexpr long CUS = 256;
     const long t64 = (long)((g.M + 127) / 128) * ((g.N + 63) / 64) * ksplit;
     const double e128 = (double)tiles128 / (double)(CUS * ((tiles128 + CUS - 1) / CUS));
     const double e64 = (double)t64 / (double)(CUS * ((t64 + CUS - 1) / CUS));
-    bn64 = bn64_env >= 0 ? bn64_env == 1 : 0.9 * e64 > e128;
+    bn64 = 0.9 * e64 > e128;
   }
   if (tiles128 >= 256) {
     if (bn64) launch<128, 64, 64, AT, BT>(g, ksplit, st);
@@ -1500,7 +1170,6 @@ void dispatch(const GemmArgs& g, int ksplit, hipStream_t st) {
 
 void dispatch_mode(int mode, const GemmArgs& g_in, int ksplit, hipStream_t st) {
   if (try_big(mode, g_in, ksplit, st)) return;
-  if (try_mid(mode, g_in, ksplit, st)) return;
   GemmArgs g = g_in;
   if (to_nn(g, mode, st)) mode = 0;
   if (mode == 0) dispatch<false, false>(g, ksplit, st);
@@ -1520,7 +1189,6 @@ struct Pending {
 }  // namespace
 
 extern "C" void mta_gemm_set_big(int on) { g_big_override = on; }
-extern "C" void mta_gemm_set_mid(int on) { g_mid_override = on; }
 
 // launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
 extern "C" void mta_gemm_flush() {

@@ -25,7 +25,10 @@ namespace {
 constexpr int BM = 64, BN = 64, BK = 32, TPB = 256;
 constexpr int LS = BK + 4;  // LDS row stride (floats)
 
-constexpr int F32X_BIAS = 1, F32X_GELU = 2, F32X_ACCUM = 8;  // epilogue flags (the EPI_* values of gemm.hip)
+// epilogue flags (the EPI_* values of gemm.hip): + bias, GELU (input saved to pre), x GELU'(pre) (the input gradient of
+// a GELU layer: pre is read), C += instead of C =, + resid[m][n] (row stride ldc: a residual connection)
+// a counter-hash dropout scale (0 or 1 / (1 - p)) regenerated from the seed, forward and backward alike
+constexpr int F32X_BIAS = 1, F32X_GELU = 2, F32X_DGELU = 4, F32X_ACCUM = 8, F32X_RESID = 16, F32X_DROPOUT = 32;
 
 struct GemmF32Args {
   const float* A;
@@ -33,7 +36,10 @@ struct GemmF32Args {
   const float* bias;
   const float* mask;
   float* C;
-  float* pre;    // F32X_GELU: the GELU input [M][ldc] (or null)
+  float* pre;    // F32X_GELU: the GELU input [M][ldc] (or null); F32X_DGELU: read
+  const float* resid;  // F32X_RESID: added to the product [M][ldc]
+  const uint64_t* seed;  // F32X_DROPOUT: the site's device-resident seed (mta_dropout_scale(seed, m, n, p))
+  float drop_p;
   int M, N, K;
   int lda, ldb, ldc, n_store, flags;
 };
@@ -191,13 +197,14 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(GemmF32Args p) {
         }
     }
   }
-  // epilogue: + bias, GELU (input saved), * mask, = or += guarded fp32 stores (lane (q, j): rows 4q..4q+3 of column
+  // epilogue: + bias, GELU (input saved), x GELU'(pre), * mask, * dropout, + resid, = or += guarded fp32 stores (lane (q, j): rows 4q..4q+3 of column
   // j of each block)
 #pragma unroll
   for (int bj = 0; bj < 2; ++bj) {
     const int n = n0 + wn * 32 + bj * 16 + j;
     if (n >= p.n_store) continue;
     const float b = (p.flags & F32X_BIAS) && p.bias ? p.bias[n] : 0.f;
+    const uint64_t sd = (p.flags & F32X_DROPOUT) ? *p.seed : 0;
 #pragma unroll
     for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
@@ -210,7 +217,10 @@ __global__ __launch_bounds__(TPB) void gemm_f32_kernel(GemmF32Args p) {
           if (p.pre) p.pre[o] = v;
           v = mta_gelu(v);
         }
+        if (p.flags & F32X_DGELU) v *= mta_gelu_grad(p.pre[o]);
         if (p.mask) v *= p.mask[(size_t)m * p.N + n];
+        if (p.flags & F32X_DROPOUT) v *= mta_dropout_scale(sd, m, n, p.drop_p);
+        if (p.flags & F32X_RESID) v += p.resid[o];
         if (p.flags & F32X_ACCUM) p.C[o] += v;
         else p.C[o] = v;
       }
@@ -265,19 +275,24 @@ int dispatch(int prec, const GemmF32Args& p, bool akm, bool bkn, hipStream_t st)
 extern "C" int mta_gemm_f32(int prec, const float* A, const float* B, const float* bias, const float* mask, float* C,
                             int M, int N, int K, int b_kn, hipStream_t st) {
   if (M < 1 || N < 1 || K < 1 || (size_t)M * N >= (1ull << 40)) return -1;
-  GemmF32Args p{A, B, bias, mask, C, nullptr, M, N, K, K, b_kn ? N : K, N, N, bias ? F32X_BIAS : 0};
+  GemmF32Args p{A, B, bias, mask, C, nullptr, nullptr, nullptr, 0.f, M, N, K, K, b_kn ? N : K, N, N,
+                bias ? F32X_BIAS : 0};
   return dispatch(prec, p, false, b_kn != 0, st);
 }
 
 // the general form: A [M][K] (lda) or stored [K][M] (a_km); B [N][K] or [K][N] (b_kn) (ldb); C [M][ldc], the first
-// n_store columns written; flags F32X_*; pre (F32X_GELU): the GELU input [M][ldc]
+// n_store columns written; flags F32X_*; pre (F32X_GELU / F32X_DGELU): the GELU input [M][ldc]; mask [M][N]
+// (dropout scale: 0 or 1 / (1 - p)) multiplies the result, as does the seed's hash mask (F32X_DROPOUT, rate drop_p);
+// resid (F32X_RESID) [M][ldc] is added to it
 extern "C" int mta_gemm_f32x(int prec, const float* A, int a_km, int lda, const float* B, int b_kn, int ldb,
                              float* C, int ldc, int n_store, int M, int N, int K, int flags, const float* bias,
-                             float* pre, hipStream_t st) {
+                             float* pre, const float* mask, const float* resid, const uint64_t* seed, float drop_p,
+                             hipStream_t st) {
   if (M < 1 || N < 1 || K < 1 || (size_t)M * N >= (1ull << 40) || n_store < 1 || n_store > N || ldc < n_store ||
-      lda < (a_km ? M : K) || ldb < (b_kn ? N : K))
+      lda < (a_km ? M : K) || ldb < (b_kn ? N : K) || ((flags & F32X_DGELU) && !pre) || ((flags & F32X_RESID) && !resid) ||
+      ((flags & F32X_DROPOUT) && (!seed || !(drop_p >= 0.f && drop_p < 1.f))))
     return -1;
-  GemmF32Args p{A, B, bias, nullptr, C, pre, M, N, K, lda, ldb, ldc, n_store, flags};
+  GemmF32Args p{A, B, bias, mask, C, pre, resid, seed, drop_p, M, N, K, lda, ldb, ldc, n_store, flags};
   return dispatch(prec, p, a_km != 0, b_kn != 0, st);
 }
 

@@ -15,10 +15,10 @@
 // corrected per-window batched NLL is windows=B, kwin=K, factor_stride=2.
 #include "common.h"
 
-#ifndef MTA_LOSS_STAMPS
-#define MTA_LOSS_STAMPS 0
+#ifndef MTA_STAMPS
+#define MTA_STAMPS 0
 #endif
-#if MTA_LOSS_STAMPS
+#if MTA_STAMPS
 // diagnostic build only (csrc/tools/losses_probe.hip): s_memtime at the phase boundaries of the training decoder
 __device__ unsigned long long mta_loss_stamps[8];
 #define LSTAMP(k)                                                                  \
@@ -346,9 +346,6 @@ __global__ __launch_bounds__(TPB) void heads_losses_train_kernel(
 }
 
 // ---- register-resident training decoder (N <= 128, n <= 32, H in {16, 32, 64, 128}, <= 4 NLL windows) ----
-#ifndef MTA_DECODER_REG
-#define MTA_DECODER_REG 1  // 0: always the wave-per-sequence kernel above (kept for comparison in the probe)
-#endif
 // The wave-per-sequence kernel above loops 16 waves over the sequences with a full 64-lane reduction per
 // sequence and quantity, and stages y and h_T through LDS first: 12.9 us for the headline step's MSE decoder
 // (r2 rocprof), almost all of it dependent latency.  Here every input is loaded ONCE, straight into registers,
@@ -637,7 +634,7 @@ static void launch_decoder_reg(const float* h, const float* wa, const float* ba,
 static bool decoder_reg_fits(const float* h, const float* y, const float* dh, const float* wa, const float* wb,
                              int H, int N, int n, int C, int windows, int kwin, int want_nll) {
   const auto al = [](const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; };
-  if (!MTA_DECODER_REG || N < 1 || N > RD_MAXN || n < 1 || n > 32 || C < 2 || (C & 1)) return false;
+  if (N < 1 || N > RD_MAXN || n < 1 || n > 32 || C < 2 || (C & 1)) return false;
   if (H != 16 && H != 32 && H != 64 && H != 128) return false;
   if ((N + 31) / 32 > RD_MAXP || ((long)N * H / 4 + TPB - 1) / TPB > RD_MAXP) return false;
   if (want_nll && (windows < 1 || windows > RD_MAXW || (long)windows * kwin != N)) return false;

@@ -20,10 +20,10 @@
 //     four gates of one sequence are one 16-byte access.
 #include "common.h"
 
-#ifndef MTA_LSTM_STAMPS
-#define MTA_LSTM_STAMPS 0
+#ifndef MTA_STAMPS
+#define MTA_STAMPS 0
 #endif
-#if MTA_LSTM_STAMPS
+#if MTA_STAMPS
 // Diagnostic build only (csrc/tools/lstm_probe.hip): per-segment s_memtime sums of block 0 / lane 0.
 __device__ unsigned long long mta_stamp_acc[2][8];
 #define STAMP_DECL unsigned long long _ts_prev = 0, _ts_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -457,17 +457,17 @@ void launch_fwd(const float* x, const float* w_ih, const float* b_ih, const floa
                 float* stash, const float* w_hh, float* hseq, int N, int Np, int T, hipStream_t st) {
   dim3 grid(Np / S), block((H / 16) * 64);
   float4* s4 = reinterpret_cast<float4*>(stash);
-#define MTA_FWD(F)                                                                                           \
+#define LSTM_FWD_CASE(F)                                                                                           \
   if (s4) lstm_fwd_kernel<H, PREC, F, true><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, s4, w_hh, hseq, N, Np, T); \
   else lstm_fwd_kernel<H, PREC, F, false><<<grid, block, 0, st>>>(x, w_ih, b_ih, b_hh, gx, s4, w_hh, hseq, N, Np, T)
   // layer 0 of the configs has F = 3 (interaction_only) or 5; other widths go through the GEMM path
   switch (fin) {
-    case 0: MTA_FWD(0); break;
-    case 3: MTA_FWD(3); break;
-    case 5: MTA_FWD(5); break;
+    case 0: LSTM_FWD_CASE(0); break;
+    case 3: LSTM_FWD_CASE(3); break;
+    case 5: LSTM_FWD_CASE(5); break;
     default: break;
   }
-#undef MTA_FWD
+#undef LSTM_FWD_CASE
 }
 
 template <int H>

@@ -176,10 +176,7 @@ extern "C" void mta_gather_batch(const float* const* src, float* const* dst, con
   // every block arrives on one counter (the last advances the cursor): keep the grid near 2048 workgroups -- at
   // B = 64 one block per 16-KB piece was ~5k same-word atomics, ~35 us per step; mlp_large B = 64 gather with a
   // target of 512 / 2048 / 8192 blocks: 27.1 / 23.6 / 23.4 us (r3 traces)
-  static const int grid_target = [] {
-    const char* e = getenv("MTA_GATHER_BLOCKS");  // A/B knob
-    return e ? atoi(e) : 2048;
-  }();
+  constexpr int grid_target = 2048;
   const int per = B * (ntensors > 0 ? ntensors : 1);
   const int target = grid_target / per > 1 ? grid_target / per : 1;
   a.span = (pieces + target - 1) / target;

@@ -26,15 +26,15 @@
 #include "common.h"
 #include "lstm_wgrad.h"
 
-#ifndef MTA_STACK_STAMPS
-#define MTA_STACK_STAMPS 0
+// diagnostic builds (csrc/tools/lstm_stack_probe.hip): -DMTA_STAMPS=1 per-segment s_memtime sums, -DMTA_STAMPS=2 the
+// timeline (s_memtime of every forward workgroup's recurrent wave 0 at entry, after the pre-loop barrier, after step
+// T/2 and at the end)
+#ifndef MTA_STAMPS
+#define MTA_STAMPS 0
 #endif
-// timeline build (probe only): s_memtime of every forward workgroup's recurrent wave 0 at entry, after the pre-loop
-// barrier, after step T/2 and at the end
-#ifndef MTA_STACK_TIMELINE
-#define MTA_STACK_TIMELINE 0
-#endif
-#if MTA_STACK_TIMELINE
+#define STACK_STAMPS (MTA_STAMPS == 1)
+#define STACK_TIMELINE (MTA_STAMPS == 2)
+#if STACK_TIMELINE
 __device__ unsigned long long mta_stack_tl[2][64][4];
 #define STACK_TL(dir, k)                                                                      \
   do {                                                                                        \
@@ -45,12 +45,16 @@ __device__ unsigned long long mta_stack_tl[2][64][4];
   do {                   \
   } while (0)
 #endif
+// s_sleep units (~64 cycles each) the backward gradient waves wait after a step barrier before their dx MFMA product:
+// right after the barrier the recurrent waves run their own MFMA chain on the same SIMDs, and two MFMA streams on one
+// SIMD serialise.  4: bwd 98.0 -> 94.5 us at the headline shape; 2: 96, 6: 95.2, 8: 98.2, 12: 104
+// (profiles/r4_lstm_knobs.txt).  The dG rows are stored by the recurrent waves (storing them from the gradient waves
+// measured slower, profiles/r4_lstm_bwd_dg_negative.txt)
+constexpr int DX_DELAY = 4;
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD: on
 // (fwd 80.0 -> 79.5 us, with DX_DELAY 4 bwd 94.1 us; profiles/r4_lstm_knobs.txt)
-#ifndef MTA_STACK_PRIO
-#define MTA_STACK_PRIO 1
-#endif
-#if MTA_STACK_STAMPS
+constexpr int STACK_PRIO = 1;
+#if STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
 __device__ unsigned long long mta_stack_stamp_acc[2][3][8];
@@ -78,11 +82,6 @@ namespace {
 
 constexpr int S = 16;
 constexpr int STASH = 5;
-// step-interleaved helper workgroups per (layer, tile): the forward projection (gx) and the backward dx products
-// each run in NPP / NPX workgroups, workgroup p taking the steps t = p (mod NP); each of them then has NP steps of
-// the recurrence's time for one plainly serialised step (poll, load, product, store, drain, publish).  Their progress
-// words sit 8 words apart in the (layer, tile) slot.
-constexpr int NPP = 2, NPX = 4;
 constexpr int MAXL = 8;
 constexpr unsigned SPIN_LIMIT = 1u << 21;  // default poll bound (env MTA_LSTM_SPIN_LIMIT overrides: fault tests)
 constexpr int FLAG_STRIDE = 32;
@@ -211,8 +210,6 @@ struct StackFwdArgs {
   float* stash[MAXL];   // BPTT stash per layer (null: inference)
   const uint64_t* seeds;  // [MAXL]: seed of the dropout applied to layer l's input
   float drop_p;
-  float* gx[MAXL];      // gx[l] (l >= 1): bias + W_ih x_t of layer l, (T, Np, H) float4 (the projection workgroups)
-  unsigned* gflags;     // [MAXL][tr8] progress words of gx[l] (projection workgroup (l, tile))
   unsigned* flags;      // [MAXL][tr8] progress words (epoch-stamped, never reset)
   unsigned* timeout;
   unsigned* ctl;
@@ -328,8 +325,8 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
     unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
     const int ts = lane >> 2, tc = 4 * (lane & 3), unit4 = 16 * w + tc;
     const unsigned E = base >> a.eshift;
-    // every store wave learns for itself whether its consumer (the projection workgroup of tile `tile` of layer
-    // + 1, which publishes its XCC) shares this XCD's L2
+    if (w == 0 && lane == 0) publish_xcc(a.xcc + layer * a.tr8 + tile, E);
+    // every store wave learns for itself whether its consumer (tile `tile` of layer + 1) shares this XCD's L2
     const bool local = a.xcd_local && !last && partner_local(a.xcc + (layer + 1) * a.tr8 + tile, E, 1u << 14);
     // step t from staging slot t & 1: hand-offs first (h, masked h), then keep word and stash (issue order per
     // interval, the loop-head vmcnt counts below depend on it)
@@ -551,61 +548,107 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
         if (t + 1 < T) interval(t + 1, xbA);
       }
     } else {
-      // Layers >= 1: gx_t = bias + W_ih x_t comes from the layer's projection workgroups (stack_proj_body, on
-      // another CU): the input waves only poll its progress and copy gx_t into the LDS slot, three steps ahead in
-      // two register sets (step s in set s & 1), so no MFMA stream shares the recurrent waves' SIMDs.
-      // Lane of input wave w: float4 f = 64 w + lane + 64 NW k of the S x H float4 block (row f / H, unit f % H).
-      constexpr int GL = S * H / (64 * NW);  // float4 per lane and step (4)
-      unsigned* gflag = a.gflags + FLAG_STRIDE * (layer * a.tr8 + tile);
-      const float* gxin = a.gx[layer];
-      struct GSet {
-        float4 v[GL];
+      // Layers >= 1: every input wave loads a QUARTER of x_t (units [16w, 16w + 16) of the 16 sequences: one
+      // float4 per lane) and writes it split into the shared LDS image; every wave then reads its MFMA A
+      // fragments from the image.  4x fewer hand-off loads and splits per wave than each wave loading all of
+      // x_t (r3 stamps: that input work set the layer-1 pace).  x_s is polled + loaded 4 intervals ahead into
+      // register set s & 1, written into image slot s & 1 two intervals ahead, consumed one interval ahead.
+      const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
+      float4 xqA = make_float4(0.f, 0.f, 0.f, 0.f), xqB = xqA;
+      unsigned seen = base;
+      auto load_q = [&](int t, float4& xq) {
+        seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
+        xq = load_sc1(xin, ((size_t)t * Np + n0 + ls) * H + lu);
       };
-      GSet gA, gB;
-      unsigned seen[NPP];
+      auto write_q = [&](int t, const float4& xq) {
+        const int slot = t & 1;
+        if constexpr (PREC == PREC_F32) {
+          *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
+        } else {
+          const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
+          if constexpr (PREC == PREC_F16X2) {  // one fp16 per element (the activation operand is not split)
+            typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+            f16x4_t v4;
 #pragma unroll
-      for (int p = 0; p < NPP; ++p) seen[p] = base;
-      auto load_gx = [&](int t, GSet& g) {
-        seen[t % NPP] = wait_progress(gflag + 8 * (t % NPP), base + (unsigned)(t + 1), seen[t % NPP], a.timeout,
-                                      a.spin_limit);
+            for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
+            *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
+          } else {
+            bf16x4 hi4, lo4;
 #pragma unroll
-        for (int k = 0; k < GL; ++k) {
-          const int f = 64 * w + lane + 64 * NW * k;
-          g.v[k] = load_sc1(gxin, (((size_t)t * Np + n0 + f / H) * H + f % H) * 4);
+            for (int e = 0; e < 4; ++e) {
+              __bf16 hi, lo;
+              split_bf16(xv[e], hi, lo);
+              hi4[e] = hi;
+              lo4[e] = lo;
+            }
+            *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
+            if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
+          }
         }
       };
-      auto write_gx = [&](int t, const GSet& g) {
+      auto compute_gx_img = [&](int t) {  // gx_t from image slot t & 1 into gxs slot t & 1
+        const int slot = t & 1;
+        f32x4 acc[4];
 #pragma unroll
-        for (int k = 0; k < GL; ++k) {
-          const int f = 64 * w + lane + 64 * NW * k;
-          gxs[t & 1][f / H][f % H] = g.v[k];
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
+        if constexpr (PREC == PREC_F32) {
+          const float* xr = &sm.x_f[slot][j][KF * q];
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) {
+            const float av = xr[kk];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
+          }
+        } else {
+          V8 ahi[KB];
+          bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            ahi[kb] = *reinterpret_cast<const V8*>(&sm.x_hi[slot][j][32 * kb + 8 * q]);
+            if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_lo[slot][j][32 * kb + 8 * q]);
+          }
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if constexpr (PREC == PREC_BF16X3) {
+                acc[g] = mfma16x16x32(alo[kb], Xhi[g][kb], acc[g]);
+                acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
+              }
+              if constexpr (PREC == PREC_F16X2) acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
+              acc[g] = mfma16x16x32(ahi[kb], Xhi[g][kb], acc[g]);
+            }
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
       };
-      load_gx(0, gA);
-      mta_wait_vmem();
-      write_gx(0, gA);
-      if (T > 1) load_gx(1, gB);
-      if (T > 2) load_gx(2, gA);
-      __syncthreads();  // P0
+      load_q(0, xqA);
+      if (T > 1) load_q(1, xqB);
+      write_q(0, xqA);
+      if (T > 1) write_q(1, xqB);
+      if (T > 2) load_q(2, xqA);
+      if (T > 3) load_q(3, xqB);
+      __syncthreads();  // P0: image slots 0 and 1 complete
+      compute_gx_img(0);
       __syncthreads();  // P1 (pre-loop): gx_0 ready
-      // interval t writes gx_{t+1} (set (t+1) & 1, loaded two intervals ago) into slot (t+1) & 1 and refills the
-      // set with gx_{t+3}; each load_gx issues 2 GL vector-memory ops
-      auto interval = [&](int t, GSet& g) {
+      // interval t: x_{t+2} (set t & 1) -> image slot t & 1 (x_t there was consumed in interval t-1); gx_{t+1}
+      // from slot (t+1) & 1; refill set t & 1 with x_{t+4}
+      auto interval = [&](int t, float4& xq) {
         SSTAMP(0)
-        if (t + 1 < T) {
-          if (t + 2 < T) mta_wait_vmcnt<2 * GL>();  // the previous interval's loads (gx_{t+2}) stay in flight
-          else mta_wait_vmem();
-          write_gx(t + 1, g);
+        {
+          if (t + 2 < T) write_q(t + 2, xq);
+          SSTAMP(1)
+          if (t + 1 < T) compute_gx_img(t + 1);
+          SSTAMP(2)
+          if (t + 4 < T) load_q(t + 4, xq);
+          SSTAMP(3)
         }
-        SSTAMP(1)
-        if (t + 3 < T) load_gx(t + 3, g);
-        SSTAMP(2)
         __syncthreads();
-        SSTAMP(3)
+        SSTAMP(4)
       };
       for (int t = 0; t < T; t += 2) {
-        interval(t, gB);
-        if (t + 1 < T) interval(t + 1, gA);
+        interval(t, xqA);
+        if (t + 1 < T) interval(t + 1, xqB);
       }
     }
     SSTAMP_FLUSH(0, 2, w == 0)
@@ -616,7 +659,7 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 
   // =========================== recurrent waves ===========================
   STACK_TL(0, 0);
-  if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
+  if (__builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(STACK_PRIO);
   const float* w_hh = a.w_hh[layer];
   const bool stash = a.stash[layer] != nullptr;
 
@@ -764,148 +807,6 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   STACK_TL(0, 3);
 }
 
-// Projection workgroup of (layer l >= 1, tile): gx_t = b_ih + b_hh + W_ih x_t for t = 0 .. T-1, where x_t is the
-// (dropout-masked) output of layer l-1, written to gx[l] for layer l's input waves.  Its own CU (block ids right
-// after layer l-1's recurrence, same XCD as the tile's producer), so this MFMA stream never shares a SIMD with a
-// recurrence.  H/16 waves (wave w: units [16w, 16w + 16), all four gates); the block's other waves only keep the
-// barrier count.  NPP of them per tile, workgroup p taking the steps t = p (mod NPP), each step plainly serialised:
-// [poll + load x_t; LDS A-operand image] [barrier] [MFMA; gx_t stores; drain] [barrier; publish t in word p]
-template <int H, int PREC>
-__device__ __forceinline__ void stack_proj_body(const StackFwdArgs& a, const int layer, const int tile, const int par,
-                                                FwdSmem<H, PREC>& sm, const unsigned base) {
-  constexpr int NW = H / 16;
-  constexpr int KB = H / 32;
-  constexpr int KF = H / 4;
-  using E = typename OpT<PREC>::E;
-  using V8 = typename OpT<PREC>::V8;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool idle = wave >= NW;
-  const int w = idle ? 0 : wave;
-  const int q = lane >> 4, j = lane & 15;
-  const int u = 16 * w + j;
-  const int n0 = tile * S;
-  const int Np = a.Np, T = a.T;
-  const float* w_ih = a.w_ih[layer];
-  const float* xin = a.xdrop[layer] ? a.xdrop[layer] : a.hseq[layer - 1];
-  unsigned* in_flag = a.flags + FLAG_STRIDE * ((layer - 1) * a.tr8 + tile);
-  unsigned* my_flag = a.gflags + FLAG_STRIDE * (layer * a.tr8 + tile) + 8 * par;
-  float* gx = a.gx[layer];
-  // the producer's store waves read this to pick plain (same XCD) or write-through stores
-  if (par == 0 && wave == 0 && lane == 0) publish_xcc(a.xcc + layer * a.tr8 + tile, base >> a.eshift);
-  float bias[4];
-  V8 Xhi[4][PREC == PREC_F32 ? 1 : KB], Xlo[4][kWeightLo<PREC> ? KB : 1];
-  float Xf[4][PREC == PREC_F32 ? KF : 1];
-  if (!idle) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
-    if constexpr (PREC == PREC_F32) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int kk = 0; kk < KF; ++kk) Xf[g][kk] = w_ih[(size_t)(g * H + u) * H + KF * q + kk];
-    } else {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            E hi, lo;
-            split_bf16(w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
-            Xhi[g][kb][e] = hi;
-            if constexpr (kWeightLo<PREC>) Xlo[g][kb][e] = lo;
-          }
-    }
-  }
-  // wave w loads a quarter of x_t (units [16w, 16w + 16) of the 16 sequences: one float4 per lane)
-  const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
-  unsigned seen = base;
-  auto issue = [&](int t, float4& xq) {
-    seen = wait_progress(in_flag, base + (unsigned)(t + 1), seen, a.timeout, a.spin_limit);
-    xq = load_sc1(xin, ((size_t)t * Np + n0 + ls) * H + lu);
-  };
-  auto write_x = [&](int t, const float4& xq) {
-    const int slot = t & 1;
-    if constexpr (PREC == PREC_F32) {
-      *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
-    } else {
-      const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
-      if constexpr (PREC == PREC_F16X2) {  // one fp16 per element (the activation operand is not split)
-        typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
-        f16x4_t v4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
-        *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
-      } else {
-        bf16x4 hi4, lo4;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          __bf16 hi, lo;
-          split_bf16(xv[e], hi, lo);
-          hi4[e] = hi;
-          lo4[e] = lo;
-        }
-        *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
-        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
-      }
-    }
-  };
-  auto compute_store = [&](int t) {
-    const int slot = t & 1;
-    f32x4 acc[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
-    if constexpr (PREC == PREC_F32) {
-      const float* xr = &sm.x_f[slot][j][KF * q];
-#pragma unroll
-      for (int kk = 0; kk < KF; ++kk) {
-        const float av = xr[kk];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
-      }
-    } else {
-      V8 ahi[KB];
-      bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        ahi[kb] = *reinterpret_cast<const V8*>(&sm.x_hi[slot][j][32 * kb + 8 * q]);
-        if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_lo[slot][j][32 * kb + 8 * q]);
-      }
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          if constexpr (PREC == PREC_BF16X3) {
-            acc[g] = mfma16x16x32(alo[kb], Xhi[g][kb], acc[g]);
-            acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
-          }
-          if constexpr (PREC == PREC_F16X2) acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
-          acc[g] = mfma16x16x32(ahi[kb], Xhi[g][kb], acc[g]);
-        }
-    }
-    // (sequence 4q + i, unit u): the four gates as one float4 -- the layout the input waves copy into their slot
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      store_sc1_x4(gx + (((size_t)t * Np + n0 + 4 * q + i) * H + u) * 4,
-                   f32x4{acc[0][i], acc[1][i], acc[2][i], acc[3][i]});
-  };
-  for (int t = par; t < T; t += NPP) {
-    if (!idle) {
-      float4 xq;
-      issue(t, xq);
-      write_x(t, xq);
-    }
-    __syncthreads();  // image slot t & 1 complete
-    if (!idle) {
-      compute_store(t);
-      mta_wait_vmem();
-    }
-    __syncthreads();  // every wave's gx_t stores drained
-    if (wave == 0 && lane == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(t + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch);
 // four independent 16-byte loads in flight per thread before their stores
 __device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P) {
@@ -950,15 +851,12 @@ __global__ __launch_bounds__((H / 16) * 192) void lstm_stack_fwd_kernel(StackFwd
     if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, cbase, a.eshift)) a.g.cursor[0] += 1;
     return;
   }
-  // [recurrence(0) | projection(1) x NPP | recurrence(1) | projection(2) x NPP | ... | recurrence(L-1)] x tr8 blocks:
-  // every hand-off's producer has the lower block id, tile i of every group the same id modulo 8 (one XCD)
-  const int grp = blockIdx.x / ((1 + NPP) * a.tr8), r = blockIdx.x % ((1 + NPP) * a.tr8), tile = r % a.tr8;
+  const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
   const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
-  __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by the role bodies
+  __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
   if (tile < a.ntiles) {
-    if (r >= a.tr8) stack_proj_body<H, PREC>(a, grp + 1, tile, r / a.tr8 - 1, sm, base);
-    else if (grp == 0) stack_fwd_body<H, PREC, FIN0, true>(a, 0, tile, sm, base);
-    else stack_fwd_body<H, PREC, FIN0, false>(a, grp, tile, sm, base);
+    if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
+    else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
   }
   // every workgroup read the cursor before arriving: the last one advances it
   if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift) && a.gather) a.g.cursor[0] += 1;
@@ -1002,29 +900,17 @@ struct BwdSmem {
   __bf16 g_hi[2][S][PREC == PREC_F32 ? 8 : ROWB];
   __bf16 g_lo[2][S][PREC == PREC_BF16X3 ? ROWB : 8];
   float g_f[2][S][PREC == PREC_F32 ? ROWF : 4];
-  float dhs[2][S][H];  // dH_t of the layer above, staged by the helper waves
+  float dhs[2][S][H];  // dH_t of the layer above, staged by the gradient waves
+  float tr[H / 16][S][TRS];  // per-gradient-wave transpose scratch of the dx store
 };
 
-// dx workgroup image: dG_t of one tile (16 rows x 4H gate columns, unit-major c = 4u + g, the global layout) as
-// the MFMA A operand (bf16 hi / lo, or fp32 for PREC_F32 in the f32-MFMA k order), plus each wave's transpose
-// scratch of the dX store
-template <int H, int PREC>
-struct DxSmem {
-  static constexpr int ROWB = 4 * H + 8, ROWF = 4 * H + 4;
-  __bf16 g_hi[S][PREC == PREC_F32 ? 8 : ROWB];
-  __bf16 g_lo[S][PREC == PREC_BF16X3 ? ROWB : 8];
-  float g_f[S][PREC == PREC_F32 ? ROWF : 4];
-  float tr[H / 16][S][TRS];
-};
-
-// Backward workgroup = 2 x (H/16) waves.
-//   RECURRENT waves [0, H/16): BPTT like lstm.hip -- dG_t from the stash, dh_{t-1} = dG_t W_hh through the LDS dG
-//     image, one barrier per step -- reading everything from LDS: the stash and dH_t of the layer above are staged
-//     by the helpers, the dG rows are written out by the helpers.  No global memory operation in the loop.
-//   HELPER waves [H/16, 2 H/16): in interval I(t) (between barriers A(t+1) and A(t)) they copy step t-1's stash and
-//     dH into LDS slot (t-1) & 1 (loaded in I(t+1)), load step t-2's, and write dG_{t+1} out of image (t+1) & 1
-//     (write-through: the dx and the fused weight-gradient workgroups read it).  The dx product runs in its own
-//     workgroups (stack_dx_body), so no second MFMA stream shares the recurrent waves' SIMDs.
+// Backward workgroup = 2 x (H/16) waves.  Waves [0, H/16) run BPTT exactly like lstm.hip (dG_t from the
+// stash, dh_{t-1} = dG_t W_hh through the LDS dG image, one barrier per step); waves [H/16, 2 H/16) are
+// GRADIENT waves: they stage dH_t of the layer above into LDS two steps ahead (progress polls and hand-off
+// latency off the recurrent path) and compute dx_t = dG_t W_ih from the same LDS image one step behind,
+// apply this layer's input-dropout mask and hand dH^{(l-1)} to the layer below.
+// Intervals: I(t) = between barriers A(t+1) and A(t); the recurrent waves read dhs[t&1] and write the
+// dG image (t&1) in I(t); the gradient waves write dhs[(t-1)&1] and read image ((t+1)&1) in I(t).
 template <int H, int PREC, bool TOP, bool BOTTOM>
 __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int layer, const int tile,
                                                BwdSmem<H, PREC>& sm, const unsigned base) {
@@ -1034,8 +920,8 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   constexpr int KF = G4 / 4;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool helper = wave >= NW;
-  const int w = helper ? wave - NW : wave;
+  const bool grad_wave = wave >= NW;
+  const int w = grad_wave ? wave - NW : wave;
   const int q = lane >> 4, j = lane & 15;
   const int u = 16 * w + j;
   const int n0 = tile * S;
@@ -1045,71 +931,183 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   auto& g_f = sm.g_f;
   auto& dhs = sm.dhs;
 
-  if (helper) {
-    // =========================== helper waves ===========================
-    // Interval I(t) (between barriers A(t+1) and A(t)).  Helper 0: copy dH_{t-1} (loaded in I(t+1)) into LDS, then
-    // poll + load dH_{t-2}; it issues no other memory operation, so a poll (whose result the compiler waits for with
-    // vmcnt(0)) never waits on anything but its own word.  Helpers 1 .. NW-1: LDS-DMA step t-2's stash of every
-    // recurrent wave into ring slot (t-2) % 3 and make sure step t-1's has landed before A(t).  The progress of the
-    // dG rows the recurrent waves store is published by helper 0 from their drain at the top of each step.
-    const int h = w;  // helper index
-    if (h == 0) {
-      const float* dH = TOP ? nullptr : a.dX[layer];
-      unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
-      // dX of the layer above: NPX progress words (steps t = p mod NPX, one dx workgroup each), 8 words apart
-      unsigned* in_flag = a.flags + FLAG_STRIDE * ((TOP ? layer : layer + 1) * a.tr8 + tile);
-      unsigned seen[NPX];
+  if (grad_wave) {
+    // =========================== gradient waves ===========================
+    const float* dH = TOP ? nullptr : a.dX[layer];
+    float* dXout = BOTTOM ? nullptr : a.dX[layer - 1];
+    const uint32_t* min = (!BOTTOM && a.dropout) ? a.mask[layer] : nullptr;
+    const float keep_scale = 1.0f / (1.0f - a.drop_p);
+    unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+    unsigned* in_flag = TOP ? my_flag : a.flags + FLAG_STRIDE * ((layer + 1) * a.tr8 + tile);
+    unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
+    const float* w_ih = a.w_ih[layer];
+    float* dG = a.dG[layer];
+    constexpr int XKB = BOTTOM ? 1 : KB, XKF = BOTTOM ? 1 : KF;
+    bf16x8 Xhi[PREC == PREC_F32 ? 1 : XKB], Xlo[PREC == PREC_BF16X3 ? XKB : 1];
+    float Xf[PREC == PREC_F32 ? XKF : 1];
+    if constexpr (!BOTTOM) {
+      if constexpr (PREC == PREC_F32) {
 #pragma unroll
-      for (int p = 0; p < NPX; ++p) seen[p] = base;
-      // the tile's 16 x H block of dH_t is contiguous: 4 float4 per lane (row f / (H/4), units 4 (f % (H/4)))
-      constexpr int DL = S * H / 4 / 64;
-      float4 dreg[DL];
-      auto load_dh = [&](int t) {
-        if constexpr (!TOP) {
-          seen[t % NPX] = wait_progress(in_flag + 8 * (t % NPX), base + (unsigned)(T - t), seen[t % NPX], a.timeout,
-                                        a.spin_limit);
+        for (int kk = 0; kk < KF; ++kk) Xf[kk] = w_ih[(size_t)(4 * kk + q) * H + u];
+      } else {
 #pragma unroll
-          for (int i = 0; i < DL; ++i) dreg[i] = load_sc1(dH, ((size_t)t * Np + n0) * H + 4 * (lane + 64 * i));
-        }
-      };
-      auto stage_dh = [&](int t) {
-        if constexpr (!TOP) {
+        for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-          for (int i = 0; i < DL; ++i) {
-            const int f = lane + 64 * i;
-            *reinterpret_cast<float4*>(&dhs[t & 1][f / (H / 4)][4 * (f % (H / 4))]) = dreg[i];
+          for (int e = 0; e < 8; ++e) {
+            __bf16 hi, lo;
+            split_bf16(w_ih[(size_t)rperm_to_r<H>(32 * kb + 8 * q + e) * H + u], hi, lo);
+            Xhi[kb][e] = hi;
+            if constexpr (PREC == PREC_BF16X3) Xlo[kb][e] = lo;
+          }
+      }
+    }
+    float dreg[4] = {0.f, 0.f, 0.f, 0.f};
+    unsigned seen = base;
+    auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
+      if constexpr (!TOP) {
+        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
+    uint32_t mreg = 0x01010101u, mnext = 0x01010101u;
+    const int ts = lane >> 2, tc = 4 * (lane & 3);
+    auto load_mask = [&](int t) {  // keep bytes of step t (row ts, units 16 w + tc + e), used one interval later
+      if constexpr (!BOTTOM) {
+        if (min) mnext = min[stack_keep_index(t, tile, a.ntiles, ts, H, 16 * w + tc)];
+      }
+    };
+    auto stage_dh = [&](int t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = dreg[i];
+    };
+    // dG_t (fp32, unit-major columns 4u + g) from the LDS image (t&1) -> write-through 16-byte stores: the fused
+    // weight-gradient workgroups read these rows.  Issued by the gradient waves (they wait at the step barrier
+    // for ~1,300 cycles, r3 stamps) instead of the recurrent waves, whose store issue + vmcnt waits were ~500
+    // cycles of every reverse step.  Lane li = 64 w + lane: row li / 16, columns 4 (li % 16) + 64 k.  bf16 images:
+    // dG = hi (+ lo) -- the weight-gradient product splits it into the same hi / lo pair again.
+    // (4 stores per lane for H = 32 and 64: NW waves cover 4 NW rows per pass, G4 / 64 column blocks per row)
+    auto store_dg = [&](int t) {
+      const int buf = t & 1, li = 64 * w + lane, c0 = 4 * (li & 15);
+#pragma unroll
+      for (int pass = 0; pass < 16 / (4 * NW); ++pass)
+#pragma unroll
+      for (int k = 0; k < G4 / 64; ++k) {
+        const int s = (li >> 4) + 4 * NW * pass;
+        float* row = dG + ((size_t)t * Np + n0 + s) * G4;
+        const int c = c0 + 64 * k;  // columns c .. c + 3 = gates 0..3 of unit c / 4
+        f32x4 v;
+        if constexpr (PREC == PREC_F32) {
+          const int uu = c >> 2;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = g_f[buf][s][(uu & 3) * KF + g * (H / 4) + (uu >> 2)];
+        } else {
+          const bf16x4 hi4 = *reinterpret_cast<const bf16x4*>(&g_hi[buf][s][c]);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) v[g] = (float)hi4[g];
+          if constexpr (PREC == PREC_BF16X3) {
+            const bf16x4 lo4 = *reinterpret_cast<const bf16x4*>(&g_lo[buf][s][c]);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) v[g] += (float)lo4[g];
           }
         }
-      };
+        store_sc1_x4(row + c, v);
+      }
+    };
+    auto dx_step = [&](int t) {  // dG_t stores and dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
+      if constexpr (!BOTTOM) {
+        const int buf = t & 1;
+        // four independent accumulation chains (even / odd k-blocks x hi / cross terms)
+        f32x4 ax[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+        if constexpr (PREC == PREC_F32) {
+          const float* arow = &g_f[buf][j][q * KF];
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) ax[kk & 3] = mfma16x16x4f32(arow[kk], Xf[kk], ax[kk & 3]);
+        } else {
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
+            if constexpr (PREC == PREC_BF16X3) {
+              const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
+              ax[2 + (kb & 1)] = mfma16x16x32(alo, Xhi[kb], ax[2 + (kb & 1)]);
+              ax[2 + (kb & 1)] = mfma16x16x32(ahi, Xlo[kb], ax[2 + (kb & 1)]);
+            }
+            ax[kb & 1] = mfma16x16x32(ahi, Xhi[kb], ax[kb & 1]);
+          }
+        }
+        // one 16-byte write-through store per lane (transpose through the wave's own LDS scratch); the input
+        // dropout mask (keep words in this store layout) is applied after the transpose
+        float (*tr)[TRS] = sm.tr[w];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tr[4 * q + i][j] = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
+        const float4 dv = *reinterpret_cast<const float4*>(&tr[ts][tc]);
+        f32x4 o{dv.x, dv.y, dv.z, dv.w};
+        if (min) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] *= ((mreg >> (8 * e)) & 0xFFu) ? keep_scale : 0.f;
+        }
+        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
+      }
+    };
+    if constexpr (!TOP) {
       load_dh(T - 1);
-      mta_wait_vmem();
       stage_dh(T - 1);
       if (T > 1) load_dh(T - 2);
-      __syncthreads();  // B0
-      for (int t = T - 1; t >= 0; --t) {
-        // dG_{t+3}: stored by the recurrent waves in I(t+3), drained by their wait at the top of I(t+1)
-        if (t + 3 <= T - 1 && lane == 0)
-          __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 3), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // B0
+    SSTAMP_DECL
+    for (int t = T - 1; t >= 0; --t) {
+      // ---- interval I(t) ----  issue order: [flags, dH loads, keep-byte load, dx store].  The dx product runs
+      // last, while the recurrent waves are in their VALU phase (their dh MFMAs run right after A(t+1); two
+      // MFMA streams on one SIMD serialise, r2 stamp probe), and its store stays in flight across the barrier:
+      // vmcnt(1) waits for this wave's loads of the previous interval and everything older than its dx store.
+      SSTAMP(0)
+      // the previous interval's dG stores (4 per lane) and dx store stay in flight; every older op (its dH and
+      // keep-byte loads, issued before them) is complete
+      if constexpr (BOTTOM) mta_wait_vmem();
+      else mta_wait_vmcnt<1>();
+      mreg = mnext;
+      SSTAMP(1)
+      // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait at
+      // the top of I(t+1) (which leaves only I(t+2)'s stores in flight), before barrier A(t+1)
+      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
+        __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // dG progress: dG_s is stored in the same dx_step(s) as dx_s, before it, so the drain argument above covers
+      // dG of steps >= t+4 too
+      if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
+        __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (!TOP) {
         if (t >= 1) {
-          mta_wait_vmem();  // dH_{t-1} (and the flag store)
           stage_dh(t - 1);
           if (t >= 2) load_dh(t - 2);
         }
-        __syncthreads();  // A(t)
       }
-      __syncthreads();  // F (the recurrent waves drained every dG store before it)
-      if (lane == 0) __hip_atomic_store(dg_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
+      load_mask(t);  // for dx_step(t) in I(t-1)
+      SSTAMP(2)
+      if (!BOTTOM) __builtin_amdgcn_s_sleep(DX_DELAY);
+      if (t + 1 <= T - 1) dx_step(t + 1);
+      SSTAMP(3)
+      __syncthreads();  // A(t)
+      SSTAMP(4)
     }
-    // helpers 1 .. NW-1: barrier count only
-    __syncthreads();  // B0
-    for (int t = T - 1; t >= 0; --t) __syncthreads();  // A(t)
+    SSTAMP_FLUSH(1, 1, w == 0)
+    mta_wait_vmem();
+    mreg = mnext;
+    dx_step(0);
+    mta_wait_vmem();
     __syncthreads();  // F
+    if (!BOTTOM && wave == NW && lane == 0)
+      __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == NW + 1 && lane == 0)
+      __hip_atomic_store(dg_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
 
   // =========================== recurrent waves ===========================
-  if (MTA_STACK_PRIO && __builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(MTA_STACK_PRIO);
+  if (__builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(STACK_PRIO);
+  const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
   const float* w_hh = a.w_hh[layer];
   bf16x8 Bhi[PREC == PREC_F32 ? 1 : KB], Blo[PREC == PREC_BF16X3 ? KB : 1];
   float Bf[PREC == PREC_F32 ? KF : 1];
@@ -1123,7 +1121,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       for (int e = 0; e < 8; ++e) {
         __bf16 hi, lo;
         split_bf16(w_hh[(size_t)rperm_to_r<H>(32 * kb + 8 * q + e) * H + u], hi, lo);
-        Bhi[kb] [e] = hi;
+        Bhi[kb][e] = hi;
         if constexpr (PREC == PREC_BF16X3) Blo[kb][e] = lo;
       }
   }
@@ -1139,41 +1137,52 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       dhr[i] = 0.f;
     }
   }
-  float* dG = a.dG[layer];
-  const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
-  // stash of step t (i, f, g, o, c) plus c_{t-1}, prefetched two steps ahead into one of two register sets (even /
-  // odd steps): a step issues its 4 dG stores, then the 6 stash loads of step t-2
-  auto load_into = [&](int t, float4 (&sb)[STASH + 1]) {
+  float pdG[4][4] = {};
+  [[maybe_unused]] float* dG = a.dG[layer];
+  auto store_step = [&](int t) {  // write-through dG rows from the recurrent waves
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      store_sc1_x4(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u,
+                   f32x4{pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]});
+  };
+  // stash of step t (i, f, g, o, c) plus c_{t-1}, prefetched ~two steps ahead into one of two register
+  // sets (even / odd steps); a step issues the 6 stash loads of step t-2 (mode 0: after the 4 dG stores of step
+  // t+1), so at the top of step t the loads it needs are followed by exactly 6 (mode 0: 10) newer ops
+  auto load_into = [&](int t, float4 (&sb)[STASH], float4& cb) {
     const float4* src = stash + stash_index(t, tile, a.ntiles, w, NW, lane);
 #pragma unroll
     for (int k = 0; k < STASH; ++k) sb[k] = src[64 * k];
-    sb[STASH] = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 64 * 4];
+    cb = stash[stash_index(t > 0 ? t - 1 : 0, tile, a.ntiles, w, NW, lane) + 64 * 4];
   };
-  float4 sA[STASH + 1], sB[STASH + 1];
-  load_into(T - 1, sA);
-  if (T > 1) load_into(T - 2, sB);
-  __syncthreads();  // B0 (dH_{T-1} staged)
+  float4 sA[STASH], cA, sB[STASH], cB;
+  load_into(T - 1, sA, cA);
+  if (T > 1) load_into(T - 2, sB, cB);
+  __syncthreads();  // B0 (dhs[(T-1)&1] staged)
+
+  // one reverse step; returns false after step 0
   SSTAMP_DECL
-  auto step = [&](int t, float4 (&st)[STASH + 1]) {
+  auto step = [&](int t, float4 (&sb)[STASH], float4& cb) {
     SSTAMP(0)
-    const int buf = t & 1;
     float dho[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[buf][4 * q + i][u];
+    for (int i = 0; i < 4; ++i) dho[i] = TOP ? 0.f : dhs[t & 1][4 * q + i][u];
     SSTAMP(1)
-    // this step's stash (loaded two steps ago) is complete; step t+1's 4 dG stores and 6 loads are newer.  The
-    // dG stores of step t+2 and older are then drained too: helper 0 publishes them after A(t)
     if (t <= T - 2) mta_wait_vmcnt<10>();
     else mta_wait_vmcnt<6>();
     SSTAMP(2)
+    // unconditional (step T-1 stores its zero pdG to row T-1, which step T-2 then overwrites in order)
+    store_step(t < T - 1 ? t + 1 : t);
+    __builtin_amdgcn_sched_barrier(0);
+    SSTAMP(3)
+    const float4* st = sb;
     const float cpm = t > 0 ? 1.f : 0.f;
-    const float cp4[4] = {st[STASH].x * cpm, st[STASH].y * cpm, st[STASH].z * cpm, st[STASH].w * cpm};
+    const float cp4[4] = {cb.x * cpm, cb.y * cpm, cb.z * cpm, cb.w * cpm};
     const float ig4[4] = {st[0].x, st[0].y, st[0].z, st[0].w};
     const float fg4[4] = {st[1].x, st[1].y, st[1].z, st[1].w};
     const float gg4[4] = {st[2].x, st[2].y, st[2].z, st[2].w};
     const float og4[4] = {st[3].x, st[3].y, st[3].z, st[3].w};
     const float ct4[4] = {st[4].x, st[4].y, st[4].z, st[4].w};
-    float pdG[4][4];
+    const int buf = t & 1;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float ig = ig4[i], fg = fg4[i], gg = gg4[i], og = og4[i];
@@ -1207,193 +1216,49 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&g_lo[buf][s4][rp]) = lo4;
       }
     }
-    SSTAMP(3)
-    // write-through dG rows (fp32, unit-major columns 4u + g): the dx and weight-gradient workgroups read them
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      store_sc1_x4(dG + ((size_t)t * Np + n0 + 4 * q + i) * G4 + 4 * u,
-                   f32x4{pdG[0][i], pdG[1][i], pdG[2][i], pdG[3][i]});
-    __builtin_amdgcn_sched_barrier(0);
-    load_into(t >= 2 ? t - 2 : 0, st);  // prefetch step t-2 into this set (dead now); unconditional: no set copy
     SSTAMP(4)
-    __syncthreads();  // A(t): dG_t image visible to this step's dh product
+    // prefetch step t-2 into this set (its values are dead now); unconditional, so the set needs no copy
+    __builtin_amdgcn_sched_barrier(0);
+    load_into(t >= 2 ? t - 2 : 0, sb, cb);
     SSTAMP(5)
+    __syncthreads();  // A(t): dG_t image visible to the gradient waves and to this step's dh product
+    SSTAMP(6)
     if (t == 0) return;
-    // every A fragment first (one LDS round trip), then four independent accumulation chains (even / odd
-    // k-blocks x hi / cross terms)
+    // four independent accumulation chains (even / odd k-blocks x hi / cross terms): the dependent-MFMA
+    // latency, not issue, bounded the two-chain form (r2 stamp probe: 795 cycles for 24 MFMAs)
     f32x4 ac[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     if constexpr (PREC == PREC_F32) {
       const float* arow = &g_f[buf][j][q * KF];
 #pragma unroll
       for (int kk = 0; kk < KF; ++kk) ac[kk & 3] = mfma16x16x4f32(arow[kk], Bf[kk], ac[kk & 3]);
     } else {
-      bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
-        ahi[kb] = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
-        if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        ac[kb & 1] = mfma16x16x32(ahi[kb], Bhi[kb], ac[kb & 1]);
+        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(&g_hi[buf][j][32 * kb + 8 * q]);
         if constexpr (PREC == PREC_BF16X3) {
-          ac[2 + (kb & 1)] = mfma16x16x32(alo[kb], Bhi[kb], ac[2 + (kb & 1)]);
-          ac[2 + (kb & 1)] = mfma16x16x32(ahi[kb], Blo[kb], ac[2 + (kb & 1)]);
+          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(&g_lo[buf][j][32 * kb + 8 * q]);
+          ac[2 + (kb & 1)] = mfma16x16x32(alo, Bhi[kb], ac[2 + (kb & 1)]);
+          ac[2 + (kb & 1)] = mfma16x16x32(ahi, Blo[kb], ac[2 + (kb & 1)]);
         }
+        ac[kb & 1] = mfma16x16x32(ahi, Bhi[kb], ac[kb & 1]);
       }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) dhr[i] = (ac[0][i] + ac[1][i]) + (ac[2][i] + ac[3][i]);
-    SSTAMP(6)
+    SSTAMP(7)
   };
-  // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip, odd T peels step 0
+  // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip (no
+  // conditional step inside, so the sets keep their registers across the back-edge), odd T peels step 0
   int t = T - 1;
   for (; t >= 1; t -= 2) {
-    step(t, sA);
-    step(t - 1, sB);
+    step(t, sA, cA);
+    step(t - 1, sB, cB);
   }
-  if (t == 0) step(0, sA);
-  mta_wait_vmem();
+  if (t == 0) step(0, sA, cA);
   SSTAMP_FLUSH(1, 0, wave == 0)
+  store_step(0);
+  mta_wait_vmem();
   __syncthreads();  // F
-}
-
-// dx workgroup of (layer l >= 1, tile, p < NPX): dX^{(l-1)}_t = mask_l . (dG^{(l)}_t W_ih^{(l)}) for the steps
-// t = T-1 .. 0 with t = p (mod NPX), the input gradient the layer below consumes.  Its own CU (block ids right
-// after layer l's recurrence, the same XCD as the tile's producer and consumer), so the recurrent waves of the
-// backward never share a SIMD with this MFMA stream; NPX of them per tile give each step NPX recurrence steps of
-// time, so a plainly serialised iteration keeps up:
-//   [poll dG progress of t; the 16 x 4H rows -> LDS A-operand image] [barrier] [MFMA; mask; dX_t store; drain]
-//   [barrier; publish t in progress word p]
-// H/16 waves (one per SIMD), wave w owns output units [16w, 16w + 16); the block's other waves keep the barrier
-// count only.
-template <int H, int PREC>
-__device__ __forceinline__ void stack_dx_body(const StackBwdArgs& a, const int layer, const int tile, const int par,
-                                              DxSmem<H, PREC>& sm, const unsigned base) {
-  constexpr int G4 = 4 * H;
-  constexpr int NW = H / 16;
-  constexpr int KB = G4 / 32;
-  constexpr int KF = G4 / 4;
-  constexpr int RL = S * G4 / 4 / (64 * NW);  // float4 row loads per lane per step (4)
-  static_assert(RL * 64 * NW * 4 == S * G4, "dx workgroup: every lane loads RL float4 of the tile's dG rows");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool idle = wave >= NW;
-  const int w = idle ? 0 : wave;
-  const int q = lane >> 4, j = lane & 15;
-  const int u = 16 * w + j;
-  const int n0 = tile * S;
-  const int Np = a.Np, T = a.T;
-  const float* dG = a.dG[layer];
-  float* dXout = a.dX[layer - 1];
-  const uint32_t* min = a.dropout ? a.mask[layer] : nullptr;
-  const float keep_scale = 1.0f / (1.0f - a.drop_p);
-  unsigned* dg_flag = a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + tile);
-  unsigned* my_flag = a.flags + FLAG_STRIDE * (layer * a.tr8 + tile) + 8 * par;
-  const float* w_ih = a.w_ih[layer];
-  // B operand: W_ih rows r(c) = (c & 3) H + (c >> 2) of gate column c, column u
-  bf16x8 Xhi[PREC == PREC_F32 ? 1 : KB], Xlo[PREC == PREC_BF16X3 ? KB : 1];
-  float Xf[PREC == PREC_F32 ? KF : 1];
-  if (!idle) {
-    if constexpr (PREC == PREC_F32) {
-#pragma unroll
-      for (int kk = 0; kk < KF; ++kk) {
-        const int c = 4 * kk + q;
-        Xf[kk] = w_ih[(size_t)((c & 3) * H + (c >> 2)) * H + u];
-      }
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < KB; ++kb)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int c = 32 * kb + 8 * q + e;
-          __bf16 hi, lo;
-          split_bf16(w_ih[(size_t)((c & 3) * H + (c >> 2)) * H + u], hi, lo);
-          Xhi[kb][e] = hi;
-          if constexpr (PREC == PREC_BF16X3) Xlo[kb][e] = lo;
-        }
-    }
-  }
-  // lane li = 64 w + lane loads float4 f = li + 64 NW k of the tile's S x G4 block: row f / (G4 / 4), col 4 (f % (G4/4))
-  const int li = 64 * w + lane;
-  const int ts = lane >> 2, tc = 4 * (lane & 3);
-  unsigned seen = base;
-  const int t_hi = (T - 1) - (((T - 1) % NPX - par + NPX) % NPX);  // the highest step = par (mod NPX)
-  for (int t = t_hi; t >= 0; t -= NPX) {
-    uint32_t mreg = 0x01010101u;
-    if (!idle) {
-      seen = wait_progress(dg_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
-      float4 v[RL];
-#pragma unroll
-      for (int k = 0; k < RL; ++k) {
-        const int f = li + 64 * NW * k, row = f / (G4 / 4), c = 4 * (f % (G4 / 4));
-        v[k] = load_sc1(dG, ((size_t)t * Np + n0 + row) * G4 + c);
-      }
-      if (min) mreg = min[stack_keep_index(t, tile, a.ntiles, ts, H, 16 * w + tc)];
-#pragma unroll
-      for (int k = 0; k < RL; ++k) {
-        const int f = li + 64 * NW * k, row = f / (G4 / 4), c = 4 * (f % (G4 / 4));
-        const float x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-        if constexpr (PREC == PREC_F32) {
-          // f32 MFMA k order: column c -> [(c & 3) KF + (c >> 2)]
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sm.g_f[row][((c + e) & 3) * KF + ((c + e) >> 2)] = x[e];
-        } else {
-          bf16x4 hi4, lo4;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            __bf16 hi, lo;
-            split_bf16(x[e], hi, lo);
-            hi4[e] = hi;
-            lo4[e] = lo;
-          }
-          *reinterpret_cast<bf16x4*>(&sm.g_hi[row][c]) = hi4;
-          if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.g_lo[row][c]) = lo4;
-        }
-      }
-    }
-    __syncthreads();  // image complete
-    if (!idle) {
-      f32x4 ax[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if constexpr (PREC == PREC_F32) {
-        const float* arow = &sm.g_f[j][q * KF];
-#pragma unroll
-        for (int kk = 0; kk < KF; ++kk) ax[kk & 3] = mfma16x16x4f32(arow[kk], Xf[kk], ax[kk & 3]);
-      } else {
-        bf16x8 ahi[KB], alo[PREC == PREC_BF16X3 ? KB : 1];
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          ahi[kb] = *reinterpret_cast<const bf16x8*>(&sm.g_hi[j][32 * kb + 8 * q]);
-          if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.g_lo[j][32 * kb + 8 * q]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kb = 0; kb < KB; ++kb) {
-          ax[kb & 1] = mfma16x16x32(ahi[kb], Xhi[kb], ax[kb & 1]);
-          if constexpr (PREC == PREC_BF16X3) {
-            ax[2 + (kb & 1)] = mfma16x16x32(alo[kb], Xhi[kb], ax[2 + (kb & 1)]);
-            ax[2 + (kb & 1)] = mfma16x16x32(ahi[kb], Xlo[kb], ax[2 + (kb & 1)]);
-          }
-        }
-      }
-      // one 16-byte write-through store per lane (transpose through the wave's own LDS scratch); the input
-      // dropout mask (keep words in this store layout) is applied after the transpose
-      float (*tr)[TRS] = sm.tr[w];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) tr[4 * q + i][j] = (ax[0][i] + ax[1][i]) + (ax[2][i] + ax[3][i]);
-      const float4 dv = *reinterpret_cast<const float4*>(&tr[ts][tc]);
-      f32x4 o{dv.x, dv.y, dv.z, dv.w};
-      if (min) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] *= ((mreg >> (8 * e)) & 0xFFu) ? keep_scale : 0.f;
-      }
-      store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
-      mta_wait_vmem();
-    }
-    __syncthreads();  // every wave's dX_t store drained (and the image free for the next step)
-    if (wave == 0 && lane == 0)
-      __hip_atomic_store(my_flag, base + (unsigned)(T - t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 template <int H, int PREC>
@@ -1401,19 +1266,12 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
   // one dynamic LDS block: the recurrence image (BwdSmem) or a weight-gradient staging image
   extern __shared__ __attribute__((aligned(16))) char dyn_lds[];
   const unsigned base = read_epoch_base(a.ctl, CTL_BWD_EPOCH, a.eshift);
-  // [recurrence(L-1) | dx(L-1) x NPX | recurrence(L-2) | dx(L-2) x NPX | ... | recurrence(0)] x tr8 blocks, then the weight
-  // gradients.  Producers of a hand-off always have lower block ids than their consumers (dispatch is in id
-  // order, so every workgroup a spinning one waits for is resident or done), and tile i of every group has
-  // the same block id modulo 8 (one XCD for the tile's whole chain)
-  const int nrec = ((1 + NPX) * (a.L - 1) + 1) * a.tr8;
+  const int nrec = a.L * a.tr8;
   if ((int)blockIdx.x < nrec) {
-    // groups of layers >= 1: [recurrence | dx of steps 0 (mod NPX) | ... | dx of steps NPX-1], layer 0: [recurrence]
-    const int grp = blockIdx.x / ((1 + NPX) * a.tr8), r = blockIdx.x % ((1 + NPX) * a.tr8);
-    const int layer = a.L - 1 - grp, tile = r % a.tr8;
-    if (r >= a.tr8) {
-      if (tile < a.ntiles)
-        stack_dx_body<H, PREC>(a, layer, tile, r / a.tr8 - 1, *reinterpret_cast<DxSmem<H, PREC>*>(dyn_lds), base);
-    } else if (tile < a.ntiles) {
+    // producers of a hand-off always have lower block ids than their consumers (dispatch is in id order,
+    // so every workgroup a spinning one waits for is already resident): top layer first here
+    const int layer = a.L - 1 - blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
+    if (tile < a.ntiles) {
       const bool top = layer == a.L - 1, bottom = layer == 0;
       auto& sm = *reinterpret_cast<BwdSmem<H, PREC>*>(dyn_lds);
       if (top && bottom) stack_bwd_body<H, PREC, true, true>(a, layer, tile, sm, base);
@@ -1460,10 +1318,8 @@ int dispatch_fwd(int prec, int fin, const StackFwdArgs& a, hipStream_t st) {
 
 template <int H, int PREC>
 int launch_bwd(const StackBwdArgs& a, size_t lds, hipStream_t st) {
-  // recurrence + dx + weight-gradient workgroups; recurrent + helper waves
-  const dim3 grid(((1 + NPX) * (a.L - 1) + 1) * a.tr8 + a.L * a.wg_per_layer), block((H / 16) * 128);
+  const dim3 grid(a.L * a.tr8 + a.L * a.wg_per_layer), block((H / 16) * 128);  // recurrent + gradient waves
   lds = lds > sizeof(BwdSmem<H, PREC>) ? lds : sizeof(BwdSmem<H, PREC>);
-  lds = lds > sizeof(DxSmem<H, PREC>) ? lds : sizeof(DxSmem<H, PREC>);
   if (lds > 64 * 1024 && hipFuncSetAttribute(reinterpret_cast<const void*>(&lstm_stack_bwd_kernel<H, PREC>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return -3;
@@ -1489,26 +1345,18 @@ unsigned spin_limit() {
 
 }  // namespace
 
-// flags (zero-initialised once, then never reset): [4][MAXL][tr8] progress words (forward h, backward dX,
-// backward dG, forward gx; FLAG_STRIDE apart) + CTL_WORDS control words (timeout, per-direction epoch + arrival
-// counter).
+// flags (zero-initialised once, then never reset): [3][MAXL][tr8] progress words (forward, backward dX,
+// backward dG; FLAG_STRIDE apart) + CTL_WORDS control words (timeout, per-direction epoch + arrival counter).
 extern "C" int mta_lstm_stack_epoch_shift(int T) { return epoch_shift(T); }
 
-// flags layout: [4][MAXL][tr8] progress words (FLAG_STRIDE apart) | [2][MAXL][tr8] XCC ids (fwd, bwd) | CTL_WORDS
-constexpr int FLAG_REGIONS = 4;
+// flags layout: [3][MAXL][tr8] progress words (FLAG_STRIDE apart) | [2][MAXL][tr8] XCC ids (fwd, bwd) | CTL_WORDS
 extern "C" long mta_lstm_stack_flag_words(int Np) {
   const int tr8 = (Np / S + 7) / 8 * 8;
-  return (long)FLAG_REGIONS * FLAG_STRIDE * MAXL * tr8 + 2L * MAXL * tr8 + CTL_WORDS;
+  return 3L * FLAG_STRIDE * MAXL * tr8 + 2L * MAXL * tr8 + CTL_WORDS;
 }
-// forward workspace of the projection workgroups: gx = bias + W_ih x of every layer >= 1, (T, Np, H) float4
-extern "C" long mta_lstm_stack_gx_floats(int L, int Np, int T, int H) { return L > 1 ? (long)(L - 1) * T * Np * 4 * H : 0; }
 namespace {
-unsigned* ctl_words(unsigned* flags, int tr8) {
-  return flags + (long)FLAG_REGIONS * FLAG_STRIDE * MAXL * tr8 + 2L * MAXL * tr8;
-}
-unsigned* xcc_words(unsigned* flags, int tr8, int dir) {
-  return flags + (long)FLAG_REGIONS * FLAG_STRIDE * MAXL * tr8 + (long)dir * MAXL * tr8;
-}
+unsigned* ctl_words(unsigned* flags, int tr8) { return flags + 3L * FLAG_STRIDE * MAXL * tr8 + 2L * MAXL * tr8; }
+unsigned* xcc_words(unsigned* flags, int tr8, int dir) { return flags + 3L * FLAG_STRIDE * MAXL * tr8 + (long)dir * MAXL * tr8; }
 int xcd_local_enabled() {
   static const int v = [] {
     const char* e = getenv("MTA_LSTM_XCD_LOCAL");
@@ -1523,7 +1371,7 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
                                     const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                     float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                     float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                    int Np, int T, const MtaBatchGather* gather, float* gx_ws, hipStream_t st) {
+                                    int Np, int T, const MtaBatchGather* gather, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
   StackFwdArgs a{};
   a.x = x;
@@ -1560,11 +1408,8 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
   a.xcc = xcc_words(flags, a.tr8, 0);
   a.timeout = a.ctl + CTL_TIMEOUT;
   a.spin_limit = spin_limit();
-  a.main_blocks = ((1 + NPP) * (a.L - 1) + 1) * a.tr8;
+  a.main_blocks = a.L * a.tr8;
   a.copy_blocks = 16;
-  a.gflags = flags + 3L * FLAG_STRIDE * MAXL * a.tr8;
-  if (L > 1 && !gx_ws) return -5;
-  for (int l = 1; l < L; ++l) a.gx[l] = gx_ws + (size_t)(l - 1) * T * Np * 4 * H;
   // the partner XCC exchange waits for the consumer workgroup to start: only with the whole grid co-resident
   a.xcd_local = xcd_local_enabled() && a.main_blocks + a.copy_blocks <= 256;
   if (H == 32) return dispatch_fwd<32>(prec, fin, a, st);
@@ -1575,9 +1420,9 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                   float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                   float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                  int Np, int T, float* gx_ws, hipStream_t st) {
+                                  int Np, int T, hipStream_t st) {
   return mta_lstm_stack_fwd_g(H, prec, L, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, mask, stash, seeds, drop_p,
-                              flags, N, Np, T, nullptr, gx_ws, st);
+                              flags, N, Np, T, nullptr, st);
 }
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's

@@ -50,12 +50,8 @@ struct WgArgs {
 __host__ __device__ inline long wg_part_elems(int H, int F) { return 4L * H * (H + F) + 4L * H; }
 
 // time steps per row chunk: the standalone kernel aims at ~30 chunks, the stack kernel's fused workgroups at
-// ~60 (short chunks keep the tail after the last layer small); MTA_WGRAD_TC overrides (tuning)
-inline int wg_time_chunk(int T, bool fused) {
-  int tc = fused ? (T + 59) / 60 : (T + 29) / 30;
-  if (const char* e = getenv("MTA_WGRAD_TC")) tc = atoi(e) > 0 ? atoi(e) : tc;
-  return tc;
-}
+// ~60 (short chunks keep the tail after the last layer small)
+inline int wg_time_chunk(int T, bool fused) { return fused ? (T + 59) / 60 : (T + 29) / 30; }
 inline int wg_nchunks(int T, bool fused) {
   const int tc = wg_time_chunk(T, fused);
   return (T + tc - 1) / tc;

@@ -480,12 +480,9 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
   }
 }
 
-#ifndef MTA_NORM_BWD_WIDE_BLOCKS
-#define MTA_NORM_BWD_WIDE_BLOCKS 512
-#endif
 // the wide backward: ~2 workgroups per CU, each a contiguous row range with two rows in flight (fewer, longer
 // blocks: half the dgamma / dbeta partial rows of the r3 grid of 1024)
-constexpr int NORM_BWD_WIDE_BLOCKS = MTA_NORM_BWD_WIDE_BLOCKS;
+constexpr int NORM_BWD_WIDE_BLOCKS = 512;
 // the one-wave-per-row backward's grid cap: transformer B=1 (M = 6,272 rows, D = 128) 0.714 ms at 512, 0.702 at
 // 1024, 0.711 at 1,568 (one row per wave: the partial-row reduce grows) (profiles/r2_norm_bwd_cap_ab.txt)
 constexpr int NORM_BWD_NARROW_BLOCKS = 1024;
@@ -719,12 +716,8 @@ int norm_blocks(int M, bool bwd) {
   const int rows_per_block = 4;
   int b = (M + rows_per_block - 1) / rows_per_block;
   // backward: cap the grid so each wave reduces several rows before the per-column atomics
-  static const int bwd_cap = [] {  // MTA_NORM_BWD_BLOCKS: A/B knob for the one-wave-per-row backward's grid
-    const char* e = getenv("MTA_NORM_BWD_BLOCKS");
-    const int v = e ? atoi(e) : NORM_BWD_NARROW_BLOCKS;
-    return v < 1 ? 1 : (v > NORM_BWD_MAX_BLOCKS ? NORM_BWD_MAX_BLOCKS : v);
-  }();
-  const int cap = bwd ? bwd_cap : 4096;
+  static_assert(NORM_BWD_NARROW_BLOCKS <= NORM_BWD_MAX_BLOCKS, "partials sized for the grid cap");
+  const int cap = bwd ? NORM_BWD_NARROW_BLOCKS : 4096;
   return b > cap ? cap : (b < 1 ? 1 : b);
 }
 
@@ -766,7 +759,7 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
                         hipStream_t st) {
   if (D % 4 || ldx % 4 || D > 2048) return 1;
   // fp32 GELU input (32-true extras): the one-wave-per-row kernels (the wide ones stage pre as bf16)
-  const bool wide_ok = D >= 1024 && getenv("MTA_NORM_NARROW") == nullptr && !(pre && pre_f32);
+  const bool wide_ok = D >= 1024 && !(pre && pre_f32);
   if ((x_bf16 || dy_bf16) && !wide_ok) return 2;  // bf16 row inputs: wide kernels only
   NormArgs a{};
   a.x = x_bf16 ? nullptr : static_cast<const float*>(x);
@@ -831,14 +824,13 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     a.part_ld = 2048;
     a.part_pass = (long)NORM_BWD_MAX_BLOCKS * 2048;
   }
-#define MTA_NORM_LAUNCH(V)                                                      \
+#define NORM_LAUNCH(V)                                                          \
   if (bwd) norm_bwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);                \
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
   if (wide) {
     if (M > 0) {
       const bool b16 = a.xb != nullptr;
-      static const bool generic = getenv("MTA_NORM_BWD_GENERIC") != nullptr;  // A/B switch
-      const bool fast = !generic && a.pre && !a.dres && b16 == (a.dyb != nullptr) &&
+      const bool fast = a.pre && !a.dres && b16 == (a.dyb != nullptr) &&
                         (D == 1024 || D == 2048) && (a.rms || a.mean);
       if (bwd && fast) {
         if (D == 1024) {
@@ -857,18 +849,17 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
       }
     }
   } else if (vpl <= 1) {
-    MTA_NORM_LAUNCH(1)
+    NORM_LAUNCH(1)
   } else if (vpl <= 2) {
-    MTA_NORM_LAUNCH(2)
+    NORM_LAUNCH(2)
   } else if (vpl <= 4) {
-    MTA_NORM_LAUNCH(4)
+    NORM_LAUNCH(4)
   } else {
-    MTA_NORM_LAUNCH(8)
+    NORM_LAUNCH(8)
   }
-#undef MTA_NORM_LAUNCH
+#undef NORM_LAUNCH
   if (bwd && (dgamma || dbeta) && wide) {
-    static const bool cols64 = getenv("MTA_NORM_REDUCE_64") != nullptr;  // A/B switch
-    if (!cols64 && D % 16 == 0)
+    if (D % 16 == 0)
       norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
     else
       norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);

@@ -1,8 +1,8 @@
 // Diagnostic probe (not part of the extension): the fused transformer FFN half (csrc/tr_ffn.hip) forward and backward
-// on the transformer_encoder B=1 shape (M = 104 x 60 tokens), timed with events, and (built with -DMTA_FFN_STAMPS=1)
+// on the transformer_encoder B=1 shape (M = 104 x 60 tokens), timed with events, and (built with -DMTA_STAMPS=1)
 // the s_memtime split of every workgroup's critical path: phase means over the workgroups, plus the spread of their
 // start and end times (how long the launch takes to fill and drain).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics -I csrc [-DMTA_FFN_STAMPS=1] \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics -I csrc [-DMTA_STAMPS=1] \
 //         csrc/tools/ffn_probe.hip -o tools_bin/ffn_probe[_s]
 //   ./tools_bin/ffn_probe [M] [nn]      (nn = 1: the transposed weight-gradient operand outputs, the default path)
 #include "../tr_ffn.hip"
@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
     }
     printf("%s M=%d nn=%d grid=%d: %.2f us per launch (event-bracketed, %d reps)\n", dir ? "bwd" : "fwd", M, nn,
            (M + FBM - 1) / FBM, 1e3f * tot / reps, reps);
-#if MTA_FFN_STAMPS
+#if MTA_STAMPS
     run();
     CK(hipDeviceSynchronize());
     static unsigned long long st[2][256][12];

@@ -1,6 +1,6 @@
 // Diagnostic probe (not part of the extension): the 256 x 256 LDS-DMA GEMM of csrc/gemm.hip on one shape, timed, and
-// (built with -DMTA_GEMM_STAMPS) the s_memtime split of its main loop per wave.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics -I csrc [-DMTA_GEMM_STAMPS] \
+// (built with -DMTA_STAMPS) the s_memtime split of its main loop per wave.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -munsafe-fp-atomics -I csrc [-DMTA_STAMPS] \
 //         csrc/tools/gemm_probe.hip -o tools_bin/gemm_probe
 //   ./tools_bin/gemm_probe M N K mode
 #include "../gemm.hip"
@@ -35,7 +35,7 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 4096, N = argc > 2 ? atoi(argv[2]) : 4096;
   const int K = argc > 3 ? atoi(argv[3]) : 4096, mode = argc > 4 ? atoi(argv[4]) : 0;
   const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 1: the MLP forward epilogue (bias + GELU, bf16 pre-activation)
-  const int ksplit = argc > 6 ? atoi(argv[6]) : 1;  // mode 2 (the mid kernel with MTA_GEMM_MID=1): split-K
+  const int ksplit = argc > 6 ? atoi(argv[6]) : 1;  // split-K
   __bf16 *A, *B;
   float* C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
@@ -80,25 +80,14 @@ int main(int argc, char** argv) {
   const double us = ts[ts.size() / 2];
   printf("gemm_probe M=%d N=%d K=%d mode=%d epi=%d: %.2f us  %.1f TFLOP/s\n", M, N, K, mode, epi, us,
          2.0 * M * N * K / (us * 1e-6) / 1e12);
-#ifdef MTA_GEMM_STAMPS
+#ifdef MTA_STAMPS
   unsigned long long zero[8][8] = {};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(big::stamp_acc), zero, sizeof(zero)));
-  CK(hipMemcpyToSymbol(HIP_SYMBOL(big::epi_stamp), zero[0], sizeof(zero[0])));
   run();
   CK(hipDeviceSynchronize());
   unsigned long long acc[8][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(big::stamp_acc), sizeof(acc)));
-  unsigned long long ek[8];
-  CK(hipMemcpyFromSymbol(ek, HIP_SYMBOL(big::epi_stamp), sizeof(ek)));
-#ifdef MTA_EPI_TWICE
-  {
-    const int nb = ((M + 255) / 256) * ((N + 255) / 256) * ksplit;
-    printf("epilogue cycles per workgroup (wave 0): first call %.0f, second call %.0f\n", (double)ek[0] / nb,
-           (double)ek[1] / nb);
-  }
-#endif
-  const char* mid = getenv("MTA_GEMM_MID");
-  const int tile = mid && mid[0] == '1' ? 128 : 256;  // the mid kernel's stamps: [wait lgkm, mfma, wait vm, barrier, dma+reads]
+  const int tile = 256;
   const int blocks = ((M + tile - 1) / tile) * ((N + tile - 1) / tile) * ksplit;
   const int nk = K / 32 / ksplit;
   const char* names[8] = {"reads", "dma_wait_r1", "barrier1", "mfma_seg", "dma_wait_r0", "barrier2", "loop", "epilogue"};

@@ -1,7 +1,7 @@
 // Diagnostic probe (not part of the extension): times the one-launch training decoder of losses.hip at the
-// headline shape (N=100 sequences, n=30 target days, H=64) and, in a -DMTA_LOSS_STAMPS=1 build, prints the
+// headline shape (N=100 sequences, n=30 target days, H=64) and, in a -DMTA_STAMPS=1 build, prints the
 // s_memtime cycles of its phases (staging, heads, losses, d(alpha,beta), dh + head grads).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_LOSS_STAMPS=1] csrc/tools/losses_probe.hip \
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STAMPS=1] csrc/tools/losses_probe.hip \
 //         -o tools_bin/losses_probe
 #include <cstdio>
 #include <vector>
@@ -63,7 +63,7 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&m, a, b));
     if (r >= 20) ms += m / (reps - 20);
   }
-  printf("N=%d want_nll=%d reg=%d: heads_losses_train %.2f us/launch\n", N, want_nll, MTA_DECODER_REG, ms * 1e3);
+  printf("N=%d want_nll=%d: heads_losses_train %.2f us/launch\n", N, want_nll, ms * 1e3);
   // one fresh call for the values (the head gradients accumulate)
   CK(hipMemset(g, 0, (2 * H + 2) * 4));
   mta_heads_losses_train(h, H, wa, ba, wb, bb, y, fac, ip, N, n, C, 1, N, 0, want_nll, 1.f, 1.f, 1.f, out, acc, dh,
@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < hg.size(); ++i) sg += hg[i] * (1.0 + i % 5);
   printf("  out = %.9g %.9g %.9g %.9g  dh.w = %.9g  g.w = %.9g  g_ba = %.9g g_bb = %.9g\n", ho[0], ho[1], ho[2],
          ho[3], sdh, sg, hg[H], hg[2 * H + 1]);
-#if MTA_LOSS_STAMPS
+#if MTA_STAMPS
   unsigned long long st[8];
   CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(mta_loss_stamps), sizeof(st)));
   const char* nm[5] = {"stage y,h", "heads", "losses", "d(alpha,beta)", "dh+head grads"};

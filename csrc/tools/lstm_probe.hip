@@ -1,6 +1,6 @@
 // Diagnostic probe (not part of the extension): runs the LSTM recurrence kernels alone on
 // random data and prints per-segment cycle shares from in-kernel s_memtime stamps.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc -DMTA_LSTM_STAMPS=1 csrc/tools/lstm_probe.hip -o build/lstm_probe
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc -DMTA_STAMPS=1 csrc/tools/lstm_probe.hip -o build/lstm_probe
 // Stamp builds are slower than the real kernel: read the SHARES, not the absolute length.
 #include <cstdio>
 #include <cstdlib>

@@ -1,7 +1,7 @@
 // Diagnostic probe (not part of the extension): times the layer-pipelined LSTM kernels of lstm_stack.hip
 // (forward, and backward with the fused weight gradients) on random data at the headline shape, and in a
-// -DMTA_STACK_STAMPS=1 build prints per-segment s_memtime cycles per step of block 0 for each wave role.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STACK_STAMPS=1] \
+// -DMTA_STAMPS=1 build prints per-segment s_memtime cycles per step of block 0 for each wave role.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I csrc [-DMTA_STAMPS=1|2] \
 //         csrc/tools/lstm_stack_probe.hip -o tools_bin/lstm_stack_probe
 //   ./tools_bin/lstm_stack_probe [N=100] [L=2] [prec=1] [T=60]
 // Stamp builds are slower than the real kernel (each stamp waits lgkmcnt): read the SHARES there and the
@@ -84,16 +84,15 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
   unsigned* flags;
   const long nflags = mta_lstm_stack_flag_words(Np);
-  float* gx_ws = L > 1 ? dev_zero((size_t)mta_lstm_stack_gx_floats(L, Np, T, H)) : nullptr;
   CK(hipMalloc(&flags, nflags * 4));
   CK(hipMemset(flags, 0, nflags * 4));
 
-#if MTA_STACK_STAMPS
+#if STACK_STAMPS
   // stamp the last layer's first tile in the forward (its input waves run the W_ih MFMAs: the slowest layer)
   // and the top layer's first tile in the backward (block 0: its gradient waves run the dx MFMAs)
   const int ntiles = Np / 16, tr8 = (ntiles + 7) / 8 * 8;
   const int which = argc > 6 ? atoi(argv[6]) : L - 1;
-  int sb[2] = {3 * which * tr8, 0};  // [rec(0) | proj(1) x NPP=2 | rec(1) | ...] forward block layout
+  int sb[2] = {which * tr8, 0};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(mta_stack_stamp_block), sb, sizeof(sb)));
   printf("stamping forward layer %d (block %d), backward block 0 (top layer)\n", which, sb[0]);
 #endif
@@ -106,7 +105,7 @@ int main(int argc, char** argv) {
     float m;
     CK(hipEventRecord(a));
     int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gx_ws, 0);
+                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -130,7 +129,7 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&m, a, b));
     if (rep >= skip) ms_b += m / (reps - skip);
   }
-#if MTA_STACK_TIMELINE
+#if STACK_TIMELINE
   {
     // the last forward of the timed loop: per layer, min over tiles of entry / loop start / step T/2 / end
     unsigned long long tl[2][64][4];
@@ -156,7 +155,7 @@ int main(int argc, char** argv) {
     for (int pass = 0; pass < 2; ++pass) {
       CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
       int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gx_ws, 0);
+                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
       CK(hipDeviceSynchronize());
       if (rc) return 1;
       for (int l = 0; l < L; ++l) {
@@ -194,21 +193,21 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
   printf("mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
          "timeouts=%u\n",
-         mode, N, L, T, prec, MTA_STACK_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         mode, N, L, T, prec, MTA_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
-#if MTA_STACK_STAMPS
+#if STACK_STAMPS
   unsigned long long acc[2][3][8];
   CK(hipMemcpyFromSymbol(acc, HIP_SYMBOL(mta_stack_stamp_acc), sizeof(acc)));
   const char* seg[2][3][8] = {
       {{"", "gx_lds_read", "mfma_chain", "activations", "lds_write", "barrier", "", ""},
        {"", "vmcnt_drain+flag", "store_step", "barrier", "", "", "", ""},
-       {"", "l0:compute_gx|l>0:wait+copy_gx", "l0:load|l>0:poll+load_gx", "l0:-|l>0:barrier", "l0:barrier", "", "",
-        ""}},
-      {{"", "lds_reads(dh+stash)", "vmcnt_wait", "elementwise+lds", "dG_store_issue", "barrier", "mfma_dh", ""},
-       {"", "stash_dma_issue", "dma_wait", "barrier", "", "", "", ""},
+       {"", "write_x(load_wait)", "compute_gx", "poll+load_issue", "barrier", "", "", ""}},
+      {{"", "dh_lds_read", "vmcnt_wait", "dG_store_issue", "elementwise+lds", "stash_prefetch", "barrier",
+        "mfma_dh"},
+       {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""},
        {"", "", "", "", "", "", "", ""}}};
   const char* dir[2] = {"fwd", "bwd"};
-  const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "dma-helper", ""}};
+  const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "gradient", ""}};
   for (int d = 0; d < 2; ++d)
     for (int r = 0; r < 3; ++r) {
       if (!role[d][r][0]) continue;

@@ -293,14 +293,10 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   a.r1 = r1;
   a.lse = lse;
   a.x1 = x1;
-  // two workgroups per sequence (query halves) unless MTA_TR_ATTN_SPLIT=0: 2 x 104 sequences still fit one wave of
-  // workgroups on the 256 CUs, and each recomputes only the shared norm / K / V (18.9 -> 16.7 us per launch,
-  // transformer B=1 0.576 -> 0.565 ms, profiles/r4_bench_transformer_attn_split_ab.jsonl)
-  static const bool split_on = [] {
-    const char* e = getenv("MTA_TR_ATTN_SPLIT");
-    return !(e && e[0] == '0');
-  }();
-  a.split = split_on && T > 32 ? 1 : 0;
+  // two workgroups per sequence (query halves): 2 x 104 sequences still fit one wave of workgroups on the 256 CUs,
+  // and each recomputes only the shared norm / K / V (18.9 -> 16.7 us per launch, transformer B=1 0.576 -> 0.565 ms,
+  // profiles/r4_bench_transformer_attn_split_ab.jsonl)
+  a.split = T > 32 ? 1 : 0;
   tr_attn_fwd_kernel<<<nseq * (a.split ? 2 : 1), ATH, sizeof(AttnFwdSmem), st>>>(a);
   return 0;
 }

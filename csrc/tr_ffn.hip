@@ -24,15 +24,10 @@
 
 namespace {
 
-#ifndef MTA_FFN_STAMPS
-#define MTA_FFN_STAMPS 0
+#ifndef MTA_STAMPS
+#define MTA_STAMPS 0
 #endif
-// probe experiments only (csrc/tools/ffn_probe.hip; results are garbage): 1 = no global weight-fragment loads,
-// 2 = no x1 row loads
-#ifndef MTA_FFN_EXP
-#define MTA_FFN_EXP 0
-#endif
-#if MTA_FFN_STAMPS
+#if MTA_STAMPS
 // probe build only (csrc/tools/ffn_probe.hip): s_memtime at the phase boundaries of every workgroup's wave 0
 // ([direction][block][phase]), the per-phase split of one workgroup's critical path
 __device__ unsigned long long mta_ffn_stamp[2][256][12];
@@ -191,14 +186,14 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
-      bw[ks][nt] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag_fm(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+      bw[ks][nt] = bfrag_fm(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
   // x1 rows: 16 threads per row, 8 columns each
   const int xr = tid >> 4, xc = 8 * (tid & 15);
   const bool rok = row0 + xr < a.M;
   float4 xv[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
-    xv[i] = (rok && MTA_FFN_EXP != 2) ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
+    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
                                       : make_float4(1.f, 1.f, 1.f, 1.f);
   {
     const float v0 = a.b1[tid];
@@ -212,7 +207,7 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   // FFN-down B fragments: this wave's 16 output features x 16 k-steps
   bf16x8 bd[16];
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bd[ks] = MTA_FFN_EXP == 1 ? bf16x8{} : bfrag_fm(a.w2, FF, 16 * wave, 32 * ks, lane);
+  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag_fm(a.w2, FF, 16 * wave, 32 * ks, lane);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 1.f;
   if (a.seed) {

@@ -18,9 +18,10 @@ GPU path = one autograd Function per encoder, built from four hand-written HIP k
 
 Precision: fp32 master weights (FlatParameters) and fp32 residual stream / gradients, bf16 GEMM
 operands with fp32 accumulation ("bf16-mixed", matmul precision "medium").  Under ``32-true`` (matmul precision
-"high" / "highest") the encoders run the fp32 graph instead (``mlp_reference`` / ``transformer_reference`` on the
-device: fp32 GEMMs, norms and attention), so the trainer's precision is never silently lowered.  Like the LSTM op, the weights' gradients are
-accumulated inside the op and ``None`` is returned for them.
+"high" / "highest") both encoders run fp32 HIP paths instead (``_MlpEncoderF32Fn`` / ``_TransformerEncoderF32Fn``:
+``gemm_f32x`` bf16x3 / exact-f32 MFMA GEMMs, fp32 norms, fp32 attention ``csrc/attention_f32.hip``), so the
+trainer's precision is never silently lowered.  Like the LSTM op, the weights' gradients are accumulated inside the
+op and ``None`` is returned for them.
 
 CPU path: the same architectures in plain fp32 PyTorch (``mlp_reference`` / ``transformer_reference``),
 which also serve as the numerics oracle of the GPU tests.
@@ -80,10 +81,10 @@ def set_deterministic(flag: bool) -> None:
     _DETERMINISTIC[0] = bool(flag)
 
 
-# workgroup target of a split-K weight gradient (MTA_WGRAD_WGS for the A/B): 128, so that a (weight-gradient,
+# workgroup target of a split-K weight gradient: 128, so that a (weight-gradient,
 # input-gradient) pair of the transformer (~128 + ~196 workgroups) runs as one wave of workgroups and the fp32 atomics
 # halve -- transformer B=1 0.565 -> 0.528 ms; 64: 0.586, 256: 0.565, 512: 0.638 (profiles/r4_wgrad_wgs_sweep.txt)
-_WGRAD_WGS = int(os.environ.get("MTA_WGRAD_WGS", "128"))
+_WGRAD_WGS = 128
 
 
 def wgrad_split(M: int, N: int, K: int) -> int:
@@ -104,8 +105,6 @@ def cast_pad(srcs: Sequence[Tensor], dsts: Sequence[Tensor], seeds: Optional[Ten
 
 def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
     return torch.empty((w.shape[0], cols_p), device=w.device, dtype=torch.bfloat16)
-
-
 
 
 def _row_dtype(D: int) -> torch.dtype:
@@ -249,7 +248,7 @@ class _MlpEncoderFn(torch.autograd.Function):
 # GELU' of the backward fused into the norm backward (fp32 GELU input), bias gradients by an ordered column sum.
 # Reference math: mlp_reference (the same architecture in fp32 PyTorch).
 # --------------------------------------------------------------------------------------------------
-F32X_BIAS, F32X_GELU, F32X_ACCUM = 1, 2, 8
+F32X_BIAS, F32X_GELU, F32X_DGELU, F32X_ACCUM, F32X_RESID, F32X_DROPOUT = 1, 2, 4, 8, 16, 32
 _F32_PREC = {"highest": 0, "high": 1, "bf16x3": 1}
 
 
@@ -633,11 +632,154 @@ class _TransformerEncoderFn(torch.autograd.Function):
         return (None,) * (7 + len(params))
 
 
+# --------------------------------------------------------------------------------------------------
+# 32-true transformer encoder on HIP kernels: every tensor fp32, the seven GEMMs of a block on gemm_f32x at the
+# resolved matmul precision (bf16x3 / exact f32) with bias, GELU (input saved), dropout (counter hash), GELU' and the
+# residual add fused into their epilogues; RMSNorm forward / backward (residual-stream gradient fused) on norm.hip;
+# RoPE attention forward / backward in fp32 on attention_f32.hip.  Reference math: transformer_reference.
+# --------------------------------------------------------------------------------------------------
+def _tr_f32_ok(d: int, heads: int, T: int) -> bool:
+    """Shapes the fp32 attention kernel covers: T <= 64, head dim 16 / 32 / 64 (the fp32 LDS image of one (sequence,
+    head) problem)."""
+    return 1 <= T <= 64 and heads >= 1 and d % heads == 0 and d // heads in (16, 32, 64)
+
+
+class _TransformerEncoderF32Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, seeds, num_layers, heads, dropout, training, need_grad, prec, *params):
+        dev = x.device
+        N, T, F = x.shape
+        M = N * T
+        L = num_layers
+        nb = len(BLOCK_NAMES)
+        d = params[0].shape[0]
+        drop = dropout > 0 and training
+        C = lib()
+        if drop:
+            C.seeds_advance(seeds)
+        f32 = dict(device=dev, dtype=torch.float32)
+        X0 = x.reshape(M, F)
+        xs = torch.empty((M, d), **f32)
+        C.gemm_f32x(prec, X0, False, F, params[0], False, F, xs, d, d, M, d, F, F32X_BIAS, params[1], None)
+        saved: List[Tensor] = [X0]
+        stats: List[Tensor] = []
+        for l in range(L):
+            g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[2 + nb * l: 2 + nb * (l + 1)]
+            dff = w1.shape[0]
+            xn, r1 = torch.empty((M, d), **f32), torch.empty(M, **f32)
+            C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, None, xn, None, r1, None, 0.0, None, None, None, None,
+                   None, None, None)
+            qkv = torch.empty((M, 3 * d), **f32)
+            C.gemm_f32x(prec, xn, False, d, wqkv, False, d, qkv, 3 * d, 3 * d, M, 3 * d, d, F32X_BIAS, bqkv, None)
+            o, lse = torch.empty((M, d), **f32), torch.empty(N * heads * 64, **f32)
+            C.attention_f32(False, qkv, o, lse, None, None, N, T, d, heads, ROPE_BASE)
+            x1 = torch.empty((M, d), **f32)
+            C.gemm_f32x(prec, o, False, d, wo, False, d, x1, d, d, M, d, d, F32X_BIAS | F32X_RESID, bo, None,
+                        resid=xs)
+            xn2, r2 = torch.empty((M, d), **f32), torch.empty(M, **f32)
+            C.norm(False, x1, d, M, d, True, RMS_EPS, g2, None, None, xn2, None, r2, None, 0.0, None, None, None, None,
+                   None, None, None)
+            pre1, u = torch.empty((M, dff), **f32), torch.empty((M, dff), **f32)
+            C.gemm_f32x(prec, xn2, False, d, w1, False, d, u, dff, dff, M, dff, d,
+                        F32X_BIAS | F32X_GELU | (F32X_DROPOUT if drop else 0), b1, pre1,
+                        seed=seeds[l:l + 1] if drop else None, drop_p=float(dropout) if drop else 0.0)
+            x2 = torch.empty((M, d), **f32)
+            C.gemm_f32x(prec, u, False, dff, w2, False, dff, x2, d, d, M, d, dff, F32X_BIAS | F32X_RESID, b2, None,
+                        resid=x1)
+            saved += [xs, xn, qkv, o, x1, xn2, pre1, u]
+            stats += [r1, lse, r2]
+            xs = x2
+        gf = params[2 + nb * L]
+        h, rf = torch.empty((N, d), **f32), torch.empty(N, **f32)
+        # final RMSNorm on the last token of each sequence: rows T*d apart
+        C.norm(False, xs.view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, h, None, rf, None, 0.0,
+               None, None, None, None, None, None, None)
+        saved.append(xs)
+        stats.append(rf)
+        ctx.meta = (N, T, F, d, L, heads, drop, float(dropout), prec)
+        ctx.params, ctx.seeds = params, seeds
+        if need_grad:
+            ctx.save_for_backward(*saved)
+            ctx.stats = stats
+        return h
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, dh):
+        N, T, F, d, L, heads, drop, p, prec = ctx.meta
+        params = ctx.params
+        saved = ctx.saved_tensors
+        stats = ctx.stats
+        C = lib()
+        M = N * T
+        nb = len(BLOCK_NAMES)
+        f32 = dict(device=dh.device, dtype=torch.float32)
+        dh = dh if (dh.dtype == torch.float32 and dh.is_contiguous()) else dh.float().contiguous()
+        # final RMSNorm backward -> residual-stream gradient on the last-token rows (zero elsewhere)
+        dX = torch.empty((M, d), **f32)
+        C.zero_(dX)
+        gf = params[2 + nb * L]
+        C.norm(True, saved[-1].view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, None, None,
+               stats[-1], None, 0.0, dh, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
+        for l in range(L - 1, -1, -1):
+            g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[2 + nb * l: 2 + nb * (l + 1)]
+            dff = w1.shape[0]
+            xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
+            r1, lse, r2 = stats[3 * l: 3 * l + 3]
+            # fc2: dW2 += dX^T u, db2; dPre1 = (dX W2) * dropout * GELU'(pre1)
+            C.gemm_f32x(prec, dX, True, d, u, True, dff, _grad_view(w2), dff, dff, d, dff, M, F32X_ACCUM, None, None)
+            C.colsum_f32(dX, M, d, d, _grad_view(b2))
+            dpre1 = torch.empty((M, dff), **f32)
+            C.gemm_f32x(prec, dX, False, d, w2, True, dff, dpre1, dff, dff, M, dff, d,
+                        F32X_DGELU | (F32X_DROPOUT if drop else 0), None, pre1,
+                        seed=ctx.seeds[l:l + 1] if drop else None, drop_p=p if drop else 0.0)
+            # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
+            C.gemm_f32x(prec, dpre1, True, dff, xn2, True, d, _grad_view(w1), d, d, dff, d, M, F32X_ACCUM, None,
+                        None)
+            C.colsum_f32(dpre1, M, dff, dff, _grad_view(b1))
+            dxn2 = torch.empty((M, d), **f32)
+            C.gemm_f32x(prec, dpre1, False, dff, w1, True, d, dxn2, d, d, M, d, dff, 0, None, None)
+            # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
+            dX1 = torch.empty((M, d), **f32)
+            C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None, None,
+                   dX1, _grad_view(g2), None)
+            # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
+            C.gemm_f32x(prec, dX1, True, d, o, True, d, _grad_view(wo), d, d, d, d, M, F32X_ACCUM, None, None)
+            C.colsum_f32(dX1, M, d, d, _grad_view(bo))
+            do = torch.empty((M, d), **f32)
+            C.gemm_f32x(prec, dX1, False, d, wo, True, d, do, d, d, M, d, d, 0, None, None)
+            # attention backward (inverse RoPE fused) -> dqkv
+            dqkv = torch.empty((M, 3 * d), **f32)
+            C.attention_f32(True, qkv, o, lse, do, dqkv, N, T, d, heads, ROPE_BASE)
+            # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
+            C.gemm_f32x(prec, dqkv, True, 3 * d, xn, True, d, _grad_view(wqkv), d, d, 3 * d, d, M, F32X_ACCUM, None,
+                        None)
+            C.colsum_f32(dqkv, M, 3 * d, 3 * d, _grad_view(bqkv))
+            dxn = torch.empty((M, d), **f32)
+            C.gemm_f32x(prec, dqkv, False, 3 * d, wqkv, True, d, dxn, d, d, M, d, 3 * d, 0, None, None)
+            grad_ready(wqkv.grad, bqkv.grad, wo.grad, bo.grad, w1.grad, b1.grad, w2.grad, b2.grad)
+            # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
+            dXn = torch.empty((M, d), **f32)
+            C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None, None,
+                   dXn, _grad_view(g1), None)
+            dX = dXn
+        # embedding: dWe += dX^T X0, dbe
+        C.gemm_f32x(prec, dX, True, d, saved[0], True, F, _grad_view(params[0]), F, F, d, F, M, F32X_ACCUM, None,
+                    None)
+        C.colsum_f32(dX, M, d, d, _grad_view(params[1]))
+        return (None,) * (8 + len(params))
+
+
 def transformer_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, heads: int,
                        dropout: float, training: bool, precision: str = "medium") -> Tensor:
-    """``precision``: as :func:`mlp_encode`."""
+    """``precision``: as :func:`mlp_encode` ("high" / "highest": :class:`_TransformerEncoderF32Fn` when the fp32
+    attention kernel covers the shape, else the fp32 PyTorch graph)."""
+    need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     if use_hip(x) and precision == "medium":
-        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _TransformerEncoderFn.apply(x.contiguous(), seeds, num_layers, heads, float(dropout), bool(training),
                                            need_grad, *params)
+    if (use_hip(x) and precision in _F32_PREC and not _F32_TORCH
+            and _tr_f32_ok(params[0].shape[0], heads, x.shape[1])):
+        return _TransformerEncoderF32Fn.apply(x.contiguous().float(), seeds, num_layers, heads, float(dropout),
+                                              bool(training), need_grad, _F32_PREC[precision], *params)
     return transformer_reference(x, params, num_layers, heads, dropout, training)

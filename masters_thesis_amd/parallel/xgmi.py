@@ -35,7 +35,7 @@ import torch.distributed as dist
 from ..ops._lib import lib
 
 _LIVE: List["XgmiAllReduce"] = []
-TWOSHOT_KB = float(os.environ.get("MTA_XGMI_TWOSHOT_KB", "512"))
+TWOSHOT_KB = 512.0  # buckets above this (and > 2 ranks) take the two-shot (reduce-scatter + all-gather) form
 
 
 def _agree(ok: bool, device: torch.device, group) -> bool:

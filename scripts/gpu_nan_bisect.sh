@@ -22,17 +22,15 @@ run() {  # name, env..., -- extra bench args
   case $rc in 124|137|134|139) echo "stopping after rc=$rc"; exit $rc;; esac
   return 0
 }
-VARIANTS=${*:-"default hwq1 nobig noslab nodrop spg1"}
+VARIANTS=${*:-"default hwq1 noslab nodrop spg1"}
 for v in $VARIANTS; do
   case $v in
     default) run default X=1 ;;
     hwq1) run hwq1 GPU_MAX_HW_QUEUES=1 ;;
-    nobig) run nobig MTA_GEMM_BIG=0 ;;
     noslab) run noslab MTA_GEMM_SLABS=0 ;;
     nodrop) run nodrop X=1 -- --set model.dropout=0 ;;
     spg1) run spg1 X=1 -- --steps-per-graph 1 ;;
     nographs) run nographs X=1 -- --no-graphs ;;
     serial) run serial AMD_SERIALIZE_KERNEL=3 ;;
-    memset) run memset MTA_ZERO_MEMSET=1 ;;
   esac
 done

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/xgmi
 mkdir -p $OUT
 fatal() { case "$1" in 0) return 0;; *) echo "FATAL rc=$1 at $2" | tee -a $OUT/status.log; exit "$1";; esac; }
-for v in "X=1" "MTA_XGMI_MAX_BLOCKS=128" "MTA_XGMI_MAX_BLOCKS=256" "MTA_XGMI_MAX_BLOCKS=32" "MTA_XGMI_COARSE=1"; do
+for v in "X=1"; do
   env $v timeout -k 10 300 python scripts/xgmi_local_bench.py --world 2 >> $OUT/local.jsonl 2>> $OUT/local.err; fatal $? "$v"
 done
 timeout -k 10 300 python scripts/xgmi_local_bench.py --world 4 >> $OUT/local.jsonl 2>> $OUT/local.err; fatal $? world4

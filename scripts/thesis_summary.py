@@ -21,23 +21,27 @@ def grab(pat, text, cast=float):
 
 def main(d):
     d = Path(d)
-    for p in ("high", "highest"):
-        for loss in ("mse", "nll", "combined"):
-            tr = (d / f"train_{loss}_{p}.log").read_text()
-            te = (d / f"test_{loss}_{p}.log").read_text()
-            summ = json.loads(re.search(r"\[test-summary\] (\{.*\})", te).group(1))
-            rec = {"loss": loss, "matmul_precision": p, "H": 32, "L": 2, "lr": 1e-3, "windows": 10000,
-                   "test_delta_mse": grab(r"Test ΔMSE: ([-0-9.eE+]+)", tr),
-                   "test_delta_nll": grab(r"Test ΔNLL: ([-0-9.eE+]+)", tr),
-                   "test_mae": grab(r"Test MAE: ([-0-9.eE+]+)", tr),
-                   "test_nll": grab(r"Test NLL: ([-0-9.eE+]+)", tr),
-                   "best_val_loss": grab(r"Best validation loss: ([-0-9.eE+]+)", tr),
-                   "best_epoch": grab(r"best_epoch=(\d+)", tr, int),
-                   "epochs_run": len(re.findall(r"^\[epoch \d+\]", tr, re.M)),
-                   **summ}
-            if rec["test_delta_mse"] is not None and rec["test_delta_nll"] is not None:
-                rec["test_delta_mix"] = rec["test_delta_nll"] + 100.0 * rec["test_delta_mse"]  # mse_weight = 100
-            print(json.dumps(rec))
+    for trf in sorted(d.glob("train_*.log")):
+        m = re.fullmatch(r"train_(mse|nll|combined)_(high|highest)(?:_s(\d+))?\.log", trf.name)
+        tef = d / trf.name.replace("train_", "test_", 1)
+        if not m or not tef.exists():
+            continue
+        loss, p, seed = m.group(1), m.group(2), int(m.group(3) or 0)
+        tr = trf.read_text()
+        te = tef.read_text()
+        summ = json.loads(re.search(r"\[test-summary\] (\{.*\})", te).group(1))
+        rec = {"loss": loss, "matmul_precision": p, "seed": seed, "H": 32, "L": 2, "lr": 1e-3, "windows": 10000,
+               "test_delta_mse": grab(r"Test ΔMSE: ([-0-9.eE+]+)", tr),
+               "test_delta_nll": grab(r"Test ΔNLL: ([-0-9.eE+]+)", tr),
+               "test_mae": grab(r"Test MAE: ([-0-9.eE+]+)", tr),
+               "test_nll": grab(r"Test NLL: ([-0-9.eE+]+)", tr),
+               "best_val_loss": grab(r"Best validation loss: ([-0-9.eE+]+)", tr),
+               "best_epoch": grab(r"best_epoch=(\d+)", tr, int),
+               "epochs_run": len(re.findall(r"^\[epoch \d+\]", tr, re.M)),
+               **summ}
+        if rec["test_delta_mse"] is not None and rec["test_delta_nll"] is not None:
+            rec["test_delta_mix"] = rec["test_delta_nll"] + 100.0 * rec["test_delta_mse"]  # mse_weight = 100
+        print(json.dumps(rec))
     print(json.dumps({"reference": REF, "units": "code: percent log-returns, Student-t(5) noise (SURVEY Q12/Q13); "
                       "thesis: decimal returns, Normal noise -> absolute ΔL is parity-unpinned, compare orderings "
                       "and the unit-free correlations"}))

@@ -3,8 +3,7 @@
 Everything but the link itself: the pushes land in this GPU's HBM, so this measures the kernel's own overhead
 (flag protocol, fine-grained inbox reads, block count) per bucket size and form.  Prints one JSON line per
 (size, form): mean us over the timed calls, algorithm bandwidth = bucket bytes / time.
-    python scripts/xgmi_local_bench.py [--world 2] [--iters 50]
-Env A/B knobs: MTA_XGMI_MAX_BLOCKS (grid cap, default 64), MTA_XGMI_COARSE=1 (coarse-grained comm buffer)."""
+    python scripts/xgmi_local_bench.py [--world 2] [--iters 50]"""
 import argparse
 import json
 import os
@@ -73,8 +72,7 @@ def main():
     res = dict(q.get(timeout=600) for _ in ps)
     for p in ps:
         p.join(timeout=60)
-    knobs = {"world": a.world, "max_blocks": os.environ.get("MTA_XGMI_MAX_BLOCKS", "64"),
-             "coarse": os.environ.get("MTA_XGMI_COARSE", "0")}
+    knobs = {"world": a.world}
     for i, r0 in enumerate(res[0]):
         worst = max(res[r][i]["us"] for r in res)
         print(json.dumps({**knobs, **r0, "us": worst, "algo_GBps": round(r0["bytes"] / worst / 1e3, 1)}), flush=True)

@@ -18,6 +18,9 @@ def _run(args, cwd, env=None, ok=True, timeout=600):
     e.update(env or {})
     e["CUDA_VISIBLE_DEVICES"] = ""
     e["HIP_VISIBLE_DEVICES"] = ""
+    # a few OpenMP threads per training process: pytest -n workers x launcher children x torch's default of one
+    # spinning thread per core oversubscribe the host by an order of magnitude
+    e.setdefault("OMP_NUM_THREADS", "2")
     r = subprocess.run([sys.executable, *args], cwd=cwd, env=e, capture_output=True, text=True, timeout=timeout)
     if ok and r.returncode != 0:
         raise AssertionError(f"{args} failed ({r.returncode}):\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}")
