@@ -112,6 +112,7 @@ inline unsigned fused_spin_limit() {
 // ~9 us launch for the 51K-parameter headline model)
 constexpr int REG_N = 4;
 constexpr int U1 = 8, U2 = 4;  // streaming form: float4 loads in flight per thread (phase 1 / phase 2)
+constexpr int STREAM_TPB = 1024;
 
 // Gradient ranges whose producer (a weight-gradient GEMM's split-K reduce, gemm.hip mta_gemm_grad_producer) wrote
 // them by overwriting and left the clip-norm partials of them: phase 1 skips them (their squares come from ext, added
@@ -131,8 +132,11 @@ __device__ __forceinline__ bool covered(const Covered& c, long i) {
   return in;
 }
 
-template <bool REG>
-__global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
+// BS threads per workgroup: TPB for the register form; STREAM_TPB for the streaming form, whose phase 2 is a pure
+// HBM stream of 28 B per parameter -- 16 waves per CU keep ~4x the bytes in flight of 4 waves, which a one-workgroup-
+// per-CU grid (the arrival wait needs them co-resident) otherwise cannot
+template <bool REG, int BS>
+__global__ __launch_bounds__(BS) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v, long n4,
                                                          float* __restrict__ partials,
                                                          unsigned long long* __restrict__ ticket,
@@ -141,15 +145,15 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
                                                          float max_norm, float scale, int adamw, int zero_grad,
                                                          float* __restrict__ norm_out, float* __restrict__ nonfinite,
                                                          unsigned spin_limit, Covered cov) {
-  __shared__ float scratch[TPB / 64];
+  __shared__ float scratch[BS / 64];
   __shared__ float s_norm;
-  const long stride = (long)gridDim.x * TPB;
+  const long stride = (long)gridDim.x * BS;
   float acc = 0.f;
   float4 rg[REG ? REG_N : 1], rp[REG ? REG_N : 1], rm[REG ? REG_N : 1], rv[REG ? REG_N : 1];
   if constexpr (REG) {
 #pragma unroll
     for (int r = 0; r < REG_N; ++r) {
-      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      const long i = (long)blockIdx.x * BS + threadIdx.x + r * stride;
       if (i < n4) {
         rg[r] = g[i];
         rp[r] = p[i];
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     }
 #pragma unroll
     for (int r = 0; r < REG_N; ++r) {
-      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      const long i = (long)blockIdx.x * BS + threadIdx.x + r * stride;
       if (cov.n && covered(cov, i)) continue;
       acc = fmaf(rg[r].x, rg[r].x, acc);
       acc = fmaf(rg[r].y, rg[r].y, acc);
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
   } else {
     // U1 independent float4 loads in flight per thread: one workgroup per CU (the arrival wait needs them all
     // co-resident) holds too few bytes in flight for HBM with one load per iteration (Little's law)
-    for (long i0 = (long)blockIdx.x * TPB + threadIdx.x; i0 < n4; i0 += stride * U1) {
+    for (long i0 = (long)blockIdx.x * BS + threadIdx.x; i0 < n4; i0 += stride * U1) {
       float4 q[U1];
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
@@ -187,7 +191,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
       }
     }
   }
-  for (int k = blockIdx.x * TPB + threadIdx.x; k < cov.n_ext; k += gridDim.x * TPB) acc += cov.ext[k];
+  for (int k = blockIdx.x * BS + threadIdx.x; k < cov.n_ext; k += gridDim.x * BS) acc += cov.ext[k];
   acc = block_sum(acc, scratch) * (scale * scale);
   // the step counter is read by every workgroup BEFORE it arrives (thread 0 loads it and its vmcnt(0) below
   // completes the load before the ticket add; the workgroup reads it from LDS); the last arriver advances it
@@ -242,7 +246,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
   if constexpr (REG) {
 #pragma unroll
     for (int r = 0; r < REG_N; ++r) {
-      const long i = (long)blockIdx.x * TPB + threadIdx.x + r * stride;
+      const long i = (long)blockIdx.x * BS + threadIdx.x + r * stride;
       if (i >= n4) continue;
       float4 pp = rp[r], gg = rg[r], mm = rm[r], vv = rv[r];
       float* pf = reinterpret_cast<float*>(&pp);
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(TPB) void adam_fused_kernel(float4* __restrict__ p,
     return;
   }
   // U2 elements' four streams in flight per thread (same reason as phase 1)
-  for (long i0 = (long)blockIdx.x * TPB + threadIdx.x; i0 < n4; i0 += stride * U2) {
+  for (long i0 = (long)blockIdx.x * BS + threadIdx.x; i0 < n4; i0 += stride * U2) {
     float4 pp[U2], gg[U2], mm[U2], vv[U2];
 #pragma unroll
     for (int u = 0; u < U2; ++u) {
@@ -317,7 +321,7 @@ inline int fused_grid_reg(long n4) {
 }
 
 inline int fused_grid(long n4) {
-  long blocks = (n4 + TPB * 4 - 1) / (TPB * 4);
+  long blocks = (n4 + STREAM_TPB * 4 - 1) / (STREAM_TPB * 4);
   if (blocks < 1) blocks = 1;
   if (blocks > FUSED_MAX_BLOCKS) blocks = FUSED_MAX_BLOCKS;
   return (int)blocks;
@@ -409,12 +413,12 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
   cov.ext = ext;
   cov.n_ext = cov.n ? n_ext : 0;
   if (fused_reg(n4))
-    adam_fused_kernel<true><<<fused_grid_reg(n4), TPB, 0, st>>>(
+    adam_fused_kernel<true, TPB><<<fused_grid_reg(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
         zero_grad, norm_out, nonfinite, spin, cov);
   else
-    adam_fused_kernel<false><<<fused_grid(n4), TPB, 0, st>>>(
+    adam_fused_kernel<false, STREAM_TPB><<<fused_grid(n4), STREAM_TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),
         reinterpret_cast<float4*>(v), n4, partials, ticket, lr, step, beta1, beta2, eps, wd, max_norm, scale, adamw,
         zero_grad, norm_out, nonfinite, spin, cov);

@@ -89,8 +89,13 @@ def main():
         err = ((out - ref).abs().max() / ref.abs().max()).item()
         us = timeit(fn)
         tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
+        # the vendor library on the same product (torch.matmul -> hipBLASLt, bf16 out, no fused epilogue)
+        Ab = A if mode != 2 else A.t()
+        Bb = B.t() if mode == 0 else B
+        blas_us = timeit(lambda: torch.matmul(Ab, Bb))
         row = {"shape": name, "big": big, "mode": mode, "M": M, "N": N, "K": K, "ksplit": ks, "us": round(us, 2),
-               "tflops": round(tf, 1), "rel_err": err}
+               "tflops": round(tf, 1), "blas_us": round(blas_us, 2),
+               "blas_tflops": round(2.0 * M * N * K / (blas_us * 1e-6) / 1e12, 1), "rel_err": err}
         rows.append(row)
         print(json.dumps(row), flush=True)
         assert err < 2e-2, row

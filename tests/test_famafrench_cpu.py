@@ -79,7 +79,7 @@ def test_train_on_real_datamodule(tmp_path):
     args = [sys.executable, str(REPO / "train.py"), "datamodule=real", f"datamodule.raw_dir={raw_dir}",
             f"datamodule.data_dir={tmp_path / 'real'}", "trainer.max_epochs=1",
             "+trainer.limit_train_batches=40", "+trainer.limit_val_batches=10", "+trainer.limit_test_batches=10"]
-    env = {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "PATH": "/usr/bin:/bin"}
+    env = {"CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": "", "PATH": "/usr/bin:/bin", "OMP_NUM_THREADS": "2"}
     r = subprocess.run(args, cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     stocks = torch.load(tmp_path / "real/stocks.pt", weights_only=True)

@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 REPO = Path(__file__).resolve().parents[1]
 # 2,222 windows -> 1,555 / 444 / 223 train / val / test batches of one window
 DATA = ["datamodule.n_samples=200000", "seed=0"]
-COMMON = [*DATA, "loss=combined", "model.dropout=0", "+trainer.matmul_precision=highest", "trainer.max_epochs=3",
-          "trainer.enable_progress_bar=false"]
+BASE = [*DATA, "loss=combined", "model.dropout=0", "trainer.max_epochs=3", "trainer.enable_progress_bar=false"]
+COMMON = [*BASE, "+trainer.matmul_precision=highest"]
 
 
 def _run(args, cwd, timeout=300):
@@ -49,6 +49,8 @@ def runs(tmp_path_factory):
     out = {}
     for name, extra in (("hip", []), ("torch", ["+model.backend=torch"])):
         out[name] = _run([str(REPO / "train.py"), *COMMON, *extra, f"logger.version={name}"], d)
+    # the default 32-true matmul precision (train.py / bench.py): "high" = fp16x2 LSTM forward, bf16x3 backward
+    out["high"] = _run([str(REPO / "train.py"), *BASE, "logger.version=high"], d)
     return d, out
 
 
@@ -86,6 +88,29 @@ def test_gpu_hip_matches_miopen_reference_path(runs):
     for what in ("MAE", "NLL"):
         x, y = _final(out["hip"], what), _final(out["torch"], what)
         assert abs(x - y) <= 1e-3 * max(abs(y), 1e-6), (what, x, y)
+
+
+def test_gpu_default_high_precision_tracks_highest(runs):
+    """The default precision ("high": TF32-class fp16x2 forward recurrent products, bf16x3 backward, the class of
+    cuDNN's TF32 LSTM the reference runs by default) over 3 epochs x 1,555 steps on the same seed and data as the
+    exact-fp32 ("highest") run: every per-epoch train / val loss and the final test metrics within 1 % (stated
+    tolerance: rounding of ~2^-21 relative per product compounds over 4,665 Adam steps), and not identical (the
+    fast path really ran)."""
+    d, out = runs
+    a = _scalars(d / "logs/FinancialLstm/synthetic/high")
+    b = _scalars(d / "logs/FinancialLstm/synthetic/hip")
+    diffs = []
+    for tag in ("loss/total/train", "loss/total/val", "loss/mse/val", "loss/nll/val"):
+        va = [v for _, v in a[tag]]
+        vb = [v for _, v in b[tag]]
+        assert len(va) == len(vb) == 3, tag
+        for x, y in zip(va, vb):
+            assert abs(x - y) <= 1e-2 * max(abs(y), 1e-6), (tag, va, vb)
+            diffs.append(abs(x - y))
+    assert max(diffs) > 0, "high and highest runs are bit-identical: the fp16x2 path did not run"
+    for what in ("MAE", "NLL"):
+        x, y = _final(out["high"], what), _final(out["hip"], what)
+        assert abs(x - y) <= 1e-2 * max(abs(y), 1e-6), (what, x, y)
 
 
 def test_gpu_plateau_halves_device_lr(tmp_path):
