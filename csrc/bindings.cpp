@@ -75,6 +75,7 @@ void mta_gemm_flush();
 void mta_gemm_set_big(int on);
 void mta_norm_flush();
 void mta_norm_defer();
+void mta_gemm_group_flush();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
                  const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds, hipStream_t st);
 int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps, const float* gamma,
@@ -568,7 +569,7 @@ void check_span(const at::Tensor& t, int64_t rows, int64_t ld, int64_t cols, con
 void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb,
                double alpha, int64_t flags, const OptT& bias, const OptT& resid, const OptT& aux_in, const OptT& seed,
                double drop_p, const OptT& out_bf16, const OptT& out_f32, const OptT& aux_pre, int64_t ldc,
-               int64_t n_store, int64_t ksplit, const OptT& bias_grad, bool defer) {
+               int64_t n_store, int64_t ksplit, const OptT& bias_grad, int64_t defer) {
   const int64_t NS = (n_store <= 0 || n_store > N) ? N : n_store;
   CHECK_GPU(A, at::kBFloat16);
   CHECK_GPU(B, at::kBFloat16);
@@ -599,7 +600,7 @@ void gemm_bf16(int64_t mode, at::Tensor A, at::Tensor B, int64_t M, int64_t N, i
                                (float)drop_p, opt_typed<void>(out_bf16, at::kBFloat16, "out_bf16"),
                                opt_typed<float>(out_f32, at::kFloat, "out_f32"),
                                opt_typed<void>(aux_pre, at::kBFloat16, "aux_pre"), (int)ldc, (int)NS, (int)ksplit,
-                               opt_typed<float>(bias_grad, at::kFloat, "bias_grad"), defer ? 1 : 0, cur_stream());
+                               opt_typed<float>(bias_grad, at::kFloat, "bias_grad"), (int)defer, cur_stream());
   TORCH_CHECK(rc == 0, "gemm_bf16: unsupported arguments (rc=", rc, ", M=", M, " N=", N, " K=", K, ")");
 }
 
@@ -1262,6 +1263,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("tr_attn_fwd", &tr_attn_fwd);
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
+  m.def("gemm_group_flush", []() { mta_gemm_group_flush(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
   m.def("norm", &norm);

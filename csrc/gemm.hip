@@ -875,6 +875,32 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
   }
 }
 
+// ---- grouped weight gradients ----
+// The transformer backward's small weight gradients (out <= 512 x 512, K = 6,272 tokens) are latency-bound one by
+// one: ~1 us per 128-deep k-step on a 64 x 64 tile, 8-12 us per launch at the best split
+// (profiles/r4_wgrad_split_sweep.txt), ~180 us of the step.  Queued over the whole backward (defer = 2) and launched
+// together (mta_gemm_group_flush: one launch per operand layout), their tiles x k-splits fill the chip with several
+// workgroups per CU, whose k-step latencies then overlap instead of adding up.
+constexpr int GROUP_MAX = 16;   // problems per launch (the table travels in the kernel arguments: < 4 KB)
+constexpr int GROUP_WGS = 1024;  // workgroup target of one grouped launch (4 per CU)
+struct GroupTable {
+  GemmArgs g[GROUP_MAX];
+  int start[GROUP_MAX + 1];  // first block of each problem; start[n] = grid size
+  int nx[GROUP_MAX], ny[GROUP_MAX], nz[GROUP_MAX];
+  int n;
+};
+static_assert(sizeof(GroupTable) < 4000, "kernel arguments");
+template <bool T>  // T: both operands stored [K][rows] (dY^T X); else both k-contiguous
+__global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_group_kernel(GroupTable t) {
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<64, 64, 128>()];
+  int b = xcd_remap(blockIdx.x, t.start[t.n]);
+  int p = 0;
+  while (p + 1 < t.n && b >= t.start[p + 1]) ++p;
+  b -= t.start[p];
+  const int nx = t.nx[p], ny = t.ny[p];
+  gemm_body<64, 64, 128, T, T>(t.g[p], b % nx, (b / nx) % ny, b / (nx * ny), t.nz[p], smem, smem + 64 * (128 + 8));
+}
+
 template <int BM, int BN, int BKT, bool AT, bool BT>
 void launch(const GemmArgs& g, int ksplit, hipStream_t st) {
   const int nx = (g.N + BN - 1) / BN, ny = (g.M + BM - 1) / BM;
@@ -1186,9 +1212,58 @@ struct Pending {
   hipStream_t st;
 } pending;
 
+// weight gradients queued for one grouped launch per layout (kind 0: k-contiguous operands, 1: [K][rows] operands)
+constexpr int GROUP_QMAX = 48;
+struct GroupQueue {
+  GemmArgs g[2][GROUP_QMAX];
+  int ks[2][GROUP_QMAX];  // requested split: 1 = none (deterministic mode), else chosen at the flush
+  int n[2] = {0, 0};
+  hipStream_t st = nullptr;
+} gq;
+
+void launch_group(int kind, int first, int count, hipStream_t st) {
+  GroupTable t{};
+  // one k-chunk for every problem of the launch, sized so that tiles x splits ~ GROUP_WGS
+  long work = 0;
+  for (int q = first; q < first + count; ++q) {
+    const GemmArgs& g = gq.g[kind][q];
+    work += (long)((g.M + 63) / 64) * ((g.N + 63) / 64) * g.K;
+  }
+  long chunk = (work + GROUP_WGS - 1) / GROUP_WGS;
+  chunk = std::max(256L, (chunk + 127) / 128 * 128);
+  int blocks = 0;
+  for (int q = 0; q < count; ++q) {
+    GemmArgs g = gq.g[kind][first + q];
+    int ks = gq.ks[kind][first + q] == 1 ? 1 : (int)std::max(1L, (g.K + chunk - 1) / chunk);
+    int kps = (g.K + ks - 1) / ks;
+    kps = (kps + BK - 1) / BK * BK;
+    ks = (g.K + kps - 1) / kps;
+    g.k_per_split = kps;
+    t.g[q] = g;
+    t.nx[q] = (g.N + 63) / 64;
+    t.ny[q] = (g.M + 63) / 64;
+    t.nz[q] = ks;
+    t.start[q] = blocks;
+    blocks += t.nx[q] * t.ny[q] * ks;
+  }
+  t.n = count;
+  t.start[count] = blocks;
+  if (kind) gemm_group_kernel<true><<<blocks, GT, 0, st>>>(t);
+  else gemm_group_kernel<false><<<blocks, GT, 0, st>>>(t);
+}
+
 }  // namespace
 
 extern "C" void mta_gemm_set_big(int on) { g_big_override = on; }
+
+// launch the queued weight gradients (end of a backward; also when the queue is full or the stream changes)
+extern "C" void mta_gemm_group_flush() {
+  for (int kind = 0; kind < 2; ++kind) {
+    for (int first = 0; first < gq.n[kind]; first += GROUP_MAX)
+      launch_group(kind, first, std::min(GROUP_MAX, gq.n[kind] - first), gq.st);
+    gq.n[kind] = 0;
+  }
+}
 
 // launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
 extern "C" void mta_gemm_flush() {
@@ -1271,6 +1346,22 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
       dispatch_mode(2, g, ksplit, st);
       if (req.norm_parts) sumsq_parts_kernel<<<NORM_PARTS, 256, 0, st>>>(out_f32, (long)M * ldc, req.norm_parts);
     }
+    return 0;
+  }
+  if (defer == 2) {
+    // a weight gradient queued for the grouped launch at mta_gemm_group_flush (too big for the 64 x 64 tiles: now)
+    if (!(mode == 2 || (mode == 0 && (flags & EPI_ACCUM)))) return 8;
+    if (big_eligible(g, ksplit) || (long)M * N * K >= (1L << 31)) {
+      dispatch_mode(mode, g, ksplit, st);
+      return 0;
+    }
+    if ((gq.n[0] || gq.n[1]) && gq.st != st) mta_gemm_group_flush();
+    const int kind = mode == 2 ? 1 : 0;
+    if (gq.n[kind] == GROUP_QMAX) mta_gemm_group_flush();
+    gq.g[kind][gq.n[kind]] = g;
+    gq.ks[kind][gq.n[kind]] = ksplit;
+    ++gq.n[kind];
+    gq.st = st;
     return 0;
   }
   if (defer) {

@@ -112,7 +112,7 @@ inline unsigned fused_spin_limit() {
 // ~9 us launch for the 51K-parameter headline model)
 constexpr int REG_N = 4;
 constexpr int U1 = 8, U2 = 4;  // streaming form: float4 loads in flight per thread (phase 1 / phase 2)
-constexpr int STREAM_TPB = 1024;
+constexpr int STREAM_TPB = TPB;
 
 // Gradient ranges whose producer (a weight-gradient GEMM's split-K reduce, gemm.hip mta_gemm_grad_producer) wrote
 // them by overwriting and left the clip-norm partials of them: phase 1 skips them (their squares come from ext, added
@@ -132,9 +132,8 @@ __device__ __forceinline__ bool covered(const Covered& c, long i) {
   return in;
 }
 
-// BS threads per workgroup: TPB for the register form; STREAM_TPB for the streaming form, whose phase 2 is a pure
-// HBM stream of 28 B per parameter -- 16 waves per CU keep ~4x the bytes in flight of 4 waves, which a one-workgroup-
-// per-CU grid (the arrival wait needs them co-resident) otherwise cannot
+// BS threads per workgroup (TPB = 256 for both forms: 1,024-thread workgroups for the streaming form measured slower,
+// 93.5 vs 80.8 us at 13.4 M parameters in the mlp_large step, profiles/r5_adam_1024_negative.txt)
 template <bool REG, int BS>
 __global__ __launch_bounds__(BS) void adam_fused_kernel(float4* __restrict__ p, float4* __restrict__ g,
                                                          float4* __restrict__ m, float4* __restrict__ v, long n4,

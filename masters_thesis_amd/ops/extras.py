@@ -60,16 +60,22 @@ def _r16(n: int) -> int:
 def gemm(mode: int, A: Tensor, B: Tensor, M: int, N: int, K: int, lda: int, ldb: int, *, flags: int = 0,
          alpha: float = 1.0, bias=None, resid=None, aux_in=None, seed=None, drop_p: float = 0.0, out_bf16=None,
          out_f32=None, aux_pre=None, ldc: Optional[int] = None, n_store: int = 0, ksplit: int = 1,
-         bias_grad=None, defer: bool = False) -> None:
+         bias_grad=None, defer: bool = False, group: bool = False) -> None:
     """``defer`` (weight-gradient GEMMs): hold the launch back and run it together with the NEXT gemm call (its
     input-gradient partner, which reads the same dY) as one paired launch (csrc/gemm.hip); ``gemm_flush()``
-    launches a held-back GEMM alone."""
+    launches a held-back GEMM alone.  ``group`` (weight-gradient GEMMs): queue it for one grouped launch of every
+    queued weight gradient at ``gemm_group_flush()`` (``ksplit`` 1: no split-K, else the flush picks it)."""
     lib().gemm_bf16(mode, A, B, M, N, K, lda, ldb, alpha, flags, bias, resid, aux_in, seed, drop_p, out_bf16,
-                    out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad, bool(defer))
+                    out_f32, aux_pre, N if ldc is None else ldc, n_store, ksplit, bias_grad,
+                    2 if group else int(bool(defer)))
 
 
 def gemm_flush() -> None:
     lib().gemm_flush()
+
+
+def gemm_group_flush() -> None:
+    lib().gemm_group_flush()
 
 
 _DETERMINISTIC = [False]
@@ -575,28 +581,28 @@ class _TransformerEncoderFn(torch.autograd.Function):
                 C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
                              p, dX, dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
                 gemm(0, dXt, u, d, dff, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
                 gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
             elif ffn:
                 # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
                 # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
                 C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
                              p, dX, dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
                 gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)  # paired with dW1
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1))
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
             else:
                 # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
                 gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), defer=True)
+                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
                 fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
                 gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1,
                      seed=ctx.seeds[l:l + 1] if drop else None, drop_p=p, out_bf16=dpre1)
                 # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), defer=True)
+                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
                 dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
                 gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
                 # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
@@ -605,7 +611,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                        dX1b, dX1, _grad_view(g2), None)
             # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
             gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
-                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), defer=True)
+                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), group=True)
             do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
             gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
             # attention backward (RoPE inverse fused) -> dqkv
@@ -613,11 +619,9 @@ class _TransformerEncoderFn(torch.autograd.Function):
             C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
             # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
             gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
-                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), defer=True)
+                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), group=True)
             dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
             gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
-            # this layer's matrices and biases are final (their norm gains are reduced at the end of the backward)
-            grad_ready(wqkv.grad, bqkv.grad, wo.grad, bo.grad, w1.grad, b1.grad, w2.grad, b2.grad)
             # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
             dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
             C.norm_defer()
@@ -626,9 +630,13 @@ class _TransformerEncoderFn(torch.autograd.Function):
             dX = dXn
         # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
         gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,
-             ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]))
-        gemm_flush()
+             ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]), group=True)
+        # every layer's weight gradients in one launch per operand layout (queued above), then the norm gains
+        gemm_group_flush()
         C.norm_flush()
+        for l in range(L):
+            base = 2 + nb * l
+            grad_ready(*(params[base + j].grad for j in (1, 2, 3, 4, 6, 7, 8, 9)))
         return (None,) * (7 + len(params))
 
 

@@ -164,6 +164,46 @@ def test_small_weight_grad(M, N, K, ks):
     assert _rel(gb - 1, A.float().sum(0)) < 2e-3
 
 
+@pytest.mark.parametrize("split", [True, False])
+def test_grouped_weight_grads(split):
+    """Weight gradients queued over a backward (``group=True``) and launched together by gemm_group_flush: both
+    operand layouts (dY^T X on [K][rows] operands, and the k-contiguous NN form), problems of different shapes in
+    one launch, split-K (fp32 atomics) and unsplit (deterministic mode), accumulated onto existing values, bias
+    gradients included -- against fp32 PyTorch."""
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(7)
+    K = 6272
+    shapes = [(384, 128), (128, 128), (512, 128), (128, 512), (128, 8)]
+    probs = []
+    for i, (M, N) in enumerate(shapes):
+        for nn in (False, True):
+            if nn:
+                A, B = _bf(torch.randn(M, K)), _bf(torch.randn(N, K))  # k-contiguous images
+                ref = A.float() @ B.float().t()
+                bsum = None
+            else:
+                A, B = _bf(torch.randn(K, M)), _bf(torch.randn(K, N))
+                ref = A.float().t() @ B.float()
+                bsum = A.float().sum(0)
+            out = torch.randn(M, N, device=DEV)
+            bg = torch.randn(M, device=DEV) if bsum is not None else None
+            probs.append((nn, A, B, M, N, out, out.clone(), ref, bg, None if bg is None else bg.clone(), bsum))
+    for nn, A, B, M, N, out, _, _, bg, _, _ in probs:
+        ks = X.wgrad_split(M, N, K) if split else 1
+        if nn:
+            X.gemm(0, A, B, M, N, K, K, K, flags=X.EPI_ACCUM, out_f32=out, ldc=N, n_store=N, ksplit=ks, group=True)
+        else:
+            X.gemm(2, A, B, M, N, K, M, N, flags=X.EPI_ACCUM, out_f32=out, ldc=N, n_store=N, ksplit=ks, bias_grad=bg,
+                   group=True)
+    X.gemm_group_flush()
+    torch.cuda.synchronize()
+    for nn, A, B, M, N, out, out0, ref, bg, bg0, bsum in probs:
+        assert _rel(out - out0, ref) < 2e-3, (nn, M, N)
+        if bg is not None:
+            assert _rel(bg - bg0, bsum) < 2e-3, (M, N)
+
+
 @pytest.mark.parametrize("rms", [False, True])
 @pytest.mark.parametrize("D", [128, 256, 1024, 1536, 2048])
 def test_norm_forward_backward(rms, D):
