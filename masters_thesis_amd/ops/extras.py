@@ -565,6 +565,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
         dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
         cast_pad([dX], [dXb])
         frag = ctx.frag  # fused FFN: W2^T / W1^T fragment-major images, written by the forward's packing launch
+        # operands of the weight gradients queued for the grouped launch: alive (and not rewritten) until the flush
+        keep: List[Tensor] = []
         for l in range(L - 1, -1, -1):
             base = 2 + nb * l
             g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
@@ -584,6 +586,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                      ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
                 gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
                      ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                keep += [dXt, dpre1]
             elif ffn:
                 # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
                 # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
@@ -593,6 +596,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                      ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
                      ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                keep += [dXb, dpre1]
             else:
                 # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
                 gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
@@ -603,6 +607,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
                 # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
                 gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
                      ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                keep += [dXb, dpre1]
                 dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
                 gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
                 # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
@@ -620,10 +625,12 @@ class _TransformerEncoderFn(torch.autograd.Function):
             # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
             gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
                  ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), group=True)
+            keep += [dX1b, dqkv]
             dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
             gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
             # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
             dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
+            dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)  # fresh: the queued dW2 may read the last one
             C.norm_defer()
             C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None, dXb,
                    dXn, _grad_view(g1), None)
@@ -633,6 +640,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
              ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]), group=True)
         # every layer's weight gradients in one launch per operand layout (queued above), then the norm gains
         gemm_group_flush()
+        del keep
         C.norm_flush()
         for l in range(L):
             base = 2 + nb * l
