@@ -72,6 +72,10 @@ struct AttnArgs {
   __bf16* out;       // [M][D]
   float* lse;        // [nseq * heads][TP]
   const __bf16* dout;
+  // backward with the output projection's input gradient fused in (dout null): dO = dX1 Wo, dX1 [M][D] bf16 rows,
+  // Wo^T as a fragment-major image (csrc/tr_ffn.hip frag_pack, transposed)
+  const __bf16* dx1;
+  const __bf16* wot;
   __bf16* dqkv;      // [M][3D]
   int T, D, heads;
   float scale, rope_base;
@@ -195,6 +199,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   if (wave == 0) a.lse[(size_t)blockIdx.x * TP + l] = s.rowv[l];
 }
 
+// B fragment (16 output features n0.., 32 k from k0) of a fragment-major [N][K] image: 1 KB contiguous per wave
+__device__ __forceinline__ bf16x8 fm_frag(const __bf16* w, int K, int n0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + ((size_t)((n0 >> 4) * (K >> 5) + (k0 >> 5)) << 9) + 8 * lane);
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   constexpr int RLD = HD + 8;
@@ -206,6 +215,48 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
     __bf16* const rm[3] = {s.q, s.k, s.v};
     __bf16* const tr[3] = {s.qt, s.kt, nullptr};
     load_qkv<HD>(a, seq, h, rm, tr, wave);  // wave 0: q, q^T; 1: k, k^T; 2: v
+  } else if (a.dx1) {
+    // wave 3: this head's dO = dX1 rows . Wo^T[head features] (64 x HD, K = D) on the matrix cores -- the output
+    // projection's input-gradient GEMM, fused -- into the dO / dO^T images, then D = rowsum(dO o O)
+    constexpr int RLD = HD + 8;
+    const size_t seqrow = (size_t)seq * a.T;
+#pragma unroll 1
+    for (int tt = 0; tt < TP / 16; ++tt) {
+      f32x4 acc[HD / 16];
+#pragma unroll
+      for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int t = 16 * tt + (l & 15);
+      const bool ok = t < a.T;
+      const __bf16* arow = a.dx1 + (seqrow + (ok ? t : 0)) * a.D + 8 * (l >> 4);
+#pragma unroll 1
+      for (int k0 = 0; k0 < a.D; k0 += 32) {
+        bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + k0);
+        if (!ok) af = bf16x8{};
+#pragma unroll
+        for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = mfma16x16x32(af, fm_frag(a.wot, a.D, h * HD + 16 * dj, k0, l), acc[dj]);
+      }
+#pragma unroll
+      for (int dj = 0; dj < HD / 16; ++dj) {
+        f32x4 rb;  // rounded as the unfused chain's bf16 dO tensor
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rb[r] = (float)(__bf16)acc[dj][r];
+        put_rows(s.dO, RLD, 16 * tt, 16 * dj, rb);
+        put_cols(s.dOt, PLD, 16 * tt, 16 * dj, rb);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dO rows are in LDS for its own lanes
+    const int t = l;
+    const bool ok = t < a.T;
+    const __bf16* osrc = a.out + (seqrow + (ok ? t : 0)) * a.D + h * HD;
+    float dsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < HD; c += 8) {
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(s.dO + t * RLD + c);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(osrc + c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += ok ? (float)dv[j] * (float)ov[j] : 0.f;
+    }
+    s.rowv[t] = dsum;
   } else {
     // wave 3: dO rows (row-major + transposed) and D = rowsum(dO o O)
     const int t = l;
@@ -291,14 +342,18 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
 }  // namespace
 
 extern "C" int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq,
-                             int T, int D, int heads, float rope_base, const float* rope, hipStream_t st) {
+                             int T, int D, int heads, float rope_base, const float* rope, const void* dx1,
+                             const void* wot, hipStream_t st) {
   if (T < 1 || T > TP || D % heads || !rope) return 1;
+  if (bwd && !dout && !(dx1 && wot && D % 32 == 0)) return 4;
   const int HD = D / heads;
   AttnArgs a;
   a.qkv = static_cast<const __bf16*>(qkv);
   a.out = static_cast<__bf16*>(out);
   a.lse = lse;
   a.dout = static_cast<const __bf16*>(dout);
+  a.dx1 = dout ? nullptr : static_cast<const __bf16*>(dx1);
+  a.wot = static_cast<const __bf16*>(wot);
   a.dqkv = static_cast<__bf16*>(dqkv);
   a.T = T;
   a.D = D;

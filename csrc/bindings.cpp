@@ -89,13 +89,15 @@ int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, c
                void* dxT, hipStream_t st);
 int mta_frag_pack(int count, const float* const* src, void* const* dst, const int* n, const int* k, const int* tr,
                   hipStream_t st);
+int mta_tr_attn_dx(int M, const void* dqkv, const void* wqkvt, const float* x, const float* r1, const float* g1,
+                   const float* dx1, float* dx, void* dxb, float* dg1, hipStream_t st);
 int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo, const float* g1,
                     const float* bqkv, const float* bo, const float* rope, float eps, void* xn, float* r1, void* qkv,
                     void* o, float* lse, float* x1, hipStream_t st);
 int mta_tr_transpose_bf16(int n, const void* const* src, void* const* dst, const int* rows, const int* cols,
                           hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
-                  int D, int heads, float rope_base, const float* rope, hipStream_t st);
+                  int D, int heads, float rope_base, const float* rope, const void* dx1, const void* wot, hipStream_t st);
 // lstm_stack.hip (layer-pipelined multi-layer LSTM)
 int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
@@ -780,6 +782,28 @@ void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::ve
   TORCH_CHECK(rc == 0, "frag_pack: N must be a multiple of 16 and K of 32 (rc=", rc, ")");
 }
 
+// backward tail of the fused attention half (csrc/tr_attn.hip tr_attn_dx_kernel): d(xn) = dqkv Wqkv, RMSNorm1
+// backward + residual -> dx (fp32), dxb (bf16); dg1 through a deferred norm slot (summed at norm_flush)
+void tr_attn_dx(at::Tensor dqkv, at::Tensor wqkvt, at::Tensor x, at::Tensor r1, at::Tensor g1, at::Tensor dx1,
+                at::Tensor dx, at::Tensor dxb, at::Tensor dg1) {
+  CHECK_GPU(dqkv, at::kBFloat16);
+  CHECK_GPU(wqkvt, at::kBFloat16);
+  CHECK_GPU(dxb, at::kBFloat16);
+  for (auto* t : {&x, &r1, &g1, &dx1, &dx, &dg1}) {
+    CHECK_F32(*t);
+  }
+  const int64_t M = x.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.size(1) == 128 && dx1.numel() == M * 128 && dx.numel() == M * 128 &&
+                  dxb.numel() == M * 128 && dqkv.numel() == M * 384 && r1.numel() >= M && g1.numel() == 128 &&
+                  dg1.numel() == 128 && wqkvt.numel() == 128 * 384,
+              "tr_attn_dx: d = 128, 4 heads (dqkv [M][384], x / dx1 / dx [M][128])");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  const int rc = mta_tr_attn_dx((int)M, dqkv.data_ptr(), wqkvt.data_ptr(), x.data_ptr<float>(), r1.data_ptr<float>(),
+                                g1.data_ptr<float>(), dx1.data_ptr<float>(), dx.data_ptr<float>(), dxb.data_ptr(),
+                                dg1.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(rc == 0, "tr_attn_dx failed (rc=", rc, ")");
+}
+
 // fused attention half of a transformer block forward (csrc/tr_attn.hip): x -> xn, r1, qkv, o, lse, x1
 void tr_attn_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope_base, at::Tensor x, at::Tensor wqkv,
                  at::Tensor wo, at::Tensor g1, at::Tensor bqkv, at::Tensor bo, at::Tensor xn, at::Tensor r1,
@@ -828,21 +852,31 @@ void transpose_bf16(std::vector<at::Tensor> src, std::vector<at::Tensor> dst) {
 }
 
 void attention(bool bwd, at::Tensor qkv, at::Tensor out, at::Tensor lse, const OptT& dout, const OptT& dqkv,
-               int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base) {
+               int64_t nseq, int64_t T, int64_t D, int64_t heads, double rope_base, const OptT& dx1,
+               const OptT& wot) {
   CHECK_GPU(qkv, at::kBFloat16);
   CHECK_GPU(out, at::kBFloat16);
   CHECK_F32(lse);
   TORCH_CHECK(qkv.numel() >= nseq * T * 3 * D && out.numel() >= nseq * T * D, "attention: qkv/out too small");
   TORCH_CHECK(lse.numel() >= nseq * heads * 64, "attention: lse must hold nseq*heads*64");
   if (bwd) {
-    TORCH_CHECK(has(dout) && has(dqkv), "attention backward needs dout and dqkv");
-    TORCH_CHECK(dout->numel() >= nseq * T * D && dqkv->numel() >= nseq * T * 3 * D, "attention: grads too small");
+    TORCH_CHECK(has(dqkv) && (has(dout) || (has(dx1) && has(wot))),
+                "attention backward needs dqkv and dout (or dx1 + wot: the fused output-projection gradient)");
+    TORCH_CHECK(dqkv->numel() >= nseq * T * 3 * D, "attention: dqkv too small");
+    if (has(dout)) TORCH_CHECK(dout->numel() >= nseq * T * D, "attention: dout too small");
+    if (has(dx1)) {
+      CHECK_GPU(*dx1, at::kBFloat16);
+      CHECK_GPU(*wot, at::kBFloat16);
+      TORCH_CHECK(dx1->numel() >= nseq * T * D && wot->numel() >= D * D, "attention: dx1 / wot too small");
+    }
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   const int rc = mta_attention(bwd ? 1 : 0, qkv.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
                                opt_typed<void>(dout, at::kBFloat16, "dout"), opt_typed<void>(dqkv, at::kBFloat16, "dqkv"),
                                (int)nseq, (int)T, (int)D, (int)heads, (float)rope_base,
-                               rope_table(qkv.device(), T, D / heads, rope_base), cur_stream());
+                               rope_table(qkv.device(), T, D / heads, rope_base),
+                               has(dx1) ? dx1->data_ptr() : nullptr, has(wot) ? wot->data_ptr() : nullptr,
+                               cur_stream());
   TORCH_CHECK(rc == 0, "attention: unsupported configuration (T=", T, ", D=", D, ", heads=", heads, ", rc=", rc, ")");
 }
 
@@ -1267,7 +1301,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
   m.def("norm", &norm);
-  m.def("attention", &attention);
+  m.def("tr_attn_dx", &tr_attn_dx);
+  m.def("attention", &attention, py::arg("bwd"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("dout"),
+        py::arg("dqkv"), py::arg("nseq"), py::arg("T"), py::arg("D"), py::arg("heads"), py::arg("rope_base"),
+        py::arg("dx1") = py::none(), py::arg("wot") = py::none());
   m.def("lstm_fwd_layer", &lstm_fwd_layer);
   m.def("lstm_bwd_layer", &lstm_bwd_layer);
   m.def("lstm_wgrad", &lstm_wgrad);

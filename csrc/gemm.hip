@@ -882,7 +882,9 @@ __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void ge
 // together (mta_gemm_group_flush: one launch per operand layout), their tiles x k-splits fill the chip with several
 // workgroups per CU, whose k-step latencies then overlap instead of adding up.
 constexpr int GROUP_MAX = 16;   // problems per launch (the table travels in the kernel arguments: < 4 KB)
-constexpr int GROUP_WGS = 1024;  // workgroup target of one grouped launch (4 per CU)
+// workgroup target of one grouped launch: 2 per CU.  The transformer B=1 set (17 problems, K = 6,272) on both launches:
+// 74.8 us at 512, 80.6 at 1,024, 94.8 at 2,048, 108.5 at 256; 128 x 128 tiles 93-148 us (profiles/r5_wgrad_group_sweep.jsonl)
+constexpr int GROUP_WGS = 512;
 struct GroupTable {
   GemmArgs g[GROUP_MAX];
   int start[GROUP_MAX + 1];  // first block of each problem; start[n] = grid size
@@ -890,15 +892,15 @@ struct GroupTable {
   int n;
 };
 static_assert(sizeof(GroupTable) < 4000, "kernel arguments");
-template <bool T>  // T: both operands stored [K][rows] (dY^T X); else both k-contiguous
+template <int BM, int BN, int BKT, bool T>  // T: both operands stored [K][rows] (dY^T X); else both k-contiguous
 __global__ __launch_bounds__(GT) __attribute__((amdgpu_waves_per_eu(2))) void gemm_group_kernel(GroupTable t) {
-  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<64, 64, 128>()];
+  __shared__ __attribute__((aligned(16))) __bf16 smem[gemm_lds_elems<BM, BN, BKT>()];
   int b = xcd_remap(blockIdx.x, t.start[t.n]);
   int p = 0;
   while (p + 1 < t.n && b >= t.start[p + 1]) ++p;
   b -= t.start[p];
   const int nx = t.nx[p], ny = t.ny[p];
-  gemm_body<64, 64, 128, T, T>(t.g[p], b % nx, (b / nx) % ny, b / (nx * ny), t.nz[p], smem, smem + 64 * (128 + 8));
+  gemm_body<BM, BN, BKT, T, T>(t.g[p], b % nx, (b / nx) % ny, b / (nx * ny), t.nz[p], smem, smem + BM * (BKT + 8));
 }
 
 template <int BM, int BN, int BKT, bool AT, bool BT>
@@ -1248,8 +1250,8 @@ void launch_group(int kind, int first, int count, hipStream_t st) {
   }
   t.n = count;
   t.start[count] = blocks;
-  if (kind) gemm_group_kernel<true><<<blocks, GT, 0, st>>>(t);
-  else gemm_group_kernel<false><<<blocks, GT, 0, st>>>(t);
+  if (kind) gemm_group_kernel<64, 64, 128, true><<<blocks, GT, 0, st>>>(t);
+  else gemm_group_kernel<64, 64, 128, false><<<blocks, GT, 0, st>>>(t);
 }
 
 }  // namespace

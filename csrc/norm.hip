@@ -752,6 +752,28 @@ extern "C" void mta_norm_flush() {
   deferred.n = 0;
 }
 
+// A deferred dgamma / dbeta reduction slot for a kernel outside this file (the transformer's fused attention-half
+// backward, csrc/tr_attn.hip): queues the job for mta_norm_flush (the same block-ordered, bit-reproducible sums) and
+// returns the base of its partial rows: row b of pass p at base + p * (*pass) + b * (*ld).  Null when D or blocks
+// exceed the slots.
+extern "C" float* mta_norm_defer_slot(float* dgamma, float* dbeta, int D, int blocks, hipStream_t st, int* ld,
+                                      long* pass) {
+  if (D > NORM_DEFER_D || blocks < 1 || blocks > NORM_BWD_MAX_BLOCKS) return nullptr;
+  if (deferred.n == NORM_DEFER_SLOTS || (deferred.n && deferred.st != st)) mta_norm_flush();
+  static float* base = [] {
+    float* p = nullptr;
+    (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_part_slots));
+    return p;
+  }();
+  float* part = base + (long)deferred.n * 2 * NORM_BWD_MAX_BLOCKS * NORM_DEFER_D;
+  *ld = NORM_DEFER_D;
+  *pass = (long)NORM_BWD_MAX_BLOCKS * NORM_DEFER_D;
+  deferred.batch.job[deferred.n] = ReduceJob{part, dgamma, dbeta, D, blocks, *ld, *pass};
+  deferred.st = st;
+  ++deferred.n;
+  return part;
+}
+
 extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps,
                         const float* gamma, const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd,
                         const uint64_t* seed, float drop_p, const void* dy, int dy_bf16, const float* dres,

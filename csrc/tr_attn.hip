@@ -267,6 +267,131 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
   }
 }
 
+// ---- backward tail of the attention half: d(xn) = dqkv Wqkv, then RMSNorm1 backward + residual ----
+// dX = dX1 + rs (g1 o dxn - xhat mean(g1 o dxn o xhat)), xhat = x rs; dg1 += sum over rows of dxn o xhat.  The
+// unfused chain was the input-gradient GEMM (6272 x 128 x 384, ~8.5 us) and the one-wave-per-row norm backward
+// (~5.7 us).  One 512-thread workgroup per 64-row tile (grid-strided): the dqkv tile, x and dX1 rows are staged
+// through LDS by 16-B loads; wave w owns output features 16 w .. 16 w + 15 (Wqkv^T B fragments in registers from a
+// fragment-major image, K = 384); the row statistic crosses the 8 waves once through LDS; dX leaves row-contiguous
+// (fp32 and bf16); the dg1 partial row of each workgroup goes to a deferred norm slot (block-ordered sums).
+constexpr int DQLD = AQ + 8;    // bf16 [64][384] dqkv tile
+constexpr int XRLD = AD + 4;    // fp32 [64][128] rows
+struct AttnDxSmem {
+  __bf16 dq[AT * DQLD];
+  float x[AT * XRLD];           // x rows, then dX rows (in place)
+  float dr[AT * XRLD];          // dX1 rows
+  float red[8][AT];             // per-wave row partials of sum(g1 dxn xhat)
+  float rs[AT];
+};
+
+struct AttnDxArgs {
+  const __bf16* dqkv;   // [M][384]
+  const __bf16* wqkvt;  // Wqkv^T fragment-major ([128][384])
+  const float* x;       // [M][128] block input (RMSNorm1 input)
+  const float* r1;      // [M] saved rstd
+  const float* g1;      // [128]
+  const float* dx1;     // [M][128] residual-stream gradient after the FFN half
+  float* dx;            // [M][128] out, fp32
+  __bf16* dxb;          // [M][128] out, bf16
+  float* part;          // dg1 partial rows ([gridDim.x][part_ld])
+  int part_ld;
+  int M;
+};
+
+__global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  AttnDxSmem& s = *reinterpret_cast<AttnDxSmem*>(smem_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rq = 4 * (lane >> 4), col = lane & 15;
+  const int c = 16 * wave + col;  // this lane's output feature
+  bf16x8 bw[AQ / 32];
+#pragma unroll
+  for (int ks = 0; ks < AQ / 32; ++ks) bw[ks] = wfrag(a.wqkvt, AQ, 16 * wave, 32 * ks, lane);
+  const float gc = a.g1[c];
+  float dg = 0.f;  // this lane's share of dg1[c] (rows 4 (lane >> 4) + r of every tile)
+  const int ntiles = (a.M + AT - 1) / AT;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const size_t row0 = (size_t)tile * AT;
+    // stage: dqkv [64][384] bf16 (3,072 16-B pieces), x and dX1 [64][128] fp32 (2,048 16-B pieces each)
+#pragma unroll
+    for (int i = 0; i < AT * (AQ / 8) / ATH; ++i) {
+      const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (row0 + r < (size_t)a.M) v = *reinterpret_cast<const uint4*>(a.dqkv + (row0 + r) * AQ + 8 * c8);
+      *reinterpret_cast<uint4*>(&s.dq[r * DQLD + 8 * c8]) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
+      const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
+      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
+      if (row0 + r < (size_t)a.M) {
+        xv = *reinterpret_cast<const float4*>(a.x + (row0 + r) * AD + 4 * c4);
+        dv = *reinterpret_cast<const float4*>(a.dx1 + (row0 + r) * AD + 4 * c4);
+      }
+      *reinterpret_cast<float4*>(&s.x[r * XRLD + 4 * c4]) = xv;
+      *reinterpret_cast<float4*>(&s.dr[r * XRLD + 4 * c4]) = dv;
+    }
+    if (tid < AT) s.rs[tid] = row0 + tid < (size_t)a.M ? a.r1[row0 + tid] : 0.f;
+    __syncthreads();
+    // dxn tile: 64 rows x this wave's 16 features, K = 384
+    f32x4 acc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
+                    f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < AQ / 32; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x16x32(lfrag(s.dq, DQLD, 16 * mt, 32 * ks, lane), bw[ks], acc[mt]);
+    // g = g1 o dxn, xhat = x rs; per-row partial of sum(g xhat) over this wave's 16 features
+    float gg[4][4], xh[4][4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + rq + r;
+        xh[mt][r] = s.x[t * XRLD + c] * s.rs[t];
+        gg[mt][r] = acc[mt][r] * gc;
+        dg = fmaf(acc[mt][r], xh[mt][r], dg);
+        float p = gg[mt][r] * xh[mt][r];
+        p += __shfl_xor(p, 1, 64);
+        p += __shfl_xor(p, 2, 64);
+        p += __shfl_xor(p, 4, 64);
+        p += __shfl_xor(p, 8, 64);
+        if (col == 0) s.red[wave][t] = p;
+      }
+    __syncthreads();  // red complete; every wave's reads of s.x done above
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * mt + rq + r;
+        float s2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) s2 += s.red[w][t];
+        s2 *= 1.0f / AD;
+        s.x[t * XRLD + c] = s.rs[t] * (gg[mt][r] - xh[mt][r] * s2) + s.dr[t * XRLD + c];
+      }
+    __syncthreads();
+    // dX rows out: fp32 and bf16, 16-B / 8-B pieces
+#pragma unroll
+    for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
+      const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
+      if (row0 + r >= (size_t)a.M) continue;
+      const float4 v = *reinterpret_cast<const float4*>(&s.x[r * XRLD + 4 * c4]);
+      *reinterpret_cast<float4*>(a.dx + (row0 + r) * AD + 4 * c4) = v;
+      bf16x4 b;
+      b[0] = (__bf16)v.x;
+      b[1] = (__bf16)v.y;
+      b[2] = (__bf16)v.z;
+      b[3] = (__bf16)v.w;
+      *reinterpret_cast<bf16x4*>(a.dxb + (row0 + r) * AD + 4 * c4) = b;
+    }
+    __syncthreads();  // staging free for the next tile
+  }
+  // dg1 partial row of this workgroup: sum over the 4 row groups of each column, fixed order
+  dg += __shfl_xor(dg, 16, 64);
+  dg += __shfl_xor(dg, 32, 64);
+  if (lane < 16) a.part[(size_t)blockIdx.x * a.part_ld + c] = dg;
+}
+
 }  // namespace
 
 extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo,
@@ -298,5 +423,37 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   // profiles/r4_bench_transformer_attn_split_ab.jsonl)
   a.split = T > 32 ? 1 : 0;
   tr_attn_fwd_kernel<<<nseq * (a.split ? 2 : 1), ATH, sizeof(AttnFwdSmem), st>>>(a);
+  return 0;
+}
+
+// d(xn) = dqkv Wqkv and the RMSNorm1 backward with the residual gradient (see tr_attn_dx_kernel); dg1 into a deferred
+// norm slot (mta_norm_flush sums it).  Returns non-zero on an unsupported shape.
+extern "C" float* mta_norm_defer_slot(float* dgamma, float* dbeta, int D, int blocks, hipStream_t st, int* ld,
+                                      long* pass);
+extern "C" int mta_tr_attn_dx(int M, const void* dqkv, const void* wqkvt, const float* x, const float* r1,
+                              const float* g1, const float* dx1, float* dx, void* dxb, float* dg1, hipStream_t st) {
+  if (M < 1) return 1;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_attn_dx_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)sizeof(AttnDxSmem)) == hipSuccess;
+  if (!attr) return 2;
+  const int tiles = (M + AT - 1) / AT;
+  const int grid = tiles < 512 ? tiles : 512;
+  AttnDxArgs a{};
+  int ld = 0;
+  long pass = 0;
+  a.part = mta_norm_defer_slot(dg1, nullptr, AD, grid, st, &ld, &pass);
+  if (!a.part) return 3;
+  a.dqkv = static_cast<const __bf16*>(dqkv);
+  a.wqkvt = static_cast<const __bf16*>(wqkvt);
+  a.x = x;
+  a.r1 = r1;
+  a.g1 = g1;
+  a.dx1 = dx1;
+  a.dx = dx;
+  a.dxb = static_cast<__bf16*>(dxb);
+  a.part_ld = ld;
+  a.M = M;
+  tr_attn_dx_kernel<<<grid, ATH, sizeof(AttnDxSmem), st>>>(a);
   return 0;
 }

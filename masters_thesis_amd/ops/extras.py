@@ -469,7 +469,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
         stats: List[Tensor] = []
         attn = _tr_attn_ok(d, heads, T)
         # fragment-major weight images of the fused halves, one packing launch: per layer the FFN's W1, W2 (forward)
-        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (its unfused backward keeps the casts)
+        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (forward), W_o^T (the backward's dO = dX1 W_o,
+        # fused into the attention backward) and W_qkv^T (its d(xn) = dqkv W_qkv, fused into the RMSNorm1 backward)
         frag, afrag = None, None
         srcs, dsts, trs = [], [], []
         if ffn:
@@ -480,10 +481,10 @@ class _TransformerEncoderFn(torch.autograd.Function):
                 dsts += [frag[l, 0], frag[l, 1], frag[l, 2], frag[l, 3]]
                 trs += [False, False, True, True]
         if attn:
-            afrag = [torch.empty_like(mats_b[1 + 4 * l + j]) for l in range(L) for j in (0, 1)]
-            srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1)]
+            afrag = [torch.empty_like(mats_b[1 + 4 * l + j]) for l in range(L) for j in (0, 1, 1, 0)]
+            srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1, 1, 0)]
             dsts += afrag
-            trs += [False] * len(afrag)
+            trs += [False, False, True, True] * L
         for i in range(0, len(srcs), 32):
             C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32])
         nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
@@ -500,7 +501,8 @@ class _TransformerEncoderFn(torch.autograd.Function):
             lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
             x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             if attn:
-                C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, afrag[2 * l], afrag[2 * l + 1], g1, bqkv, bo, xn, r1, qkv, o, lse, x1)
+                C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, afrag[4 * l], afrag[4 * l + 1], g1, bqkv, bo, xn, r1, qkv,
+                              o, lse, x1)
             else:
                 C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
                        None, None, None, None)
@@ -534,7 +536,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
         saved.append(xs)
         stats.append(rf)
         ctx.meta = (N, Np, T, F, Fp, d, L, heads, drop, float(dropout), ffn, nn)
-        ctx.params, ctx.mats_b, ctx.seeds, ctx.frag = params, mats_b, seeds, frag
+        ctx.params, ctx.mats_b, ctx.seeds, ctx.frag, ctx.afrag = params, mats_b, seeds, frag, afrag
         if need_grad:
             ctx.save_for_backward(*saved)
             ctx.stats = stats
@@ -544,6 +546,7 @@ class _TransformerEncoderFn(torch.autograd.Function):
     @torch.autograd.function.once_differentiable
     def backward(ctx, dh):
         N, Np, T, F, Fp, d, L, heads, drop, p, ffn, nn = ctx.meta
+        afrag = ctx.afrag  # fused attention half: W_o^T / W_qkv^T images for its fused backward GEMMs
         params, mats_b = ctx.params, ctx.mats_b
         saved = ctx.saved_tensors
         stats = ctx.stats
@@ -617,23 +620,30 @@ class _TransformerEncoderFn(torch.autograd.Function):
             # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
             gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
                  ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), group=True)
-            do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-            gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
-            # attention backward (RoPE inverse fused) -> dqkv
+            # attention backward (RoPE inverse fused) -> dqkv; d(o) = dX1 Wo inside it (fused half) or a GEMM before it
             dqkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
-            C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
+            if afrag is not None:
+                C.attention(True, qkv, o, lse, None, dqkv, Np, T, d, heads, ROPE_BASE, dX1b, afrag[4 * l + 2])
+            else:
+                do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
+                C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
             # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
             gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
                  ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), group=True)
             keep += [dX1b, dqkv]
-            dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
-            gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
-            # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
             dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
             dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)  # fresh: the queued dW2 may read the last one
-            C.norm_defer()
-            C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None, dXb,
-                   dXn, _grad_view(g1), None)
+            if afrag is not None:
+                # d(xn) = dqkv Wqkv and the RMSNorm1 backward + residual in one launch (dg1: deferred norm slot)
+                C.tr_attn_dx(dqkv, afrag[4 * l + 3], xs, r1, g1, dX1, dXn, dXb, _grad_view(g1))
+            else:
+                dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
+                gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
+                # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
+                C.norm_defer()
+                C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None,
+                       dXb, dXn, _grad_view(g1), None)
             dX = dXn
         # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
         gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,

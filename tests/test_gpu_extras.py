@@ -316,6 +316,42 @@ def test_transformer_encoder_matches_fp32_reference():
     _encoder_parity(FinancialTransformerMse, dict(hidden_size=128, num_layers=2, num_heads=4, dropout=0.0), 3e-2, 8e-2)
 
 
+@pytest.mark.parametrize("M", [6272, 2400 + 40])
+def test_tr_attn_dx_matches_reference(M):
+    """csrc/tr_attn.hip tr_attn_dx: d(xn) = dqkv Wqkv (Wqkv^T fragment-major image) and the RMSNorm1 backward with
+    the residual gradient, against fp32 PyTorch autograd of rms_norm on the same bf16 operands: dX (fp32 and bf16)
+    and dg1 (summed from the deferred norm slot at norm_flush).  M = 2,440: a partial last 64-row tile."""
+    import torch.nn.functional as Fn
+
+    from masters_thesis_amd.ops._lib import lib
+
+    C = lib()
+    torch.manual_seed(11)
+    dqkv = _bf(torch.randn(M, 384) * 0.5)
+    wqkv = torch.randn(384, 128, device=DEV) * 0.05
+    x = torch.randn(M, 128, device=DEV)
+    g1 = 1.0 + 0.1 * torch.randn(128, device=DEV)
+    dx1 = torch.randn(M, 128, device=DEV)
+    r1 = torch.rsqrt(x.pow(2).mean(-1) + 1e-6)
+    wt = torch.empty(128, 384, device=DEV, dtype=torch.bfloat16)
+    C.frag_pack([wqkv], [wt], [True])
+    dx = torch.empty(M, 128, device=DEV)
+    dxb = torch.empty(M, 128, device=DEV, dtype=torch.bfloat16)
+    dg = torch.full((128,), 0.5, device=DEV)
+    C.tr_attn_dx(dqkv, wt, x, r1, g1, dx1, dx, dxb, dg)
+    C.norm_flush()
+    torch.cuda.synchronize()
+    dxn = dqkv.float() @ wqkv.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    gr = g1.clone().requires_grad_(True)
+    y = Fn.rms_norm(xr, (128,), gr, 1e-6)
+    y.backward(dxn)
+    ref = xr.grad + dx1
+    assert _rel(dx, ref) < 1e-4
+    assert _rel(dxb.float(), ref) < 1e-2
+    assert _rel(dg - 0.5, gr.grad) < 1e-4
+
+
 @pytest.mark.parametrize("dropout,N,T", [(0.0, 100, 60), (0.2, 37, 60), (0.0, 20, 33)])
 def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
     """csrc/tr_ffn.hip (the FFN half of every block in one launch forward and one backward, plus split-K weight
@@ -347,7 +383,14 @@ def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
             seeds = seeds0.clone()
             h = X.transformer_encode(x, params, seeds, 2, 4, dropout, True)
             g = torch.randn(h.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
-            h.backward(g)
+            # the fused attention half's backward: dO = dX1 Wo inside the attention backward, d(xn) = dqkv Wqkv with
+            # the RMSNorm1 backward in tr_attn_dx; every weight gradient in the grouped launches
+            with torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA]) as prof:
+                h.backward(g)
+                torch.cuda.synchronize()
+            names = {e.key for e in prof.key_averages()}
+            assert any("tr_attn_dx_kernel" in n for n in names) == fused, sorted(names)
+            assert any("gemm_group_kernel" in n for n in names), sorted(names)
             outs.append(h.detach().clone())
             grads.append([p.grad.detach().clone() for p in params])
     finally:
