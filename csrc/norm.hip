@@ -171,62 +171,80 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
 // one thread, so the backward's dgamma/dbeta partials stay in registers and leave as one plain row per block.
 template <int VPT>
 __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
-  __shared__ float red[2][4];
+  // grid-strided rows (~4 workgroups per CU): gamma / beta loaded once per workgroup instead of once per row, and
+  // the next row's loads issued before the current row's reductions (one HBM round trip per row hidden)
+  __shared__ float red[2][2][4];  // [row parity][mean / var][wave]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row = blockIdx.x;
   const float invD = 1.0f / (float)a.D;
-  float4 v[VPT], gm[VPT], bt[VPT];
+  float4 gm[VPT], bt[VPT], v[VPT], vn[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     const bool ok = c < a.D;
-    v[i] = ok ? ld4(a.x, a.xb, (size_t)row * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     gm[i] = (ok && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     bt[i] = (ok && a.beta) ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   const uint64_t seed = a.seed ? *a.seed : 0ull;
-  float s = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-  s = wave_sum(s);
-  if (lane == 0) red[0][wave] = s;
-  __syncthreads();
-  const float mu = a.rms ? 0.f : ((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * invD;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    if (4 * (tid + NT_THREADS * i) < a.D) {
-      const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
-      q += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-    }
-  }
-  q = wave_sum(q);
-  if (lane == 0) red[1][wave] = q;
-  __syncthreads();
-  const float rs = rsqrtf(((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * invD + a.eps);
-  if (tid == 0) {
-    if (a.mean) a.mean[row] = mu;
-    a.rstd[row] = rs;
-  }
+  int row = blockIdx.x;
+  if (row >= a.M) return;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
-    if (c >= a.D) continue;
-    const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-    const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w}, bs[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
-    float o[4];
+    v[i] = c < a.D ? ld4(a.x, a.xb, (size_t)row * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int it = 0; row < a.M; row += gridDim.x, ++it) {
+    const int nrow = row + (int)gridDim.x < a.M ? row + (int)gridDim.x : row;  // clamped: the load is unconditional
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] = (xs[j] - mu) * rs * gs[j] + bs[j];
-      if (a.seed) o[j] *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+    for (int i = 0; i < VPT; ++i) {
+      const int c = 4 * (tid + NT_THREADS * i);
+      vn[i] = c < a.D ? ld4(a.x, a.xb, (size_t)nrow * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
-    if (a.y_bf16) {
-      bf16x4 b;
+    const int par = it & 1;
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
-      *reinterpret_cast<bf16x4*>(a.y_bf16 + (size_t)row * a.D + c) = b;
+    for (int i = 0; i < VPT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    s = wave_sum(s);
+    if (lane == 0) red[par][0][wave] = s;
+    __syncthreads();
+    const float mu = a.rms ? 0.f : ((red[par][0][0] + red[par][0][1]) + (red[par][0][2] + red[par][0][3])) * invD;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      if (4 * (tid + NT_THREADS * i) < a.D) {
+        const float d0 = v[i].x - mu, d1 = v[i].y - mu, d2 = v[i].z - mu, d3 = v[i].w - mu;
+        q += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+      }
     }
+    q = wave_sum(q);
+    if (lane == 0) red[par][1][wave] = q;
+    __syncthreads();
+    const float rs = rsqrtf(((red[par][1][0] + red[par][1][1]) + (red[par][1][2] + red[par][1][3])) * invD + a.eps);
+    if (tid == 0) {
+      if (a.mean) a.mean[row] = mu;
+      a.rstd[row] = rs;
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = 4 * (tid + NT_THREADS * i);
+      if (c >= a.D) continue;
+      const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+      const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w}, bs[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = (xs[j] - mu) * rs * gs[j] + bs[j];
+        if (a.seed) o[j] *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+      }
+      if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
+      if (a.y_bf16) {
+        bf16x4 b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
+        *reinterpret_cast<bf16x4*>(a.y_bf16 + (size_t)row * a.D + c) = b;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) v[i] = vn[i];
   }
 }
 
@@ -483,6 +501,8 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
 // the wide backward: ~2 workgroups per CU, each a contiguous row range with two rows in flight (fewer, longer
 // blocks: half the dgamma / dbeta partial rows of the r3 grid of 1024)
 constexpr int NORM_BWD_WIDE_BLOCKS = 512;
+// the wide forward's grid: ~4 workgroups per CU, each striding over rows with the next row in flight
+constexpr int NORM_FWD_WIDE_BLOCKS = 1024;
 // the one-wave-per-row backward's grid cap: transformer B=1 (M = 6,272 rows, D = 128) 0.714 ms at 512, 0.702 at
 // 1024, 0.711 at 1,568 (one row per wave: the partial-row reduce grows) (profiles/r2_norm_bwd_cap_ab.txt)
 constexpr int NORM_BWD_NARROW_BLOCKS = 1024;
@@ -818,7 +838,7 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     if (rows_per_block < 2) rows_per_block = 2;
     blocks = (M + rows_per_block - 1) / rows_per_block;
   } else if (wide) {
-    blocks = M;
+    blocks = M < NORM_FWD_WIDE_BLOCKS ? M : NORM_FWD_WIDE_BLOCKS;
   }
   // deferred slot when the caller asked for it (dgamma pointer tagged by mta_norm_defer) and D fits
   const bool defer = bwd && (dgamma || dbeta) && defer_next && D <= NORM_DEFER_D;

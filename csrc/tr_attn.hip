@@ -274,14 +274,15 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 // through LDS by 16-B loads; wave w owns output features 16 w .. 16 w + 15 (Wqkv^T B fragments in registers from a
 // fragment-major image, K = 384); the row statistic crosses the 8 waves once through LDS; dX leaves row-contiguous
 // (fp32 and bf16); the dg1 partial row of each workgroup goes to a deferred norm slot (block-ordered sums).
-constexpr int DQLD = AQ + 8;    // bf16 [64][384] dqkv tile
-constexpr int XRLD = AD + 4;    // fp32 [64][128] rows
+constexpr int DXR = 32;         // rows per tile: 196 workgroups at the B=1 shape (64-row tiles: 98, 14.4 us)
+constexpr int DQLD = AQ + 8;    // bf16 [32][384] dqkv tile
+constexpr int XRLD = AD + 4;    // fp32 [32][128] rows
 struct AttnDxSmem {
-  __bf16 dq[AT * DQLD];
-  float x[AT * XRLD];           // x rows, then dX rows (in place)
-  float dr[AT * XRLD];          // dX1 rows
-  float red[8][AT];             // per-wave row partials of sum(g1 dxn xhat)
-  float rs[AT];
+  __bf16 dq[DXR * DQLD];
+  float x[DXR * XRLD];          // x rows, then dX rows (in place)
+  float dr[DXR * XRLD];         // dX1 rows
+  float red[8][DXR];            // per-wave row partials of sum(g1 dxn xhat)
+  float rs[DXR];
 };
 
 struct AttnDxArgs {
@@ -309,19 +310,19 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
   for (int ks = 0; ks < AQ / 32; ++ks) bw[ks] = wfrag(a.wqkvt, AQ, 16 * wave, 32 * ks, lane);
   const float gc = a.g1[c];
   float dg = 0.f;  // this lane's share of dg1[c] (rows 4 (lane >> 4) + r of every tile)
-  const int ntiles = (a.M + AT - 1) / AT;
+  const int ntiles = (a.M + DXR - 1) / DXR;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const size_t row0 = (size_t)tile * AT;
+    const size_t row0 = (size_t)tile * DXR;
     // stage: dqkv [64][384] bf16 (3,072 16-B pieces), x and dX1 [64][128] fp32 (2,048 16-B pieces each)
 #pragma unroll
-    for (int i = 0; i < AT * (AQ / 8) / ATH; ++i) {
+    for (int i = 0; i < DXR * (AQ / 8) / ATH; ++i) {
       const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (row0 + r < (size_t)a.M) v = *reinterpret_cast<const uint4*>(a.dqkv + (row0 + r) * AQ + 8 * c8);
       *reinterpret_cast<uint4*>(&s.dq[r * DQLD + 8 * c8]) = v;
     }
 #pragma unroll
-    for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
+    for (int i = 0; i < DXR * (AD / 4) / ATH; ++i) {
       const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
       float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
       if (row0 + r < (size_t)a.M) {
@@ -331,19 +332,21 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
       *reinterpret_cast<float4*>(&s.x[r * XRLD + 4 * c4]) = xv;
       *reinterpret_cast<float4*>(&s.dr[r * XRLD + 4 * c4]) = dv;
     }
-    if (tid < AT) s.rs[tid] = row0 + tid < (size_t)a.M ? a.r1[row0 + tid] : 0.f;
+    if (tid < DXR) s.rs[tid] = row0 + tid < (size_t)a.M ? a.r1[row0 + tid] : 0.f;
     __syncthreads();
-    // dxn tile: 64 rows x this wave's 16 features, K = 384
-    f32x4 acc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},
-                    f32x4{0.f, 0.f, 0.f, 0.f}};
+    // dxn tile: 32 rows x this wave's 16 features, K = 384
+    constexpr int MT = DXR / 16;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < AQ / 32; ++ks)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = mfma16x16x32(lfrag(s.dq, DQLD, 16 * mt, 32 * ks, lane), bw[ks], acc[mt]);
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma16x16x32(lfrag(s.dq, DQLD, 16 * mt, 32 * ks, lane), bw[ks], acc[mt]);
     // g = g1 o dxn, xhat = x rs; per-row partial of sum(g xhat) over this wave's 16 features
-    float gg[4][4], xh[4][4];
+    float gg[MT][4], xh[MT][4];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = 16 * mt + rq + r;
@@ -359,7 +362,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
       }
     __syncthreads();  // red complete; every wave's reads of s.x done above
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int t = 16 * mt + rq + r;
@@ -372,7 +375,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
     __syncthreads();
     // dX rows out: fp32 and bf16, 16-B / 8-B pieces
 #pragma unroll
-    for (int i = 0; i < AT * (AD / 4) / ATH; ++i) {
+    for (int i = 0; i < DXR * (AD / 4) / ATH; ++i) {
       const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
       if (row0 + r >= (size_t)a.M) continue;
       const float4 v = *reinterpret_cast<const float4*>(&s.x[r * XRLD + 4 * c4]);
@@ -437,8 +440,8 @@ extern "C" int mta_tr_attn_dx(int M, const void* dqkv, const void* wqkvt, const 
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)sizeof(AttnDxSmem)) == hipSuccess;
   if (!attr) return 2;
-  const int tiles = (M + AT - 1) / AT;
-  const int grid = tiles < 512 ? tiles : 512;
+  const int tiles = (M + DXR - 1) / DXR;
+  const int grid = tiles < 1024 ? tiles : 1024;
   AttnDxArgs a{};
   int ld = 0;
   long pass = 0;
