@@ -88,12 +88,15 @@ int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, c
                const void* prein, void* dpre, float* dx1, void* dx1b, float* dg2, void* uT, void* xn2T, void* dpreT,
                void* dxT, hipStream_t st);
 int mta_frag_pack(int count, const float* const* src, void* const* dst, const int* n, const int* k, const int* tr,
+                  int ncast, const float* const* csrc, void* const* cdst, const int* crows, const int* ccols,
+                  const int* crows_p, const int* ccols_p, const int* cld, uint64_t* seeds, int nseeds,
                   hipStream_t st);
 int mta_tr_attn_dx(int M, const void* dqkv, const void* wqkvt, const float* x, const float* r1, const float* g1,
                    const float* dx1, float* dx, void* dxb, float* dg1, hipStream_t st);
 int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo, const float* g1,
                     const float* bqkv, const float* bo, const float* rope, float eps, void* xn, float* r1, void* qkv,
-                    void* o, float* lse, float* x1, hipStream_t st);
+                    void* o, float* lse, float* x1, const float* in, const float* we, const float* be, int F, int rows_in,
+                    float* x_out, hipStream_t st);
 int mta_tr_transpose_bf16(int n, const void* const* src, void* const* dst, const int* rows, const int* cols,
                           hipStream_t st);
 int mta_attention(int bwd, const void* qkv, void* out, float* lse, const void* dout, void* dqkv, int nseq, int T,
@@ -653,10 +656,10 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
   TORCH_CHECK(rstd.numel() >= M, "rstd too small");
   if (!rms) TORCH_CHECK(has(mean) && mean->numel() >= M, "LayerNorm needs mean");
   if (bwd) TORCH_CHECK(has(dy), "norm backward needs dy");
-  for (const OptT* o : {&y_bf16, &y_f32, &dy, &pre, &dx_bf16}) {
+  for (const OptT* o : {&y_bf16, &y_f32, &dy, &pre}) {
     if (has(*o)) check_span(**o, M, D, D, "row tensor");
   }
-  for (const OptT* o : {&dres, &dx_f32}) {
+  for (const OptT* o : {&dres, &dx_f32, &dx_bf16}) {
     if (has(*o)) check_span(**o, M, ldx, D, "residual-stride tensor");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
@@ -761,9 +764,11 @@ void tr_ffn_bwd(at::Tensor x1, at::Tensor w1t, at::Tensor w2t, at::Tensor g2, at
 
 // fp32 matrices -> bf16 fragment-major [N][K] images (csrc/tr_ffn.hip): src [N][K], or with transposed[i] src [K][N]
 // and image(n, k) = src[k][n] -- the fused transformer halves' weights, every layer in one launch
-void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::vector<bool> transposed) {
+void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::vector<bool> transposed,
+               std::vector<at::Tensor> cast_src, std::vector<at::Tensor> cast_dst, const OptT& seeds) {
   TORCH_CHECK(!src.empty() && src.size() == dst.size() && src.size() == transposed.size() && src.size() <= 32,
               "frag_pack: 1..32 matrices");
+  TORCH_CHECK(cast_src.size() == cast_dst.size() && cast_src.size() <= 4, "frag_pack: at most 4 riding casts");
   std::vector<const float*> sp;
   std::vector<void*> dp;
   std::vector<int> n, k, tr;
@@ -777,8 +782,36 @@ void frag_pack(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, std::ve
     k.push_back((int)src[i].size(transposed[i] ? 0 : 1));
     tr.push_back(transposed[i] ? 1 : 0);
   }
+  // riding casts: the cast_pad contract (fp32 rows -> zero-padded bf16)
+  std::vector<const float*> csp;
+  std::vector<void*> cdp;
+  std::vector<int> rows, cols, rows_p, cols_p, ld;
+  for (size_t i = 0; i < cast_src.size(); ++i) {
+    auto s2 = cast_src[i].dim() == 1 ? cast_src[i].view({1, -1}) : cast_src[i];
+    auto d2 = cast_dst[i].dim() == 1 ? cast_dst[i].view({1, -1}) : cast_dst[i];
+    TORCH_CHECK(s2.dim() == 2 && d2.dim() == 2, "frag_pack casts: 1-D or 2-D tensors");
+    TORCH_CHECK(s2.is_cuda() && s2.scalar_type() == at::kFloat && s2.stride(1) == 1, "frag_pack casts: src fp32 rows");
+    CHECK_GPU(d2, at::kBFloat16);
+    TORCH_CHECK(d2.size(0) >= s2.size(0) && d2.size(1) >= s2.size(1), "frag_pack casts: dst smaller than src");
+    csp.push_back(s2.data_ptr<float>());
+    cdp.push_back(d2.data_ptr());
+    rows.push_back((int)s2.size(0));
+    cols.push_back((int)s2.size(1));
+    rows_p.push_back((int)d2.size(0));
+    cols_p.push_back((int)d2.size(1));
+    ld.push_back((int)s2.stride(0));
+  }
+  uint64_t* sd = nullptr;
+  int ns = 0;
+  if (seeds.has_value() && seeds->defined()) {
+    CHECK_GPU(*seeds, at::kLong);
+    sd = reinterpret_cast<uint64_t*>(seeds->data_ptr<int64_t>());
+    ns = (int)seeds->numel();
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dst[0].device());
-  const int rc = mta_frag_pack((int)sp.size(), sp.data(), dp.data(), n.data(), k.data(), tr.data(), cur_stream());
+  const int rc = mta_frag_pack((int)sp.size(), sp.data(), dp.data(), n.data(), k.data(), tr.data(), (int)csp.size(),
+                               csp.data(), cdp.data(), rows.data(), cols.data(), rows_p.data(), cols_p.data(),
+                               ld.data(), sd, ns, cur_stream());
   TORCH_CHECK(rc == 0, "frag_pack: N must be a multiple of 16 and K of 32 (rc=", rc, ")");
 }
 
@@ -807,8 +840,20 @@ void tr_attn_dx(at::Tensor dqkv, at::Tensor wqkvt, at::Tensor x, at::Tensor r1, 
 // fused attention half of a transformer block forward (csrc/tr_attn.hip): x -> xn, r1, qkv, o, lse, x1
 void tr_attn_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope_base, at::Tensor x, at::Tensor wqkv,
                  at::Tensor wo, at::Tensor g1, at::Tensor bqkv, at::Tensor bo, at::Tensor xn, at::Tensor r1,
-                 at::Tensor qkv, at::Tensor o, at::Tensor lse, at::Tensor x1) {
+                 at::Tensor qkv, at::Tensor o, at::Tensor lse, at::Tensor x1, const OptT& in, const OptT& we,
+                 const OptT& be) {
+  // in / we / be given: the block input x = in We^T + be is computed in the kernel (the embedding) and WRITTEN to x
   const int64_t d = x.size(-1), M = nseq * T;
+  const bool emb = has(in);
+  if (emb) {
+    TORCH_CHECK(has(we) && has(be), "tr_attn_fwd: the embedding needs in, we and be");
+    CHECK_F32(*in);
+    CHECK_F32(*we);
+    CHECK_F32(*be);
+    TORCH_CHECK(in->dim() == 2 && in->size(1) <= 8 && we->size(0) == d && we->size(1) == in->size(1) &&
+                    be->numel() == d && in->size(0) <= M,
+                "tr_attn_fwd: embedding shapes (in [rows][F <= 8], we [d][F], be [d])");
+  }
   for (auto* t : {&x, &r1, &lse, &x1, &g1, &bqkv, &bo}) {
     CHECK_F32(*t);
   }
@@ -825,7 +870,10 @@ void tr_attn_fwd(int64_t nseq, int64_t T, int64_t heads, double eps, double rope
                                  wo.data_ptr(), g1.data_ptr<float>(), bqkv.data_ptr<float>(), bo.data_ptr<float>(),
                                  rope_table(x.device(), T, d / heads, rope_base), (float)eps, xn.data_ptr(),
                                  r1.data_ptr<float>(), qkv.data_ptr(), o.data_ptr(), lse.data_ptr<float>(),
-                                 x1.data_ptr<float>(), cur_stream());
+                                 x1.data_ptr<float>(), emb ? in->data_ptr<float>() : nullptr,
+                                 emb ? we->data_ptr<float>() : nullptr, emb ? be->data_ptr<float>() : nullptr,
+                                 emb ? (int)in->size(1) : 0, emb ? (int)in->size(0) : 0,
+                                 emb ? x.data_ptr<float>() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "tr_attn_fwd: unsupported configuration (d=", d, ", heads=", heads, ", T=", T, ", rc=", rc, ")");
 }
 
@@ -1291,10 +1339,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     mta_zero_bytes(t.data_ptr(), (long)(t.numel() * t.element_size()), cur_stream());
   });
   m.def("tr_ffn_fwd", &tr_ffn_fwd);
-  m.def("frag_pack", &frag_pack);
+  m.def("frag_pack", &frag_pack, py::arg("src"), py::arg("dst"), py::arg("transposed"),
+        py::arg("cast_src") = std::vector<at::Tensor>{}, py::arg("cast_dst") = std::vector<at::Tensor>{},
+        py::arg("seeds") = py::none());
   m.def("tr_ffn_bwd", &tr_ffn_bwd);
   m.def("transpose_bf16", &transpose_bf16);
-  m.def("tr_attn_fwd", &tr_attn_fwd);
+  m.def("tr_attn_fwd", &tr_attn_fwd, py::arg("nseq"), py::arg("T"), py::arg("heads"), py::arg("eps"),
+        py::arg("rope_base"), py::arg("x"), py::arg("wqkv"), py::arg("wo"), py::arg("g1"), py::arg("bqkv"),
+        py::arg("bo"), py::arg("xn"), py::arg("r1"), py::arg("qkv"), py::arg("o"), py::arg("lse"), py::arg("x1"),
+        py::arg("in") = py::none(), py::arg("we") = py::none(), py::arg("be") = py::none());
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("gemm_group_flush", []() { mta_gemm_group_flush(); });

@@ -197,6 +197,21 @@ __device__ __forceinline__ uint32_t mta_pair_hash(uint32_t pseed, uint32_t pair,
 __device__ __forceinline__ bool mta_pair_keep(uint32_t hash, int e, float p) {
   return (float)((hash >> (16 * e)) & 0xFFFFu) * (1.0f / 65536.0f) >= p;
 }
+// Dropout scales (0 or 1/(1-p)) of the 4 consecutive columns c .. c+3 (c % 4 == 0) of one row: two lowbias32-style
+// hashes of (row, column pair) give the four 16-bit uniforms (p resolved to 1/65536) -- 2 quarter-rate integer
+// multiplies per element instead of mta_hash3's ~8, which made the wide LayerNorm forward VALU-bound.  The norm
+// kernels' dropout, forward and backward alike.
+__device__ __forceinline__ void mta_dropout_scale4(uint64_t seed, uint32_t row, uint32_t c, float p, float (&s)[4]) {
+  const uint32_t ps = mta_pair_seed(seed);
+  const uint32_t thr = (uint32_t)(p * 65536.f + 0.5f);
+  const float sc = 1.0f / (1.0f - p);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t x = mta_pair_hash(ps, row, mta_pair_col((c >> 1) + h));
+    s[2 * h] = (x & 0xFFFFu) >= thr ? sc : 0.f;
+    s[2 * h + 1] = (x >> 16) >= thr ? sc : 0.f;
+  }
+}
 // 0 or 1/(1-p)
 __device__ __forceinline__ float mta_dropout_scale(uint64_t seed, uint32_t row, uint32_t col, float p) {
   const float u = (float)(mta_hash3(seed, row, col) >> 8) * (1.0f / 16777216.0f);

@@ -10,6 +10,7 @@
 // One wave per row, VPL float4 per lane (D <= 256 * VPL), rows grid-strided over the workgroup's 4 waves so
 // the dgamma/dbeta partials stay in registers until one LDS reduction at the end.
 #include "common.h"
+#include "cast.h"
 
 #include <type_traits>
 
@@ -17,11 +18,6 @@ namespace {
 
 constexpr int NT_THREADS = 256;
 
-struct CastItem {
-  const float* src;
-  __bf16* dst;
-  int rows, cols, rows_p, cols_p, ld_src;
-};
 struct CastArgs {
   CastItem item[16];
   int n;
@@ -29,40 +25,10 @@ struct CastArgs {
   int nseeds;
 };
 
-// 8 consecutive columns per thread (16-B bf16 store; two 16-B loads when the source row allows), 32-bit index math;
-// rows past `rows` and columns past `cols` are written as zeros (the padded operand)
 __global__ void cast_pad_kernel(CastArgs a) {
   if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < a.nseeds)
     a.seeds[threadIdx.x] += 0x9E3779B97F4A7C15ull;  // fresh counter-hash seed per step for every dropout site
-  const CastItem it = a.item[blockIdx.y];
-  if ((it.cols_p & 7) == 0 && (long)it.rows_p * it.cols_p < (1L << 31)) {
-    const int c8 = it.cols_p >> 3;
-    const int total = it.rows_p * c8;
-    const bool vsrc = (it.ld_src & 3) == 0 && (((uintptr_t)it.src) & 15) == 0;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-      const int r = e / c8, c = (e - r * c8) * 8;
-      float v[8];
-      if (r < it.rows && vsrc && c + 8 <= it.cols) {
-        const float4 x0 = *reinterpret_cast<const float4*>(it.src + (size_t)r * it.ld_src + c);
-        const float4 x1 = *reinterpret_cast<const float4*>(it.src + (size_t)r * it.ld_src + c + 4);
-        v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = (r < it.rows && c + k < it.cols) ? it.src[(size_t)r * it.ld_src + c + k] : 0.f;
-      }
-      bf16x8 o;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) o[k] = (__bf16)v[k];
-      *reinterpret_cast<bf16x8*>(it.dst + (size_t)r * it.cols_p + c) = o;
-    }
-    return;
-  }
-  const long total = (long)it.rows_p * it.cols_p;
-  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(e / it.cols_p), c = (int)(e % it.cols_p);
-    const float v = (r < it.rows && c < it.cols) ? it.src[(size_t)r * it.ld_src + c] : 0.f;
-    it.dst[e] = (__bf16)v;
-  }
+  cast_item_run(a.item[blockIdx.y], blockIdx.x, gridDim.x);
 }
 
 struct NormArgs {
@@ -147,8 +113,10 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
       float o[4] = {(v[i].x - mu) * rs * gm[i].x + bt[i].x, (v[i].y - mu) * rs * gm[i].y + bt[i].y,
                     (v[i].z - mu) * rs * gm[i].z + bt[i].z, (v[i].w - mu) * rs * gm[i].w + bt[i].w};
       if (a.seed) {
+        float ds4[4];
+        mta_dropout_scale4(*a.seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] *= mta_dropout_scale(*a.seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+        for (int j = 0; j < 4; ++j) o[j] *= ds4[j];
       }
       if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.y_bf16) {
@@ -229,12 +197,10 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
       if (c >= a.D) continue;
       const float xs[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
       const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w}, bs[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
-      float o[4];
+      float o[4], ds4[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.seed) mta_dropout_scale4(seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o[j] = (xs[j] - mu) * rs * gs[j] + bs[j];
-        if (a.seed) o[j] *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
-      }
+      for (int j = 0; j < 4; ++j) o[j] = ((xs[j] - mu) * rs * gs[j] + bs[j]) * ds4[j];
       if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.y_bf16) {
         bf16x4 b;
@@ -312,10 +278,11 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, i
         const float xs[4] = {cur.x[i].x, cur.x[i].y, cur.x[i].z, cur.x[i].w};
         const float ds[4] = {cur.dy[i].x, cur.dy[i].y, cur.dy[i].z, cur.dy[i].w};
         const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+        float ds4[4] = {1.f, 1.f, 1.f, 1.f};
+        if (a.seed && ok) mta_dropout_scale4(seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float d = ds[j];
-          if (a.seed && ok) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+          float d = ds[j] * ds4[j];
           xh[i][j] = ok ? (xs[j] - cur.mu) * cur.rs : 0.f;
           db[i][j] += d;
           dg[i][j] += d * xh[i][j];
@@ -350,7 +317,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_kernel(NormArgs a, i
           bf16x4 b;
 #pragma unroll
           for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
-          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.ldx + c) = b;
         }
       }
     }
@@ -448,10 +415,11 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
         fast_f4<B16>(cur.x[i], xs);
         fast_f4<B16>(cur.dy[i], ds);
         const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+        float ds4[4] = {1.f, 1.f, 1.f, 1.f};
+        if (a.seed) mta_dropout_scale4(seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          float d = ds[j];
-          if (a.seed) d *= mta_dropout_scale(seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+          float d = ds[j] * ds4[j];
           xh[i][j] = (xs[j] - mu) * cur.rs;
           db[i][j] += d;
           dg[i][j] += d * xh[i][j];
@@ -481,7 +449,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
           bf16x4 b;
 #pragma unroll
           for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
-          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+          *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.ldx + c) = b;
         }
       }
     }
@@ -555,10 +523,11 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
       }
       const float xs[4] = {xv.x, xv.y, xv.z, xv.w}, ds[4] = {dv.x, dv.y, dv.z, dv.w};
       const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
+      float ds4[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.seed && c < a.D) mta_dropout_scale4(*a.seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float d = ds[j];
-        if (a.seed && c < a.D) d *= mta_dropout_scale(*a.seed, (uint32_t)row, (uint32_t)(c + j), a.drop_p);
+        float d = ds[j] * ds4[j];
         xh[i][j] = (xs[j] - mu) * rs;
         db[i][j] += d;
         dg[i][j] += d * xh[i][j];
@@ -596,7 +565,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_kernel(NormArgs a) {
         bf16x4 b;
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
-        *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.D + c) = b;
+        *reinterpret_cast<bf16x4*>(a.dx_bf16 + (size_t)row * a.ldx + c) = b;
       }
     }
   }

@@ -46,6 +46,13 @@ struct AttnFwdArgs {
   __bf16 *xn, *qkv, *o;
   float *r1, *lse, *x1;
   int split;  // 1: two workgroups per sequence, one per 32-query half (each recomputes the shared xn / k / v)
+  // first block: the embedding x = in We^T + be computed here from the fp32 input tokens instead of read (in null:
+  // x is read); x is then written to x_out (own rows) for the backward
+  const float* in;   // [rows_in][F] (rows past rows_in: zero tokens, the padded sequences)
+  const float* we;   // [128][F]
+  const float* be;   // [128]
+  int F, rows_in;
+  float* x_out;
 };
 
 // B fragment from a fragment-major weight image (csrc/tr_ffn.hip frag_pack: 16 x 32 blocks of 1 KB, lane l's 8
@@ -80,9 +87,33 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
   const int xr = tid >> 3, xc = 16 * (tid & 7);
   const bool rok = xr < T;
   float4 xv[4];
+  if (a.in) {
+    // embedding: 16 features x F inputs per thread (F = 3 for the financial windows)
+    float tok[8];
+    const size_t gr = grow0 + xr;
+    const bool tin = rok && gr < (size_t)a.rows_in;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
-    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x + (grow0 + xr) * AD + xc + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int f = 0; f < 8; ++f) tok[f] = (f < a.F && tin) ? a.in[gr * a.F + f] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float e[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int c = xc + 4 * i + kk;
+        float v = a.be[c];
+#pragma unroll
+        for (int f = 0; f < 8; ++f)
+          if (f < a.F) v = fmaf(tok[f], a.we[c * a.F + f], v);
+        e[kk] = rok ? v : 0.f;
+      }
+      xv[i] = make_float4(e[0], e[1], e[2], e[3]);
+      if (rok && own(xr)) *reinterpret_cast<float4*>(a.x_out + gr * AD + xc + 4 * i) = xv[i];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      xv[i] = rok ? *reinterpret_cast<const float4*>(a.x + (grow0 + xr) * AD + xc + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (tid < AD) {
     s.g1[tid] = a.g1[tid];
     s.bo[tid] = a.bo[tid];
@@ -399,8 +430,10 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
 
 extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x, const void* wqkv, const void* wo,
                                const float* g1, const float* bqkv, const float* bo, const float* rope, float eps,
-                               void* xn, float* r1, void* qkv, void* o, float* lse, float* x1, hipStream_t st) {
+                               void* xn, float* r1, void* qkv, void* o, float* lse, float* x1, const float* in,
+                               const float* we, const float* be, int F, int rows_in, float* x_out, hipStream_t st) {
   if (d != AD || heads != AHEADS || T < 1 || T > AT || !rope) return 1;
+  if (in && (F < 1 || F > 8 || !we || !be || !x_out)) return 3;
   static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_attn_fwd_kernel),
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)sizeof(AttnFwdSmem)) == hipSuccess;
@@ -421,6 +454,12 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   a.r1 = r1;
   a.lse = lse;
   a.x1 = x1;
+  a.in = in;
+  a.we = we;
+  a.be = be;
+  a.F = F;
+  a.rows_in = rows_in;
+  a.x_out = x_out;
   // two workgroups per sequence (query halves): 2 x 104 sequences still fit one wave of workgroups on the 256 CUs,
   // and each recomputes only the shared norm / K / V (18.9 -> 16.7 us per launch, transformer B=1 0.576 -> 0.565 ms,
   // profiles/r4_bench_transformer_attn_split_ab.jsonl)

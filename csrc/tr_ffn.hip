@@ -21,6 +21,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "cast.h"
 
 namespace {
 
@@ -640,12 +641,25 @@ extern "C" int mta_tr_transpose_bf16(int n, const void* const* src, void* const*
 // the fused attention half's W_qkv, W_o ----
 namespace {
 constexpr int FP_MAX = 32;
+constexpr int FP_CAST_MAX = 4;
 struct FragPackBatch {
   const float* src[FP_MAX];
   __bf16* dst[FP_MAX];
   int n[FP_MAX], k[FP_MAX], tr[FP_MAX];
+  int count;
+  // padded row-major casts riding along (the transformer's input tokens and embedding weight: the step's only other
+  // cast work once the fused halves read fragment-major images) and the dropout seeds to advance: one launch
+  CastItem cast[FP_CAST_MAX];
+  int ncast;
+  uint64_t* seeds;
+  int nseeds;
 };
 __global__ __launch_bounds__(256) void frag_pack_kernel(FragPackBatch b) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && (int)threadIdx.x < b.nseeds) b.seeds[threadIdx.x] += 0x9E3779B97F4A7C15ull;
+  if ((int)blockIdx.y >= b.count) {
+    cast_item_run(b.cast[blockIdx.y - b.count], blockIdx.x, gridDim.x);
+    return;
+  }
   const int mi = blockIdx.y, N = b.n[mi], K = b.k[mi];
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= N * K / 8) return;
@@ -668,10 +682,23 @@ __global__ __launch_bounds__(256) void frag_pack_kernel(FragPackBatch b) {
 }  // namespace
 
 extern "C" int mta_frag_pack(int count, const float* const* src, void* const* dst, const int* n, const int* k,
-                             const int* tr, hipStream_t st) {
-  if (count < 1 || count > FP_MAX) return 1;
+                             const int* tr, int ncast, const float* const* csrc, void* const* cdst, const int* crows,
+                             const int* ccols, const int* crows_p, const int* ccols_p, const int* cld,
+                             uint64_t* seeds, int nseeds, hipStream_t st) {
+  if (count < 1 || count > FP_MAX || ncast < 0 || ncast > FP_CAST_MAX || nseeds < 0 || nseeds > 256 ||
+      (nseeds && !seeds))
+    return 1;
   FragPackBatch b{};
+  b.count = count;
+  b.ncast = ncast;
+  b.seeds = seeds;
+  b.nseeds = nseeds;
   int chunks = 1;
+  for (int i = 0; i < ncast; ++i) {
+    b.cast[i] = CastItem{csrc[i], static_cast<__bf16*>(cdst[i]), crows[i], ccols[i], crows_p[i], ccols_p[i], cld[i]};
+    const long e = (long)crows_p[i] * ccols_p[i] / ((ccols_p[i] & 7) == 0 ? 8 : 1);
+    chunks = (int)std::max<long>(chunks, std::min<long>(e, 2048L * 256));
+  }
   for (int i = 0; i < count; ++i) {
     if (n[i] < 16 || n[i] % 16 || k[i] < 32 || k[i] % 32) return 2;
     b.src[i] = src[i];
@@ -681,6 +708,6 @@ extern "C" int mta_frag_pack(int count, const float* const* src, void* const* ds
     b.tr[i] = tr[i];
     chunks = std::max(chunks, n[i] * k[i] / 8);
   }
-  frag_pack_kernel<<<dim3((chunks + 255) / 256, count), 256, 0, st>>>(b);
+  frag_pack_kernel<<<dim3((chunks + 255) / 256, count + ncast), 256, 0, st>>>(b);
   return 0;
 }

@@ -114,9 +114,10 @@ def _padded_bf16(w: Tensor, cols_p: int) -> Tensor:
 
 
 def _row_dtype(D: int) -> torch.dtype:
-    """Storage of a GEMM -> norm row tensor (activation or its gradient): fp32.  The bf16 form measured slower end to
-    end -- mlp_large B=64 1.277 -> 1.327 ms, the wide norm backward 50 -> 62 us per call on 8-byte row loads, no gain
-    in the GEMM epilogues (profiles/r3_bf16_rows_negative.txt) -- and was removed."""
+    """Storage of a GEMM -> norm row tensor (activation or its gradient): fp32.  bf16 rows measured no faster --
+    r3: mlp_large B=64 1.277 -> 1.327 ms (profiles/r3_bf16_rows_negative.txt); r5, with the bf16-row form of the wide
+    norm backward: 1.1318 -> 1.1293 ms, within noise, at a bf16 rounding of every LayerNorm input
+    (profiles/r5_bf16_rows_negative.txt)."""
     return torch.float32
 
 
@@ -457,20 +458,13 @@ class _TransformerEncoderFn(torch.autograd.Function):
             mats += [params[base + 1], params[base + 3], params[base + 6], params[base + 8]]
         mats_b = [_padded_bf16(w, _r8(w.shape[1])) for w in mats]
         ffn = _tr_ffn_ok(d, mats_b[3].shape[0] if L else 0)
-        # fused FFN: its weights go to fragment-major images instead (W1, W2 for the forward, W2^T, W1^T for the
-        # backward; csrc/tr_ffn.hip frag_pack), so the cast skips them
-        cast = [i for i in range(len(mats)) if not (ffn and i > 0 and (i - 1) % 4 >= 2)]
-        # rows of the padded sequences (Np > N) are zero-filled by the cast itself
-        cast_pad([x.reshape(N * T, F)] + [mats[i] for i in cast], [Xin] + [mats_b[i] for i in cast],
-                 seeds if drop else None)
-        xs = torch.empty((M, d), device=dev, dtype=torch.float32)
-        gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
-        saved: List[Tensor] = [Xin]
-        stats: List[Tensor] = []
         attn = _tr_attn_ok(d, heads, T)
-        # fragment-major weight images of the fused halves, one packing launch: per layer the FFN's W1, W2 (forward)
-        # and W2^T, W1^T (backward), the attention half's W_qkv, W_o (forward), W_o^T (the backward's dO = dX1 W_o,
-        # fused into the attention backward) and W_qkv^T (its d(xn) = dqkv W_qkv, fused into the RMSNorm1 backward)
+        # fused halves: their weights go to fragment-major images instead (FFN: W1, W2 for the forward, W2^T, W1^T
+        # for the backward; attention: W_qkv, W_o forward, W_o^T for the backward's dO = dX1 W_o fused into the
+        # attention backward, W_qkv^T for its d(xn) = dqkv W_qkv fused into the RMSNorm1 backward), so the
+        # row-major casts skip them
+        cast = [i for i in range(len(mats))
+                if not (i > 0 and ((ffn and (i - 1) % 4 >= 2) or (attn and (i - 1) % 4 < 2)))]
         frag, afrag = None, None
         srcs, dsts, trs = [], [], []
         if ffn:
@@ -485,8 +479,26 @@ class _TransformerEncoderFn(torch.autograd.Function):
             srcs += [mats[1 + 4 * l + j] for l in range(L) for j in (0, 1, 1, 0)]
             dsts += afrag
             trs += [False, False, True, True] * L
+        # the remaining row-major casts (input tokens -- rows of the padded sequences zero-filled -- and whatever
+        # matrices the fused halves do not cover) and the dropout-seed advance: riding on the first packing launch
+        # when they fit (one launch for all operand preparation), else cast_pad
+        csrc = [x.reshape(N * T, F)] + [mats[i] for i in cast]
+        cdst = [Xin] + [mats_b[i] for i in cast]
+        ride = bool(srcs) and len(csrc) <= 4
+        if not ride:
+            cast_pad(csrc, cdst, seeds if drop else None)
         for i in range(0, len(srcs), 32):
-            C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32])
+            first = i == 0 and ride
+            C.frag_pack(srcs[i:i + 32], dsts[i:i + 32], trs[i:i + 32], csrc if first else [], cdst if first else [],
+                        seeds if (first and drop) else None)
+        xs = torch.empty((M, d), device=dev, dtype=torch.float32)
+        # the embedding x = in We^T + be: inside the first fused attention half (fp32 FMAs over the F = 3 inputs),
+        # else one GEMM
+        embed_fused = attn and L > 0
+        if not embed_fused:
+            gemm(0, Xin, mats_b[0], M, d, Fp, Fp, Fp, flags=EPI_BIAS, bias=params[1], out_f32=xs)
+        saved: List[Tensor] = [Xin]
+        stats: List[Tensor] = []
         nn = ffn and _TR_WGRAD_NN[0]  # saved xn2 / u are then the transposed images
         for l in range(L):
             base = 2 + nb * l
@@ -501,8 +513,9 @@ class _TransformerEncoderFn(torch.autograd.Function):
             lse = torch.empty(Np * heads * 64, device=dev, dtype=torch.float32)
             x1 = torch.empty((M, d), device=dev, dtype=torch.float32)
             if attn:
+                emb = (x.reshape(N * T, F), params[0], params[1]) if (embed_fused and l == 0) else (None, None, None)
                 C.tr_attn_fwd(Np, T, heads, RMS_EPS, ROPE_BASE, xs, afrag[4 * l], afrag[4 * l + 1], g1, bqkv, bo, xn, r1, qkv,
-                              o, lse, x1)
+                              o, lse, x1, *emb)
             else:
                 C.norm(False, xs, d, M, d, True, RMS_EPS, g1, None, xn, None, None, r1, None, 0.0, None, None, None,
                        None, None, None, None)
@@ -556,17 +569,19 @@ class _TransformerEncoderFn(torch.autograd.Function):
         nb = len(BLOCK_NAMES)
         Xin = saved[0]
         x_final = saved[-1]
-        # final RMSNorm over the last-token rows -> residual-stream gradient (zero elsewhere)
-        dX = torch.empty((M, d), device=dev, dtype=torch.float32)
-        C.zero_(dX)  # memset node, not an ATen fill kernel
+        # final RMSNorm over the last-token rows -> residual-stream gradient, fp32 and bf16 (zero elsewhere): both
+        # views of one buffer, zeroed by one kernel
+        zbuf = torch.empty(M * d * 6, device=dev, dtype=torch.uint8)
+        dX = zbuf[:M * d * 4].view(torch.float32).view(M, d)
+        dXb = zbuf[M * d * 4:].view(torch.bfloat16).view(M, d)
+        C.zero_(zbuf)
         # the N real sequences only (the padded ones have no output gradient): dh is read in place
         dh = dh if (dh.dtype == torch.float32 and dh.is_contiguous()) else dh.float().contiguous()
         gf = params[2 + nb * L]
         C.norm_defer()
         C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, None, None,
-               stats[-1], None, 0.0, dh, None, None, None, dX.view(-1)[(T - 1) * d:], _grad_view(gf), None)
-        dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-        cast_pad([dX], [dXb])
+               stats[-1], None, 0.0, dh, None, None, dXb.view(-1)[(T - 1) * d:], dX.view(-1)[(T - 1) * d:],
+               _grad_view(gf), None)
         frag = ctx.frag  # fused FFN: W2^T / W1^T fragment-major images, written by the forward's packing launch
         # operands of the weight gradients queued for the grouped launch: alive (and not rewritten) until the flush
         keep: List[Tensor] = []
