@@ -93,7 +93,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
     const size_t gr = grow0 + xr;
     const bool tin = rok && gr < (size_t)a.rows_in;
 #pragma unroll
-    for (int f = 0; f < 8; ++f) tok[f] = (f < a.F && tin) ? a.in[gr * a.F + f] : 0.f;
+    for (int f = 0; f < 8; ++f) tok[f] = (f < a.F && tin) ? (float)(__bf16)a.in[gr * a.F + f] : 0.f;  // bf16 operands:
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float e[4];
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
         float v = a.be[c];
 #pragma unroll
         for (int f = 0; f < 8; ++f)
-          if (f < a.F) v = fmaf(tok[f], a.we[c * a.F + f], v);
+          if (f < a.F) v = fmaf(tok[f], (float)(__bf16)a.we[c * a.F + f], v);  // the unfused embedding GEMM's math
         e[kk] = rok ? v : 0.f;
       }
       xv[i] = make_float4(e[0], e[1], e[2], e[3]);
