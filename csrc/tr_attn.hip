@@ -93,17 +93,45 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
     const size_t gr = grow0 + xr;
     const bool tin = rok && gr < (size_t)a.rows_in;
 #pragma unroll
-    for (int f = 0; f < 8; ++f) tok[f] = (f < a.F && tin) ? (float)(__bf16)a.in[gr * a.F + f] : 0.f;  // bf16 operands:
+    for (int f = 0; f < 8; ++f) tok[f] = (f < a.F && tin) ? (float)(__bf16)a.in[gr * a.F + f] : 0.f;
+    // this thread's 16 rows of We ([128][F] row-major: 16 F contiguous floats) and biases, as 16-B loads when F = 3
+    // (the financial windows: 12 float4), scalar loads otherwise
+    float wv[16 * 3], bv[16];
+    const bool f3 = a.F == 3;
+    if (f3) {
+#pragma unroll
+      for (int q4 = 0; q4 < 12; ++q4) {
+        const float4 t4 = *reinterpret_cast<const float4*>(a.we + xc * 3 + 4 * q4);
+        wv[4 * q4] = t4.x;
+        wv[4 * q4 + 1] = t4.y;
+        wv[4 * q4 + 2] = t4.z;
+        wv[4 * q4 + 3] = t4.w;
+      }
+    }
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const float4 t4 = *reinterpret_cast<const float4*>(a.be + xc + 4 * q4);
+      bv[4 * q4] = t4.x;
+      bv[4 * q4 + 1] = t4.y;
+      bv[4 * q4 + 2] = t4.z;
+      bv[4 * q4 + 3] = t4.w;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float e[4];
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const int c = xc + 4 * i + kk;
-        float v = a.be[c];
+        const int cc = 4 * i + kk, c = xc + cc;
+        float v = bv[cc];
+        // bf16 operands: the math of the unfused embedding GEMM
+        if (f3) {
 #pragma unroll
-        for (int f = 0; f < 8; ++f)
-          if (f < a.F) v = fmaf(tok[f], (float)(__bf16)a.we[c * a.F + f], v);  // the unfused embedding GEMM's math
+          for (int f = 0; f < 3; ++f) v = fmaf(tok[f], (float)(__bf16)wv[3 * cc + f], v);
+        } else {
+#pragma unroll
+          for (int f = 0; f < 8; ++f)
+            if (f < a.F) v = fmaf(tok[f], (float)(__bf16)a.we[c * a.F + f], v);
+        }
         e[kk] = rok ? v : 0.f;
       }
       xv[i] = make_float4(e[0], e[1], e[2], e[3]);

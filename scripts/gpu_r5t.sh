@@ -1,0 +1,16 @@
+#!/bin/bash
+# heads backward grid split over columns: losses / heads tests, mlp_large bench + trace
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r5t
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_extras.py -m gpu -x -v --timeout 300 \
+  --timeout-method thread -k "heads or loss or mlp or decoder" > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
+echo "pytest ok" >> $O/status.log
+timeout -k 10 300 python bench.py --model mlp_large --loss mse --batch 64 --trainer gpu_fast --steps 100 --warmup 10 \
+  > $O/mlp_large.json 2> $O/mlp_large.err || exit $?
+timeout -k 10 300 python bench.py --model small --loss mse --batch 64 --steps 100 --warmup 10 \
+  > $O/small_b64.json 2> $O/small_b64.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mlp -o mlp -- \
+  python bench.py --model mlp_large --trainer gpu_fast --batch 64 --steps 50 --warmup 10 > $O/prof_mlp.log 2>&1 || exit $?
+echo done >> $O/status.log
