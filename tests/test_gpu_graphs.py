@@ -69,3 +69,14 @@ def test_step_graphs_hold_kernel_nodes_only(model, trainer, loss, spg):
         assert c["memset"] == 0 and c["memcpy"] == 0 and c["other"] == 0, (key, c)
     if spg > 1:
         assert any(len(k) == 5 and k[-1] == spg for k in census), "no grouped graph was captured"
+
+
+@pytest.mark.parametrize("model,trainer,limit", [("small", "fast", 4), ("transformer_encoder", "gpu_fast", 30)])
+@pytest.mark.parametrize("spg", [1, 4])
+def test_step_graph_launch_budget(model, trainer, limit, spg):
+    """Kernel nodes per training step: the headline LSTM step is 4 launches (forward with the batch gather folded
+    in, one-launch decoder, backward with the weight gradients, clip + Adam); the transformer_encoder step at most 30
+    (VERDICT r4 #6: fused attention / FFN halves, grouped weight gradients, embedding and operand casts folded in)."""
+    census = _census(model, trainer, spg, "mse")
+    per_step = max(c["kernel"] for c in census.values()) / spg
+    assert per_step <= limit, (per_step, census)
