@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
   const int K = argc > 3 ? atoi(argv[3]) : 4096, mode = argc > 4 ? atoi(argv[4]) : 0;
   const int epi = argc > 5 ? atoi(argv[5]) : 0;  // 1: the MLP forward epilogue (bias + GELU, bf16 pre-activation)
   const int ksplit = argc > 6 ? atoi(argv[6]) : 1;  // split-K
+  if (argc > 7) mta_gemm_set_big(atoi(argv[7]));      // -1 default, 0 off, 1 on
   __bf16 *A, *B;
   float* C;
   CK(hipMalloc(&A, (size_t)M * K * 2));

@@ -47,7 +47,10 @@ def timeit(fn, reps=20, warm=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--ab", action="store_true", help="every shape on the 256x256 kernel and on the 128-tile path")
+    ap.add_argument("--ab", action="store_true", help="every shape on the default path (-1), the 256x256 kernel forced (1) and the 128-tile path (0)")
+    ap.add_argument("--only", default=None, help="substring filter on the shape names")
+    ap.add_argument("--variants", default=None, help="comma-separated gemm_set_big values (default: -1, or -1,1,0 with --ab)")
+    ap.add_argument("--no-blas", action="store_true")
     args = ap.parse_args()
     from masters_thesis_amd.ops import _lib
     from masters_thesis_amd.ops.extras import EPI_ACCUM, gemm, gemm_flush, wgrad_split
@@ -56,8 +59,11 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     rows = []
-    variants = (1, 0) if args.ab else (-1,)
-    for (name, mode, M, N, K), big in [(sh, v) for sh in SHAPES for v in variants]:
+    variants = (-1, 1, 0) if args.ab else (-1,)
+    if args.variants:
+        variants = tuple(int(v) for v in args.variants.split(","))
+    shapes = [sh for sh in SHAPES if args.only is None or args.only in sh[0]]
+    for (name, mode, M, N, K), big in [(sh, v) for sh in shapes for v in variants]:
         _lib.lib().gemm_set_big(big)
         if mode == 0:
             A = torch.randn(M, K, device=dev).bfloat16()
@@ -92,7 +98,7 @@ def main():
         # the vendor library on the same product (torch.matmul -> hipBLASLt, bf16 out, no fused epilogue)
         Ab = A if mode != 2 else A.t()
         Bb = B.t() if mode == 0 else B
-        blas_us = timeit(lambda: torch.matmul(Ab, Bb))
+        blas_us = float("nan") if args.no_blas else timeit(lambda: torch.matmul(Ab, Bb))
         row = {"shape": name, "big": big, "mode": mode, "M": M, "N": N, "K": K, "ksplit": ks, "us": round(us, 2),
                "tflops": round(tf, 1), "blas_us": round(blas_us, 2),
                "blas_tflops": round(2.0 * M * N * K / (blas_us * 1e-6) / 1e12, 1), "rel_err": err}
