@@ -400,8 +400,8 @@ constexpr int AHEAD = 3;              // k-tiles in flight beyond the one multip
 constexpr int SLOTS = AHEAD + 2;      // + the slot being read + the one whose reads retire during the issue
 constexpr int OP_BYTES = 256 * KT * 2;     // one operand's k-tile image: 16 KB
 constexpr int SLOT_BYTES = 2 * OP_BYTES;  // A | B
-constexpr int EPI_ROW = 68;                                   // staged row: 64 f32 + 4 pad (conflict-free writes)
-constexpr int EPI_WAVE_BYTES = 64 * EPI_ROW * 4;               // 64 rows of one wave's 128 x 64 tile per pass
+constexpr int EPI_ROW = 68;                                   // staged column: 64 f32 + 4 pad (epi_sidx)
+constexpr int EPI_WAVE_BYTES = 64 * EPI_ROW * 4;               // 64 columns x 64 rows of one wave per pass
 constexpr int LDS_BYTES = SLOTS * SLOT_BYTES > 8 * EPI_WAVE_BYTES ? SLOTS * SLOT_BYTES : 8 * EPI_WAVE_BYTES;
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -435,6 +435,7 @@ __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, in
 // diagnostic build (csrc/tools/gemm_probe.hip): s_memtime stamps of the main loop's segments, summed per wave
 #ifdef MTA_STAMPS
 __device__ unsigned long long stamp_acc[8][8];  // [wave][segment]
+__device__ unsigned long long epi2_acc[8];       // MTA_EPI_TWICE: [wave] the second epilogue
 #define GSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define GACC(i, a, b) dsum[i] += (unsigned)((b) - (a))
 #else
@@ -488,23 +489,82 @@ __device__ __forceinline__ void wait_tiles(int n) {
 }
 
 // Epilogue through LDS (the ring is free once the loop's last barrier passed: every DMA and fragment read retired):
-// each wave stages 64 of its 128 x 64 output rows at a time as [row][64 f32] and reads them back row-contiguous, so
+// each wave stages 64 of its 128 x 64 output rows at a time and reads them back row-contiguous, so
 //   * plain outputs / operand reads are 16-B (f32) or 8-B (bf16) per lane, four full 256-B row segments per
 //     instruction (the accumulator layout stores 4 rows x 64 B per instruction, 2-byte stores for bf16);
 //   * split-K atomics are one 256-B row segment per instruction (lane = column).
-// The read-back loops are ROLLED (the r3 stamp probe measured ~85k cycles per tile for fully unrolled epilogues of
-// ~30k instructions: every wave of the chip streams a cold instruction path at once) and read the staging image with
-// inline-asm ds_reads: hipcc would otherwise wait vmcnt(0) -- the previous iteration's stores -- ahead of every LDS
-// access in a kernel that issues LDS-DMA.  `vec` = every pointer / ldc allows the wide forms.
-__device__ __forceinline__ float4 stage_read4(const float* p) {
-  float4 v;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
-  return v;
+// Its INSTRUCTION FOOTPRINT is what it costs: the instruction cache is cold when a tile gets there (every launch starts
+// one), and every CU of the chip fetches the epilogue's lines one L2 round trip at a time.  The r5 stamp probe ran the
+// same epilogue twice per tile: 68-94k cycles the first time, 30-43k the second (into a fresh buffer too: not a
+// first-touch effect), against a ~100k-cycle main loop.  So the staging is column-major (ds_write_b128 of an
+// accumulator's 4 rows: 16 writes per pass instead of 64 ds_write_b32 + selects), the read-back loops are ROLLED, and
+// the common flag sets run a straight-line row loop specialised at compile time (rows_out_fast) instead of the
+// general one's per-feature branches.  Staged element (col c, row r) of a wave's 64 x 64 pass sits at
+// c * EPI_SP + (r ^ 4 ((c >> 2) & 7)): the b128 writes of 8 lanes (8 columns) and the ds_read2_b32 reads of a row's 4
+// columns (c, c+1, c+2, c+3: dword offsets 0, 68, 136, 204) are both at most 2-way bank-conflicted.
+// The reads are inline asm: hipcc would otherwise wait vmcnt(0) -- the previous iteration's stores -- ahead of every
+// LDS access in a kernel that issues LDS-DMA.  `vec` = every pointer / ldc allows the wide forms.
+constexpr int EPI_SP = 68;  // staged column pitch (floats)
+__device__ __forceinline__ int epi_sidx(int c, int r) { return c * EPI_SP + (r ^ (((c >> 2) & 7) << 2)); }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// staged row r, columns c0 .. c0 + 3 (c0 % 4 == 0), times alpha
+__device__ __forceinline__ float4 stage_row4(const float* stage, int c0, int r, float alpha) {
+  f32x2 lo, hi;
+  const unsigned a = (unsigned)(uintptr_t)(stage + epi_sidx(c0, r));
+  asm volatile("ds_read2_b32 %0, %2 offset1:68\n\tds_read2_b32 %1, %2 offset0:136 offset1:204\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(lo), "=v"(hi)
+               : "v"(a)
+               : "memory");
+  return make_float4(lo.x * alpha, lo.y * alpha, hi.x * alpha, hi.y * alpha);
 }
-__device__ __forceinline__ float stage_read1(const float* p) {
+__device__ __forceinline__ float stage_one(const float* stage, int c, int r, float alpha) {
   float v;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((unsigned)(uintptr_t)p) : "memory");
-  return v;
+  const unsigned a = (unsigned)(uintptr_t)(stage + epi_sidx(c, r));
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v * alpha;
+}
+// one pass's 4 x 4 accumulators (rows 16 ii + 4 (lane >> 4) + 0..3, column 16 j + (lane & 15)) into the stage
+__device__ __forceinline__ void stage_pass(float* stage, const f32x4 (&acc)[8][4], const int i0, const int lane) {
+#pragma unroll
+  for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned a = (unsigned)(uintptr_t)(stage + epi_sidx(16 * j + (lane & 15), 16 * ii + 4 * (lane >> 4)));
+      asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(acc[i0 + ii][j]) : "memory");
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Straight-line row loop of the common flag sets (no accumulate, dropout, residual or GELU' operand; the wave's 128 x
+// 64 block inside M x n_store; vec): F = EF_* bits, compile time
+constexpr int EF_BIAS = 1, EF_GELU = 2, EF_F32 = 4, EF_BF16 = 8, EF_PRE = 16;
+template <int F>
+__device__ __forceinline__ void rows_out_fast(const GemmArgs& g, const float* stage, const int mrow, const int n,
+                                              const int lane, const float (&bias4)[4]) {
+  const int c0 = 4 * (lane & 15);
+#pragma unroll 1
+  for (int q = 0; q < 16; ++q) {
+    const int rr = 4 * q + (lane >> 4);
+    const float4 t = stage_row4(stage, c0, rr, g.alpha);
+    const size_t o = (size_t)(mrow + rr) * g.ldc + n;
+    float v[4] = {t.x, t.y, t.z, t.w};
+    Bf8 pre;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (F & EF_BIAS) v[e] += bias4[e];
+      if (F & EF_PRE) pre.e[e] = (__bf16)v[e];
+      if (F & EF_GELU) v[e] = mta_gelu(v[e]);
+    }
+    if (F & EF_F32) *reinterpret_cast<float4*>(g.out_f32 + o) = make_float4(v[0], v[1], v[2], v[3]);
+    if (F & EF_BF16) {
+      Bf8 b;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) b.e[e] = (__bf16)v[e];
+      *reinterpret_cast<uint2*>(g.out_bf16 + o) = make_uint2(b.u.x, b.u.y);
+    }
+    if (F & EF_PRE) *reinterpret_cast<uint2*>(g.aux_pre + o) = make_uint2(pre.u.x, pre.u.y);
+  }
 }
 
 // IN: the epilogue reads an operand per output (residual, GELU input of a DGELU, the fp32 output of a non-split
@@ -513,37 +573,35 @@ __device__ __forceinline__ float stage_read1(const float* p) {
 // one store round trip per row, which was ~40 % of a 256 x 256 tile's time (r4 epilogue probe).
 template <bool IN>
 __device__ __forceinline__ void big_rows_out(const GemmArgs& g, const float* stage, const int mrow, const int n,
-                                          const int lane, const bool vec, const bool split, const int bz,
+                                          const int nc, const int lane, const bool vec, const bool split, const int bz,
                                           const float (&bias4)[4],
                                           const uint32_t dseed, const uint32_t dthr, const float dscale) {
   const bool accum = (g.flags & EPI_ACCUM) != 0;
+  const int c0 = 4 * (lane & 15);
   if (accum && split && g.slab) {
     // split-K partial: plain 16-B stores into this split's slab; splitk_reduce_kernel adds the slabs afterwards
-    const int cc = 4 * (lane & 15);
     float* slab = g.slab + (size_t)bz * g.M * g.N;
 #pragma unroll 1
     for (int q = 0; q < 16; ++q) {
       const int rr = 4 * q + (lane >> 4);
-      const float4 t = stage_read4(stage + rr * EPI_ROW + cc);
+      const float4 t = stage_row4(stage, c0, rr, g.alpha);
       if (mrow + rr < g.M && n + 3 < g.N) epi_store(reinterpret_cast<float4*>(slab + (size_t)(mrow + rr) * g.N + n), t, g.flags);
     }
     return;
   }
-  if (accum && split) {
-    const int nc = n - 4 * (lane & 15) + lane;  // lane = column of the 64-wide slice
+  if (accum && split) {  // nc: this lane's column of the 64-wide slice
 #pragma unroll 1
     for (int rr = 0; rr < 64; ++rr) {
-      const float v = stage_read1(stage + rr * EPI_ROW + lane);
+      const float v = stage_one(stage, lane, rr, g.alpha);
       if (mrow + rr < g.M && nc < g.n_store) atomicAdd(g.out_f32 + (size_t)(mrow + rr) * g.ldc + nc, v);
     }
     return;
   }
-  const int cc = 4 * (lane & 15);
 #pragma unroll 1
   for (int q = 0; q < 16; ++q) {
     const int rr = 4 * q + (lane >> 4);
     const int m = mrow + rr;
-    const float4 t = stage_read4(stage + rr * EPI_ROW + cc);
+    const float4 t = stage_row4(stage, c0, rr, g.alpha);
     if (m >= g.M) continue;
     const size_t o = (size_t)m * g.ldc + n;
     const bool wide = vec && n + 3 < g.n_store;
@@ -620,6 +678,18 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
   const bool accum = (g.flags & EPI_ACCUM) != 0;
   const bool vec = (g.ldc & 3) == 0 && ((uintptr_t)g.out_f32 & 15) == 0 && ((uintptr_t)g.out_bf16 & 7) == 0 &&
                    ((uintptr_t)g.aux_pre & 7) == 0 && ((uintptr_t)g.resid & 15) == 0 && ((uintptr_t)g.aux_in & 7) == 0;
+  const int n = nbase + 4 * (lane & 15);  // this lane's 4 columns in the row-contiguous walk
+  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
+  if (!accum && (g.flags & EPI_BIAS)) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias4[e] = n + e < g.N ? g.bias[n + e] : 0.f;
+  }
+  // the specialised form: its flag set, or -1
+  int fast = -1;
+  if (!accum && !(g.flags & (EPI_DROPOUT | EPI_DGELU | EPI_RESID)) && vec && mbase + 128 <= g.M &&
+      nbase + 64 <= g.n_store)
+    fast = ((g.flags & EPI_BIAS) ? EF_BIAS : 0) | ((g.flags & EPI_GELU) ? EF_GELU : 0) | (g.out_f32 ? EF_F32 : 0) |
+           (g.out_bf16 ? EF_BF16 : 0) | (g.aux_pre ? EF_PRE : 0);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 0.f;
   if (g.flags & EPI_DROPOUT) {
@@ -628,29 +698,30 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& g, const f32x4 (&ac
     dthr = (uint32_t)(g.drop_p * 65536.f + 0.5f);
     dscale = 1.0f / (1.0f - g.drop_p);
   }
-  const int n = nbase + 4 * (lane & 15);  // this lane's 4 columns in the row-contiguous walk
-  float bias4[4] = {0.f, 0.f, 0.f, 0.f};
-  if (!accum && (g.flags & EPI_BIAS)) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias4[e] = n + e < g.N ? g.bias[n + e] : 0.f;
-  }
   const bool in = (g.flags & (EPI_RESID | EPI_DGELU)) || (accum && !split);
-  // ROLLED over the two 64-row passes (the half of acc staged is a select, not an index): one copy of the row-out
-  // code, whose first run streams it into the instruction cache of every CU at once (~half the epilogue, r4 probe)
 #pragma unroll 1
   for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          stage[(16 * ii + 4 * (lane >> 4) + r) * EPI_ROW + 16 * j + (lane & 15)] =
-              g.alpha * (pass ? acc[4 + ii][j][r] : acc[ii][j][r]);
-    // the asm reads below are invisible to hipcc: order them behind the staging writes
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (in) big_rows_out<true>(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
-    else big_rows_out<false>(g, stage, mbase + 64 * pass, n, lane, vec, split, bz, bias4, dseed, dthr, dscale);
+    if (pass == 0) stage_pass(stage, acc, 0, lane);
+    else stage_pass(stage, acc, 4, lane);
+    const int mrow = mbase + 64 * pass;
+    switch (fast) {
+      case EF_F32: rows_out_fast<EF_F32>(g, stage, mrow, n, lane, bias4); break;
+      case EF_BIAS | EF_F32: rows_out_fast<EF_BIAS | EF_F32>(g, stage, mrow, n, lane, bias4); break;
+      case EF_BIAS | EF_GELU | EF_F32 | EF_PRE:
+        rows_out_fast<EF_BIAS | EF_GELU | EF_F32 | EF_PRE>(g, stage, mrow, n, lane, bias4);
+        break;
+      case EF_BF16: rows_out_fast<EF_BF16>(g, stage, mrow, n, lane, bias4); break;
+      case EF_BIAS | EF_BF16: rows_out_fast<EF_BIAS | EF_BF16>(g, stage, mrow, n, lane, bias4); break;
+      case EF_BIAS | EF_GELU | EF_BF16 | EF_PRE:
+        rows_out_fast<EF_BIAS | EF_GELU | EF_BF16 | EF_PRE>(g, stage, mrow, n, lane, bias4);
+        break;
+      default: {
+        const int nc = nbase + lane;
+        if (in) big_rows_out<true>(g, stage, mrow, n, nc, lane, vec, split, bz, bias4, dseed, dthr, dscale);
+        else big_rows_out<false>(g, stage, mrow, n, nc, lane, vec, split, bz, bias4, dseed, dthr, dscale);
+      }
+    }
+    // the next pass re-stages over this one: every wave's reads above retired (inline-asm waits)
   }
 }
 
@@ -783,12 +854,31 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 #ifdef MTA_STAMPS
   GSTAMP(tepi0);
 #endif
+#ifdef MTA_EPI_SKIP  // probe build: no epilogue (the accumulators kept live), main loop + launch only
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc[i][j]));
+#else
   big_epilogue(g, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
                reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
+#endif
   if (want_rowsum) flush_rowsum(g, rowsum, m0 + wm * 128, lane);
 #ifdef MTA_STAMPS
   GSTAMP(tend);
   if (lane == 0) atomicAdd(&stamp_acc[wave][7], (unsigned long long)(unsigned)(tend - tepi0));  // epilogue
+#ifdef MTA_EPI_TWICE  // probe build: the same epilogue again, its code now in the instruction cache
+  GemmArgs g2 = g;
+#ifdef MTA_EPI_TWICE_FRESH  // ... into a second output buffer (pages and lines not touched before)
+  g2.out_f32 = g.out_f32 ? g.out_f32 + (size_t)g.M * g.ldc : nullptr;
+  g2.aux_pre = g.aux_pre ? g.aux_pre + (size_t)g.M * g.ldc : nullptr;
+#endif
+  GSTAMP(t2a);
+  big_epilogue(g2, acc, m0 + wm * 128, n0 + wn * 64, gz > 1, bz, lane,
+               reinterpret_cast<float*>(lds + wave * EPI_WAVE_BYTES));
+  GSTAMP(t2b);
+  if (lane == 0) atomicAdd(&epi2_acc[wave], (unsigned long long)(unsigned)(t2b - t2a));
+#endif
 #endif
 }
 

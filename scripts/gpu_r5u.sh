@@ -1,13 +1,14 @@
 #!/bin/bash
-# r5u: 8-phase 64-deep 256x256 GEMM -- numerics (big-tile tests), A/B against the 32-deep ring, mlp_large bench + trace
+# r5u: compact 256x256 GEMM epilogue -- numerics (big-tile + fused-step tests), gemm A/B, mlp_large bench + trace
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r5u
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_extras.py -k "big_tile or fused_training_step or small_weight_grad or grouped" -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_extras.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
 echo "pytest ok" >> $O/status.log
 timeout -k 10 300 python -u scripts/gemm_bench.py --ab --json $O/gemm_ab.jsonl > $O/gemm_ab.log 2>&1 || { echo "gemm_bench rc=$?" >> $O/status.log; exit 1; }
 echo "gemm ok" >> $O/status.log
 timeout -k 10 300 python bench.py --model mlp_large --loss mse --batch 64 --trainer gpu_fast --steps 100 --warmup 10 > $O/mlp_large.json 2> $O/mlp_large.err || { echo "bench rc=$?" >> $O/status.log; exit 1; }
+timeout -k 10 300 python bench.py --model transformer_encoder --loss combined --batch 8 --trainer gpu_fast --steps 100 --warmup 10 > $O/tr_b8.json 2> $O/tr_b8.err || { echo "bench rc=$?" >> $O/status.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mlp -o mlp -- python bench.py --model mlp_large --trainer gpu_fast --batch 64 --steps 50 --warmup 10 > $O/prof_mlp.log 2>&1 || { echo "prof rc=$?" >> $O/status.log; exit 1; }
 echo done >> $O/status.log
