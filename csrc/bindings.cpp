@@ -644,10 +644,11 @@ void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, const Op
 void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, double eps, const OptT& gamma,
           const OptT& beta, const OptT& y_bf16, const OptT& y_f32, const OptT& mean, at::Tensor rstd,
           const OptT& seed, double drop_p, const OptT& dy, const OptT& dres, const OptT& pre, const OptT& dx_bf16,
-          const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta) {
+          const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta, bool gelu_x) {
   TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "x must be fp32 or bf16 GPU");
   const bool xb = x.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(!gelu_x || xb, "gelu_x: x is the bf16 GELU input");
   const bool dyb = has(dy) && dy->scalar_type() == at::kBFloat16;
   const bool pre_f = has(pre) && pre->scalar_type() == at::kFloat;  // fp32 GELU input (32-true extras)
   if (dyb) TORCH_CHECK(dy->is_cuda() && dy->is_contiguous(), "dy: contiguous GPU tensor");
@@ -663,7 +664,7 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
     if (has(*o)) check_span(**o, M, ldx, D, "residual-stride tensor");
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  const int rc = mta_norm(bwd ? 1 : 0, x.data_ptr(), xb ? 1 : 0, (int)ldx, (int)M, (int)D, rms ? 1 : 0, (float)eps,
+  const int rc = mta_norm(bwd ? 1 : 0, x.data_ptr(), gelu_x ? 2 : xb ? 1 : 0, (int)ldx, (int)M, (int)D, rms ? 1 : 0, (float)eps,
                           opt_typed<float>(gamma, at::kFloat, "gamma"), opt_typed<float>(beta, at::kFloat, "beta"),
                           opt_typed<void>(y_bf16, at::kBFloat16, "y_bf16"), opt_typed<float>(y_f32, at::kFloat, "y_f32"),
                           opt_typed<float>(mean, at::kFloat, "mean"), rstd.data_ptr<float>(),
@@ -1353,7 +1354,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_group_flush", []() { mta_gemm_group_flush(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
-  m.def("norm", &norm);
+  m.def("norm", &norm, py::arg("bwd"), py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("D"), py::arg("rms"),
+        py::arg("eps"), py::arg("gamma"), py::arg("beta"), py::arg("y_bf16"), py::arg("y_f32"), py::arg("mean"),
+        py::arg("rstd"), py::arg("seed"), py::arg("drop_p"), py::arg("dy"), py::arg("dres"), py::arg("pre"),
+        py::arg("dx_bf16"), py::arg("dx_f32"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gelu_x") = false);
   m.def("tr_attn_dx", &tr_attn_dx);
   m.def("attention", &attention, py::arg("bwd"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("dout"),
         py::arg("dqkv"), py::arg("nseq"), py::arg("T"), py::arg("D"), py::arg("heads"), py::arg("rope_base"),

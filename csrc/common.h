@@ -151,6 +151,13 @@ __device__ __forceinline__ float mta_gelu_grad(float x) {
   const float e = __expf(-0.5f * x * x);
   return 0.5f * (1.0f + mta_erf_sqrt1_2(x, e)) + x * 0.3989422804014327f * e;
 }
+// both, sharing the exp and the erf (the norm backward that recomputes the GELU output from its input)
+__device__ __forceinline__ void mta_gelu_and_grad(float x, float& g, float& gp) {
+  const float e = __expf(-0.5f * x * x);
+  const float phi = 0.5f * (1.0f + mta_erf_sqrt1_2(x, e));
+  g = x * phi;
+  gp = phi + x * 0.3989422804014327f * e;
+}
 
 // Counter-based dropout: keep(seed, row, col) from a stateless 32-bit hash (murmur3-style finaliser of
 // two rounds), so forward and backward regenerate the same mask without storing it and a captured

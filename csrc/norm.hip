@@ -58,7 +58,13 @@ struct NormArgs {
   float* part;          // per-block partial rows of dgamma / dbeta: [2][blocks][part_ld]
   int part_ld;
   long part_pass;       // floats between the dgamma and dbeta planes
+  int gelu_x;           // wide kernels: xb is the bf16 GELU INPUT; the normalised row is gelu(xb) (the MLP's GEMM
+                        // then stores only its bf16 pre-activation: no fp32 GELU output written and read back twice)
 };
+
+__device__ __forceinline__ float4 gelu4(float4 v) {
+  return make_float4(mta_gelu(v.x), mta_gelu(v.y), mta_gelu(v.z), mta_gelu(v.w));
+}
 
 __device__ __forceinline__ float4 ld4(const float* pf, const __bf16* pb, size_t i) {
   if (pb) {
@@ -137,7 +143,20 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_kernel(NormArgs a) {
 // (the backward also prefetches the NEXT row's operands before reducing the current one), the row sums go
 // through one LDS exchange (parity double-buffered: one barrier per row), and each column belongs to exactly
 // one thread, so the backward's dgamma/dbeta partials stay in registers and leave as one plain row per block.
-template <int VPT>
+// one row's float4 (D-guarded: columns past D read 0), of the input type B16 chosen at compile time -- a runtime
+// fp32 / bf16 select around the load made hipcc branch per load and wait for it (the next row's prefetch drained
+// before the current row's reductions)
+template <bool B16>
+__device__ __forceinline__ float4 ld4t(const NormArgs& a, size_t i) {
+  if constexpr (B16) {
+    const bf16x4 b = *reinterpret_cast<const bf16x4*>(a.xb + i);
+    return make_float4((float)b[0], (float)b[1], (float)b[2], (float)b[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(a.x + i);
+  }
+}
+
+template <int VPT, bool B16>
 __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
   // grid-strided rows (~4 workgroups per CU): gamma / beta loaded once per workgroup instead of once per row, and
   // the next row's loads issued before the current row's reductions (one HBM round trip per row hidden)
@@ -158,16 +177,21 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
-    v[i] = c < a.D ? ld4(a.x, a.xb, (size_t)row * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[i] = ld4t<B16>(a, (size_t)row * a.ldx + min(c, a.D - 4));
   }
   for (int it = 0; row < a.M; row += gridDim.x, ++it) {
     const int nrow = row + (int)gridDim.x < a.M ? row + (int)gridDim.x : row;  // clamped: the load is unconditional
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = 4 * (tid + NT_THREADS * i);
-      vn[i] = c < a.D ? ld4(a.x, a.xb, (size_t)nrow * a.ldx + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      vn[i] = ld4t<B16>(a, (size_t)nrow * a.ldx + min(c, a.D - 4));  // unconditional (clamped column)
     }
     const int par = it & 1;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      if (a.gelu_x) v[i] = gelu4(v[i]);
+      if (4 * (tid + NT_THREADS * i) >= a.D) v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
@@ -347,17 +371,18 @@ struct FastRow {
   float mu, rs;
 };
 
-template <int VPT, bool B16>
+// GX: the row is gelu(pre) (NormArgs::gelu_x): no x load, x recomputed from the pre-activation the GELU' needs anyway
+template <int VPT, bool B16, bool GX>
 __device__ __forceinline__ void fast_load(const NormArgs& a, const float* mean, int row, FastRow<VPT, B16>& r) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     if constexpr (B16) {
-      r.x[i] = *reinterpret_cast<const bf16x4*>(a.xb + (size_t)row * a.ldx + c);
+      if constexpr (!GX) r.x[i] = *reinterpret_cast<const bf16x4*>(a.xb + (size_t)row * a.ldx + c);
       r.dy[i] = *reinterpret_cast<const bf16x4*>(a.dyb + (size_t)row * a.D + c);
     } else {
-      r.x[i] = *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c);
+      if constexpr (!GX) r.x[i] = *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c);
       r.dy[i] = *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c);
     }
     r.pre[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
@@ -376,7 +401,7 @@ __device__ __forceinline__ void fast_f4(const typename std::conditional<B16, bf1
   }
 }
 
-template <int VPT, bool B16>
+template <int VPT, bool B16, bool GX>
 __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs a, int rows_per_block) {
   __shared__ float red[2][2][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -396,23 +421,28 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
   const int r1 = min(a.M, r0 + rows_per_block);
   if (r0 >= r1) return;
   FastRow<VPT, B16> rb[3];
-  fast_load<VPT, B16>(a, mean, r0, rb[0]);
-  fast_load<VPT, B16>(a, mean, min(r0 + 1, r1 - 1), rb[1]);
+  fast_load<VPT, B16, GX>(a, mean, r0, rb[0]);
+  fast_load<VPT, B16, GX>(a, mean, min(r0 + 1, r1 - 1), rb[1]);
   for (int base = r0; base < r1; base += 3) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int row = base + k;
       if (row >= r1) break;
-      fast_load<VPT, B16>(a, mean, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
+      fast_load<VPT, B16, GX>(a, mean, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
       const FastRow<VPT, B16>& cur = rb[k];
       const float mu = a.rms ? 0.f : cur.mu;
-      float xh[VPT][4], g[VPT][4];
+      float xh[VPT][4], g[VPT][4], gd[VPT][4];  // gd: GELU' (GX: computed with the GELU itself)
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int i = 0; i < VPT; ++i) {
         const int c = 4 * (tid + NT_THREADS * i);
         float xs[4], ds[4];
-        fast_f4<B16>(cur.x[i], xs);
+        if constexpr (GX) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mta_gelu_and_grad((float)cur.pre[i][j], xs[j], gd[i][j]);
+        } else {
+          fast_f4<B16>(cur.x[i], xs);
+        }
         fast_f4<B16>(cur.dy[i], ds);
         const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
         float ds4[4] = {1.f, 1.f, 1.f, 1.f};
@@ -443,7 +473,8 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
         const int c = 4 * (tid + NT_THREADS * i);
         float o[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) * mta_gelu_grad((float)cur.pre[i][j]);
+        for (int j = 0; j < 4; ++j)
+          o[j] = cur.rs * (g[i][j] - s1 - xh[i][j] * s2) * (GX ? gd[i][j] : mta_gelu_grad((float)cur.pre[i][j]));
         if (a.dx_f32) *reinterpret_cast<float4*>(a.dx_f32 + (size_t)row * a.ldx + c) = make_float4(o[0], o[1], o[2], o[3]);
         if (a.dx_bf16) {
           bf16x4 b;
@@ -775,6 +806,8 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   NormArgs a{};
   a.x = x_bf16 ? nullptr : static_cast<const float*>(x);
   a.xb = x_bf16 ? static_cast<const __bf16*>(x) : nullptr;
+  a.gelu_x = x_bf16 == 2;  // 2: x is the bf16 GELU input (wide kernels)
+  if (a.gelu_x && !(wide_ok && (!bwd || (pre && !pre_f32 && !dres && (D == 1024 || D == 2048))))) return 3;
   a.ldx = ldx;
   a.M = M;
   a.D = D;
@@ -807,7 +840,9 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     if (rows_per_block < 2) rows_per_block = 2;
     blocks = (M + rows_per_block - 1) / rows_per_block;
   } else if (wide) {
-    blocks = M < NORM_FWD_WIDE_BLOCKS ? M : NORM_FWD_WIDE_BLOCKS;
+    // the GELU-on-load form computes per element: twice the workgroups to hide its latency
+    const int cap = a.gelu_x ? 2 * NORM_FWD_WIDE_BLOCKS : NORM_FWD_WIDE_BLOCKS;
+    blocks = M < cap ? M : cap;
   }
   // deferred slot when the caller asked for it (dgamma pointer tagged by mta_norm_defer) and D fits
   const bool defer = bwd && (dgamma || dbeta) && defer_next && D <= NORM_DEFER_D;
@@ -840,23 +875,30 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
   if (wide) {
     if (M > 0) {
-      const bool b16 = a.xb != nullptr;
-      const bool fast = a.pre && !a.dres && b16 == (a.dyb != nullptr) &&
+      const bool b16 = a.gelu_x ? a.dyb != nullptr : a.xb != nullptr;
+      const bool fast = a.pre && !a.dres && (a.gelu_x || b16 == (a.dyb != nullptr)) &&
                         (D == 1024 || D == 2048) && (a.rms || a.mean);
+#define NORM_FAST(V, B)                                                                                   \
+  if (a.gelu_x) norm_bwd_wide_fast_kernel<V, B, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block); \
+  else norm_bwd_wide_fast_kernel<V, B, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
       if (bwd && fast) {
         if (D == 1024) {
-          if (b16) norm_bwd_wide_fast_kernel<1, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
-          else norm_bwd_wide_fast_kernel<1, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+          if (b16) { NORM_FAST(1, true) } else { NORM_FAST(1, false) }
         } else {
-          if (b16) norm_bwd_wide_fast_kernel<2, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
-          else norm_bwd_wide_fast_kernel<2, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+          if (b16) { NORM_FAST(2, true) } else { NORM_FAST(2, false) }
         }
+#undef NORM_FAST
       } else if (bwd) {
         if (D <= 1024) norm_bwd_wide_kernel<1><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
         else norm_bwd_wide_kernel<2><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
       } else {
-        if (D <= 1024) norm_fwd_wide_kernel<1><<<blocks, NT_THREADS, 0, st>>>(a);
-        else norm_fwd_wide_kernel<2><<<blocks, NT_THREADS, 0, st>>>(a);
+        if (D <= 1024) {
+          if (a.xb) norm_fwd_wide_kernel<1, true><<<blocks, NT_THREADS, 0, st>>>(a);
+          else norm_fwd_wide_kernel<1, false><<<blocks, NT_THREADS, 0, st>>>(a);
+        } else {
+          if (a.xb) norm_fwd_wide_kernel<2, true><<<blocks, NT_THREADS, 0, st>>>(a);
+          else norm_fwd_wide_kernel<2, false><<<blocks, NT_THREADS, 0, st>>>(a);
+        }
       }
     }
   } else if (vpl <= 1) {

@@ -121,6 +121,14 @@ def _row_dtype(D: int) -> torch.dtype:
     return torch.float32
 
 
+def _gelu_in_norm(D: int) -> bool:
+    """bf16 MLP layer of width D: the GEMM stores only the bf16 pre-activation and the wide norm kernels apply the
+    GELU on load (csrc/norm.hip NormArgs::gelu_x) -- the LayerNorm input is gelu(bf16 pre-activation), as under
+    autocast, instead of an fp32 GELU output written by the GEMM and read back by both norm kernels (78 -> 26 MB
+    written per mlp_large layer).  The wide kernels' widths: D = 1024 / 2048."""
+    return D in (1024, 2048)
+
+
 def _row_out(t: Tensor) -> dict:
     return {"out_bf16": t} if t.dtype == torch.bfloat16 else {"out_f32": t}
 
@@ -174,20 +182,26 @@ class _MlpEncoderFn(torch.autograd.Function):
             D = dims[i + 1]
             assert D % 8 == 0, "MLP hidden size must be a multiple of 8"
             pre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
-            # the GELU output rows are fp32 (_row_dtype)
-            act = torch.empty((Mp, D), device=dev, dtype=_row_dtype(D))
-            gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU, bias=params[per * i + 1],
-                 aux_pre=pre, **_row_out(act))
+            if _gelu_in_norm(D):
+                # the GEMM stores only the bf16 pre-activation; both norm kernels apply the GELU on load
+                act = None
+                gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS, bias=params[per * i + 1],
+                     out_bf16=pre)
+            else:
+                # the GELU output rows are fp32 (_row_dtype)
+                act = torch.empty((Mp, D), device=dev, dtype=_row_dtype(D))
+                gemm(0, Xs[i], wb[i], Mp, D, kp[i], kp[i], kp[i], flags=EPI_BIAS | EPI_GELU,
+                     bias=params[per * i + 1], aux_pre=pre, **_row_out(act))
             mean = None if rms else torch.empty(Mp, device=dev, dtype=torch.float32)
             rstd = torch.empty(Mp, device=dev, dtype=torch.float32)
             last = i == L - 1
             y = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16) if not last else None
             if last:
                 h = torch.empty((Mp, D), device=dev, dtype=torch.float32)
-            lib().norm(False, act, D, Mp, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
-                       None if rms else params[per * i + 3], y, h if last else None, mean, rstd,
+            lib().norm(False, pre if act is None else act, D, Mp, D, rms, RMS_EPS if rms else LN_EPS,
+                       params[per * i + 2], None if rms else params[per * i + 3], y, h if last else None, mean, rstd,
                        seeds[i:i + 1] if (drop and not last) else None, float(dropout), None, None, None, None, None,
-                       None, None)
+                       None, None, gelu_x=act is None)
             pres.append(pre)
             acts.append(act)
             means.append(mean)
@@ -226,10 +240,11 @@ class _MlpEncoderFn(torch.autograd.Function):
             D, Din = dims[i + 1], dims[i]
             dpre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
             dropped = drop and i < L - 1
-            lib().norm(True, acts[i], D, Mp, D, rms, RMS_EPS if rms else LN_EPS, params[per * i + 2],
-                       None if rms else params[per * i + 3], None, None, means[i], rstds[i],
+            lib().norm(True, pres[i] if acts[i] is None else acts[i], D, Mp, D, rms, RMS_EPS if rms else LN_EPS,
+                       params[per * i + 2], None if rms else params[per * i + 3], None, None, means[i], rstds[i],
                        ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], dpre, None,
-                       _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]))
+                       _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]),
+                       gelu_x=acts[i] is None)
             # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre).  A big dW_i is
             # a gradient PRODUCER of the fused optimizer (ops/optim.py register_grad_producer): its split-K reduce
             # overwrites the range and leaves the clip-norm partials, so the update neither zeroes nor re-reads it

@@ -257,6 +257,45 @@ def test_norm_forward_backward(rms, D):
     assert torch.equal(dgam2, dgam3)
 
 
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("D", [1024, 2048])
+def test_norm_gelu_on_load(rms, D):
+    """The bf16 MLP's norm pair with the GELU applied on load (gelu_x: x is the bf16 pre-activation, the normalised row
+    is gelu(x)): forward against fp32 PyTorch LayerNorm / RMSNorm of gelu(pre), backward (dx through the norm and the
+    GELU, dgamma, dbeta) against autograd of the same fp32 composition."""
+    from masters_thesis_amd.ops import _lib
+    from masters_thesis_amd.ops.extras import LN_EPS, RMS_EPS
+
+    C = _lib.lib()
+    torch.manual_seed(5)
+    M = 2600
+    pre = _bf(torch.randn(M, D) * 1.5)
+    g, b = (torch.rand(D) + 0.5).to(DEV), torch.randn(D).to(DEV)
+    dy = torch.randn(M, D).to(DEV)
+    eps = RMS_EPS if rms else LN_EPS
+    yb = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    yf = torch.empty(M, D, device=DEV)
+    mean = None if rms else torch.empty(M, device=DEV)
+    rstd = torch.empty(M, device=DEV)
+    C.norm(False, pre, D, M, D, rms, eps, g, None if rms else b, yb, yf, mean, rstd, None, 0.0, None, None, None, None,
+           None, None, None, gelu_x=True)
+    p = pre.float().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    act = Fn.gelu(p)
+    ref = Fn.rms_norm(act, (D,), gr, eps) if rms else Fn.layer_norm(act, (D,), gr, br, eps)
+    assert _rel(yf, ref) < 1e-5 and _rel(yb.float(), ref) < 5e-3
+    dxb = torch.empty(M, D, device=DEV, dtype=torch.bfloat16)
+    dgam = torch.zeros(D, device=DEV)
+    dbet = torch.zeros(D, device=DEV)
+    C.norm(True, pre, D, M, D, rms, eps, g, None if rms else b, None, None, mean, rstd, None, 0.0, dy, None, pre, dxb,
+           None, dgam, None if rms else dbet, gelu_x=True)
+    gp, gg, gb = torch.autograd.grad(ref, (p, gr, br), dy, allow_unused=True)
+    assert _rel(dxb.float(), gp) < 8e-3
+    assert _rel(dgam, gg) < 1e-4
+    if not rms:
+        assert _rel(dbet, gb) < 1e-4
+
+
 @pytest.mark.parametrize("T,heads,hd", [(60, 4, 32), (64, 2, 64), (17, 3, 32)])
 def test_attention_forward_backward(T, heads, hd):
     from masters_thesis_amd.ops import _lib
