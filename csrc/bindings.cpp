@@ -28,6 +28,7 @@ int mta_gemm_f32(int prec, const float* A, const float* B, const float* bias, co
 int mta_gemm_f32x(int prec, const float* A, int a_km, int lda, const float* B, int b_kn, int ldb, float* C, int ldc,
                   int n_store, int M, int N, int K, int flags, const float* bias, float* pre, const float* mask, const float* resid, const uint64_t* seed, float drop_p, hipStream_t st);
 void mta_colsum_f32(const float* A, int M, int N, int lda, float* out, hipStream_t st);
+void mta_pair_colsum(const float* ab, int n, float* sa, float* sb, hipStream_t st);
 int mta_attention_f32(int bwd, const float* qkv, const float* out, const float* dout, float* o, float* lse, float* dqkv,
                       int nseq, int T, int D, int heads, const float* rope, hipStream_t st);
 void mta_seeds_advance(uint64_t* seeds, int n, hipStream_t st);
@@ -81,7 +82,8 @@ int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* ro
 int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps, const float* gamma,
              const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd, const uint64_t* seed,
              float drop_p, const void* dy, int dy_bf16, const float* dres, const void* pre, int pre_f32, void* dx_bf16,
-             float* dx_f32, float* dgamma, float* dbeta, hipStream_t st);
+             float* dx_f32, float* dgamma, float* dbeta, const float* hw_a, const float* hb_a, const float* hw_b, const float* hb_b,
+             float* ab, int ab_rows, float* g_wa, float* g_wb, hipStream_t st);
 int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const void* w1, const void* w2, const float* b1,
                const float* b2, const float* g2, const float* x1, const uint64_t* seed, float drop_p, void* xn2,
                void* pre, void* u, float* r2, float* x2, const void* dxb, const float* dx, const float* r2in,
@@ -269,6 +271,16 @@ void gemm_f32x(int64_t prec, at::Tensor A, bool a_km, int64_t lda, at::Tensor B,
 }
 
 // out[:N] += column sums of A[:M][:N] (lda): bias gradients of the 32-true extras
+// sa += sum of ab[:, 0], sb += sum of ab[:, 1] (ab: contiguous (n, 2) fp32)
+void pair_colsum(at::Tensor ab, int64_t n, at::Tensor sa, at::Tensor sb) {
+  TORCH_CHECK(ab.is_cuda() && ab.scalar_type() == at::kFloat && ab.is_contiguous() && ab.numel() >= 2 * n,
+              "pair_colsum: contiguous (n, 2) fp32 GPU tensor");
+  CHECK_F32(sa);
+  CHECK_F32(sb);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(ab.device());
+  mta_pair_colsum(ab.data_ptr<float>(), (int)n, sa.data_ptr<float>(), sb.data_ptr<float>(), cur_stream());
+}
+
 void colsum_f32(at::Tensor A, int64_t M, int64_t N, int64_t lda, at::Tensor out) {
   TORCH_CHECK(A.is_cuda() && A.scalar_type() == at::kFloat && out.is_cuda() && out.scalar_type() == at::kFloat &&
               out.numel() >= N && A.numel() >= (M - 1) * lda + N, "colsum_f32: fp32 GPU tensors");
@@ -322,6 +334,7 @@ void gather_batch(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::
   TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 tensors");
   TORCH_CHECK(perm.scalar_type() == at::kInt && cursor.scalar_type() == at::kInt && arrive.scalar_type() == at::kInt,
               "perm/cursor/arrive must be int32");
+  TORCH_CHECK(arrive.is_cuda() && arrive.numel() >= 65, "arrive: 65 int32 words (top + 64 sub-counters)");
   const float* s[4];
   float* d[4];
   long rf[4];
@@ -644,11 +657,18 @@ void cast_pad(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, const Op
 void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, double eps, const OptT& gamma,
           const OptT& beta, const OptT& y_bf16, const OptT& y_f32, const OptT& mean, at::Tensor rstd,
           const OptT& seed, double drop_p, const OptT& dy, const OptT& dres, const OptT& pre, const OptT& dx_bf16,
-          const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta, bool gelu_x) {
+          const OptT& dx_f32, const OptT& dgamma, const OptT& dbeta, bool gelu_x, const OptT& hw_a,
+          const OptT& hb_a, const OptT& hw_b, const OptT& hb_b, const OptT& ab, int64_t ab_rows, const OptT& g_wa,
+          const OptT& g_wb) {
   TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16),
               "x must be fp32 or bf16 GPU");
   const bool xb = x.scalar_type() == at::kBFloat16;
   TORCH_CHECK(!gelu_x || xb, "gelu_x: x is the bf16 GELU input");
+  if (has(ab)) {
+    TORCH_CHECK(ab->is_contiguous() && ab->numel() >= 2 * (bwd ? ab_rows : M), "ab: contiguous (rows, 2) fp32");
+    for (const OptT* o : {&hw_a, &hw_b}) TORCH_CHECK(has(*o) && (*o)->numel() >= D, "fused heads: (1, D) weights");
+    if (bwd) TORCH_CHECK(has(g_wa) && has(g_wb) && g_wa->numel() >= D && g_wb->numel() >= D, "head-weight grads");
+  }
   const bool dyb = has(dy) && dy->scalar_type() == at::kBFloat16;
   const bool pre_f = has(pre) && pre->scalar_type() == at::kFloat;  // fp32 GELU input (32-true extras)
   if (dyb) TORCH_CHECK(dy->is_cuda() && dy->is_contiguous(), "dy: contiguous GPU tensor");
@@ -656,7 +676,7 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
   CHECK_F32(rstd);
   TORCH_CHECK(rstd.numel() >= M, "rstd too small");
   if (!rms) TORCH_CHECK(has(mean) && mean->numel() >= M, "LayerNorm needs mean");
-  if (bwd) TORCH_CHECK(has(dy), "norm backward needs dy");
+  if (bwd) TORCH_CHECK(has(dy) || has(ab), "norm backward needs dy (or the fused heads' d(alpha, beta))");
   for (const OptT* o : {&y_bf16, &y_f32, &dy, &pre}) {
     if (has(*o)) check_span(**o, M, D, D, "row tensor");
   }
@@ -677,8 +697,12 @@ void norm(bool bwd, at::Tensor x, int64_t ldx, int64_t M, int64_t D, bool rms, d
                           pre_f ? 1 : 0,
                           opt_typed<void>(dx_bf16, at::kBFloat16, "dx_bf16"),
                           opt_typed<float>(dx_f32, at::kFloat, "dx_f32"), opt_typed<float>(dgamma, at::kFloat, "dgamma"),
-                          opt_typed<float>(dbeta, at::kFloat, "dbeta"), cur_stream());
-  TORCH_CHECK(rc == 0, "norm: unsupported arguments (D=", D, ")");
+                          opt_typed<float>(dbeta, at::kFloat, "dbeta"), opt_typed<float>(hw_a, at::kFloat, "hw_a"),
+                          opt_typed<float>(hb_a, at::kFloat, "hb_a"), opt_typed<float>(hw_b, at::kFloat, "hw_b"),
+                          opt_typed<float>(hb_b, at::kFloat, "hb_b"), opt_typed<float>(ab, at::kFloat, "ab"),
+                          (int)ab_rows, opt_typed<float>(g_wa, at::kFloat, "g_wa"),
+                          opt_typed<float>(g_wb, at::kFloat, "g_wb"), cur_stream());
+  TORCH_CHECK(rc == 0, "norm: unsupported arguments (D=", D, ", rc=", rc, ")");
 }
 
 // RoPE (cos, sin) table [T][HD/2] in fp64 -> fp32, built once per (device, T, HD, base) on the first (eager) call;
@@ -1354,10 +1378,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_group_flush", []() { mta_gemm_group_flush(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
+  m.def("pair_colsum", &pair_colsum);
   m.def("norm", &norm, py::arg("bwd"), py::arg("x"), py::arg("ldx"), py::arg("M"), py::arg("D"), py::arg("rms"),
         py::arg("eps"), py::arg("gamma"), py::arg("beta"), py::arg("y_bf16"), py::arg("y_f32"), py::arg("mean"),
         py::arg("rstd"), py::arg("seed"), py::arg("drop_p"), py::arg("dy"), py::arg("dres"), py::arg("pre"),
-        py::arg("dx_bf16"), py::arg("dx_f32"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gelu_x") = false);
+        py::arg("dx_bf16"), py::arg("dx_f32"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gelu_x") = false,
+        py::arg("hw_a") = py::none(), py::arg("hb_a") = py::none(), py::arg("hw_b") = py::none(),
+        py::arg("hb_b") = py::none(), py::arg("ab") = py::none(), py::arg("ab_rows") = 0,
+        py::arg("g_wa") = py::none(), py::arg("g_wb") = py::none());
   m.def("tr_attn_dx", &tr_attn_dx);
   m.def("attention", &attention, py::arg("bwd"), py::arg("qkv"), py::arg("out"), py::arg("lse"), py::arg("dout"),
         py::arg("dqkv"), py::arg("nseq"), py::arg("T"), py::arg("D"), py::arg("heads"), py::arg("rope_base"),

@@ -435,7 +435,7 @@ __device__ __forceinline__ void dma_src(const __bf16* base, int ld, int rows, in
 // diagnostic build (csrc/tools/gemm_probe.hip): s_memtime stamps of the main loop's segments, summed per wave
 #ifdef MTA_STAMPS
 __device__ unsigned long long stamp_acc[8][8];  // [wave][segment]
-__device__ unsigned long long epi2_acc[8];       // MTA_EPI_TWICE: [wave] the second epilogue
+__device__ unsigned long long epi2_acc[8];       // GEMM_PROBE_EPI_TWICE: [wave] the second epilogue
 #define GSTAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #define GACC(i, a, b) dsum[i] += (unsigned)((b) - (a))
 #else
@@ -854,7 +854,7 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 #ifdef MTA_STAMPS
   GSTAMP(tepi0);
 #endif
-#ifdef MTA_EPI_SKIP  // probe build: no epilogue (the accumulators kept live), main loop + launch only
+#ifdef GEMM_PROBE_EPI_SKIP  // probe build: no epilogue (the accumulators kept live), main loop + launch only
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -867,9 +867,9 @@ __device__ __forceinline__ void body(const GemmArgs& g, int bx, int by, int bz, 
 #ifdef MTA_STAMPS
   GSTAMP(tend);
   if (lane == 0) atomicAdd(&stamp_acc[wave][7], (unsigned long long)(unsigned)(tend - tepi0));  // epilogue
-#ifdef MTA_EPI_TWICE  // probe build: the same epilogue again, its code now in the instruction cache
+#ifdef GEMM_PROBE_EPI_TWICE  // probe build: the same epilogue again, its code now in the instruction cache
   GemmArgs g2 = g;
-#ifdef MTA_EPI_TWICE_FRESH  // ... into a second output buffer (pages and lines not touched before)
+#ifdef GEMM_PROBE_EPI_FRESH  // ... into a second output buffer (pages and lines not touched before)
   g2.out_f32 = g.out_f32 ? g.out_f32 + (size_t)g.M * g.ldc : nullptr;
   g2.aux_pre = g.aux_pre ? g.aux_pre + (size_t)g.M * g.ldc : nullptr;
 #endif

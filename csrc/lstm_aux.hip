@@ -56,6 +56,7 @@ __global__ void lstm_prep_kernel(const float* __restrict__ w_ih, const float* __
 // to arrive advances the cursor (every block reads it before arriving, so the update is race-free).
 // ---------------------------------------------------------------------------------------------
 constexpr int GATHER_TPB = 256;
+constexpr int GATHER_SUBS = 64;  // arrival sub-counters (the arrive buffer holds 1 + GATHER_SUBS words)
 constexpr int GATHER_CHUNK = GATHER_TPB * 4;  // float4 per block
 
 struct GatherArgs {
@@ -80,11 +81,12 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
     for (int piece = chunk * a.span; piece < (chunk + 1) * a.span; ++piece) {
       const long lo = (long)piece * GATHER_CHUNK, hi = lo + GATHER_CHUNK < n / 4 ? lo + GATHER_CHUNK : n / 4;
       if (lo >= hi) break;
+      // unconditional loads (clamped index): a guarded load makes hipcc branch around it and wait for each one
       float4 v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long i = lo + r * GATHER_TPB + threadIdx.x;
-        if (i < hi) v[r] = s4[i];
+        v[r] = s4[i < hi ? i : hi - 1];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -99,11 +101,20 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    // two-level arrival: block i adds to sub-counter 1 + i % 64, the last of each sub-counter to the top word, the
+    // last of those advances the cursor -- ~32 adds per word instead of all ~2,048 on one (same-word atomics
+    // serialise at the memory side: the one-word form was ~20 us of the mlp_large B = 64 gather)
     const int total = gridDim.x * gridDim.y;
-    const int prev = atomicAdd(arrive, 1);
-    if (prev == total - 1) {
-      arrive[0] = 0;
-      cursor[0] = cursor[0] + 1;
+    const int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int g = bid % GATHER_SUBS;
+    const int gsize = (total - g + GATHER_SUBS - 1) / GATHER_SUBS;
+    if (atomicAdd(arrive + 1 + g, 1) == gsize - 1) {
+      arrive[1 + g] = 0;
+      const int ng = total < GATHER_SUBS ? total : GATHER_SUBS;
+      if (atomicAdd(arrive, 1) == ng - 1) {
+        arrive[0] = 0;
+        cursor[0] = cursor[0] + 1;
+      }
     }
   }
 }

@@ -60,6 +60,16 @@ struct NormArgs {
   long part_pass;       // floats between the dgamma and dbeta planes
   int gelu_x;           // wide kernels: xb is the bf16 GELU INPUT; the normalised row is gelu(xb) (the MLP's GEMM
                         // then stores only its bf16 pre-activation: no fp32 GELU output written and read back twice)
+  // fused alpha / beta heads of the encoder's last layer (wide kernels): forward ab[row] = (h . wa + ba, h . wb + bb)
+  // of the normalised row h; backward dy = d_alpha wa + d_beta wb from ab[row] = d(alpha, beta) (rows >= ab_rows: 0)
+  // and the head-weight gradients' partial rows (sum over rows of d_alpha h, d_beta h) into hpart
+  const float* hw_a;
+  const float* hw_b;
+  const float* hb_a;
+  const float* hb_b;
+  float2* ab;
+  int ab_rows;
+  float* hpart;
 };
 
 __device__ __forceinline__ float4 gelu4(float4 v) {
@@ -161,16 +171,22 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
   // grid-strided rows (~4 workgroups per CU): gamma / beta loaded once per workgroup instead of once per row, and
   // the next row's loads issued before the current row's reductions (one HBM round trip per row hidden)
   __shared__ float red[2][2][4];  // [row parity][mean / var][wave]
+  __shared__ float redh[2][2][4];  // [row parity][alpha / beta][wave] (fused heads)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float invD = 1.0f / (float)a.D;
-  float4 gm[VPT], bt[VPT], v[VPT], vn[VPT];
+  const bool heads = a.ab != nullptr;
+  float4 gm[VPT], bt[VPT], v[VPT], vn[VPT], wa4[VPT], wb4[VPT];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     const bool ok = c < a.D;
     gm[i] = (ok && a.gamma) ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
     bt[i] = (ok && a.beta) ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // head weights: slices of the flat parameter buffer (no alignment to rely on)
+    wa4[i] = (ok && heads) ? make_float4(a.hw_a[c], a.hw_a[c + 1], a.hw_a[c + 2], a.hw_a[c + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    wb4[i] = (ok && heads) ? make_float4(a.hw_b[c], a.hw_b[c + 1], a.hw_b[c + 2], a.hw_b[c + 3]) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  const float hba = heads ? a.hb_a[0] : 0.f, hbb = heads ? a.hb_b[0] : 0.f;
   const uint64_t seed = a.seed ? *a.seed : 0ull;
   int row = blockIdx.x;
   if (row >= a.M) return;
@@ -215,6 +231,7 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
       if (a.mean) a.mean[row] = mu;
       a.rstd[row] = rs;
     }
+    float pa = 0.f, pb = 0.f;  // fused heads: this thread's share of h . wa, h . wb
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
       const int c = 4 * (tid + NT_THREADS * i);
@@ -225,6 +242,10 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
       if (a.seed) mta_dropout_scale4(seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = ((xs[j] - mu) * rs * gs[j] + bs[j]) * ds4[j];
+      if (heads) {
+        pa += (o[0] * wa4[i].x + o[1] * wa4[i].y) + (o[2] * wa4[i].z + o[3] * wa4[i].w);
+        pb += (o[0] * wb4[i].x + o[1] * wb4[i].y) + (o[2] * wb4[i].z + o[3] * wb4[i].w);
+      }
       if (a.y_f32) *reinterpret_cast<float4*>(a.y_f32 + (size_t)row * a.D + c) = make_float4(o[0], o[1], o[2], o[3]);
       if (a.y_bf16) {
         bf16x4 b;
@@ -232,6 +253,18 @@ __global__ __launch_bounds__(NT_THREADS) void norm_fwd_wide_kernel(NormArgs a) {
         for (int j = 0; j < 4; ++j) b[j] = (__bf16)o[j];
         *reinterpret_cast<bf16x4*>(a.y_bf16 + (size_t)row * a.D + c) = b;
       }
+    }
+    if (heads) {  // uniform: one more row reduction (fixed wave order)
+      pa = wave_sum(pa);
+      pb = wave_sum(pb);
+      if (lane == 0) {
+        redh[par][0][wave] = pa;
+        redh[par][1][wave] = pb;
+      }
+      __syncthreads();
+      if (tid == 0)
+        a.ab[row] = make_float2(((redh[par][0][0] + redh[par][0][1]) + (redh[par][0][2] + redh[par][0][3])) + hba,
+                                ((redh[par][1][0] + redh[par][1][1]) + (redh[par][1][2] + redh[par][1][3])) + hbb);
     }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) v[i] = vn[i];
@@ -369,21 +402,24 @@ struct FastRow {
   typename std::conditional<B16, bf16x4, float4>::type x[VPT], dy[VPT];
   bf16x4 pre[VPT];
   float mu, rs;
+  float2 dab;  // HD: d(alpha, beta) of the row
 };
 
 // GX: the row is gelu(pre) (NormArgs::gelu_x): no x load, x recomputed from the pre-activation the GELU' needs anyway
-template <int VPT, bool B16, bool GX>
+// HD: the row's dy is d_alpha wa + d_beta wb (fused heads): only d(alpha, beta) loaded
+template <int VPT, bool B16, bool GX, bool HD>
 __device__ __forceinline__ void fast_load(const NormArgs& a, const float* mean, int row, FastRow<VPT, B16>& r) {
   const int tid = threadIdx.x;
+  if constexpr (HD) r.dab = a.ab[min(row, a.ab_rows - 1)];  // rows past ab_rows: zeroed at use
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     if constexpr (B16) {
       if constexpr (!GX) r.x[i] = *reinterpret_cast<const bf16x4*>(a.xb + (size_t)row * a.ldx + c);
-      r.dy[i] = *reinterpret_cast<const bf16x4*>(a.dyb + (size_t)row * a.D + c);
+      if constexpr (!HD) r.dy[i] = *reinterpret_cast<const bf16x4*>(a.dyb + (size_t)row * a.D + c);
     } else {
       if constexpr (!GX) r.x[i] = *reinterpret_cast<const float4*>(a.x + (size_t)row * a.ldx + c);
-      r.dy[i] = *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c);
+      if constexpr (!HD) r.dy[i] = *reinterpret_cast<const float4*>(a.dy + (size_t)row * a.D + c);
     }
     r.pre[i] = *reinterpret_cast<const bf16x4*>(a.pre + (size_t)row * a.D + c);
   }
@@ -401,34 +437,39 @@ __device__ __forceinline__ void fast_f4(const typename std::conditional<B16, bf1
   }
 }
 
-template <int VPT, bool B16, bool GX>
+template <int VPT, bool B16, bool GX, bool HD>
 __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs a, int rows_per_block) {
   __shared__ float red[2][2][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const float invD = 1.0f / (float)a.D;
   const uint64_t seed = a.seed ? *a.seed : 0ull;
   const float* mean = a.rms ? a.rstd : a.mean;
-  float4 gm[VPT];
-  float dg[VPT][4], db[VPT][4];
+  float4 gm[VPT], bt[VPT], wa4[VPT], wb4[VPT];
+  float dg[VPT][4], db[VPT][4], gwa[VPT][4], gwb[VPT][4];
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int c = 4 * (tid + NT_THREADS * i);
     gm[i] = a.gamma ? *reinterpret_cast<const float4*>(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+    if constexpr (HD) {
+      bt[i] = a.beta ? *reinterpret_cast<const float4*>(a.beta + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      wa4[i] = make_float4(a.hw_a[c], a.hw_a[c + 1], a.hw_a[c + 2], a.hw_a[c + 3]);
+      wb4[i] = make_float4(a.hw_b[c], a.hw_b[c + 1], a.hw_b[c + 2], a.hw_b[c + 3]);
+    }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = 0.f;
+    for (int j = 0; j < 4; ++j) dg[i][j] = db[i][j] = gwa[i][j] = gwb[i][j] = 0.f;
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(a.M, r0 + rows_per_block);
   if (r0 >= r1) return;
   FastRow<VPT, B16> rb[3];
-  fast_load<VPT, B16, GX>(a, mean, r0, rb[0]);
-  fast_load<VPT, B16, GX>(a, mean, min(r0 + 1, r1 - 1), rb[1]);
+  fast_load<VPT, B16, GX, HD>(a, mean, r0, rb[0]);
+  fast_load<VPT, B16, GX, HD>(a, mean, min(r0 + 1, r1 - 1), rb[1]);
   for (int base = r0; base < r1; base += 3) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const int row = base + k;
       if (row >= r1) break;
-      fast_load<VPT, B16, GX>(a, mean, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
+      fast_load<VPT, B16, GX, HD>(a, mean, min(row + 2, r1 - 1), rb[(k + 2) % 3]);
       const FastRow<VPT, B16>& cur = rb[k];
       const float mu = a.rms ? 0.f : cur.mu;
       float xh[VPT][4], g[VPT][4], gd[VPT][4];  // gd: GELU' (GX: computed with the GELU itself)
@@ -443,7 +484,16 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
         } else {
           fast_f4<B16>(cur.x[i], xs);
         }
-        fast_f4<B16>(cur.dy[i], ds);
+        float2 dab = make_float2(0.f, 0.f);
+        if constexpr (HD) {
+          dab = row < a.ab_rows ? cur.dab : make_float2(0.f, 0.f);
+          ds[0] = dab.x * wa4[i].x + dab.y * wb4[i].x;
+          ds[1] = dab.x * wa4[i].y + dab.y * wb4[i].y;
+          ds[2] = dab.x * wa4[i].z + dab.y * wb4[i].z;
+          ds[3] = dab.x * wa4[i].w + dab.y * wb4[i].w;
+        } else {
+          fast_f4<B16>(cur.dy[i], ds);
+        }
         const float gs[4] = {gm[i].x, gm[i].y, gm[i].z, gm[i].w};
         float ds4[4] = {1.f, 1.f, 1.f, 1.f};
         if (a.seed) mta_dropout_scale4(seed, (uint32_t)row, (uint32_t)c, a.drop_p, ds4);
@@ -451,6 +501,12 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
         for (int j = 0; j < 4; ++j) {
           float d = ds[j] * ds4[j];
           xh[i][j] = (xs[j] - mu) * cur.rs;
+          if constexpr (HD) {  // the head input h = (xhat gamma + beta) * dropout scale
+            const float bs4[4] = {bt[i].x, bt[i].y, bt[i].z, bt[i].w};
+            const float hv = fmaf(xh[i][j], gs[j], bs4[j]) * ds4[j];
+            gwa[i][j] = fmaf(dab.x, hv, gwa[i][j]);
+            gwb[i][j] = fmaf(dab.y, hv, gwb[i][j]);
+          }
           db[i][j] += d;
           dg[i][j] += d * xh[i][j];
           g[i][j] = d * gs[j];
@@ -485,6 +541,16 @@ __global__ __launch_bounds__(NT_THREADS) void norm_bwd_wide_fast_kernel(NormArgs
       }
     }
   }
+  if constexpr (HD) {
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+      const int c = 4 * (tid + NT_THREADS * i);
+      *reinterpret_cast<float4*>(a.hpart + (long)blockIdx.x * a.part_ld + c) =
+          make_float4(gwa[i][0], gwa[i][1], gwa[i][2], gwa[i][3]);
+      *reinterpret_cast<float4*>(a.hpart + a.part_pass + (long)blockIdx.x * a.part_ld + c) =
+          make_float4(gwb[i][0], gwb[i][1], gwb[i][2], gwb[i][3]);
+    }
+  }
   if (!a.dgamma && !a.dbeta) return;
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
@@ -507,6 +573,7 @@ constexpr int NORM_FWD_WIDE_BLOCKS = 1024;
 constexpr int NORM_BWD_NARROW_BLOCKS = 1024;
 // per-block column partials of dgamma / dbeta (static: no allocation, graph-capture safe; stream-ordered use)
 __device__ float mta_norm_part[2][NORM_BWD_MAX_BLOCKS][2048];
+__device__ float mta_norm_hpart[2][NORM_BWD_MAX_BLOCKS][2048];  // fused heads: head-weight gradient partial rows
 // deferred reductions (D <= NORM_DEFER_D): each backward call gets its own slot and ONE batched launch sums every
 // pending slot at the end of the encoder backward (9 launches -> 1 for the 4-layer transformer)
 constexpr int NORM_DEFER_SLOTS = 12, NORM_DEFER_D = 256;
@@ -663,8 +730,10 @@ __global__ __launch_bounds__(1024) void norm_param_reduce_wide_kernel(float* __r
 // 64 B per wave instruction, wave sums by a fixed xor tree, block sum in wave order (deterministic).  The 64-column
 // form (64 blocks, 4 B per lane) took 8.3 us per call at mlp_large; a two-level form with a last-arriver ticket
 // 12.9 us (its agent-scope release writes back the XCD's dirty L2 behind the norm backward) (r3 traces).
+// part: a [2][NORM_BWD_MAX_BLOCKS][2048] partial region (mta_norm_part, or mta_norm_hpart for the fused heads)
 __global__ __launch_bounds__(1024) void norm_param_reduce_cols_kernel(float* __restrict__ dgamma,
-                                                                      float* __restrict__ dbeta, int D, int blocks) {
+                                                                      float* __restrict__ dbeta, int D, int blocks,
+                                                                      const float* __restrict__ part) {
   __shared__ float4 red[16][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x * 16 + 4 * (lane & 3);  // over [0, 2D); D % 16 == 0: a block never straddles the planes
@@ -673,7 +742,7 @@ __global__ __launch_bounds__(1024) void norm_param_reduce_cols_kernel(float* __r
   if (dst == nullptr) return;  // uniform over the block
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int b = wave * 16 + (lane >> 2); b < blocks; b += 256) {
-    const float4 v = *reinterpret_cast<const float4*>(&mta_norm_part[pass][b][col]);
+    const float4 v = *reinterpret_cast<const float4*>(part + ((size_t)pass * NORM_BWD_MAX_BLOCKS + b) * 2048 + col);
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
 #pragma unroll
@@ -798,7 +867,8 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
                         const float* gamma, const float* beta, void* y_bf16, float* y_f32, float* mean, float* rstd,
                         const uint64_t* seed, float drop_p, const void* dy, int dy_bf16, const float* dres,
                         const void* pre, int pre_f32, void* dx_bf16, float* dx_f32, float* dgamma, float* dbeta,
-                        hipStream_t st) {
+                        const float* hw_a, const float* hb_a, const float* hw_b, const float* hb_b, float* ab,
+                        int ab_rows, float* g_wa, float* g_wb, hipStream_t st) {
   if (D % 4 || ldx % 4 || D > 2048) return 1;
   // fp32 GELU input (32-true extras): the one-wave-per-row kernels (the wide ones stage pre as bf16)
   const bool wide_ok = D >= 1024 && !(pre && pre_f32);
@@ -807,6 +877,15 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   a.x = x_bf16 ? nullptr : static_cast<const float*>(x);
   a.xb = x_bf16 ? static_cast<const __bf16*>(x) : nullptr;
   a.gelu_x = x_bf16 == 2;  // 2: x is the bf16 GELU input (wide kernels)
+  a.hw_a = hw_a;
+  a.hw_b = hw_b;
+  a.hb_a = hb_a;
+  a.hb_b = hb_b;
+  a.ab = reinterpret_cast<float2*>(ab);
+  a.ab_rows = ab_rows;
+  // fused heads: wide kernels only; the backward form is the GELU-on-load fast one, into both head gradients
+  if (ab && !(wide_ok && hw_a && hw_b && (bwd ? (a.gelu_x && g_wa && g_wb && ab_rows > 0) : (hb_a && hb_b))))
+    return 4;
   if (a.gelu_x && !(wide_ok && (!bwd || (pre && !pre_f32 && !dres && (D == 1024 || D == 2048))))) return 3;
   a.ldx = ldx;
   a.M = M;
@@ -878,9 +957,19 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
       const bool b16 = a.gelu_x ? a.dyb != nullptr : a.xb != nullptr;
       const bool fast = a.pre && !a.dres && (a.gelu_x || b16 == (a.dyb != nullptr)) &&
                         (D == 1024 || D == 2048) && (a.rms || a.mean);
-#define NORM_FAST(V, B)                                                                                   \
-  if (a.gelu_x) norm_bwd_wide_fast_kernel<V, B, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block); \
-  else norm_bwd_wide_fast_kernel<V, B, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
+      if (bwd && a.ab && !fast) return 4;
+      if (bwd && a.ab) {
+        static float* hbase = [] {
+          float* p = nullptr;
+          (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_hpart));
+          return p;
+        }();
+        a.hpart = hbase;
+      }
+#define NORM_FAST(V, B)                                                                                          \
+  if (a.ab) norm_bwd_wide_fast_kernel<V, B, true, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);       \
+  else if (a.gelu_x) norm_bwd_wide_fast_kernel<V, B, true, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block); \
+  else norm_bwd_wide_fast_kernel<V, B, false, false><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);
       if (bwd && fast) {
         if (D == 1024) {
           if (b16) { NORM_FAST(1, true) } else { NORM_FAST(1, false) }
@@ -913,12 +1002,44 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
 #undef NORM_LAUNCH
   if (bwd && (dgamma || dbeta) && wide) {
     if (D % 16 == 0)
-      norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
+      norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(dgamma, dbeta, D, blocks, a.part);
     else
       norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
   } else if (bwd && (dgamma || dbeta) && !defer)
     norm_param_reduce_kernel<<<(2 * D + 3) / 4, 256, 0, st>>>(dgamma, dbeta, D, blocks);
+  if (bwd && a.ab)  // the head weights' gradients (D in {1024, 2048}: the column-block reduction)
+    norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(g_wa, g_wb, D, blocks, a.hpart);
   return 0;
+}
+
+// sa += sum_i ab[i].x, sb += sum_i ab[i].y (the fused heads' bias gradients): one 1,024-thread workgroup, fixed
+// order (thread-strided partials, then wave-order block sum): bit-reproducible
+__global__ __launch_bounds__(1024) void pair_colsum_kernel(const float2* __restrict__ ab, int n, float* sa, float* sb) {
+  __shared__ float part[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float x = 0.f, y = 0.f;
+  for (int i = tid; i < n; i += 1024) {
+    const float2 v = ab[i];
+    x += v.x;
+    y += v.y;
+  }
+  x = wave_sum(x);
+  y = wave_sum(y);
+  if (lane == 0) {
+    part[0][wave] = x;
+    part[1][wave] = y;
+  }
+  __syncthreads();
+  if (tid < 2) {
+    float t = 0.f;
+    for (int w = 0; w < 16; ++w) t += part[tid][w];
+    if (tid == 0) sa[0] += t;
+    else sb[0] += t;
+  }
+}
+
+extern "C" void mta_pair_colsum(const float* ab, int n, float* sa, float* sb, hipStream_t st) {
+  pair_colsum_kernel<<<1, 1024, 0, st>>>(reinterpret_cast<const float2*>(ab), n, sa, sb);
 }
 
 // the next mta_norm backward call defers its parameter reduction to mta_norm_flush

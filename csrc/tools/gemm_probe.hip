@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
   float* C;
   CK(hipMalloc(&A, (size_t)M * K * 2));
   CK(hipMalloc(&B, (size_t)N * K * 2));
-  CK(hipMalloc(&C, (size_t)M * N * 4 * 2));  // x2: MTA_EPI_TWICE_FRESH
+  CK(hipMalloc(&C, (size_t)M * N * 4 * 2));  // x2: GEMM_PROBE_EPI_FRESH
   __bf16* pre = nullptr;
   float* bias = nullptr;
   if (epi) {
@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
       printf(" %7.0f", (double)acc[w][i] / blocks / (i == 7 ? 1 : (i == 6 ? 1 : nk)) / (i == 6 ? nk : 1));
     printf("\n");
   }
-#ifdef MTA_EPI_TWICE
+#ifdef GEMM_PROBE_EPI_TWICE
   unsigned long long e2[8];
   CK(hipMemcpyFromSymbol(e2, HIP_SYMBOL(big::epi2_acc), sizeof(e2)));
   printf("%-12s", "epilogue2");  // accumulated over the 24 timed + warm-up runs: per tile and run

@@ -22,7 +22,7 @@ from torch import Tensor
 
 from ..ops import extras as xops
 from ..ops._lib import use_hip
-from ..ops.losses import heads_losses_train, train_decoder_fits
+from ..ops.losses import decoder_losses, heads_losses_train, train_decoder_fits
 from . import register_model_class
 from .lstm import FinancialLstmCombined, FinancialLstmMse, FinancialLstmNll
 
@@ -168,6 +168,25 @@ def _make(base, arch: str):
         self.encoder.precision = self.matmul_precision
         return self.encoder(x)
 
+    def _losses(self, batch, want_nll: bool, acc, coeffs=None):
+        """The MLP's bf16 HIP path with the alpha / beta heads fused into its last norm kernels
+        (``ops.extras.mlp_encode_heads``: no h / dh round trip, no separate head kernels) and the losses on the
+        resulting (N, 2) ``ab`` (``ops.losses.decoder_losses``); every other case: the reference composition."""
+        enc = getattr(self, "encoder", None)
+        if arch != "mlp" or self.backend == "torch":
+            return base._losses(self, batch, want_nll, acc, coeffs)
+        context, target, factor, inv_psi, B = self._unpack(batch)
+        enc.precision = self.matmul_precision
+        params = enc.flat_params()
+        if not xops.mlp_heads_fusable(context, params, enc.num_layers, enc.norm, enc.precision):
+            return base._losses(self, batch, want_nll, acc, coeffs)
+        heads = (self.alpha_head.weight, self.alpha_head.bias, self.beta_head.weight, self.beta_head.bias)
+        ab = xops.mlp_encode_heads(context, params, enc.seeds, enc.num_layers, enc.norm, enc.dropout, enc.training,
+                                   enc.precision, heads)
+        c_nll, c_mse = coeffs if coeffs is not None else self.loss_coefficients
+        return decoder_losses(ab, target, factor, inv_psi, batch_windows=B, want_nll=want_nll,
+                              nll_mode=self.nll_mode, c_nll=c_nll, c_mse=c_mse, acc=acc.acc, with_total=True)
+
     def fused_step_supported(self, batch) -> bool:
         """The training step as [encoder forward (HIP autograd Function), the one-launch decoder (losses, metrics,
         dh, head grads: ops.losses.heads_losses_train), encoder backward from dh]: two decoder launches (the
@@ -205,7 +224,8 @@ def _make(base, arch: str):
         self._log_stage("train", self.train_acc, self.train_log_names)
         return out[3]
 
-    cls = type(name, (base,), {"__init__": __init__, "encode": encode, "fused_step_supported": fused_step_supported,
+    cls = type(name, (base,), {"__init__": __init__, "encode": encode, "_losses": _losses,
+                               "fused_step_supported": fused_step_supported,
                                "fused_training_step": fused_training_step,
                                "__doc__": f"{base.__name__} with the {arch} encoder (north-star extra)."})
     return cls

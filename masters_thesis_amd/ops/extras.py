@@ -159,8 +159,16 @@ def mlp_reference(x: Tensor, params: Sequence[Tensor], num_layers: int, norm: st
 
 
 class _MlpEncoderFn(torch.autograd.Function):
+    """bf16 MLP encoder.  ``n_heads`` = 4: the last four of ``params`` are the alpha / beta heads (wa, ba, wb, bb)
+    and they are FUSED into the last layer's norm kernels (csrc/norm.hip NormArgs::ab): the forward returns
+    ab = [h wa^T + ba | h wb^T + bb] (N, 2) without writing h, the backward takes d(ab) and forms the last layer's dy =
+    d_alpha wa + d_beta wb on the fly, accumulating the head-weight gradients from h recomputed as xhat gamma + beta
+    -- the heads kernel, the head backward kernel, and h / dh written and read back (52 MB each for mlp_large) go."""
+
     @staticmethod
-    def forward(ctx, x, seeds, num_layers, norm, dropout, training, need_grad, *params):
+    def forward(ctx, x, seeds, num_layers, norm, dropout, training, need_grad, n_heads, *params):
+        heads = params[len(params) - n_heads:] if n_heads else None
+        params = params[:len(params) - n_heads]
         dev = x.device
         N = x.shape[0]
         Mp = _r16(N)
@@ -196,12 +204,18 @@ class _MlpEncoderFn(torch.autograd.Function):
             rstd = torch.empty(Mp, device=dev, dtype=torch.float32)
             last = i == L - 1
             y = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16) if not last else None
-            if last:
+            hk = {}
+            if last and heads is not None:
+                assert act is None, "fused heads need the GELU-on-load norm (ops.extras._gelu_in_norm)"
+                h = None
+                ab = torch.empty((Mp, 2), device=dev, dtype=torch.float32)
+                hk = dict(hw_a=heads[0], hb_a=heads[1], hw_b=heads[2], hb_b=heads[3], ab=ab)
+            elif last:
                 h = torch.empty((Mp, D), device=dev, dtype=torch.float32)
             lib().norm(False, pre if act is None else act, D, Mp, D, rms, RMS_EPS if rms else LN_EPS,
                        params[per * i + 2], None if rms else params[per * i + 3], y, h if last else None, mean, rstd,
                        seeds[i:i + 1] if (drop and not last) else None, float(dropout), None, None, None, None, None,
-                       None, None, gelu_x=act is None)
+                       None, None, gelu_x=act is None, **hk)
             pres.append(pre)
             acts.append(act)
             means.append(mean)
@@ -210,12 +224,13 @@ class _MlpEncoderFn(torch.autograd.Function):
                 Xs.append(y)
         ctx.meta = (N, Mp, L, per, rms, drop, float(dropout), dims, kp)
         ctx.params = params
+        ctx.heads = heads
         ctx.wb = wb
         ctx.seeds = seeds
         if need_grad:
             ctx.save_for_backward(*Xs, *pres, *acts)
             ctx.stats = (means, rstds)
-        return h[:N]
+        return ab[:N] if heads is not None else h[:N]
 
     @staticmethod
     @torch.autograd.function.once_differentiable
@@ -226,8 +241,12 @@ class _MlpEncoderFn(torch.autograd.Function):
         Xs, pres, acts = saved[:L], saved[L:2 * L], saved[2 * L:]
         means, rstds = ctx.stats
         dev = dh.device
+        heads = ctx.heads
         base = dh._base
-        if Mp == N and dh.dtype == torch.float32 and dh.is_contiguous():
+        if heads is not None:
+            dab = dh.contiguous().float()  # d(alpha, beta): the last layer's dy is formed in its norm kernel
+            dy = None
+        elif Mp == N and dh.dtype == torch.float32 and dh.is_contiguous():
             dy = dh  # read-only below: no zero-fill + copy of the output gradient
         elif (getattr(base, "_mta_zero_pad", False) and base.shape == (Mp, dims[-1]) and base.is_contiguous()
               and dh.data_ptr() == base.data_ptr() and dh.shape[0] == N):
@@ -240,11 +259,19 @@ class _MlpEncoderFn(torch.autograd.Function):
             D, Din = dims[i + 1], dims[i]
             dpre = torch.empty((Mp, D), device=dev, dtype=torch.bfloat16)
             dropped = drop and i < L - 1
+            hk = {}
+            if heads is not None and i == L - 1:
+                wa, ba, wb_, bb = heads
+                hk = dict(hw_a=wa, hb_a=ba, hw_b=wb_, hb_b=bb, ab=dab, ab_rows=N, g_wa=_grad_view(wa),
+                          g_wb=_grad_view(wb_))
             lib().norm(True, pres[i] if acts[i] is None else acts[i], D, Mp, D, rms, RMS_EPS if rms else LN_EPS,
                        params[per * i + 2], None if rms else params[per * i + 3], None, None, means[i], rstds[i],
                        ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], dpre, None,
                        _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]),
-                       gelu_x=acts[i] is None)
+                       gelu_x=acts[i] is None, **hk)
+            if hk:  # head biases: ordered column sums of d(alpha, beta)
+                lib().pair_colsum(dab, N, _grad_view(ba), _grad_view(bb))
+                grad_ready(wa.grad, ba.grad, wb_.grad, bb.grad)
             # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre).  A big dW_i is
             # a gradient PRODUCER of the fused optimizer (ops/optim.py register_grad_producer): its split-K reduce
             # overwrites the range and leaves the clip-norm partials, so the update neither zeroes nor re-reads it
@@ -260,7 +287,7 @@ class _MlpEncoderFn(torch.autograd.Function):
             # W_i, b_i final (their GEMM is launched: deferred ones go with the input-gradient GEMM above)
             grad_ready(params[per * i].grad, params[per * i + 1].grad)
         gemm_flush()
-        return (None,) * (7 + len(params))
+        return (None,) * (8 + len(params) + (4 if heads is not None else 0))
 
 
 # --------------------------------------------------------------------------------------------------
@@ -354,12 +381,34 @@ def mlp_encode(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num
     if use_hip(x) and precision == "medium":
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _MlpEncoderFn.apply(x.contiguous(), seeds, num_layers, norm, float(dropout), bool(training),
-                                   need_grad, *params)
+                                   need_grad, 0, *params)
     if use_hip(x) and precision in _F32_PREC and not _F32_TORCH:
         need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         return _MlpEncoderF32Fn.apply(x.contiguous().float(), seeds, num_layers, norm, float(dropout), bool(training),
                                       need_grad, _F32_PREC[precision], *params)
     return mlp_reference(x, params, num_layers, norm, dropout, training)
+
+
+def mlp_heads_fusable(x: Tensor, params: Sequence[Tensor], num_layers: int, norm: str, precision: str) -> bool:
+    """Whether :func:`mlp_encode_heads` fuses the alpha / beta heads into the last norm (bf16 HIP path, last width
+    taking the GELU-on-load wide kernels)."""
+    per = 4 if norm == "layernorm" else 3
+    return (use_hip(x) and precision == "medium" and num_layers >= 1
+            and _gelu_in_norm(int(params[per * (num_layers - 1)].shape[0])))
+
+
+def mlp_encode_heads(x: Tensor, params: Sequence[Tensor], seeds: Optional[Tensor], num_layers: int, norm: str,
+                     dropout: float, training: bool, precision: str, heads: Sequence[Tensor]) -> Tensor:
+    """``[alpha | beta]`` (N, 2) of the MLP encoder followed by the two Linear(H, 1) heads (``heads`` = (wa (1, H),
+    ba (1,), wb, bb)): fused into the last norm kernels when :func:`mlp_heads_fusable`, else encoder + addmm."""
+    if mlp_heads_fusable(x, params, num_layers, norm, precision):
+        all_p = list(params) + list(heads)
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in all_p)
+        return _MlpEncoderFn.apply(x.contiguous(), seeds, num_layers, norm, float(dropout), bool(training),
+                                   need_grad, 4, *all_p)
+    h = mlp_encode(x, params, seeds, num_layers, norm, dropout, training, precision)
+    wa, ba, wb, bb = heads
+    return torch.addmm(torch.cat([ba, bb]), h, torch.cat([wa, wb], 0).t())
 
 
 _F32_TORCH = os.environ.get("MTA_EXTRAS_F32_TORCH", "0") == "1"

@@ -296,6 +296,43 @@ def test_norm_gelu_on_load(rms, D):
         assert _rel(dbet, gb) < 1e-4
 
 
+@pytest.mark.parametrize("norm", ["layernorm", "rmsnorm"])
+def test_mlp_fused_heads_match_unfused(norm):
+    """The alpha / beta heads fused into the MLP's last norm kernels (ops.extras.mlp_encode_heads: ab from the
+    normalised rows in-kernel, dy = d_alpha wa + d_beta wb formed in the norm backward, head-weight gradients from h
+    recomputed there) against the same bf16 encoder returning h followed by an fp32 addmm and autograd: ab, every
+    encoder gradient and the four head gradients.  N = 300 exercises the 16-row padding (pad rows: zero d(ab))."""
+    from masters_thesis_amd.models.extras import MLPEncoder
+    from masters_thesis_amd.ops import extras as X
+
+    torch.manual_seed(7)
+    N, T, F, H, L = 300, 60, 3, 1024, 2
+    enc = MLPEncoder(F, T, H, L, 0.0, norm).to(DEV)
+    x = torch.randn(N, T, F, device=DEV)
+    heads = [torch.randn(1, H, device=DEV) * 0.03, torch.randn(1, device=DEV) * 0.1,
+             torch.randn(1, H, device=DEV) * 0.03, torch.randn(1, device=DEV) * 0.1]
+    heads = [t.requires_grad_(True) for t in heads]
+    G = torch.randn(N, 2, device=DEV)
+    params = enc.flat_params()
+    assert X.mlp_heads_fusable(x, params, L, norm, "medium")
+    runs = []
+    for fused in (True, False):
+        for t in list(params) + heads:
+            t.grad = None
+        if fused:
+            ab = X.mlp_encode_heads(x, params, enc.seeds, L, norm, 0.0, True, "medium", heads)
+        else:
+            h = X.mlp_encode(x, params, enc.seeds, L, norm, 0.0, True, "medium")
+            ab = torch.addmm(torch.cat([heads[1], heads[3]]), h, torch.cat([heads[0], heads[2]], 0).t())
+        (ab * G).sum().backward()
+        torch.cuda.synchronize()
+        runs.append((ab.detach().clone(), [t.grad.detach().clone() for t in list(params) + heads]))
+    (ab_f, g_f), (ab_u, g_u) = runs
+    assert _rel(ab_f, ab_u) < 1e-5
+    for k, (a, b) in enumerate(zip(g_f, g_u)):
+        assert _rel(a, b) < (1e-5 if k >= len(params) else 2e-3), (k, _rel(a, b))
+
+
 @pytest.mark.parametrize("T,heads,hd", [(60, 4, 32), (64, 2, 64), (17, 3, 32)])
 def test_attention_forward_backward(T, heads, hd):
     from masters_thesis_amd.ops import _lib
