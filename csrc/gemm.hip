@@ -1306,6 +1306,7 @@ struct Pending {
 
 // weight gradients queued for one grouped launch per layout (kind 0: k-contiguous operands, 1: [K][rows] operands)
 constexpr int GROUP_QMAX = 48;
+constexpr long GROUP_SMALL_OUT = 512L * 512;  // outputs this small are always grouped (any K)
 struct GroupQueue {
   GemmArgs g[2][GROUP_QMAX];
   int ks[2][GROUP_QMAX];  // requested split: 1 = none (deterministic mode), else chosen at the flush
@@ -1443,7 +1444,10 @@ int gemm_bf16_impl(int mode, const void* A, const void* B, int M, int N, int K, 
   if (defer == 2) {
     // a weight gradient queued for the grouped launch at mta_gemm_group_flush (too big for the 64 x 64 tiles: now)
     if (!(mode == 2 || (mode == 0 && (flags & EPI_ACCUM)))) return 8;
-    if (big_eligible(g, ksplit) || (long)M * N * K >= (1L << 31)) {
+    // small outputs (the transformer's <= 512 x 512 weights) stay grouped whatever K: at B = 8 (K = 50,176 tokens)
+    // the 256 x 256 kernel re-split them ~128 ways into fp32 slabs, and the 16 slab reduces per step cost more than
+    // the products (splitk_reduce 35 us each, profiles/r5_transformer_b8_grouped_wgrad.txt)
+    if ((big_eligible(g, ksplit) || (long)M * N * K >= (1L << 31)) && (long)M * N > GROUP_SMALL_OUT) {
       dispatch_mode(mode, g, ksplit, st);
       return 0;
     }
