@@ -203,8 +203,19 @@ def decoder_losses(ab: Tensor, y: Tensor, factor: Tensor, inv_psi: Tensor, *, ba
     return res if with_total else res[:3]
 
 
+# Above this many sequences the one-workgroup training decoder loses to the grid decoder path (heads / losses /
+# head-backward kernels over the whole chip): at N = 800 (B = 8 windows) heads_losses_train_kernel took 185 us per
+# step; with the grid path the LSTM small B = 8 step went 0.349 -> 0.334 ms, the combined-loss one 0.421 -> 0.403,
+# transformer B = 8 2.186 -> 2.133 (profiles/r5_decoder_maxn_ab.txt, cap 256: B <= 2 windows keep the one-launch
+# decoder and with it the LSTM's 4-launch fused step; the register-resident decoder covers N <= 128).
+TRAIN_DECODER_MAX_N = 256
+
+
 def train_decoder_fits(N: int, n: int, H: int = 0) -> bool:
-    """Whether :func:`heads_losses_train`'s one-workgroup kernel takes (N sequences, n target days)."""
+    """Whether :func:`heads_losses_train`'s one-workgroup kernel takes (N sequences, n target days) -- and is the
+    faster choice (N <= :data:`TRAIN_DECODER_MAX_N`)."""
+    if N > TRAIN_DECODER_MAX_N:
+        return False
     ut = ((n + 3) & ~3) + 16 * n  # u_t + one partial row per wave (csrc/losses.hip ut_floats)
     base = (3 * 2 * ((N + 1) & ~1) + ((ut + 3) & ~3)) * 4
     return base + N * n * 8 + N * H * 4 <= 96 * 1024 or base <= 60 * 1024
