@@ -334,7 +334,7 @@ void gather_batch(std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::
   TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 tensors");
   TORCH_CHECK(perm.scalar_type() == at::kInt && cursor.scalar_type() == at::kInt && arrive.scalar_type() == at::kInt,
               "perm/cursor/arrive must be int32");
-  TORCH_CHECK(arrive.is_cuda() && arrive.numel() >= 65, "arrive: 65 int32 words (top + 64 sub-counters)");
+  TORCH_CHECK(arrive.is_cuda() && arrive.numel() >= 65 * 32, "arrive: 65 x 32 int32 words (top + 64 sub-counters, one line each)");
   const float* s[4];
   float* d[4];
   long rf[4];

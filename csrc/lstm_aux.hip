@@ -56,7 +56,8 @@ __global__ void lstm_prep_kernel(const float* __restrict__ w_ih, const float* __
 // to arrive advances the cursor (every block reads it before arriving, so the update is race-free).
 // ---------------------------------------------------------------------------------------------
 constexpr int GATHER_TPB = 256;
-constexpr int GATHER_SUBS = 64;  // arrival sub-counters (the arrive buffer holds 1 + GATHER_SUBS words)
+constexpr int GATHER_SUBS = 64;        // arrival sub-counters
+constexpr int GATHER_SUB_STRIDE = 32;  // ints between counters: the arrive buffer holds (1 + GATHER_SUBS) x 32 words
 constexpr int GATHER_CHUNK = GATHER_TPB * 4;  // float4 per block
 
 struct GatherArgs {
@@ -108,8 +109,9 @@ __global__ __launch_bounds__(GATHER_TPB) void gather_batch_kernel(GatherArgs a, 
     const int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int g = bid % GATHER_SUBS;
     const int gsize = (total - g + GATHER_SUBS - 1) / GATHER_SUBS;
-    if (atomicAdd(arrive + 1 + g, 1) == gsize - 1) {
-      arrive[1 + g] = 0;
+    int* sub = arrive + GATHER_SUB_STRIDE * (1 + g);  // one 128-B line per sub-counter (same-line atomics serialise)
+    if (atomicAdd(sub, 1) == gsize - 1) {
+      sub[0] = 0;
       const int ng = total < GATHER_SUBS ? total : GATHER_SUBS;
       if (atomicAdd(arrive, 1) == ng - 1) {
         arrive[0] = 0;

@@ -111,7 +111,7 @@ class TensorBatchLoader:
                         for t in self.tensors]
         self._perm = torch.zeros(max(self._rows_per_rank(), 1), dtype=torch.int32, device=dev)
         self._cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._arrive = torch.zeros(65, dtype=torch.int32, device=dev)  # gather arrival words
+        self._arrive = torch.zeros(65 * 32, dtype=torch.int32, device=dev)  # gather arrival counters, one line each
 
     def begin_epoch(self, epoch: int) -> int:
         self._ensure_static()

@@ -54,7 +54,7 @@ class StreamingLoader:
         b = torch.arange(B).repeat(max_batches)
         self._perm = ((s % R) * B + b).to(torch.int32).to(dev)
         self._cursor = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._arrive = torch.zeros(65, dtype=torch.int32, device=dev)  # gather arrival words
+        self._arrive = torch.zeros(65 * 32, dtype=torch.int32, device=dev)  # gather arrival counters, one line each
         self.copy_stream = torch.cuda.Stream(device=dev)
         self._copied = [torch.cuda.Event() for _ in range(R)]
         self._consumed = [torch.cuda.Event() for _ in range(R)]
