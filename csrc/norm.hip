@@ -726,35 +726,63 @@ __global__ __launch_bounds__(1024) void norm_param_reduce_wide_kernel(float* __r
   }
 }
 
-// Column sums of the wide backward's partial rows, 16 columns per block (2D / 16 = 256 blocks at D = 2048): 16 rows x
-// 64 B per wave instruction, wave sums by a fixed xor tree, block sum in wave order (deterministic).  The 64-column
+// Column sums of the wide backward's partial rows, 32 columns per block (2D / 32 = 128 blocks at D = 2048, see
+// param_reduce_cols), wave sums by a fixed xor tree, block sum in wave order (deterministic).  The 64-column
 // form (64 blocks, 4 B per lane) took 8.3 us per call at mlp_large; a two-level form with a last-arriver ticket
 // 12.9 us (its agent-scope release writes back the XCD's dirty L2 behind the norm backward) (r3 traces).
 // part: a [2][NORM_BWD_MAX_BLOCKS][2048] partial region (mta_norm_part, or mta_norm_hpart for the fused heads)
+__device__ __forceinline__ void param_reduce_cols(float* __restrict__ dgamma, float* __restrict__ dbeta, int D,
+                                                  int blocks, const float* __restrict__ part, long pass_stride,
+                                                  int bx);
 __global__ __launch_bounds__(1024) void norm_param_reduce_cols_kernel(float* __restrict__ dgamma,
                                                                       float* __restrict__ dbeta, int D, int blocks,
                                                                       const float* __restrict__ part) {
-  __shared__ float4 red[16][4];
+  param_reduce_cols(dgamma, dbeta, D, blocks, part, (long)NORM_BWD_MAX_BLOCKS * 2048, blockIdx.x);
+}
+// deferred wide reductions (the MLP backward's dgamma / dbeta and fused-head partials of every layer): one launch,
+// blockIdx.y = job, the same fixed-order sums
+constexpr int NORM_WIDE_SLOTS = 8, NORM_WIDE_SLOT_BLOCKS = 512;
+struct WideJob {
+  const float* part;
+  float* dgamma;
+  float* dbeta;
+  int D, blocks;
+};
+struct WideBatch {
+  WideJob job[NORM_WIDE_SLOTS];
+};
+__global__ __launch_bounds__(1024) void norm_param_reduce_cols_batch_kernel(WideBatch b) {
+  const WideJob& j = b.job[blockIdx.y];
+  if ((int)blockIdx.x >= 2 * j.D / 32) return;
+  param_reduce_cols(j.dgamma, j.dbeta, j.D, j.blocks, j.part, (long)NORM_WIDE_SLOT_BLOCKS * 2048, blockIdx.x);
+}
+// 32 columns per 1,024-thread block: 8 lanes x float4 = one whole 128-B line of a partial row per 8 lanes (16-column
+// blocks read half lines: the 5-layer MLP batch reduce ran at ~1.8 TB/s), rows strided over 8-lane groups, then a
+// fixed-order xor tree and wave-order sum: bit-reproducible
+__device__ __forceinline__ void param_reduce_cols(float* __restrict__ dgamma, float* __restrict__ dbeta, int D,
+                                                  int blocks, const float* __restrict__ part, long pass_stride,
+                                                  int bx) {
+  __shared__ float4 red[16][8];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x * 16 + 4 * (lane & 3);  // over [0, 2D); D % 16 == 0: a block never straddles the planes
+  const int c = bx * 32 + 4 * (lane & 7);  // over [0, 2D); D % 32 == 0: a block never straddles the planes
   const int pass = c >= D ? 1 : 0, col = c - pass * D;
   float* dst = pass == 0 ? dgamma : dbeta;
   if (dst == nullptr) return;  // uniform over the block
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int b = wave * 16 + (lane >> 2); b < blocks; b += 256) {
-    const float4 v = *reinterpret_cast<const float4*>(part + ((size_t)pass * NORM_BWD_MAX_BLOCKS + b) * 2048 + col);
+  for (int b = wave * 8 + (lane >> 3); b < blocks; b += 128) {
+    const float4 v = *reinterpret_cast<const float4*>(part + pass * pass_stride + (size_t)b * 2048 + col);
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
 #pragma unroll
-  for (int m = 4; m < 64; m <<= 1) {
+  for (int m = 8; m < 64; m <<= 1) {
     s.x += __shfl_xor(s.x, m, 64);
     s.y += __shfl_xor(s.y, m, 64);
     s.z += __shfl_xor(s.z, m, 64);
     s.w += __shfl_xor(s.w, m, 64);
   }
-  if (lane < 4) red[wave][lane] = s;
+  if (lane < 8) red[wave][lane] = s;
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (threadIdx.x < 8) {
     float4 t = red[0][threadIdx.x];
     for (int w = 1; w < 16; ++w) {
       const float4 v = red[w][threadIdx.x];
@@ -833,7 +861,39 @@ extern "C" int mta_cast_pad(int n, const float* const* src, void* const* dst, co
 }
 
 // launch every deferred parameter reduction (one launch)
+__device__ float mta_norm_wide_slots[NORM_WIDE_SLOTS][2][NORM_WIDE_SLOT_BLOCKS][2048];
+struct WideDeferState {
+  int n = 0;
+  WideBatch batch;
+  hipStream_t st = nullptr;
+} wide_deferred;
+
+void norm_wide_flush() {
+  if (wide_deferred.n == 0) return;
+  int maxD = 0;
+  for (int i = 0; i < wide_deferred.n; ++i) maxD = std::max(maxD, wide_deferred.batch.job[i].D);
+  norm_param_reduce_cols_batch_kernel<<<dim3(2 * maxD / 32, wide_deferred.n), 1024, 0, wide_deferred.st>>>(
+      wide_deferred.batch);
+  wide_deferred.n = 0;
+}
+
+// a wide deferred slot's partial base (two planes of NORM_WIDE_SLOT_BLOCKS x 2048), its job queued
+float* norm_wide_slot(float* dgamma, float* dbeta, int D, int blocks, hipStream_t st) {
+  if (wide_deferred.n == NORM_WIDE_SLOTS || (wide_deferred.n && wide_deferred.st != st)) norm_wide_flush();
+  static float* base = [] {
+    float* p = nullptr;
+    (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_wide_slots));
+    return p;
+  }();
+  float* part = base + (long)wide_deferred.n * 2 * NORM_WIDE_SLOT_BLOCKS * 2048;
+  wide_deferred.batch.job[wide_deferred.n] = WideJob{part, dgamma, dbeta, D, blocks};
+  wide_deferred.st = st;
+  ++wide_deferred.n;
+  return part;
+}
+
 extern "C" void mta_norm_flush() {
+  norm_wide_flush();
   if (deferred.n == 0) return;
   int maxD = 0;
   for (int i = 0; i < deferred.n; ++i) maxD = deferred.batch.job[i].D > maxD ? deferred.batch.job[i].D : maxD;
@@ -925,6 +985,9 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   }
   // deferred slot when the caller asked for it (dgamma pointer tagged by mta_norm_defer) and D fits
   const bool defer = bwd && (dgamma || dbeta) && defer_next && D <= NORM_DEFER_D;
+  // wide backward of a deferring caller (the bf16 MLP): its dgamma / dbeta and fused-head partial rows go to wide
+  // slots, reduced for every layer by ONE launch at mta_norm_flush (the per-call reduce was ~6 us + a launch gap)
+  const bool defer_wide = bwd && defer_next && wide_ok && D % 32 == 0 && D <= 2048;
   defer_next = false;
   if (defer) {
     if (deferred.n == NORM_DEFER_SLOTS || (deferred.n && deferred.st != st)) mta_norm_flush();
@@ -949,6 +1012,11 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     a.part_ld = 2048;
     a.part_pass = (long)NORM_BWD_MAX_BLOCKS * 2048;
   }
+  const bool wide_slots = defer_wide && blocks <= NORM_WIDE_SLOT_BLOCKS;
+  if (wide_slots) {
+    a.part_pass = (long)NORM_WIDE_SLOT_BLOCKS * 2048;  // the plane stride of every wide slot (norm and head)
+    if (dgamma || dbeta) a.part = norm_wide_slot(dgamma, dbeta, D, blocks, st);
+  }
 #define NORM_LAUNCH(V)                                                          \
   if (bwd) norm_bwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);                \
   else norm_fwd_kernel<V><<<blocks, NT_THREADS, 0, st>>>(a);
@@ -964,7 +1032,8 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
           (void)hipGetSymbolAddress(reinterpret_cast<void**>(&p), HIP_SYMBOL(mta_norm_hpart));
           return p;
         }();
-        a.hpart = hbase;
+        a.hpart = wide_slots ? norm_wide_slot(g_wa, g_wb, D, blocks, st) : hbase;
+        // (the head slot shares the norm slot's plane stride: both NORM_WIDE_SLOT_BLOCKS x 2048 when deferred)
       }
 #define NORM_FAST(V, B)                                                                                          \
   if (a.ab) norm_bwd_wide_fast_kernel<V, B, true, true><<<blocks, NT_THREADS, 0, st>>>(a, rows_per_block);       \
@@ -1000,15 +1069,15 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
     NORM_LAUNCH(8)
   }
 #undef NORM_LAUNCH
-  if (bwd && (dgamma || dbeta) && wide) {
-    if (D % 16 == 0)
-      norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(dgamma, dbeta, D, blocks, a.part);
+  if (bwd && (dgamma || dbeta) && wide && !wide_slots) {
+    if (D % 32 == 0)
+      norm_param_reduce_cols_kernel<<<2 * D / 32, 1024, 0, st>>>(dgamma, dbeta, D, blocks, a.part);
     else
       norm_param_reduce_wide_kernel<<<(2 * D + 63) / 64, 1024, 0, st>>>(dgamma, dbeta, D, blocks);
-  } else if (bwd && (dgamma || dbeta) && !defer)
+  } else if (bwd && (dgamma || dbeta) && !defer && !wide_slots)
     norm_param_reduce_kernel<<<(2 * D + 3) / 4, 256, 0, st>>>(dgamma, dbeta, D, blocks);
-  if (bwd && a.ab)  // the head weights' gradients (D in {1024, 2048}: the column-block reduction)
-    norm_param_reduce_cols_kernel<<<2 * D / 16, 1024, 0, st>>>(g_wa, g_wb, D, blocks, a.hpart);
+  if (bwd && a.ab && !wide_slots)  // the head weights' gradients (D in {1024, 2048}: the column-block reduction)
+    norm_param_reduce_cols_kernel<<<2 * D / 32, 1024, 0, st>>>(g_wa, g_wb, D, blocks, a.hpart);
   return 0;
 }
 

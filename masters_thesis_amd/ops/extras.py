@@ -264,14 +264,15 @@ class _MlpEncoderFn(torch.autograd.Function):
                 wa, ba, wb_, bb = heads
                 hk = dict(hw_a=wa, hb_a=ba, hw_b=wb_, hb_b=bb, ab=dab, ab_rows=N, g_wa=_grad_view(wa),
                           g_wb=_grad_view(wb_))
+            if acts[i] is None:
+                lib().norm_defer()  # dgamma / dbeta (+ head) partials: one reduction launch for all layers at the end
             lib().norm(True, pres[i] if acts[i] is None else acts[i], D, Mp, D, rms, RMS_EPS if rms else LN_EPS,
                        params[per * i + 2], None if rms else params[per * i + 3], None, None, means[i], rstds[i],
                        ctx.seeds[i:i + 1] if dropped else None, p, dy, None, pres[i], dpre, None,
                        _grad_view(params[per * i + 2]), None if rms else _grad_view(params[per * i + 3]),
                        gelu_x=acts[i] is None, **hk)
-            if hk:  # head biases: ordered column sums of d(alpha, beta)
+            if hk:  # head biases: ordered column sums of d(alpha, beta) (the head weights' sums: at norm_flush)
                 lib().pair_colsum(dab, N, _grad_view(ba), _grad_view(bb))
-                grad_ready(wa.grad, ba.grad, wb_.grad, bb.grad)
             # dW_i += dPre^T X_i (fp32 straight into the flat gradient buffer), db_i += colsum(dPre).  A big dW_i is
             # a gradient PRODUCER of the fused optimizer (ops/optim.py register_grad_producer): its split-K reduce
             # overwrites the range and leaves the clip-norm partials, so the update neither zeroes nor re-reads it
@@ -287,6 +288,9 @@ class _MlpEncoderFn(torch.autograd.Function):
             # W_i, b_i final (their GEMM is launched: deferred ones go with the input-gradient GEMM above)
             grad_ready(params[per * i].grad, params[per * i + 1].grad)
         gemm_flush()
+        lib().norm_flush()  # the deferred norm-parameter (and head-weight) reductions of every layer: one launch
+        norm_grads = [t.grad for i in range(L) for t in params[per * i + 2:per * i + per]]
+        grad_ready(*norm_grads, *([t.grad for t in heads] if heads is not None else []))
         return (None,) * (8 + len(params) + (4 if heads is not None else 0))
 
 
