@@ -821,10 +821,12 @@ struct LgWin {
 __device__ LgPart mta_lg_part[LG_MAXP];
 __device__ LgWin mta_lg_win[LG_MAXW];
 
+// the grid losses from this many sequences on (the single-workgroup kernel took 36 us at N = 800, B = 8 windows)
+constexpr int LG_MIN_N = 512;
 inline bool losses_grid_ok(const LossArgs& A) {
   if (getenv("MTA_LOSSES_SINGLE")) return false;
   const int J = A.kwin <= 0 ? 0 : min(LG_MAXJ, (A.kwin + LG_SEQ - 1) / LG_SEQ);
-  return A.N >= 1024 && A.n <= 64 && A.n >= 1 && A.windows <= LG_MAXW && (long)A.windows * A.kwin == A.N &&
+  return A.N >= LG_MIN_N && A.n <= 64 && A.n >= 1 && A.windows <= LG_MAXW && (long)A.windows * A.kwin == A.N &&
          (long)A.windows * J <= LG_MAXP;
 }
 

@@ -1,11 +1,13 @@
 #!/bin/bash
-# r5z: double-buffered Adam streaming loop: optimizer / kernel tests, mlp_large bench + trace, headline
+# r5z: grid losses from N = 512: kernel tests, LSTM / transformer B=8 bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r5z
+O=gpurun_out/r5z2
 mkdir -p $O
-timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_extras.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
+timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
 echo "pytest ok" >> $O/status.log
-timeout -k 10 300 python bench.py --model mlp_large --loss mse --batch 64 --trainer gpu_fast --steps 100 --warmup 10 > $O/mlp_large.json 2> $O/mlp_large.err || { echo "bench rc=$?" >> $O/status.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_mlp -o mlp -- python bench.py --model mlp_large --trainer gpu_fast --batch 64 --steps 50 --warmup 10 > $O/prof_mlp.log 2>&1 || { echo "prof rc=$?" >> $O/status.log; exit 1; }
+for m in "--model small --loss mse --batch 8" "--model small --loss combined --batch 8" "--model transformer_encoder --loss combined --batch 8 --trainer gpu_fast"; do
+  echo -n "$m :: " >> $O/b8.log
+  timeout -k 10 200 python bench.py $m --steps 100 --warmup 10 2>/dev/null | python -c "import sys,json; print(json.loads(sys.stdin.readline())['p50_step_ms'])" >> $O/b8.log || exit 1
+done
 echo done >> $O/status.log

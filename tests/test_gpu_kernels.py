@@ -333,13 +333,15 @@ def test_train_step_graph_matches_eager():
     torch.testing.assert_close(acc_graph, acc_eager, rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("B", [64, 8])
 @pytest.mark.parametrize("mode", ["reference", "per_window"])
-def test_grid_losses_match_single_workgroup(mode, monkeypatch):
-    """N >= 1024: the three-launch grid losses (csrc/losses.hip L1-L3) agree with the single-workgroup kernel."""
+def test_grid_losses_match_single_workgroup(mode, B, monkeypatch):
+    """N >= 512 (LG_MIN_N): the three-launch grid losses (csrc/losses.hip L1-L3) agree with the single-workgroup
+    kernel."""
     from masters_thesis_amd.ops.losses import decoder_losses
 
     torch.manual_seed(5)
-    B, K, n = 64, 100, 30
+    K, n = 100, 30
     N = B * K
     ab = (torch.randn(N, 2) * 0.3 + torch.tensor([0.0, 1.0])).to(DEV)
     y = torch.randn(N, n, 4, device=DEV)
