@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     const int layer = a.L - 1 - idx / a.wg_per_layer, rem = idx % a.wg_per_layer;
     const mta_wgrad::WgArgs& w = a.wg[layer];
     const int chunk = w.nchunks - 1 - rem / a.wg_nq, quarter = rem % a.wg_nq;
-    const int t_lo = chunk * (w.rows_per_chunk / a.Np);
+    const int t_lo = (int)((long)chunk * w.rows_per_chunk / a.Np);  // earliest step of the chunk's rows
     if (threadIdx.x < a.ntiles)
       wait_progress(a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + threadIdx.x), base + (unsigned)(a.T - t_lo), base,
                     a.timeout, a.spin_limit);
@@ -1427,6 +1427,11 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's
 // (dropped-out) input sequence (T, Np, H); the gradients accumulate into g_* (the flat gradient buffer).
+// rows of one fused weight-gradient workgroup's chunk above which the chunk is split (B=64, Np = 6400: two
+// workgroups per step and c' block; 1,600 rows per workgroup is slower again: more partial atomics and spinning
+// workgroups, profiles/r5_lstm_wgrad_row_split.txt)
+constexpr int WG_FUSED_MAX_ROWS = 4096;
+
 extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
@@ -1467,6 +1472,13 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     const int nwaves = H / 8, cq = 16 * nwaves;
     const int tc = mta_wgrad::wg_time_chunk(T, true);
     a.wg_nq = 4 * H / cq;
+    // large batches: split a time chunk's rows over several workgroups, so the chunk of the earliest steps
+    // (drained last) is not a serial tail of tc * Np rows behind the recurrence
+    int rpc = tc * Np;
+    if (!part && rpc > WG_FUSED_MAX_ROWS) {  // (deterministic mode keeps tc-step chunks: its partials are sized so)
+      const int split = (rpc + WG_FUSED_MAX_ROWS - 1) / WG_FUSED_MAX_ROWS;
+      rpc = ((rpc + split - 1) / split + mta_wgrad::WG_KS - 1) / mta_wgrad::WG_KS * mta_wgrad::WG_KS;
+    }
     for (int l = 0; l < L; ++l) {
       mta_wgrad::WgArgs& w = a.wg[l];
       w.dG = dG[l];
@@ -1479,8 +1491,8 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
       w.H = H;
       w.F = l == 0 ? fin : H;
       w.FP = (w.F + 15) / 16 * 16;
-      w.rows_per_chunk = tc * Np;
-      w.nchunks = (T + tc - 1) / tc;
+      w.rows_per_chunk = rpc;
+      w.nchunks = (T * Np + rpc - 1) / rpc;
       w.g_wih = g_wih[l];
       w.g_whh = g_whh[l];
       w.g_bih = g_bih[l];

@@ -97,13 +97,16 @@ def test_pipelined_matches_fp64(prec, N, T, F, H, L):
         assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad w{i}: err {e} (scale {sc})"
 
 
-def test_pipelined_grid_beyond_one_workgroup_per_cu():
+@pytest.mark.parametrize("N", [2100, 4200])
+def test_pipelined_grid_beyond_one_workgroup_per_cu(N):
     """L x tiles > 256 workgroups (not all co-resident): producers always precede consumers in block order, so
-    the grid drains in waves and stays exact (large batches take this path instead of per-layer launches)."""
+    the grid drains in waves and stays exact (large batches take this path instead of per-layer launches).
+    N=4200: a step's 4,208 rows exceed WG_FUSED_MAX_ROWS, so each fused weight-gradient chunk is split over
+    two workgroups that start at mid-step rows (csrc/lstm_stack.hip mta_lstm_stack_bwd)."""
     from masters_thesis_amd.ops import lstm as op
 
     torch.manual_seed(7)
-    N, T, F, H, L = 2100, 10, 3, 64, 3   # 132 tiles -> 136 x 3 = 408 workgroups per launch
+    T, F, H, L = 10, 3, 64, 3   # N=2100: 132 tiles -> 136 x 3 = 408 workgroups per launch
     x = torch.randn(N, T, F)
     ws = _weights(F, H, L, seed=5)
     R = torch.randn(N, H)
