@@ -1427,10 +1427,10 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's
 // (dropped-out) input sequence (T, Np, H); the gradients accumulate into g_* (the flat gradient buffer).
-// rows of one fused weight-gradient workgroup's chunk above which the chunk is split (B=64, Np = 6400: two
-// workgroups per step and c' block; 1,600 rows per workgroup is slower again: more partial atomics and spinning
-// workgroups, profiles/r5_lstm_wgrad_row_split.txt)
-constexpr int WG_FUSED_MAX_ROWS = 4096;
+// rows of one fused weight-gradient workgroup's chunk above which the chunk is split in two (B >= 8 windows:
+// Np >= 800).  Two parts beat three or more at every measured batch -- more parts mean more partial atomics and
+// more spinning workgroups (profiles/r5_lstm_wgrad_row_split.txt)
+constexpr int WG_FUSED_SPLIT_ROWS = 512;
 
 extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
@@ -1472,13 +1472,11 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     const int nwaves = H / 8, cq = 16 * nwaves;
     const int tc = mta_wgrad::wg_time_chunk(T, true);
     a.wg_nq = 4 * H / cq;
-    // large batches: split a time chunk's rows over several workgroups, so the chunk of the earliest steps
+    // large batches: split a time chunk's rows over two workgroups, so the chunk of the earliest steps
     // (drained last) is not a serial tail of tc * Np rows behind the recurrence
     int rpc = tc * Np;
-    if (!part && rpc > WG_FUSED_MAX_ROWS) {  // (deterministic mode keeps tc-step chunks: its partials are sized so)
-      const int split = (rpc + WG_FUSED_MAX_ROWS - 1) / WG_FUSED_MAX_ROWS;
-      rpc = ((rpc + split - 1) / split + mta_wgrad::WG_KS - 1) / mta_wgrad::WG_KS * mta_wgrad::WG_KS;
-    }
+    if (!part && rpc > WG_FUSED_SPLIT_ROWS)  // (deterministic mode keeps tc-step chunks: its partials are sized so)
+      rpc = ((rpc + 1) / 2 + mta_wgrad::WG_KS - 1) / mta_wgrad::WG_KS * mta_wgrad::WG_KS;
     for (int l = 0; l < L; ++l) {
       mta_wgrad::WgArgs& w = a.wg[l];
       w.dG = dG[l];

@@ -101,8 +101,8 @@ def test_pipelined_matches_fp64(prec, N, T, F, H, L):
 def test_pipelined_grid_beyond_one_workgroup_per_cu(N):
     """L x tiles > 256 workgroups (not all co-resident): producers always precede consumers in block order, so
     the grid drains in waves and stays exact (large batches take this path instead of per-layer launches).
-    N=4200: a step's 4,208 rows exceed WG_FUSED_MAX_ROWS, so each fused weight-gradient chunk is split over
-    two workgroups that start at mid-step rows (csrc/lstm_stack.hip mta_lstm_stack_bwd)."""
+    A step's 2,112 / 4,208 rows exceed WG_FUSED_SPLIT_ROWS, so each fused weight-gradient chunk is split over
+    two workgroups, the second starting at a mid-step row (csrc/lstm_stack.hip mta_lstm_stack_bwd)."""
     from masters_thesis_amd.ops import lstm as op
 
     torch.manual_seed(7)
