@@ -2,7 +2,7 @@
 # r5w3: whole GPU suite + LSTM small B=64 bench and kernel trace after the fused weight-gradient row split
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r5w3
+O=gpurun_out/${R5W_TAG:-r5w3}
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest rc=$?" >> $O/status.log; exit 1; }
 echo "pytest ok" >> $O/status.log
