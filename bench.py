@@ -7,9 +7,11 @@ features, 30-day target).  Config: the reference defaults (`configs/config.yaml`
 (51,074 params), fp32 parameters/activations (trainer precision ``32-true``),
 Adam + grad-norm clip 5.0 — random-init weights, synthetic data from the
 reference DGP generated on the device.  Every timed step is the full training
-step: batch gather, forward, fused loss, backward, RCCL gradient all-reduce
-(N > 1), clip + Adam, metric accumulation — replayed from the captured HIP graph
-exactly as ``train.py`` runs it.
+step: batch gather, forward, fused loss, backward, gradient all-reduce (N > 1:
+the xGMI one-/two-shot kernel of ``parallel/xgmi.py`` inside the step graph; RCCL
+when its start-up self-check fails or ``MTA_ALLREDUCE=rccl``, with the reason in
+``allreduce_fallback_reason``), clip + Adam, metric accumulation — replayed from
+the captured HIP graph exactly as ``train.py`` runs it.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--model M] [--trainer T] [--concurrent k]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -285,6 +287,7 @@ def main(argv=None):
                                if key in SAME_NODE_TORCH_EAGER and args.backend == "auto" else None),
             "vs_cpu_yardstick": (round(value / YARDSTICK[key], 3) if key in YARDSTICK else None),
             "allreduce": trainer.ddp.backend_name,
+            "allreduce_fallback_reason": trainer.ddp.fallback_reason,
             "allreduce_us": round(allreduce_us, 2) if allreduce_us is not None else None,
             "grad_bucket_bytes": int(trainer.flat.padded * 4),
             # the compute dtype that actually ran: the extras' bf16 HIP kernels run only at matmul precision

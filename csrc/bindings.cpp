@@ -75,8 +75,10 @@ int mta_gemm_bf16(int mode, const void* A, const void* B, int M, int N, int K, i
 void mta_gemm_flush();
 void mta_gemm_set_big(int on);
 void mta_norm_flush();
+void mta_norm_discard();
 void mta_norm_defer();
 void mta_gemm_group_flush();
+void mta_gemm_group_discard();
 int mta_cast_pad(int n, const float* const* src, void* const* dst, const int* rows, const int* cols,
                  const int* rows_p, const int* cols_p, const int* ld_src, uint64_t* seeds, int nseeds, hipStream_t st);
 int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int D, int rms, float eps, const float* gamma,
@@ -541,7 +543,9 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
                  (float)max_norm, (float)scale, adamw ? 1 : 0, zero_grad ? 1 : 0, opt_mut(norm_out),
                  opt_mut(nonfinite), (int)cs.size(), cs.data(), ce.data(),
                  has(ext) ? ext->data_ptr<float>() : nullptr,
-                 has(ext) ? (int)std::min<int64_t>(ext->numel(), (int64_t)cs.size() * mta_gemm_norm_parts()) : 0,
+                 // every partial the caller passes is summed (FusedAdam.step hands over slots [0, last used slot],
+                 // the unowned ones zeroed)
+                 has(ext) ? (int)ext->numel() : 0,
                  cur_stream());
 }
 
@@ -1376,6 +1380,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_set_big", [](int64_t on) { mta_gemm_set_big((int)on); });
   m.def("norm_defer", []() { mta_norm_defer(); });
   m.def("gemm_group_flush", []() { mta_gemm_group_flush(); });
+  m.def("gemm_group_discard", []() { mta_gemm_group_discard(); });
+  m.def("norm_discard", []() { mta_norm_discard(); });
   m.def("norm_flush", []() { mta_norm_flush(); });
   m.def("cast_pad", &cast_pad, py::arg("src"), py::arg("dst"), py::arg("seeds") = py::none());
   m.def("pair_colsum", &pair_colsum);

@@ -1358,6 +1358,13 @@ extern "C" void mta_gemm_group_flush() {
   }
 }
 
+// drop the queued weight gradients and a held-back GEMM unlaunched: their raw operand pointers are only kept alive by
+// the caller of the backward that queued them (a backward that raised part-way must not leave them for the next flush)
+extern "C" void mta_gemm_group_discard() {
+  gq.n[0] = gq.n[1] = 0;
+  pending.on = false;
+}
+
 // launch a deferred GEMM on its own (the caller's next GEMM was not its partner, or end of a backward)
 extern "C" void mta_gemm_flush() {
   if (pending.on) {

@@ -878,6 +878,12 @@ void norm_wide_flush() {
 }
 
 // a wide deferred slot's partial base (two planes of NORM_WIDE_SLOT_BLOCKS x 2048), its job queued
+// make room for k more slots before queuing any of them (a fused-head backward takes two: its norm slot, then its
+// head slot -- a flush between the two would launch the first slot's reduction before its kernel has written it)
+void norm_wide_reserve(int k, hipStream_t st) {
+  if (wide_deferred.n + k > NORM_WIDE_SLOTS || (wide_deferred.n && wide_deferred.st != st)) norm_wide_flush();
+}
+
 float* norm_wide_slot(float* dgamma, float* dbeta, int D, int blocks, hipStream_t st) {
   if (wide_deferred.n == NORM_WIDE_SLOTS || (wide_deferred.n && wide_deferred.st != st)) norm_wide_flush();
   static float* base = [] {
@@ -890,6 +896,12 @@ float* norm_wide_slot(float* dgamma, float* dbeta, int D, int blocks, hipStream_
   wide_deferred.st = st;
   ++wide_deferred.n;
   return part;
+}
+
+// drop every queued reduction unlaunched (a backward that raised part-way: its slots may never have been written)
+extern "C" void mta_norm_discard() {
+  wide_deferred.n = 0;
+  deferred.n = 0;
 }
 
 extern "C" void mta_norm_flush() {
@@ -1015,6 +1027,7 @@ extern "C" int mta_norm(int bwd, const void* x, int x_bf16, int ldx, int M, int 
   const bool wide_slots = defer_wide && blocks <= NORM_WIDE_SLOT_BLOCKS;
   if (wide_slots) {
     a.part_pass = (long)NORM_WIDE_SLOT_BLOCKS * 2048;  // the plane stride of every wide slot (norm and head)
+    norm_wide_reserve(bwd && a.ab ? 2 : 1, st);
     if (dgamma || dbeta) a.part = norm_wide_slot(dgamma, dbeta, D, blocks, st);
   }
 #define NORM_LAUNCH(V)                                                          \

@@ -646,95 +646,102 @@ class _TransformerEncoderFn(torch.autograd.Function):
         # the N real sequences only (the padded ones have no output gradient): dh is read in place
         dh = dh if (dh.dtype == torch.float32 and dh.is_contiguous()) else dh.float().contiguous()
         gf = params[2 + nb * L]
-        C.norm_defer()
-        C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, None, None,
-               stats[-1], None, 0.0, dh, None, None, dXb.view(-1)[(T - 1) * d:], dX.view(-1)[(T - 1) * d:],
-               _grad_view(gf), None)
-        frag = ctx.frag  # fused FFN: W2^T / W1^T fragment-major images, written by the forward's packing launch
-        # operands of the weight gradients queued for the grouped launch: alive (and not rewritten) until the flush
-        keep: List[Tensor] = []
-        for l in range(L - 1, -1, -1):
-            base = 2 + nb * l
-            g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
-            wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
-            dff = w1_b.shape[0]
-            xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
-            r1, lse, r2 = stats[3 * l: 3 * l + 3]
-            dpre1 = torch.empty((dff, M) if nn else (M, dff), device=dev, dtype=torch.bfloat16)
-            dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
-            dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-            if nn:
-                # same chain; the weight gradients then run on the transposed images as NN products (one paired launch)
-                dXt = torch.empty((d, M), device=dev, dtype=torch.bfloat16)
-                C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
-                             p, dX, dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
-                gemm(0, dXt, u, d, dff, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
-                gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
-                keep += [dXt, dpre1]
-            elif ffn:
-                # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
-                # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
-                C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
-                             p, dX, dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
-                gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
-                gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
-                keep += [dXb, dpre1]
-            else:
-                # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
-                gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
-                     ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
-                fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
-                gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1,
-                     seed=ctx.seeds[l:l + 1] if drop else None, drop_p=p, out_bf16=dpre1)
-                # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
-                gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
-                     ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
-                keep += [dXb, dpre1]
-                dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
-                gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
-                # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
-                C.norm_defer()  # dgamma: one batched reduction launch at the end of the backward
-                C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None,
-                       dX1b, dX1, _grad_view(g2), None)
-            # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
-            gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
-                 ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), group=True)
-            # attention backward (RoPE inverse fused) -> dqkv; d(o) = dX1 Wo inside it (fused half) or a GEMM before it
-            dqkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
-            if afrag is not None:
-                C.attention(True, qkv, o, lse, None, dqkv, Np, T, d, heads, ROPE_BASE, dX1b, afrag[4 * l + 2])
-            else:
-                do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
-                gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
-                C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
-            # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
-            gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
-                 ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), group=True)
-            keep += [dX1b, dqkv]
-            dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
-            dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)  # fresh: the queued dW2 may read the last one
-            if afrag is not None:
-                # d(xn) = dqkv Wqkv and the RMSNorm1 backward + residual in one launch (dg1: deferred norm slot)
-                C.tr_attn_dx(dqkv, afrag[4 * l + 3], xs, r1, g1, dX1, dXn, dXb, _grad_view(g1))
-            else:
-                dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
-                gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
-                # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
-                C.norm_defer()
-                C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None,
-                       dXb, dXn, _grad_view(g1), None)
-            dX = dXn
-        # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
-        gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,
-             ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]), group=True)
-        # every layer's weight gradients in one launch per operand layout (queued above), then the norm gains
-        gemm_group_flush()
-        del keep
-        C.norm_flush()
+        try:
+            C.norm_defer()
+            C.norm(True, x_final.view(-1)[(T - 1) * d:], T * d, N, d, True, RMS_EPS, gf, None, None, None, None,
+                   stats[-1], None, 0.0, dh, None, None, dXb.view(-1)[(T - 1) * d:], dX.view(-1)[(T - 1) * d:],
+                   _grad_view(gf), None)
+            frag = ctx.frag  # fused FFN: W2^T / W1^T fragment-major images, written by the forward's packing launch
+            # operands of the weight gradients queued for the grouped launch: alive (and not rewritten) until the flush
+            keep: List[Tensor] = []
+            for l in range(L - 1, -1, -1):
+                base = 2 + nb * l
+                g1, wqkv, bqkv, wo, bo, g2, w1, b1, w2, b2 = params[base: base + nb]
+                wqkv_b, wo_b, w1_b, w2_b = mats_b[1 + 4 * l: 5 + 4 * l]
+                dff = w1_b.shape[0]
+                xs, xn, qkv, o, x1, xn2, pre1, u = saved[1 + 8 * l: 9 + 8 * l]
+                r1, lse, r2 = stats[3 * l: 3 * l + 3]
+                dpre1 = torch.empty((dff, M) if nn else (M, dff), device=dev, dtype=torch.bfloat16)
+                dX1 = torch.empty((M, d), device=dev, dtype=torch.float32)
+                dX1b = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                if nn:
+                    # same chain; the weight gradients then run on the transposed images as NN products (one paired launch)
+                    dXt = torch.empty((d, M), device=dev, dtype=torch.bfloat16)
+                    C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
+                                 p, dX, dXb, None, dX1, dX1b, _grad_view(g2), dpre1, dXt)
+                    gemm(0, dXt, u, d, dff, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                         ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
+                    gemm(0, dpre1, xn2, dff, d, M, M, M, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                         ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                    keep += [dXt, dpre1]
+                elif ffn:
+                    # d(u) = dX W2 -> dPre1 -> d(xn2) = dPre1 W1 -> dX1 = norm2_bwd(d(xn2)) + dX, one launch; then the
+                    # two weight gradients dW2 += dX^T u (db2), dW1 += dPre1^T xn2 (db1)
+                    C.tr_ffn_bwd(x1, frag[l, 3].view(d, dff), frag[l, 2], g2, r2, pre1, ctx.seeds[l:l + 1] if drop else None,
+                                 p, dX, dXb, dpre1, dX1, dX1b, _grad_view(g2), None, None)
+                    gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                         ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
+                    gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                         ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                    keep += [dXb, dpre1]
+                else:
+                    # fc2: dW2 += dX^T u, db2; d(u) -> dPre1 = d(u) * dropout * gelu'(pre1)
+                    gemm(2, dXb, u, d, dff, M, d, dff, flags=EPI_ACCUM, out_f32=_grad_view(w2), ldc=dff,
+                         ksplit=wgrad_split(d, dff, M), bias_grad=_grad_view(b2), group=True)
+                    fl = EPI_DGELU | (EPI_DROPOUT if drop else 0)
+                    gemm(1, dXb, w2_b, M, dff, d, d, dff, flags=fl, aux_in=pre1,
+                         seed=ctx.seeds[l:l + 1] if drop else None, drop_p=p, out_bf16=dpre1)
+                    # fc1: dW1 += dPre1^T xn2, db1; d(xn2) = dPre1 W1
+                    gemm(2, dpre1, xn2, dff, d, M, dff, d, flags=EPI_ACCUM, out_f32=_grad_view(w1), ldc=d,
+                         ksplit=wgrad_split(dff, d, M), bias_grad=_grad_view(b1), group=True)
+                    keep += [dXb, dpre1]
+                    dxn2 = torch.empty((M, d), device=dev, dtype=torch.float32)
+                    gemm(1, dpre1, w1_b, M, d, dff, dff, d, out_f32=dxn2)
+                    # RMSNorm2 backward + residual: dX1 = norm2_bwd(dxn2) + dX
+                    C.norm_defer()  # dgamma: one batched reduction launch at the end of the backward
+                    C.norm(True, x1, d, M, d, True, RMS_EPS, g2, None, None, None, None, r2, None, 0.0, dxn2, dX, None,
+                           dX1b, dX1, _grad_view(g2), None)
+                # proj: dWo += dX1^T o, dbo; d(o) = dX1 Wo
+                gemm(2, dX1b, o, d, d, M, d, d, flags=EPI_ACCUM, out_f32=_grad_view(wo), ldc=d,
+                     ksplit=wgrad_split(d, d, M), bias_grad=_grad_view(bo), group=True)
+                # attention backward (RoPE inverse fused) -> dqkv; d(o) = dX1 Wo inside it (fused half) or a GEMM before it
+                dqkv = torch.empty((M, 3 * d), device=dev, dtype=torch.bfloat16)
+                if afrag is not None:
+                    C.attention(True, qkv, o, lse, None, dqkv, Np, T, d, heads, ROPE_BASE, dX1b, afrag[4 * l + 2])
+                else:
+                    do = torch.empty((M, d), device=dev, dtype=torch.bfloat16)
+                    gemm(1, dX1b, wo_b, M, d, d, d, d, out_bf16=do)
+                    C.attention(True, qkv, o, lse, do, dqkv, Np, T, d, heads, ROPE_BASE)
+                # qkv: dWqkv += dqkv^T xn, dbqkv; d(xn) = dqkv Wqkv
+                gemm(2, dqkv, xn, 3 * d, d, M, 3 * d, d, flags=EPI_ACCUM, out_f32=_grad_view(wqkv), ldc=d,
+                     ksplit=wgrad_split(3 * d, d, M), bias_grad=_grad_view(bqkv), group=True)
+                keep += [dX1b, dqkv]
+                dXn = torch.empty((M, d), device=dev, dtype=torch.float32)
+                dXb = torch.empty((M, d), device=dev, dtype=torch.bfloat16)  # fresh: the queued dW2 may read the last one
+                if afrag is not None:
+                    # d(xn) = dqkv Wqkv and the RMSNorm1 backward + residual in one launch (dg1: deferred norm slot)
+                    C.tr_attn_dx(dqkv, afrag[4 * l + 3], xs, r1, g1, dX1, dXn, dXb, _grad_view(g1))
+                else:
+                    dxn = torch.empty((M, d), device=dev, dtype=torch.float32)
+                    gemm(1, dqkv, wqkv_b, M, d, 3 * d, 3 * d, d, out_f32=dxn)
+                    # RMSNorm1 backward + residual: dX = norm1_bwd(dxn) + dX1
+                    C.norm_defer()
+                    C.norm(True, xs, d, M, d, True, RMS_EPS, g1, None, None, None, None, r1, None, 0.0, dxn, dX1, None,
+                           dXb, dXn, _grad_view(g1), None)
+                dX = dXn
+            # embedding: dWe += dX^T Xin (F real columns of Fp), dbe
+            gemm(2, dXb, Xin, d, Fp, M, d, Fp, flags=EPI_ACCUM, out_f32=_grad_view(params[0]), ldc=F, n_store=F,
+                 ksplit=wgrad_split(d, Fp, M), bias_grad=_grad_view(params[1]), group=True)
+            # every layer's weight gradients in one launch per operand layout (queued above), then the norm gains
+            gemm_group_flush()
+            del keep
+            C.norm_flush()
+        except BaseException:
+            # the queued weight gradients hold raw pointers to operands only ``keep`` keeps alive, and the deferred
+            # norm slots may be unwritten: drop both so the next flush cannot launch them on freed memory
+            C.gemm_group_discard()
+            C.norm_discard()
+            raise
         for l in range(L):
             base = 2 + nb * l
             grad_ready(*(params[base + j].grad for j in (1, 2, 3, 4, 6, 7, 8, 9)))

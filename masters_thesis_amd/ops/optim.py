@@ -198,10 +198,20 @@ class FusedAdam:
             plan = sorted(self._plan.values(), key=lambda r: r[2])
             self._plan = {}
             self._dropped = set()
+            ext = None
+            if plan:
+                # the kernel sums every partial of ext: hand it slots [0, last used] and zero the slots in between
+                # that no covered range owns (a range dropped by a double registration left its stale partials there)
+                top = plan[-1][2] + 1
+                used = {r[2] for r in plan}
+                for s in range(top):
+                    if s not in used:
+                        self.ext_parts[s * self._nparts:(s + 1) * self._nparts].zero_()
+                ext = self.ext_parts[:top * self._nparts]
             lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
                              self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
                              float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health,
-                             [r[0] for r in plan], [r[1] for r in plan], self.ext_parts if plan else None)
+                             [r[0] for r in plan], [r[1] for r in plan], ext)
             # covered ranges keep this step's gradient (their producers overwrite them next step)
             self.grads_zeroed = bool(zero_grad)
             return

@@ -161,6 +161,16 @@ class FlatDDP:
         return "xgmi" if self.xgmi is not None else dist.get_backend(self.group)
 
     @property
+    def fallback_reason(self):
+        """Why the gradient all-reduce is the process group's rather than the xGMI kernel (None when xGMI runs or
+        world == 1): the configuration check, the set-up error or the failed self-check round."""
+        if self.world == 1 or self.xgmi is not None:
+            return None
+        from .xgmi import FALLBACK_REASON
+
+        return FALLBACK_REASON[0] or "xGMI all-reduce not attempted (no GPU process group or not on one node)"
+
+    @property
     def graph_safe(self) -> bool:
         """The gradient sync can live inside the captured step graph (a plain kernel: xGMI one-shot)."""
         return self.world == 1 or self.xgmi is not None

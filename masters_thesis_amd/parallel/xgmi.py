@@ -149,10 +149,12 @@ class XgmiAllReduce:
         the configuration does not allow it or its set-up / self-check fails anywhere."""
         mode = os.environ.get("MTA_ALLREDUCE", "auto").lower()
         if mode == "rccl":
+            FALLBACK_REASON[0] = "MTA_ALLREDUCE=rccl"
             return None
         required = mode == "xgmi"
 
         def no(reason: str):
+            FALLBACK_REASON[0] = reason
             if required:
                 raise RuntimeError(f"MTA_ALLREDUCE=xgmi but the xGMI all-reduce is unavailable: {reason}")
             if dist.get_rank(group) == 0:
@@ -173,6 +175,7 @@ class XgmiAllReduce:
         if not _agree(ok, device, group):
             ar.close()
             return no(f"self-check failed: {why or 'on another rank'}")
+        FALLBACK_REASON[0] = None
         return ar
 
     def _self_check(self, group, rounds: int = 3):
@@ -198,6 +201,10 @@ class XgmiAllReduce:
             return False, str(e)
         finally:
             self.force_twoshot = None
+
+
+# why the last XgmiAllReduce.create returned None (the bench record's allreduce_fallback_reason), None after a success
+FALLBACK_REASON: List[Optional[str]] = [None]
 
 
 def check_all_health() -> None:

@@ -13,6 +13,7 @@ case "$1" in
   *)
     hipcc $F csrc/tools/lstm_stack_probe.hip -o tools_bin/stack_s0 &
     hipcc $F -DMTA_STAMPS=1 csrc/tools/lstm_stack_probe.hip -o tools_bin/stack_s1 &
+    hipcc $F -DMTA_STAMPS=2 csrc/tools/lstm_stack_probe.hip -o tools_bin/stack_tl &
     ;;
 esac
 wait

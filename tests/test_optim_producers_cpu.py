@@ -84,3 +84,29 @@ def test_active_optimizer_hook(monkeypatch):
         assert O.register_grad_producer(params[0].grad) is not None
     finally:
         O.set_producer_optimizer(None)
+
+
+def test_step_hands_packed_partials_after_double_registration(monkeypatch):
+    """after A (slot 0), B (slot 1) and a second registration of A, only B is covered, in slot 1.
+    The kernel sums every partial it is handed, so step() must pass slots [0, 1] with A's stale slot 0 zeroed (not
+    slot 0 alone, which would drop B's partials and add A's stale ones to the clip norm)."""
+    opt, params = _opt([(8, 4), (4, 4)], monkeypatch)
+    pa = opt.register_producer(params[0].grad)
+    pb = opt.register_producer(params[1].grad)
+    pa.fill_(7.0)  # A's first producer wrote its partials
+    pb.fill_(1.0)  # B's producer wrote its partials
+    assert opt.register_producer(params[0].grad) is None  # A again: accumulates, its range leaves the plan
+    seen = {}
+
+    class _C:
+        def adam_fused(self, *a):
+            seen["cov_s"], seen["cov_e"], seen["ext"] = a[-3], a[-2], a[-1]
+
+    monkeypatch.setattr(O, "lib", lambda *a, **k: _C())
+    opt.partials = torch.zeros(4)
+    opt.ticket = torch.zeros(1, dtype=torch.int64)
+    opt.step(max_norm=5.0)
+    assert seen["cov_s"] == [8] and seen["cov_e"] == [12]
+    ext = seen["ext"]
+    assert ext.numel() == 2 * opt._nparts
+    assert float(ext.sum()) == float(opt._nparts)  # B's partials only; A's stale slot zeroed
