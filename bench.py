@@ -316,14 +316,14 @@ def main(argv=None):
                 "steps_per_graph": S,
                 "residency": args.residency,
                 # optional fused paths in force (env switches, ops/extras.py / ops/optim.py)
-                "fused_paths": _fused_paths(cfg),
+                "fused_paths": _fused_paths(cfg, trainer),
             },
         }
         print(json.dumps(rec), flush=True)
     pdist.destroy()
 
 
-def _fused_paths(cfg) -> dict:
+def _fused_paths(cfg, trainer) -> dict:
     arch = cfg.model.get("arch", "lstm")
     if arch == "transformer":
         from masters_thesis_amd.ops import extras as X
@@ -331,7 +331,10 @@ def _fused_paths(cfg) -> dict:
         return {"transformer_ffn": bool(X._TR_FFN[0]), "transformer_attn": bool(X._TR_ATTN[0]),
                 "transformer_wgrad_nn": bool(X._TR_FFN[0] and X._TR_WGRAD_NN[0])}
     if arch == "mlp":
-        return {"optimizer_grad_producers": os.environ.get("MTA_OPTIM_PRODUCERS", "1") != "0"}
+        # producers on (single process, or world > 1 with the xGMI all-reduce's clip-norm partials)
+        return {"optimizer_grad_producers": bool(getattr(trainer, "grad_producers", False))
+                and os.environ.get("MTA_OPTIM_PRODUCERS", "1") != "0",
+                "clip_norm_from_allreduce": trainer.ddp.norm_parts is not None}
     return {}
 
 

@@ -50,8 +50,13 @@ struct XgmiArgs {
   unsigned* peer_flags[XG_MAX];  // this channel's flag rows in every rank's buffer: [2 phases][world][32]
   unsigned* ctl;               // this channel's ctl line
   unsigned* timeout;
+  // clip-norm partials of the reduced bucket (nullable): workgroup b writes the sum of squares of the values it
+  // stored into the gradient to sq[b] (the fused optimizer sums them instead of re-reading the buffer)
+  float* sq;
   int rank, world, twoshot;
 };
+
+__device__ __forceinline__ float f4sq(float4 v) { return fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, v.w * v.w))); }
 
 __device__ __forceinline__ float4 f4add(float4 s, float4 v) {
   s.x += v.x;
@@ -104,6 +109,7 @@ __global__ __launch_bounds__(XG_TPB) void xgmi_allreduce_kernel(XgmiArgs a) {
   const long par = epoch & 1;
   const long stride = (long)gridDim.x * XG_TPB, first = (long)blockIdx.x * XG_TPB + threadIdx.x;
   const float4* my_inbox = a.peer_inbox[a.rank] + par * a.world * a.cap4 + a.off4;
+  float sq = 0.f;  // squares of every value this workgroup stores into the gradient (its last pass over them)
   if (!a.twoshot) {
     for (long i = first; i < a.n4; i += stride) {
       const float4 v = a.grad[i];
@@ -114,6 +120,7 @@ __global__ __launch_bounds__(XG_TPB) void xgmi_allreduce_kernel(XgmiArgs a) {
       float4 s = my_inbox[i];
       for (int p = 1; p < a.world; ++p) s = f4add(s, my_inbox[(long)p * a.cap4 + i]);
       a.grad[i] = s;
+      sq += f4sq(s);
     }
   } else {
     // reduce-scatter: element i belongs to chunk i / chunk4 (owner rank)
@@ -130,7 +137,16 @@ __global__ __launch_bounds__(XG_TPB) void xgmi_allreduce_kernel(XgmiArgs a) {
     }
     xg_signal_wait(a, 1, epoch);
     const float4* g = a.peer_gather[a.rank] + par * a.cap4 + a.off4;
-    for (long i = first; i < a.n4; i += stride) a.grad[i] = g[i];
+    for (long i = first; i < a.n4; i += stride) {
+      const float4 v = g[i];
+      a.grad[i] = v;
+      sq += f4sq(v);
+    }
+  }
+  if (a.sq) {
+    __shared__ float scr[XG_TPB / 64];
+    sq = block_sum(sq, scr);  // the same workgroup -> slot and summation order every step: deterministic
+    if (threadIdx.x == 0) a.sq[blockIdx.x] = sq;
   }
 }
 
@@ -183,8 +199,11 @@ int mta_xgmi_timeout_word() { return XG_TIMEOUT; }
 
 // grad: the bucket's n floats (n % 4 == 0) at flat offset `off` (off % 4 == 0, off + n <= cap); bufs[p]: rank p's
 // comm buffer as mapped here (own included); twoshot: reduce-scatter + all-gather instead of one-shot
+int mta_xgmi_max_blocks() { return XG_BIG_BLOCKS; }
+
+// sq (nullable): mta_xgmi_max_blocks() floats of clip-norm partials of this bucket (zero where no workgroup ran)
 int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int channels, int twoshot,
-                       void* const* bufs, int rank, int world, unsigned* ctl, hipStream_t st) {
+                       void* const* bufs, int rank, int world, unsigned* ctl, float* sq, hipStream_t st) {
   if (world < 1 || world > XG_MAX || rank < 0 || rank >= world || n % 4 || off % 4 || cap % 4 || off + n > cap ||
       channel < 0 || channel >= channels || channels > XG_MAX_CHANNELS || n <= 0)
     return -1;
@@ -206,6 +225,7 @@ int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int
   a.rank = rank;
   a.world = world;
   a.twoshot = twoshot ? 1 : 0;
+  a.sq = sq;
   // grid cap by bucket size (profiles/r4_xgmi_local.txt, 2 processes on one GPU): up to 8 MB the flag protocol
   // dominates and fewer workgroups are faster (3.2 MB one-shot: 29 us at 32, 31 at 64, 35 at 128); a 52 MB bucket
   // is bandwidth-bound (547 / 330 / 233 / 224 us at 32 / 64 / 128 / 256).  At most 256 (one per CU: every

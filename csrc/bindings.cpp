@@ -59,7 +59,7 @@ int mta_adam_fused_partials();
 void mta_adam_fused(float* p, float* g, float* m, float* v, long n, float* partials, unsigned long long* ticket,
                     const float* lr, float* step, float beta1, float beta2, float eps, float wd, float max_norm,
                     float scale, int adamw, int zero_grad, float* norm_out, float* nonfinite, int n_cov,
-                    const long* cov_s, const long* cov_e, const float* ext, int n_ext, hipStream_t st);
+                    const long* cov_s, const long* cov_e, const float* ext, int n_ext, int ext_only, hipStream_t st);
 void mta_gemm_grad_producer(float* norm_parts, int overwrite);
 int mta_gemm_norm_parts();
 void mta_adam(float* p, float* g, float* m, float* v, long n, const float* partials, const float* lr,
@@ -110,17 +110,18 @@ int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float* x, const 
                          const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                          float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
                          const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
-                         const MtaBatchGather* gather, hipStream_t st);
+                         const MtaBatchGather* gather, unsigned long long* gran, int decoupled, hipStream_t st);
 int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* x, const float* const* w_ih,
                        const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                        float* const* hseq, float* const* xdrop, uint32_t* const* mask, float* const* stash,
-                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T, hipStream_t st);
+                       const uint64_t* seeds, float drop_p, unsigned* flags, int N, int Np, int T,
+                       unsigned long long* gran, int decoupled, hipStream_t st);
 int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                        const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
                        float* const* g_bih, float* const* g_bhh, const uint32_t* const* mask, float* const* part,
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
-                       hipStream_t st);
+                       int gran, hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 int mta_lstm_stack_epoch_shift(int T);
 // allreduce.hip (one-shot / two-shot all-reduce over xGMI peer memory, one channel per bucket)
@@ -134,7 +135,8 @@ int mta_xgmi_ctl_words();
 int mta_xgmi_max_channels();
 int mta_xgmi_timeout_word();
 int mta_xgmi_allreduce(float* grad, long n, long off, long cap, int channel, int channels, int twoshot,
-                       void* const* bufs, int rank, int world, unsigned* ctl, hipStream_t st);
+                       void* const* bufs, int rank, int world, unsigned* ctl, float* sq, hipStream_t st);
+int mta_xgmi_max_blocks();
 // data.hip (dataset build)
 int mta_dgp(uint64_t seed, int n_stocks, long n_samples, int mkt_df, float mkt_loc, float mkt_scale, int idio_df,
             float idio_loc, float idio_scale, float a_loc, float a_scale, float b_loc, float b_scale, float* r_market,
@@ -515,7 +517,7 @@ int64_t adam_fused_partials() { return mta_adam_fused_partials(); }
 void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tensor partials, at::Tensor ticket,
                 at::Tensor lr, at::Tensor step, double beta1, double beta2, double eps, double wd, double max_norm,
                 double scale, bool adamw, bool zero_grad, const OptT& norm_out, const OptT& nonfinite,
-                std::vector<int64_t> cov_s, std::vector<int64_t> cov_e, const OptT& ext) {
+                std::vector<int64_t> cov_s, std::vector<int64_t> cov_e, const OptT& ext, bool ext_only) {
   CHECK_F32(p);
   CHECK_F32(g);
   CHECK_F32(m);
@@ -532,6 +534,9 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
   for (size_t k = 0; k < cov_s.size(); ++k)
     TORCH_CHECK(0 <= cov_s[k] && cov_s[k] <= cov_e[k] && cov_e[k] <= n / 4, "adam_fused: covered range out of bounds");
   TORCH_CHECK(cov_s.empty() || has(ext), "adam_fused: covered ranges need their producer partials");
+  // ext_only: ext holds the squares of the WHOLE gradient (the xGMI all-reduce's partials): no norm pass at all;
+  // the covered ranges then only mark what is left unzeroed
+  TORCH_CHECK(!ext_only || has(ext), "adam_fused: ext_only needs ext");
   if (has(ext)) {
     CHECK_F32(*ext);
   }
@@ -545,7 +550,7 @@ void adam_fused(at::Tensor p, at::Tensor g, at::Tensor m, at::Tensor v, at::Tens
                  has(ext) ? ext->data_ptr<float>() : nullptr,
                  // every partial the caller passes is summed (FusedAdam.step hands over slots [0, last used slot],
                  // the unowned ones zeroed)
-                 has(ext) ? (int)ext->numel() : 0,
+                 has(ext) ? (int)ext->numel() : 0, ext_only ? 1 : 0,
                  cur_stream());
 }
 
@@ -1004,8 +1009,15 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
                                 std::vector<at::Tensor> b_hh, std::vector<at::Tensor> hseq,
                                 std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
                                 std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags,
-                                int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather) {
+                                int64_t N, int64_t Np, int64_t T, const MtaBatchGather* gather, const OptT& gran) {
   const int64_t L = (int64_t)w_hh.size();
+  // gran: the decoupled form's layer hand-off granules, int64[(L - 1) * T * Np * H] (L = 1: any, even empty);
+  // None selects the barrier form (MTA_LSTM_DEC=0)
+  const bool dec = has(gran);
+  if (dec) {
+    TORCH_CHECK(gran->is_cuda() && gran->scalar_type() == at::kLong && gran->numel() >= (L - 1) * T * Np * H,
+                "gran: int64[(L - 1) * T * Np * H] hand-off granules");
+  }
   CHECK_F32(x);
   TORCH_CHECK(x.numel() == N * T * fin, "x must be (N, T, F)");
   TORCH_CHECK(w_ih.size() == (size_t)L && b_ih.size() == (size_t)L && b_hh.size() == (size_t)L &&
@@ -1036,7 +1048,10 @@ static void lstm_stack_fwd_impl(int64_t H, int64_t prec, int64_t fin, at::Tensor
                                       cwh.data(), cbi.data(), cbh.data(), hs.data(), xd.data(), mk.data(), sh.data(),
                                       reinterpret_cast<const uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p,
                                       reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T,
-                                      gather, cur_stream());
+                                      gather,
+                                      dec && L > 1 ? reinterpret_cast<unsigned long long*>(gran->data_ptr<int64_t>())
+                                                   : nullptr,
+                                      dec ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_fwd: unsupported configuration (rc=", rc, ")");
 }
 
@@ -1044,9 +1059,9 @@ void lstm_stack_fwd(int64_t H, int64_t prec, int64_t fin, at::Tensor x, std::vec
                     std::vector<at::Tensor> w_hh, std::vector<at::Tensor> b_ih, std::vector<at::Tensor> b_hh,
                     std::vector<at::Tensor> hseq, std::vector<at::Tensor> xdrop, std::vector<at::Tensor> masks,
                     std::vector<at::Tensor> stash, at::Tensor seeds, double drop_p, at::Tensor flags, int64_t N,
-                    int64_t Np, int64_t T) {
+                    int64_t Np, int64_t T, const OptT& gran) {
   lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N, Np,
-                      T, nullptr);
+                      T, nullptr, gran);
 }
 
 // the same launch with the training step's batch gather folded in: src[k] (rows, ...) -> dst[k] (B, ...) at rows
@@ -1057,7 +1072,7 @@ void lstm_stack_fwd_gather(int64_t H, int64_t prec, int64_t fin, at::Tensor x, s
                            std::vector<at::Tensor> masks, std::vector<at::Tensor> stash, at::Tensor seeds,
                            double drop_p, at::Tensor flags, int64_t N, int64_t Np, int64_t T,
                            std::vector<at::Tensor> src, std::vector<at::Tensor> dst, at::Tensor perm, at::Tensor cursor,
-                           int64_t B) {
+                           int64_t B, const OptT& gran) {
   TORCH_CHECK(src.size() == dst.size() && src.size() >= 1 && src.size() <= 4, "1..4 gathered tensors");
   TORCH_CHECK(perm.is_cuda() && cursor.is_cuda() && perm.scalar_type() == at::kInt &&
               cursor.scalar_type() == at::kInt, "perm/cursor: int32 GPU tensors");
@@ -1076,7 +1091,7 @@ void lstm_stack_fwd_gather(int64_t H, int64_t prec, int64_t fin, at::Tensor x, s
   g.cursor = cursor.data_ptr<int>();
   g.B = (int)B;
   lstm_stack_fwd_impl(H, prec, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, masks, stash, seeds, drop_p, flags, N, Np,
-                      T, &g);
+                      T, &g, gran);
 }
 
 // grads: [] (weight gradients by the caller) or 4 lists g_wih, g_whh, g_bih, g_bhh of per-layer gradient
@@ -1086,7 +1101,8 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
                     std::vector<at::Tensor> dX, std::vector<at::Tensor> hseq, std::vector<at::Tensor> inp,
                     std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks,
                     std::vector<at::Tensor> parts, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
-                    int64_t N, int64_t Np, int64_t T) {
+                    int64_t N, int64_t Np, int64_t T, bool gran) {
+  // gran: dX[l] hold (T, Np, H) tagged 8-byte granules (2 H floats per row), the decoupled hand-off
   const int64_t L = (int64_t)w_hh.size();
   CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
@@ -1094,7 +1110,7 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
               dX.size() == (size_t)L, "per-layer lists");
   for (int64_t l = 0; l < L; ++l) {
     TORCH_CHECK(stash[l].numel() == T * Np * 5 * H && dG[l].numel() == T * Np * 4 * H, "stash/dG shapes");
-    TORCH_CHECK(l == L - 1 || dX[l].numel() == T * Np * H, "dX shape");
+    TORCH_CHECK(l == L - 1 || dX[l].numel() == (gran ? 2 : 1) * T * Np * H, "dX shape");
   }
   const bool fused = !grads.empty();
   if (fused) {
@@ -1151,7 +1167,7 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
       fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr, mk.data(),
       pt.empty() ? nullptr : pt.data(),
       reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p, dropout ? 1 : 0,
-      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, cur_stream());
+      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, gran ? 1 : 0, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
 }
 
@@ -1190,15 +1206,20 @@ void xgmi_ipc_close(int64_t p) { mta_xgmi_ipc_close(reinterpret_cast<void*>(p));
 // bufs: every rank's comm buffer as mapped in this process; ctl: int32[xgmi_ctl_words] zero-initialised once
 // (per-channel epoch and arrival counters, the shared timeout count)
 void xgmi_allreduce(at::Tensor grad, int64_t off, int64_t cap, int64_t channel, int64_t channels, bool twoshot,
-                    std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl) {
+                    std::vector<int64_t> bufs, int64_t rank, at::Tensor ctl, const OptT& sq) {
   CHECK_F32(grad);
   TORCH_CHECK(ctl.is_cuda() && ctl.scalar_type() == at::kInt && ctl.numel() >= mta_xgmi_ctl_words(), "ctl words");
+  if (has(sq)) {
+    CHECK_F32(*sq);
+    TORCH_CHECK(sq->numel() >= mta_xgmi_max_blocks(), "sq: xgmi_max_blocks() floats of clip-norm partials");
+  }
   std::vector<void*> b;
   for (auto v : bufs) b.push_back(reinterpret_cast<void*>(v));
   c10::hip::HIPGuardMasqueradingAsCUDA guard(grad.device());
   const int rc = mta_xgmi_allreduce(grad.data_ptr<float>(), (long)grad.numel(), (long)off, (long)cap, (int)channel,
                                     (int)channels, twoshot ? 1 : 0, b.data(), (int)rank, (int)b.size(),
-                                    reinterpret_cast<unsigned*>(ctl.data_ptr<int>()), cur_stream());
+                                    reinterpret_cast<unsigned*>(ctl.data_ptr<int>()),
+                                    has(sq) ? sq->data_ptr<float>() : nullptr, cur_stream());
   TORCH_CHECK(rc == 0, "xgmi_allreduce: bad arguments (rc=", rc, ")");
 }
 
@@ -1419,6 +1440,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_heads_deterministic", [](bool on) { mta_set_heads_deterministic(on ? 1 : 0); });
   m.def("xgmi_max_channels", []() { return (int64_t)mta_xgmi_max_channels(); });
   m.def("xgmi_timeout_word", []() { return (int64_t)mta_xgmi_timeout_word(); });
+  m.def("xgmi_max_blocks", []() { return (int64_t)mta_xgmi_max_blocks(); });
   m.def("lstm_wgrad_part_floats", [](int64_t fused, int64_t T, int64_t H, int64_t F) {
     return (int64_t)mta_lstm_wgrad_part_floats((int)fused, (int)T, (int)H, (int)F);
   });

@@ -223,6 +223,9 @@ struct StackFwdArgs {
   // separate gather launch per training step
   int gather, copy_blocks, main_blocks;
   MtaBatchGather g;
+  // decoupled form (stack_fwd_dec): gran[l] (l >= 1) = layer l's input as tagged granules (T, Np, H) x 8 bytes
+  unsigned long long* gran[MAXL];
+  int dec;  // 1: stack_fwd_dec (the default), 0: the barrier form (MTA_LSTM_DEC=0, A/B)
 };
 
 // Forward workgroup = 3 x (H/16) waves in three roles (one wave of each role per SIMD):
@@ -807,41 +810,602 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
   STACK_TL(0, 3);
 }
 
+// ---------------------------------------------------------------------------------------------
+// forward, decoupled roles (round 6): no per-step workgroup barrier
+// ---------------------------------------------------------------------------------------------
+// The barrier form above makes every step as long as the slowest of its three roles: the recurrent waves' own work
+// was ~1,700 of the ~2,450 cycles of a step, the rest waiting at s_barrier for input / store waves that lose the
+// SIMD's issue arbitration to them (profiles/r4_lstm_f16x2_ab.txt).  Here the roles hand LDS ring slots to each other
+// through per-wave monotonic step counters (the ring-gemm FULL / FREE words of MI355X_MICROARCH.md): a wave waits
+// only for the slots it reads, so input and store waves run ahead / behind within their rings and the recurrent
+// waves wait for each other alone (their h slices: one counter word per wave).  Every dependency is 1:1 by wave
+// index w (recurrent wave w reads the gate pre-activations of units [16w, 16w + 16), written by input wave w, and
+// stages its step for store wave w), except the recurrent waves' h exchange and the input waves' x image.
+//
+// Layer hand-off: the store waves publish the next layer's input (dropout(h), or h) as data-tagged 8-byte granules
+// {value, epoch-stamped step} the moment a step is staged (no progress word, no drain); the consumer's input waves
+// load and check the tags themselves (MI355X_MICROARCH.md handoff-1to1: the granule form, ~0.8-1.0 us idle, about
+// half the flag form's latency).  The barrier form published a step ~5 steps after computing it and its consumer
+// pre-loaded 4 steps ahead: ~10 steps (~13 us) of fill per layer boundary in each direction.
+constexpr int DG = 3;   // gate pre-activation ring (input wave w -> recurrent wave w)
+constexpr int HSL = 3;  // h image slots: h_t in slot (t + 1) % 3 (a wave writing h_t knows every wave read h_{t-2})
+constexpr int XA = 2;   // layers >= 1: an input wave writes its quarter of x_{t+XA} after computing gx_t
+constexpr int DX = XA + 2;  // x image slots (layers >= 1: the four input waves' quarters of x_t)
+constexpr int DS = 3;   // stage slots: step t's fp32 h and BPTT stash in slot t % DS (recurrent wave w -> store wave w)
+enum { SY_H = 0, SY_GX = 1, SY_STG = 2, SY_FREE = 3, SY_XQ = 4, SY_ROWS = 5 };
+
+template <int H, int PREC>
+struct FwdSmemD {
+  static constexpr int ROWB = H + 8, ROWF = H + 4;
+  using E = typename OpT<PREC>::E;
+  float4 gxs[DG][S][H];
+  E h_hi[HSL][S][PREC == PREC_F32 ? 8 : ROWB];
+  __bf16 h_lo[HSL][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  float h_f[HSL][S][PREC == PREC_F32 ? ROWF : 4];
+  E x_hi[DX][S][PREC == PREC_F32 ? 8 : ROWB];
+  __bf16 x_lo[DX][S][PREC == PREC_BF16X3 ? ROWB : 8];
+  float x_f[DX][S][PREC == PREC_F32 ? ROWF : 4];
+  float hout[DS][S][ROWF];
+  float4 st[DS][H / 16][STASH][64];
+  unsigned sy[SY_ROWS][H / 16];  // per-wave step counters: [row][wave] = steps done (monotonic within a launch)
+};
+
+__device__ __forceinline__ unsigned sy_read(const unsigned* p) {
+  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until the NWD counters at p all reach `need` (wave-uniform; need <= 0 returns at once).  Bounded like the
+// global waits: a give-up counts in the timeout word (the host raises) so the grid always drains.
+template <int NWD>
+__device__ __forceinline__ void sy_wait(const unsigned* p, int need, unsigned* tmo, unsigned limit) {
+  if (need <= 0) return;
+  for (unsigned spins = 0;; ++spins) {
+    unsigned m = sy_read(p);
+#pragma unroll
+    for (int k = 1; k < NWD; ++k) {
+      const unsigned v = sy_read(p + k);
+      m = v < m ? v : m;
+    }
+    if ((int)__builtin_amdgcn_readfirstlane(m) >= need) break;
+    if (spins >= limit) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(0);
+  }
+  asm volatile("" ::: "memory");  // the guarded reads are issued after the counter reads (in-order LDS)
+}
+// publish this wave's counter.  The LDS executes one wave's operations in issue order, so a reader that sees the
+// word sees every slot write (or has every slot read) the wave issued before it: the compiler barrier keeps that
+// issue order; no s_waitcnt is needed (a release fence waited lgkmcnt(0): ~150 cycles per post on the recurrent
+// waves' critical path, r6 stamps)
+__device__ __forceinline__ void sy_post(unsigned* p, unsigned v) {
+  asm volatile("" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  asm volatile("" ::: "memory");
+}
+
+// one 8-byte granule {value bits, tag}: agent-scope relaxed load (global_load_dwordx2 sc1: L1 bypass, untorn)
+__device__ __forceinline__ unsigned long long gran_load(const unsigned long long* p) {
+  return __hip_atomic_load(const_cast<unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// two granules {v0, tag}, {v1, tag} as one 16-byte store: write-through (sc1) for a consumer on another XCD, plain
+// (stays in this XCD's L2, where the consumer's sc1 loads find it) for a same-XCD consumer
+__device__ __forceinline__ void gran_store2(unsigned long long* p, float v0, float v1, unsigned tag, bool local) {
+  const f32x4 g{v0, __builtin_bit_cast(float, tag), v1, __builtin_bit_cast(float, tag)};
+  if (local) store_plain_x4(reinterpret_cast<float*>(p), g);
+  else store_sc1_x4(reinterpret_cast<float*>(p), g);
+}
+
+template <int H, int PREC, int FIN0, bool FIRST>
+__device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int layer, const int tile,
+                                              FwdSmemD<H, PREC>& sm, const unsigned base) {
+  constexpr int NW = H / 16;
+  constexpr int KB = H / 32;
+  constexpr int KF = H / 4;
+  constexpr int ROWB = H + 8;
+  constexpr int ROWF = H + 4;
+  using E = typename OpT<PREC>::E;
+  using V8 = typename OpT<PREC>::V8;
+  const bool last = layer == a.L - 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int role = wave / NW;  // 0 recurrent, 1 input, 2 store
+  const int w = wave - role * NW;
+  const int q = lane >> 4, j = lane & 15;
+  const int u = 16 * w + j;
+  const int n0 = tile * S;
+  const int N = a.N, Np = a.Np, T = a.T;
+  unsigned* const tmo = a.timeout;
+  const unsigned lim = a.spin_limit;
+  auto& sy = sm.sy;
+
+  // counters and h_{-1} (image slot 0) start at zero
+  for (int idx = threadIdx.x; idx < SY_ROWS * NW; idx += NW * 192) (&sy[0][0])[idx] = 0u;
+  if constexpr (PREC == PREC_F32) {
+    for (int idx = threadIdx.x; idx < S * ROWF; idx += NW * 192) (&sm.h_f[0][0][0])[idx] = 0.f;
+  } else {
+    for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 192) (&sm.h_hi[0][0][0])[idx] = (E)0.f;
+    if constexpr (PREC == PREC_BF16X3)
+      for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 192) (&sm.h_lo[0][0][0])[idx] = (__bf16)0.f;
+  }
+  __syncthreads();  // P0 (the only barrier before the final one)
+
+  if (role == 2) {
+    // =========================== store waves ===========================
+    float* hseq = a.hseq[layer];
+    float4* stash = reinterpret_cast<float4*>(a.stash[layer]);
+    float* xout = last ? nullptr : a.xdrop[layer + 1];
+    uint32_t* mout = xout ? a.mask[layer + 1] : nullptr;
+    unsigned long long* gout = last ? nullptr : a.gran[layer + 1];
+    const uint32_t pseed = mout ? mta_pair_seed(a.seeds[layer + 1]) : 0;
+    const float keep_scale = 1.0f / (1.0f - a.drop_p);
+    const int ts = lane >> 2, tc = 4 * (lane & 3), unit4 = 16 * w + tc;
+    const unsigned E = base >> a.eshift;
+    if (w == 0 && lane == 0) publish_xcc(a.xcc + layer * a.tr8 + tile, E);
+    const bool local = a.xcd_local && !last && partner_local(a.xcc + (layer + 1) * a.tr8 + tile, E, 1u << 14);
+    SSTAMP_DECL
+    for (int t = 0; t < T; ++t) {
+      SSTAMP(0)
+      sy_wait<1>(&sy[SY_STG][w], t + 1, tmo, lim);
+      SSTAMP(1)
+      const int slot = t % DS;
+      const float4 hv = *reinterpret_cast<const float4*>(&sm.hout[slot][ts][unit4]);
+      f32x4 sv[STASH];  // (an array of HIP's float4 struct stayed in scratch memory)
+      if (stash) {
+#pragma unroll
+        for (int k = 0; k < STASH; ++k) sv[k] = *reinterpret_cast<const f32x4*>(&sm.st[slot][w][k][lane]);
+      }
+      sy_post(&sy[SY_FREE][w], t + 1);  // (its fence completes the reads above)
+      SSTAMP(2)
+      const size_t o = ((size_t)t * Np + n0 + ts) * H + unit4;
+      if (gout) {
+        // the hand-off first: dropout(h) (keep bytes: pair hash, common.h) or h as tagged granules
+        float4 xv = hv;
+        if (xout) {
+          const uint32_t kw = stack_keep_word(pseed, (uint32_t)(t * Np + n0 + ts), unit4, a.drop_p);
+          xv = make_float4(hv.x * ((kw & 0xFFu) ? keep_scale : 0.f), hv.y * ((kw & 0xFF00u) ? keep_scale : 0.f),
+                           hv.z * ((kw & 0xFF0000u) ? keep_scale : 0.f), hv.w * ((kw & 0xFF000000u) ? keep_scale : 0.f));
+          const unsigned tag = base + (unsigned)(t + 1);
+          gran_store2(gout + o, xv.x, xv.y, tag, local);
+          gran_store2(gout + o + 2, xv.z, xv.w, tag, local);
+          store_plain_x4(xout + o, f32x4{xv.x, xv.y, xv.z, xv.w});  // the backward's W_ih gradient input
+          mout[stack_keep_index(t, tile, a.ntiles, ts, H, unit4)] = kw;
+        } else {
+          const unsigned tag = base + (unsigned)(t + 1);
+          gran_store2(gout + o, xv.x, xv.y, tag, local);
+          gran_store2(gout + o + 2, xv.z, xv.w, tag, local);
+        }
+      }
+      store_plain_x4(hseq + o, f32x4{hv.x, hv.y, hv.z, hv.w});
+      if (stash) {
+#pragma unroll
+        for (int k = 0; k < STASH; ++k)
+          *reinterpret_cast<f32x4*>(&stash[stash_index(t, tile, a.ntiles, w, NW, lane) + 64 * k]) = sv[k];
+      }
+      SSTAMP(3)
+    }
+    SSTAMP_FLUSH(0, 1, w == 0)
+    mta_wait_vmem();
+    __syncthreads();  // F
+    return;
+  }
+
+  float bias[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) bias[g] = a.b_ih[layer][g * H + u] + a.b_hh[layer][g * H + u];
+
+  if (role == 1) {
+    // =========================== input waves ===========================
+    const float* w_ih = a.w_ih[layer];
+    if constexpr (FIRST) {
+      float wi[4][FIN0];
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int f = 0; f < FIN0; ++f) wi[g][f] = w_ih[(g * H + u) * FIN0 + f];
+      float nmask[4];
+      const float* xbase[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + 4 * q + i;
+        const int nr = n < N ? n : N - 1;
+        nmask[i] = n < N ? 1.f : 0.f;
+        if (a.gather) {
+          const int K = N / a.g.B, b = nr / K, s = nr - b * K;
+          const int wd = a.g.perm[a.g.cursor[0] * a.g.B + b];
+          xbase[i] = a.g.src[0] + (size_t)wd * a.g.row[0] + (size_t)s * T * FIN0;
+        } else {
+          xbase[i] = a.x + (size_t)nr * T * FIN0;
+        }
+      }
+      struct XBuf {
+        float x0[4][FIN0];
+      };
+      XBuf xbA, xbB;
+      auto load_input = [&](int t, XBuf& xb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int f = 0; f < FIN0; ++f) xb.x0[i][f] = xbase[i][(size_t)t * FIN0 + f];
+      };
+      // interval t: gx_t from the set loaded two intervals ago, then refill it with x_{t+2}
+      SSTAMP_DECL
+      auto body = [&](int t, XBuf& xb) {
+        SSTAMP(0)
+        sy_wait<1>(&sy[SY_H][w], t - DG + 1, tmo, lim);  // slot t % DG: recurrent wave w read gx_{t-DG}
+        SSTAMP(1)
+        const int slot = t % DG;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float acc[4];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float sacc = bias[g];
+#pragma unroll
+            for (int f = 0; f < FIN0; ++f) sacc = fmaf(xb.x0[i][f] * nmask[i], wi[g][f], sacc);
+            acc[g] = sacc;
+          }
+          sm.gxs[slot][4 * q + i][u] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        }
+        sy_post(&sy[SY_GX][w], t + 1);
+        SSTAMP(2)
+        if (t + 2 < T) load_input(t + 2, xb);
+        SSTAMP(3)
+      };
+      load_input(0, xbA);
+      if (T > 1) load_input(1, xbB);
+      for (int t = 0; t < T; t += 2) {
+        body(t, xbA);
+        if (t + 1 < T) body(t + 1, xbB);
+      }
+      SSTAMP_FLUSH(0, 2, w == 0)
+    } else {
+      constexpr int XKB = KB, XKF = KF;
+      V8 Xhi[4][PREC == PREC_F32 ? 1 : XKB], Xlo[4][kWeightLo<PREC> ? XKB : 1];
+      float Xf[4][PREC == PREC_F32 ? XKF : 1];
+      if constexpr (PREC == PREC_F32) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) Xf[g][kk] = w_ih[(size_t)(g * H + u) * H + KF * q + kk];
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              E hi, lo;
+              split_bf16(w_ih[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
+              Xhi[g][kb][e] = hi;
+              if constexpr (kWeightLo<PREC>) Xlo[g][kb][e] = lo;
+            }
+      }
+      // This wave's quarter of x_t (row ls of the tile, units lu .. lu + 3: four granules of the producer layer) goes
+      // into a shared LDS image that every input wave reads its MFMA A operand from.  (Each wave reading all of x_t
+      // from the granules instead -- 16 scattered 8-byte loads per lane -- took ~3,000 cycles a step and crowded
+      // the memory pipe: L=2 forward 79 -> 140 us, profiles/r6_lstm_decoupled.txt.)
+      const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
+      const unsigned long long* gin = a.gran[layer];
+      unsigned long long gq[4];
+      auto issue = [&](int t) {
+        const unsigned long long* p = gin + ((size_t)t * Np + n0 + ls) * H + lu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gq[e] = gran_load(p + e);
+      };
+      // x_t's quarter: every lane's four tags must carry step t of this launch; reload until they do (bounded)
+      auto ready = [&](int t) -> float4 {
+        const unsigned tag = base + (unsigned)(t + 1);
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) ok &= (unsigned)(gq[e] >> 32) == tag;
+          if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+          if (spins >= lim) {
+            if (lane == 0) __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          issue(t);
+        }
+        return make_float4(__builtin_bit_cast(float, (unsigned)gq[0]), __builtin_bit_cast(float, (unsigned)gq[1]),
+                           __builtin_bit_cast(float, (unsigned)gq[2]), __builtin_bit_cast(float, (unsigned)gq[3]));
+      };
+      auto write_x = [&](int t, const float4& xq) {
+        // image slot t % DX last held x_{t-DX}: every input wave has computed gx_{t-DX} from it
+        sy_wait<NW>(&sy[SY_GX][0], t - DX + 1, tmo, lim);
+        const int slot = t % DX;
+        if constexpr (PREC == PREC_F32) {
+          *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
+        } else {
+          const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
+          if constexpr (PREC == PREC_F16X2) {
+            typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+            f16x4_t v4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
+            *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
+          } else {
+            bf16x4 hi4, lo4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              __bf16 hi, lo;
+              split_bf16(xv[e], hi, lo);
+              hi4[e] = hi;
+              lo4[e] = lo;
+            }
+            *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
+            if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
+          }
+        }
+        sy_post(&sy[SY_XQ][w], t + 1);
+      };
+      auto compute_gx_img = [&](int t) {
+        const int xs = t % DX, slot = t % DG;
+        f32x4 acc[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = f32x4{bias[g], bias[g], bias[g], bias[g]};
+        if constexpr (PREC == PREC_F32) {
+          const float* xr = &sm.x_f[xs][j][KF * q];
+#pragma unroll
+          for (int kk = 0; kk < KF; ++kk) {
+            const float av = xr[kk];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Xf[g][kk], acc[g]);
+          }
+        } else {
+          V8 ahi[KB];
+          bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb) {
+            ahi[kb] = *reinterpret_cast<const V8*>(&sm.x_hi[xs][j][32 * kb + 8 * q]);
+            if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.x_lo[xs][j][32 * kb + 8 * q]);
+          }
+#pragma unroll
+          for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              if constexpr (PREC == PREC_BF16X3) {
+                acc[g] = mfma16x16x32(alo[kb], Xhi[g][kb], acc[g]);
+                acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
+              }
+              if constexpr (PREC == PREC_F16X2) acc[g] = mfma16x16x32(ahi[kb], Xlo[g][kb], acc[g]);
+              acc[g] = mfma16x16x32(ahi[kb], Xhi[g][kb], acc[g]);
+            }
+        }
+        sy_wait<1>(&sy[SY_H][w], t - DG + 1, tmo, lim);  // gx slot: recurrent wave w read gx_{t-DG}
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          sm.gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+        sy_post(&sy[SY_GX][w], t + 1);
+      };
+      // iteration t: gx_t, then x_{t+XA}'s quarter into the image (its granules were issued an iteration ago): the
+      // quarters of x_t were written XA - 1 iterations before they are needed, so one slow input wave does not hold
+      // the other three at the image every step (XA = 1 spent ~1,300 of ~2,560 cycles a step of the layer-1 input
+      // waves in quarter / slot waits, r6 stamps).  (Writing x_{t+1} first whenever its granules had already arrived
+      // measured slower: 82.0 -> 86.1 us, profiles/r6_lstm_decoupled.txt)
+      for (int t = 0; t < XA && t < T; ++t) {
+        issue(t);
+        write_x(t, ready(t));
+      }
+      if (XA < T) issue(XA);
+      SSTAMP_DECL
+      for (int t = 0; t < T; ++t) {
+        SSTAMP(0)
+        sy_wait<NW>(&sy[SY_XQ][0], t + 1, tmo, lim);  // x_t's image complete (all four quarters)
+        SSTAMP(1)
+        compute_gx_img(t);
+        SSTAMP(2)
+        if (t + XA < T) {
+          const float4 xq = ready(t + XA);
+          SSTAMP(3)
+          if (t + XA + 1 < T) issue(t + XA + 1);
+          write_x(t + XA, xq);
+          SSTAMP(4)
+        }
+      }
+      SSTAMP_FLUSH(0, 2, w == 0)
+    }
+    __syncthreads();  // F
+    return;
+  }
+
+  // =========================== recurrent waves ===========================
+  if (__builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(STACK_PRIO);
+  const float* w_hh = a.w_hh[layer];
+  const bool stash = a.stash[layer] != nullptr;
+  V8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][kWeightLo<PREC> ? KB : 1];
+  float Bf[4][PREC == PREC_F32 ? KF : 1];
+  if constexpr (PREC == PREC_F32) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk) Bf[g][kk] = w_hh[(size_t)(g * H + u) * H + 4 * kk + q];
+  } else {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          E hi, lo;
+          split_bf16(w_hh[(size_t)(g * H + u) * H + 32 * kb + 8 * q + e], hi, lo);
+          Bhi[g][kb][e] = hi;
+          if constexpr (kWeightLo<PREC>) Blo[g][kb][e] = lo;
+        }
+  }
+  float c[4] = {0.f, 0.f, 0.f, 0.f};
+  f32x4 pgi, pgf, pgg, pgo, pcc;
+  float h[4];
+  // step t's fp32 h and BPTT stash -> stage slot t % DS (store wave w read step t - DS out of it first; free_seen:
+  // its counter as read with the step's batch)
+  unsigned free_seen = 0;
+  auto stage = [&](int t) {
+    if ((int)__builtin_amdgcn_readfirstlane(free_seen) < t - DS + 1) sy_wait<1>(&sy[SY_FREE][w], t - DS + 1, tmo, lim);
+    const int slot = t % DS;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sm.hout[slot][4 * q + i][u] = h[i];
+    if (stash) {
+      sm.st[slot][w][0][lane] = make_float4(pgi[0], pgi[1], pgi[2], pgi[3]);
+      sm.st[slot][w][1][lane] = make_float4(pgf[0], pgf[1], pgf[2], pgf[3]);
+      sm.st[slot][w][2][lane] = make_float4(pgg[0], pgg[1], pgg[2], pgg[3]);
+      sm.st[slot][w][3][lane] = make_float4(pgo[0], pgo[1], pgo[2], pgo[3]);
+      sm.st[slot][w][4][lane] = make_float4(pcc[0], pcc[1], pcc[2], pcc[3]);
+    }
+  };
+  SSTAMP_DECL
+  // A step reads its counters and the slots they guard in ONE batch (counters first: the LDS serves a wave's reads in
+  // order, so a slot read issued after a counter that shows it ready returns its final content) and waits once; only
+  // when a counter is behind does it poll and re-read (rare: the input waves run DG steps ahead, and the h counters
+  // of the four recurrent waves are usually all posted by the time the batch is served).  Polling first and reading
+  // after cost two LDS round trips per dependency (~600 of ~2,460 cycles a step, r6 stamps).
+  f32x4 acc[4];
+  V8 ahi[PREC == PREC_F32 ? 1 : KB];
+  bf16x8 alo[PREC == PREC_BF16X3 ? KB : 1];
+  auto read_gx = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 v = sm.gxs[t % DG][4 * q + i][u];
+      acc[0][i] = v.x;
+      acc[1][i] = v.y;
+      acc[2][i] = v.z;
+      acc[3][i] = v.w;
+    }
+  };
+  auto read_a = [&](int hs) {
+    if constexpr (PREC != PREC_F32) {
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        ahi[kb] = *reinterpret_cast<const V8*>(&sm.h_hi[hs][j][32 * kb + 8 * q]);
+        if constexpr (PREC == PREC_BF16X3) alo[kb] = *reinterpret_cast<const bf16x8*>(&sm.h_lo[hs][j][32 * kb + 8 * q]);
+      }
+    }
+  };
+  for (int t = 0; t < T; ++t) {
+    SSTAMP(0)
+    const int hs = t % HSL, hn = (t + 1) % HSL;
+    const unsigned cg = sy_read(&sy[SY_GX][w]);  // gx_t of this wave's units
+    unsigned hmin = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {  // every recurrent wave's slice of h_{t-1}
+      const unsigned v = sy_read(&sy[SY_H][k]);
+      hmin = v < hmin ? v : hmin;
+    }
+    free_seen = sy_read(&sy[SY_FREE][w]);  // the stage slot of step t-1 (checked by stage())
+    asm volatile("" ::: "memory");
+    read_gx(t);
+    read_a(hs);
+    SSTAMP(1)
+    if ((int)__builtin_amdgcn_readfirstlane(cg) < t + 1 || (int)__builtin_amdgcn_readfirstlane(hmin) < t) {
+      sy_wait<1>(&sy[SY_GX][w], t + 1, tmo, lim);
+      sy_wait<NW>(&sy[SY_H][0], t, tmo, lim);
+      read_gx(t);
+      read_a(hs);
+    }
+    SSTAMP(2)
+    if constexpr (PREC == PREC_F32) {
+      if (t > 0) stage(t - 1);
+      const float* hrow = &sm.h_f[hs][j][q * KF];
+#pragma unroll
+      for (int kk = 0; kk < KF; ++kk) {
+        const float av = hrow[kk];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Bf[g][kk], acc[g]);
+      }
+    } else {
+      if (t > 0) stage(t - 1);
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+#pragma unroll
+        for (int sg = 0; sg < kPasses<PREC>; ++sg) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            if constexpr (PREC == PREC_BF16X3) {
+              if (sg == 0) acc[g] = mfma16x16x32(alo[kb], Bhi[g][kb], acc[g]);
+              else if (sg == 1) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
+              else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            } else if constexpr (PREC == PREC_F16X2) {
+              if (sg == 0) acc[g] = mfma16x16x32(ahi[kb], Blo[g][kb], acc[g]);
+              else acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            } else {
+              acc[g] = mfma16x16x32(ahi[kb], Bhi[g][kb], acc[g]);
+            }
+          }
+        }
+      }
+    }
+    // step t-1 staged (posted behind the MFMA chain: its fence then finds the stage writes long complete)
+    __builtin_amdgcn_sched_barrier(0);
+    if (t > 0) sy_post(&sy[SY_STG][w], (unsigned)t);
+    SSTAMP(3)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pgi[i] = mta_sigmoid(acc[0][i]);
+      pgf[i] = mta_sigmoid(acc[1][i]);
+      pgg[i] = mta_tanh(acc[2][i]);
+      pgo[i] = mta_sigmoid(acc[3][i]);
+      c[i] = fmaf(pgf[i], c[i], pgi[i] * pgg[i]);
+      pcc[i] = c[i];
+      h[i] = pgo[i] * mta_tanh(c[i]);
+    }
+    SSTAMP(4)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s4 = 4 * q + i;
+      if constexpr (PREC == PREC_F32) {
+        sm.h_f[hn][s4][(u & 3) * KF + (u >> 2)] = h[i];
+      } else if constexpr (PREC == PREC_F16X2) {
+        sm.h_hi[hn][s4][u] = (_Float16)h[i];
+      } else {
+        __bf16 hi, lo;
+        split_bf16(h[i], hi, lo);
+        sm.h_hi[hn][s4][u] = hi;
+        if constexpr (PREC == PREC_BF16X3) sm.h_lo[hn][s4][u] = lo;
+      }
+    }
+    sy_post(&sy[SY_H][w], (unsigned)(t + 1));
+    SSTAMP(5)
+  }
+  SSTAMP_FLUSH(0, 0, wave == 0)
+  stage(T - 1);
+  sy_post(&sy[SY_STG][w], (unsigned)T);
+  __syncthreads();  // F
+}
+
 // batch rows -> static buffers, spread over workgroups [0, P) (the gather of csrc/lstm_aux.hip, in this launch);
 // four independent 16-byte loads in flight per thread before their stores
 __device__ __forceinline__ void batch_copy(const MtaBatchGather& g, int p, int P) {
+  // 32-bit indices (a batch is B x row floats, far below 2^31): the 64-bit division's two-path expansion branched
+  // around the loads and kept v[] in scratch memory
   const int cur = g.cursor[0];
-  const long stride = (long)P * blockDim.x, first = (long)p * blockDim.x + threadIdx.x;
+  const int stride = P * (int)blockDim.x, first = p * (int)blockDim.x + (int)threadIdx.x;
   for (int k = 0; k < g.nt; ++k) {
-    const long row = g.row[k], total = (long)g.B * row;
+    const int row = (int)g.row[k], total = g.B * row;
     if ((row & 3) == 0 && ((((uintptr_t)g.src[k]) | ((uintptr_t)g.dst[k])) & 15) == 0) {
-      const long row4 = row / 4, n4 = total / 4;
-      const float4* s4 = reinterpret_cast<const float4*>(g.src[k]);
-      float4* d4 = reinterpret_cast<float4*>(g.dst[k]);
-      for (long e0 = first; e0 < n4; e0 += 4 * stride) {
-        float4 v[4];
+      const int row4 = row / 4, n4 = total / 4;
+      const f32x4* s4 = reinterpret_cast<const f32x4*>(g.src[k]);
+      f32x4* d4 = reinterpret_cast<f32x4*>(g.dst[k]);
+      for (int e0 = first; e0 < n4; e0 += 4 * stride) {
+        f32x4 v[4];  // (HIP's float4 struct kept this array in scratch memory)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const long e = e0 + r * stride;
-          if (e < n4) {
-            const long b = e / row4;
-            v[r] = s4[(long)g.perm[cur * g.B + b] * row4 + (e - b * row4)];
-          }
+          const int e = e0 + r * stride < n4 ? e0 + r * stride : n4 - 1;  // clamped, unconditional
+          const int b = e / row4;
+          v[r] = s4[(size_t)g.perm[cur * g.B + b] * row4 + (e - b * row4)];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           if (e0 + r * stride < n4) d4[e0 + r * stride] = v[r];
       }
     } else {
-      for (long e = first; e < total; e += stride) {
-        const long b = e / row;
-        g.dst[k][e] = g.src[k][(long)g.perm[cur * g.B + b] * row + (e - b * row)];
+      for (int e = first; e < total; e += stride) {
+        const int b = e / row;
+        g.dst[k][e] = g.src[k][(size_t)g.perm[cur * g.B + b] * row + (e - b * row)];
       }
     }
   }
 }
 
-template <int H, int PREC, int FIN0>
+template <int H, int PREC, int FIN0, bool DEC>
 __global__ __launch_bounds__((H / 16) * 192) void lstm_stack_fwd_kernel(StackFwdArgs a) {
   // layer l's workgroups follow layer l-1's in block-id order (its producers are already resident)
   if ((int)blockIdx.x >= a.main_blocks) {
@@ -853,10 +1417,18 @@ __global__ __launch_bounds__((H / 16) * 192) void lstm_stack_fwd_kernel(StackFwd
   }
   const int layer = blockIdx.x / a.tr8, tile = blockIdx.x % a.tr8;
   const unsigned base = read_epoch_base(a.ctl, CTL_FWD_EPOCH, a.eshift);
-  __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
-  if (tile < a.ntiles) {
-    if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
-    else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
+  if constexpr (DEC) {
+    __shared__ __attribute__((aligned(16))) FwdSmemD<H, PREC> sm;  // one image shared by both role bodies
+    if (tile < a.ntiles) {
+      if (layer == 0) stack_fwd_dec<H, PREC, FIN0, true>(a, layer, tile, sm, base);
+      else stack_fwd_dec<H, PREC, FIN0, false>(a, layer, tile, sm, base);
+    }
+  } else {
+    __shared__ __attribute__((aligned(16))) FwdSmem<H, PREC> sm;  // one image shared by both role bodies
+    if (tile < a.ntiles) {
+      if (layer == 0) stack_fwd_body<H, PREC, FIN0, true>(a, layer, tile, sm, base);
+      else stack_fwd_body<H, PREC, FIN0, false>(a, layer, tile, sm, base);
+    }
   }
   // every workgroup read the cursor before arriving: the last one advances it
   if (finish_launch(a.ctl, CTL_FWD_EPOCH, CTL_FWD_DONE, base, a.eshift) && a.gather) a.g.cursor[0] += 1;
@@ -892,6 +1464,9 @@ struct StackBwdArgs {
   // fused weight gradients: wg_per_layer workgroups per layer follow the L x tr8 recurrence workgroups
   mta_wgrad::WgArgs wg[MAXL];
   int wg_nq, wg_per_layer;
+  // dX[l] as tagged granules {value, epoch-stamped reverse step} (8 bytes each): no progress word, no drain; the
+  // consumer layer checks the tags (the hand-off of stack_fwd_dec).  0: fp32 rows + progress words (MTA_LSTM_DEC=0)
+  int gran;
 };
 
 template <int H, int PREC>
@@ -963,13 +1538,42 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     }
     float dreg[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned seen = base;
+    const bool gr = a.gran != 0;
+    unsigned long long gq[4] = {0, 0, 0, 0};
     auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
       if constexpr (!TOP) {
-        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
+        if (gr) {  // granules: issued now, checked (and re-polled if stale) by complete_dh before they are staged
+          const unsigned long long* g = reinterpret_cast<const unsigned long long*>(dH);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
-                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int i = 0; i < 4; ++i) gq[i] = gran_load(g + ((size_t)t * Np + n0 + 4 * q + i) * H + u);
+        } else {
+          seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    };
+    auto complete_dh = [&](int t) {  // granule form: every tag must carry reverse step T - t of this launch
+      if constexpr (!TOP) {
+        if (gr) {
+          const unsigned tag = base + (unsigned)(T - t);
+          for (unsigned spins = 0;; ++spins) {
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ok &= (unsigned)(gq[i] >> 32) == tag;
+            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+            if (spins >= a.spin_limit) {
+              if (lane == 0) __hip_atomic_fetch_add(a.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            load_dh(t);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dreg[i] = __builtin_bit_cast(float, (unsigned)gq[i]);
+        }
       }
     };
     uint32_t mreg = 0x01010101u, mnext = 0x01010101u;
@@ -1048,11 +1652,19 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] *= ((mreg >> (8 * e)) & 0xFFu) ? keep_scale : 0.f;
         }
-        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
+        if (gr) {
+          unsigned long long* g = reinterpret_cast<unsigned long long*>(dXout) + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc;
+          const unsigned tag = base + (unsigned)(T - t);
+          gran_store2(g, o[0], o[1], tag, false);
+          gran_store2(g + 2, o[2], o[3], tag, false);
+        } else {
+          store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
+        }
       }
     };
     if constexpr (!TOP) {
       load_dh(T - 1);
+      complete_dh(T - 1);
       stage_dh(T - 1);
       if (T > 1) load_dh(T - 2);
     }
@@ -1066,20 +1678,23 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       SSTAMP(0)
       // the previous interval's dG stores (4 per lane) and dx store stay in flight; every older op (its dH and
       // keep-byte loads, issued before them) is complete
+      // (granule form: the dx stores need no drain; the dH loads are waited for where complete_dh reads them)
       if constexpr (BOTTOM) mta_wait_vmem();
-      else mta_wait_vmcnt<1>();
+      else if (!gr) mta_wait_vmcnt<1>();
       mreg = mnext;
       SSTAMP(1)
       // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait at
       // the top of I(t+1) (which leaves only I(t+2)'s stores in flight), before barrier A(t+1)
-      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
+      if (!gr && !BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // dG progress: dG_s is stored in the same dx_step(s) as dx_s, before it, so the drain argument above covers
-      // dG of steps >= t+4 too
+      // dG progress: the recurrent waves store dG_{s} in their step s-1 and pass their vmcnt(10) wait at the top of
+      // step s-3 only once those stores are complete, before barrier A(s-3): at I(t) (after A(t+1)) every dG_s with
+      // s >= t+4 is drained
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (!TOP) {
         if (t >= 1) {
+          complete_dh(t - 1);
           stage_dh(t - 1);
           if (t >= 2) load_dh(t - 2);
         }
@@ -1098,7 +1713,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
     dx_step(0);
     mta_wait_vmem();
     __syncthreads();  // F
-    if (!BOTTOM && wave == NW && lane == 0)
+    if (!gr && !BOTTOM && wave == NW && lane == 0)
       __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == NW + 1 && lane == 0)
       __hip_atomic_store(dg_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1302,9 +1917,16 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
 template <int H, int PREC>
 int launch_fwd(int fin, const StackFwdArgs& a, hipStream_t st) {
   const dim3 grid(a.main_blocks + (a.gather ? a.copy_blocks : 0)), block((H / 16) * 192);  // + batch-copy blocks
-  if (fin == 3) lstm_stack_fwd_kernel<H, PREC, 3><<<grid, block, 0, st>>>(a);
-  else if (fin == 5) lstm_stack_fwd_kernel<H, PREC, 5><<<grid, block, 0, st>>>(a);
-  else return -1;
+  const bool dec = a.dec != 0;
+  if (fin == 3) {
+    if (dec) lstm_stack_fwd_kernel<H, PREC, 3, true><<<grid, block, 0, st>>>(a);
+    else lstm_stack_fwd_kernel<H, PREC, 3, false><<<grid, block, 0, st>>>(a);
+  } else if (fin == 5) {
+    if (dec) lstm_stack_fwd_kernel<H, PREC, 5, true><<<grid, block, 0, st>>>(a);
+    else lstm_stack_fwd_kernel<H, PREC, 5, false><<<grid, block, 0, st>>>(a);
+  } else {
+    return -1;
+  }
   return 0;
 }
 
@@ -1371,10 +1993,16 @@ extern "C" int mta_lstm_stack_fwd_g(int H, int prec, int L, int fin, const float
                                     const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                     float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                     float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                    int Np, int T, const MtaBatchGather* gather, hipStream_t st) {
+                                    int Np, int T, const MtaBatchGather* gather, unsigned long long* gran,
+                                    int decoupled, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64)) return -1;
   StackFwdArgs a{};
   a.x = x;
+  // decoupled form: L = 1 needs no hand-off buffer; deeper stacks take gran = (L - 1) x (T, Np, H) granules
+  if (decoupled && L > 1 && !gran) return -5;
+  if (decoupled && L > 1)
+    for (int l = 1; l < L; ++l) a.gran[l] = gran + (size_t)(l - 1) * T * Np * H;
+  a.dec = decoupled ? 1 : 0;
   if (gather) {
     if (gather->B < 1 || N % gather->B || gather->nt < 1 || gather->nt > 4 || gather->src[0] == nullptr ||
         gather->row[0] != (long)(N / gather->B) * T * fin)
@@ -1420,9 +2048,9 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* w_hh, const float* const* b_ih, const float* const* b_hh,
                                   float* const* hseq, float* const* xdrop, uint32_t* const* mask,
                                   float* const* stash, const uint64_t* seeds, float drop_p, unsigned* flags, int N,
-                                  int Np, int T, hipStream_t st) {
+                                  int Np, int T, unsigned long long* gran, int decoupled, hipStream_t st) {
   return mta_lstm_stack_fwd_g(H, prec, L, fin, x, w_ih, w_hh, b_ih, b_hh, hseq, xdrop, mask, stash, seeds, drop_p,
-                              flags, N, Np, T, nullptr, st);
+                              flags, N, Np, T, nullptr, gran, decoupled, st);
 }
 
 // Weight gradients are fused when g_whh is given: inp[0] = x (N, T, fin) batch-first, inp[l >= 1] = the layer's
@@ -1437,7 +2065,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
                                   float* const* g_whh, float* const* g_bih, float* const* g_bhh,
                                   const uint32_t* const* mask, float* const* part, uint64_t* seeds, float drop_p,
-                                  int dropout, unsigned* flags, int N, int Np, int T, hipStream_t st) {
+                                  int dropout, unsigned* flags, int N, int Np, int T, int gran, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T + 8 >= (1 << MAX_EPOCH_SHIFT)) return -1;
   if (prec == PREC_F16X2) prec = PREC_BF16X3;  // a forward mode: backward products in bf16x3
   StackBwdArgs a{};
@@ -1451,6 +2079,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     if (dropout && l > 0 && !a.mask[l]) return -2;
   }
   a.dh_last = dh_last;
+  a.gran = gran;  // dX[l]: (T, Np, H) granules of 8 bytes
   a.seeds = seeds;
   a.drop_p = drop_p;
   a.dropout = dropout;

@@ -124,6 +124,9 @@ struct Covered {
   long s[MAX_COVERED], e[MAX_COVERED];
   const float* ext;  // producer partials
   int n_ext;
+  // ext holds the squares of the WHOLE gradient (world > 1: the xGMI all-reduce's partials of the reduced buffer,
+  // csrc/allreduce.hip): phase 1 reads no gradient for the norm; the covered ranges only mark what stays unzeroed
+  int ext_only;
 };
 __device__ __forceinline__ bool covered(const Covered& c, long i) {
   bool in = false;
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(BS) void adam_fused_kernel(float4* __restrict__ p, 
 #pragma unroll
     for (int r = 0; r < REG_N; ++r) {
       const long i = (long)blockIdx.x * BS + threadIdx.x + r * stride;
-      if (cov.n && covered(cov, i)) continue;
+      if (cov.ext_only || (cov.n && covered(cov, i))) continue;
       acc = fmaf(rg[r].x, rg[r].x, acc);
       acc = fmaf(rg[r].y, rg[r].y, acc);
       acc = fmaf(rg[r].z, rg[r].z, acc);
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(BS) void adam_fused_kernel(float4* __restrict__ p, 
   } else {
     // U1 independent float4 loads in flight per thread: one workgroup per CU (the arrival wait needs them all
     // co-resident) holds too few bytes in flight for HBM with one load per iteration (Little's law)
-    for (long i0 = (long)blockIdx.x * BS + threadIdx.x; i0 < n4; i0 += stride * U1) {
+    for (long i0 = (long)blockIdx.x * BS + threadIdx.x; !cov.ext_only && i0 < n4; i0 += stride * U1) {
       float4 q[U1];
 #pragma unroll
       for (int u = 0; u < U1; ++u) {
@@ -400,7 +403,7 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
                                unsigned long long* ticket, const float* lr, float* step, float beta1, float beta2,
                                float eps, float wd, float max_norm, float scale, int adamw, int zero_grad,
                                float* norm_out, float* nonfinite, int n_cov, const long* cov_s, const long* cov_e,
-                               const float* ext, int n_ext, hipStream_t st) {
+                               const float* ext, int n_ext, int ext_only, hipStream_t st) {
   const long n4 = n / 4;
   const unsigned spin = fused_spin_limit();
   Covered cov{};
@@ -410,7 +413,8 @@ extern "C" void mta_adam_fused(float* p, float* g, float* m, float* v, long n, f
     cov.e[k] = cov_e[k];
   }
   cov.ext = ext;
-  cov.n_ext = cov.n ? n_ext : 0;
+  cov.ext_only = ext_only && ext ? 1 : 0;
+  cov.n_ext = (cov.n || cov.ext_only) ? n_ext : 0;
   if (fused_reg(n4))
     adam_fused_kernel<true, TPB><<<fused_grid_reg(n4), TPB, 0, st>>>(
         reinterpret_cast<float4*>(p), reinterpret_cast<float4*>(g), reinterpret_cast<float4*>(m),

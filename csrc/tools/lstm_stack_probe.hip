@@ -67,7 +67,7 @@ int main(int argc, char** argv) {
       xdrop[l] = dev_zero((size_t)T * Np * H);
       CK(hipMalloc(&mask[l], (size_t)T * Np * H));
     }
-    if (l < L - 1) dX[l] = dev_zero((size_t)T * Np * H);
+    if (l < L - 1) dX[l] = dev_zero((size_t)2 * T * Np * H);  // room for the granule hand-off (8 bytes per value)
     stash[l] = mode == 2 ? nullptr : dev_zero((size_t)T * Np * 5 * H);
     dG[l] = dev_zero((size_t)T * Np * 4 * H);
     gwih[l] = dev_zero((size_t)4 * H * fin);
@@ -82,6 +82,12 @@ int main(int argc, char** argv) {
   std::vector<uint64_t> hs(8);
   for (int i = 0; i < 8; ++i) hs[i] = 0x1234567ull * (i + 1);
   CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
+  // decoupled forward (default; DEC=0 in the environment selects the barrier form): (L - 1) x (T, Np, H) granules
+  const int dec = getenv("DEC") && atoi(getenv("DEC")) == 0 ? 0 : 1;
+  const int bgran = getenv("BGRAN") && atoi(getenv("BGRAN")) == 1 ? 1 : 0;  // backward granule hand-off (A/B)
+  unsigned long long* gran = nullptr;
+  CK(hipMalloc(&gran, (size_t)(L > 1 ? L - 1 : 1) * T * Np * H * 8));
+  CK(hipMemset(gran, 0, (size_t)(L > 1 ? L - 1 : 1) * T * Np * H * 8));
   unsigned* flags;
   const long nflags = mta_lstm_stack_flag_words(Np);
   CK(hipMalloc(&flags, nflags * 4));
@@ -105,7 +111,7 @@ int main(int argc, char** argv) {
     float m;
     CK(hipEventRecord(a));
     int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
+                                xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gran, dec, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -119,7 +125,7 @@ int main(int argc, char** argv) {
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
                             hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
                             const_cast<const uint32_t* const*>(mask.data()), nullptr, seeds, p,
-                            mode == 0 ? 1 : 0, flags, N, Np, T, 0);
+                            mode == 0 ? 1 : 0, flags, N, Np, T, bgran, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -155,7 +161,7 @@ int main(int argc, char** argv) {
     for (int pass = 0; pass < 2; ++pass) {
       CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
       int rc = mta_lstm_stack_fwd(H, prec, L, FIN, x, wih.data(), whh.data(), bih.data(), bhh.data(), hseq.data(),
-                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, 0);
+                                  xdrop.data(), mask.data(), stash.data(), seeds, p, flags, N, Np, T, gran, dec, 0);
       CK(hipDeviceSynchronize());
       if (rc) return 1;
       for (int l = 0; l < L; ++l) {
@@ -191,9 +197,9 @@ int main(int argc, char** argv) {
   }
   unsigned tmo = 0;
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
-  printf("mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
+  printf("dec=%d bgran=%d mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
          "timeouts=%u\n",
-         mode, N, L, T, prec, MTA_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         dec, bgran, mode, N, L, T, prec, MTA_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
 #if STACK_STAMPS
   unsigned long long acc[2][3][8];
@@ -206,6 +212,13 @@ int main(int argc, char** argv) {
         "mfma_dh"},
        {"", "vmem_wait", "flags+stage+loads", "dx_step", "barrier", "", "", ""},
        {"", "", "", "", "", "", "", ""}}};
+  if (dec) {  // the decoupled forward's segments (csrc/lstm_stack.hip stack_fwd_dec)
+    const char* d0[3][8] = {{"", "gx_wait+read", "h_wait", "a_read+stage+mfma", "activations", "h_write+post", "", ""},
+                            {"", "stg_wait", "lds_read+post", "stores", "", "", "", ""},
+                            {"", "slot/xq_wait", "gx_compute+post", "x_ready(poll)", "x_write+issue", "", "", ""}};
+    for (int r = 0; r < 3; ++r)
+      for (int k = 0; k < 8; ++k) seg[0][r][k] = d0[r][k];
+  }
   const char* dir[2] = {"fwd", "bwd"};
   const char* role[2][3] = {{"recurrent", "store", "input"}, {"recurrent", "gradient", ""}};
   for (int d = 0; d < 2; ++d)
@@ -219,5 +232,5 @@ int main(int argc, char** argv) {
       printf("\n");
     }
 #endif
-  return 0;
+  return tmo ? 3 : 0;  // a hand-off that gave up waiting: the results are invalid
 }

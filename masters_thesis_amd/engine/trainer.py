@@ -283,9 +283,11 @@ class Trainer:
         self.ddp = FlatDDP(self.flat)
         self.ddp.broadcast_parameters()
         # gradient producers (weight-gradient GEMMs that overwrite their range and hand the clip norm its partials,
-        # ops/optim.py) need the optimizer to see exactly what the backward wrote: one process only (with DDP the
-        # all-reduce rewrites the buffer between the producers and the norm)
-        set_producer_optimizer(self.optimizer if self.ddp.world == 1 else None)
+        # ops/optim.py): one process, or world > 1 with the xGMI all-reduce, whose kernel writes the clip norm's
+        # partials of the REDUCED gradient (FlatDDP.norm_parts: the optimizer then reads no gradient for the norm).
+        # The process group's all-reduce rewrites the buffer after the producers' partials: producers off there.
+        self.grad_producers = self.ddp.world == 1 or self.ddp.norm_parts is not None
+        set_producer_optimizer(self.optimizer if self.grad_producers else None)
 
     def _model_summary(self, model) -> None:
         if not (self.enable_model_summary and self.is_global_zero):
@@ -348,7 +350,8 @@ class Trainer:
             self.ddp.allreduce_grads()
             self._debug_norm("summed grad", self.flat.grad)
             phase("optim")
-            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True,
+                                ext_norm=self.ddp.norm_parts)
             self._debug_norm("optimizer", None)
         return loss
 
@@ -358,7 +361,8 @@ class Trainer:
             self._debug_check("local grad (replayed graph)", self.flat.grad)
             self.ddp.allreduce_grads()
             self._debug_norm("summed grad", self.flat.grad)
-            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True)
+            self.optimizer.step(self.gradient_clip_val, self.ddp.grad_scale, zero_grad=True,
+                                ext_norm=self.ddp.norm_parts)
             self._debug_norm("optimizer", None)
 
     def _debug_norm(self, what: str, buf: Optional[torch.Tensor]) -> None:

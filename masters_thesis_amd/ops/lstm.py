@@ -20,7 +20,7 @@ CPU path: ``torch._VF.lstm`` (the exact kernel behind ``nn.LSTM``).
 """
 from __future__ import annotations
 
-from typing import List, Sequence
+from typing import List, Optional, Sequence
 
 import os
 
@@ -205,6 +205,26 @@ def _stack_flags(C, Np: int, L: int, device, T: int = 60) -> Tensor:
     return _FLAGS[key]
 
 
+_GRAN = {}
+
+
+def _stack_gran(C, Np: int, L: int, device, T: int, H: int) -> Optional[Tensor]:
+    """Hand-off granules of the decoupled forward (csrc/lstm_stack.hip stack_fwd_dec): layer l >= 1's input as
+    {value, epoch-stamped step} pairs, int64 (L - 1, T, Np, H).  None selects the barrier form (``MTA_LSTM_DEC=0``).
+
+    Tags carry the forward epoch of the flag buffer (``_stack_flags``), so the granule buffer is keyed like it (plus
+    T and H): every launch that writes it draws its epoch from that one buffer, and a stale granule always carries an
+    older epoch than the one a launch waits for."""
+    import os
+
+    if os.environ.get("MTA_LSTM_DEC", "1") == "0":
+        return None
+    key = (C.lstm_stack_flag_words(Np), int(L), str(device), int(C.lstm_stack_epoch_shift(int(T))), int(T), int(H))
+    if key not in _GRAN:
+        _GRAN[key] = torch.zeros(max(L - 1, 1) * T * Np * H, dtype=torch.int64, device=device)
+    return _GRAN[key]
+
+
 def stack_timeouts(flags: Tensor) -> int:
     """Number of hand-off waits that gave up since the last check (host sync)."""
     return int(flags[flags.numel() - _CTL_WORDS].item())
@@ -295,16 +315,17 @@ def pipelined_forward(x: Tensor, seeds: Tensor, prec: int, dropout: float, train
     masks = [EB] + [torch.empty((T, Np, H), device=dev, dtype=torch.uint8) if drop else EB for _ in range(1, L)]
     stash = [torch.empty(T * Np * 5 * H, device=dev, dtype=torch.float32) if need_grad else E for _ in range(L)]
     flags = _stack_flags(C, Np, L, dev, T)
+    gran = _stack_gran(C, Np, L, dev, T, H)
     if gather is not None:
         src, dst, perm, cursor, B = gather
         if x.data_ptr() != dst[0].data_ptr() or not x.is_contiguous():
             raise ValueError("deferred gather: x must be the static batch buffer")
         C.lstm_stack_fwd_gather(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]),
                                 list(flat[3::4]), hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T,
-                                src, dst, perm, cursor, B)
+                                src, dst, perm, cursor, B, gran)
     else:
         C.lstm_stack_fwd(H, prec, F, x, list(flat[0::4]), list(flat[1::4]), list(flat[2::4]), list(flat[3::4]),
-                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T)
+                         hseq, xdrop, masks, stash, seeds, float(dropout), flags, N, Np, T, gran)
     st = PipelinedState()
     st.meta = (L, H, N, Np, T, F, prec, float(dropout), drop)
     st.params, st.seeds, st.x = tuple(flat), seeds, x
@@ -330,14 +351,18 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
         for t in flat:
             t.grad = torch.zeros_like(t)
     dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
-    dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
+    # dX hand-off: fp32 rows + progress words.  The kernel also has a tagged-granule form (gran=True: 2 H floats per
+    # row), measured slower at every depth (profiles/r6_lstm_decoupled.txt; the probe's BGRAN=1 A/B)
+    gran = False
+    dX = [torch.empty((T, Np, (2 if gran else 1) * H), device=dev, dtype=torch.float32)
+          for _ in range(L - 1)] + [_empty(dev)]
     flags = _stack_flags(C, Np, L, dev, T)
     inp = [st.x] + [st.xdrop[l] if drop else st.hseq[l - 1] for l in range(1, L)]
     grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
     parts = _parts(C, True, T, H, [F] + [H] * (L - 1), dev)
     C.lstm_stack_bwd(H, prec, F, list(st.stash), list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
                      list(st.hseq), inp, grads, list(st.masks) if drop else [], parts, st.seeds, p, drop, flags, N,
-                     Np, T)
+                     Np, T, gran)
     if st.pad is not None:
         real, H0 = st.pad
         idx = _padded_rows_index(H0, H, dev)

@@ -17,8 +17,8 @@ MI355X design:
   clip + Adam with ``lr`` and the step counter in device memory, i.e. it can be captured once
   in a HIP graph and replayed forever; the plateau scheduler only writes the lr scalar.  With
   ``zero_grad=True`` the kernel leaves the gradient zeroed, which replaces the per-step fill
-  (``grads_zeroed`` tells the trainer).  ``MTA_OPTIM_TWO_LAUNCH=1`` selects the older
-  norm + update pair.
+  (``grads_zeroed`` tells the trainer).  ``single_launch=False`` selects the older
+  norm + update pair (slower: profiles/r5_adam_two_launch_ab.jsonl; kept as the test oracle).
 """
 from __future__ import annotations
 
@@ -93,7 +93,7 @@ class FusedAdam:
     """Adam (coupled L2, torch.optim.Adam semantics) or AdamW over a FlatParameters buffer."""
 
     def __init__(self, flat: FlatParameters, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, adamw: bool = False):
+                 weight_decay: float = 0.0, adamw: bool = False, single_launch: bool = True):
         self.flat = flat
         dev = flat.data.device
         self.exp_avg = torch.zeros_like(flat.data)
@@ -118,7 +118,7 @@ class FusedAdam:
         self._dropped: set = set()  # ranges produced twice this step: accumulated, not covered
         if self.hip:
             C = lib()
-            self.single_launch = os.environ.get("MTA_OPTIM_TWO_LAUNCH", "0") != "1"
+            self.single_launch = bool(single_launch)
             n = C.adam_fused_partials() if self.single_launch else C.optim_num_partials(flat.padded)
             self.partials = torch.zeros(n, device=dev, dtype=torch.float32)
             self.ticket = torch.zeros(1, device=dev, dtype=torch.int64)
@@ -185,11 +185,15 @@ class FusedAdam:
             self.set_lr(self.param_groups[0]["lr"])
 
     # ---- step -------------------------------------------------------------------
-    def step(self, max_norm: float = 0.0, grad_scale: float = 1.0, zero_grad: bool = False) -> None:
+    def step(self, max_norm: float = 0.0, grad_scale: float = 1.0, zero_grad: bool = False,
+             ext_norm: Optional[Tensor] = None) -> None:
         """Clip (if max_norm > 0) the flat gradient scaled by ``grad_scale`` and apply one Adam step.
 
         ``zero_grad``: leave the flat gradient zeroed (the fused kernel writes 0 instead of the clipped
-        gradient; ``grads_zeroed`` reports whether that happened)."""
+        gradient; ``grads_zeroed`` reports whether that happened).  ``ext_norm``: partial sums of squares of the
+        WHOLE gradient written by its producer (world > 1: the xGMI all-reduce kernel, ``FlatDDP.norm_parts``): the
+        fused kernel takes the clip norm from them instead of re-reading the gradient, and the producers' ranges only
+        stay unzeroed."""
         self.sync_lr_from_groups()
         f = self.flat
         b1, b2 = self.betas
@@ -199,6 +203,14 @@ class FusedAdam:
             self._plan = {}
             self._dropped = set()
             ext = None
+            if ext_norm is not None:
+                # the producers' own partials are of the local gradient (the all-reduce rewrote their ranges): unused
+                lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
+                                 self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
+                                 float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health,
+                                 [r[0] for r in plan], [r[1] for r in plan], ext_norm, True)
+                self.grads_zeroed = bool(zero_grad)
+                return
             if plan:
                 # the kernel sums every partial of ext: hand it slots [0, last used] and zero the slots in between
                 # that no covered range owns (a range dropped by a double registration left its stale partials there)
@@ -211,7 +223,7 @@ class FusedAdam:
             lib().adam_fused(f.data, f.grad, self.exp_avg, self.exp_avg_sq, self.partials, self.ticket, self.lr_t,
                              self.step_t, b1, b2, self.eps, self.weight_decay, float(max_norm or 0.0),
                              float(grad_scale), self.adamw, bool(zero_grad), self.grad_norm, self._health,
-                             [r[0] for r in plan], [r[1] for r in plan], ext)
+                             [r[0] for r in plan], [r[1] for r in plan], ext, False)
             # covered ranges keep this step's gradient (their producers overwrite them next step)
             self.grads_zeroed = bool(zero_grad)
             return

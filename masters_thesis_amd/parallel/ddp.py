@@ -68,6 +68,38 @@ class FlatDDP:
         # (captured once) in graph replays alike.
         self._chan_of: dict = {}
         self._plan: List[tuple] = []      # the ranges of the last overlapped step, in launch order
+        # clip-norm partials of the reduced gradient (xGMI only): every range reduced in a step writes the squares of
+        # its reduced values into a slot of its own (fixed per range, like its channel), so the fused optimizer takes
+        # the norm from here (``norm_parts``) and the weight-gradient producers stay on with world > 1
+        self.sq: Optional[torch.Tensor] = None
+        self._sq_of: dict = {}
+        if self.xgmi is not None:
+            from ..ops._lib import lib
+
+            self._sq_block = int(lib().xgmi_max_blocks())
+            self.sq = torch.zeros(self.SQ_SLOTS * self._sq_block, device=flat.grad.device, dtype=torch.float32)
+
+    SQ_SLOTS = 256  # ranges per step with a norm-partials slot of their own
+
+    @property
+    def norm_parts(self) -> Optional[torch.Tensor]:
+        """The clip-norm partials of the whole reduced gradient (FusedAdam.step ``ext_norm``), or None when this
+        sync does not produce them (world 1, the process group's all-reduce, a test's replacement launch)."""
+        return self.sq if (self.xgmi is not None and self._reduce_fn is None) else None
+
+    def _sq_slot(self, a: int, b: int) -> Optional[torch.Tensor]:
+        if self.sq is None:
+            return None
+        k = self._sq_of.get((a, b))
+        if k is None:
+            k = len(self._sq_of)
+            if k >= self.SQ_SLOTS:
+                raise RuntimeError(f"more than {self.SQ_SLOTS} all-reduce ranges per step: raise FlatDDP.SQ_SLOTS")
+            self._sq_of[(a, b)] = k
+        return self.sq[k * self._sq_block:(k + 1) * self._sq_block]
+
+    def _xg(self, g: torch.Tensor, a: int, b: int, channel: int) -> None:
+        self.xgmi.allreduce_(g[a:b], off=a, channel=channel, sq=self._sq_slot(a, b))
 
     # ------------------------------------------------------------------ overlapped sync
     def begin_backward(self) -> None:
@@ -139,9 +171,9 @@ class FlatDDP:
             ev.record(torch.cuda.current_stream(g.device))
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
-                self.xgmi.allreduce_(g[a:b], off=a, channel=k)
+                self._xg(g, a, b, k)
         else:
-            self.xgmi.allreduce_(g[a:b], off=a, channel=k)
+            self._xg(g, a, b, k)
 
     def _remaining(self, n: int) -> List[tuple]:
         """[0, n) minus the ranges already reduced, in order."""
@@ -213,10 +245,10 @@ class FlatDDP:
                 # an un-armed sync after overlapped steps (bench.py's allreduce_us loop): the same ranges on the same
                 # channels as those steps, in stream order
                 for a, b in self._plan:
-                    self.xgmi.allreduce_(g[a:b], off=a, channel=self.channel_of(a, b))
+                    self._xg(g, a, b, self.channel_of(a, b))
                 return
             for b in self.xgmi_buckets:
-                self.xgmi.allreduce_(g[b], off=b.start, channel=self.channel_of(b.start, b.stop))
+                self._xg(g, b.start, b.stop, self.channel_of(b.start, b.stop))
             return
         if self._gloo_cpu:
             t = g.cpu()

@@ -101,13 +101,16 @@ class XgmiAllReduce:
             return self.force_twoshot
         return numel * 4 > TWOSHOT_KB * 1024 and self.world > 2
 
-    def allreduce_(self, t: torch.Tensor, off: int = 0, channel: int = 0) -> torch.Tensor:
+    def allreduce_(self, t: torch.Tensor, off: int = 0, channel: int = 0,
+                   sq: Optional[torch.Tensor] = None) -> torch.Tensor:
         """In-place sum over the ranks of a contiguous fp32 CUDA tensor: the bucket [off, off + numel) of the flat
-        gradient this object was sized for, on ``channel`` (concurrent buckets need distinct channels)."""
+        gradient this object was sized for, on ``channel`` (concurrent buckets need distinct channels).  ``sq``
+        (``xgmi_max_blocks()`` floats): the kernel's workgroups write the sums of squares of the reduced values
+        there (the clip norm's partials, FusedAdam ``ext_norm``)."""
         if t.numel() % 4 or off % 4:
             raise ValueError("xgmi all-reduce needs 4-element-aligned buckets")
         self._C.xgmi_allreduce(t, int(off), self.cap, int(channel), self.channels, self.twoshot(t.numel()),
-                               self.bufs, self.rank, self.ctl)
+                               self.bufs, self.rank, self.ctl, sq)
         return t
 
     def timeouts(self) -> int:

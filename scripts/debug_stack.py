@@ -49,8 +49,9 @@ def main():
         hseq = [torch.full((T, Np, H), float("nan"), device="cuda") for _ in range(L)]
         flags = torch.zeros(C.lstm_stack_flag_words(Np), device="cuda", dtype=torch.int32)
         seeds = torch.zeros(8, dtype=torch.int64, device="cuda")
+        gran = torch.zeros(max(L - 1, 1) * T * Np * H, dtype=torch.int64, device="cuda")
         C.lstm_stack_fwd(H, prec, F, x.cuda(), wd[0::4], wd[1::4], wd[2::4], wd[3::4], hseq, [E] * L, [E] * L, [E] * L,
-                         seeds, 0.0, flags, N, Np, T)
+                         seeds, 0.0, flags, N, Np, T, gran)
         torch.cuda.synchronize()
         fl = flags.cpu()
         print(f"[{mode}] prec={prec} H={H} L={L} flags={fl[:256:32].tolist()} ... timeout={fl[-160].item()}", flush=True)

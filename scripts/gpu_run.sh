@@ -6,7 +6,7 @@
 #   OUT=<subdir of gpurun_out> PLAN='<step>;<step>;...' bash scripts/gpu_run.sh
 #   OUT=... bash scripts/gpu_run.sh plan.txt          (one step per line, '#' comments)
 #
-# steps (arguments after the keyword are passed through):
+# steps (arguments after the keyword are passed through; leading KEY=VALUE tokens set that step's environment):
 #   pytest <pytest args>            python -m pytest ... -x -v --timeout 120 --timeout-method thread  -> pytest.log
 #   bench <bench.py args>           one JSON line appended to bench.jsonl
 #   prof <tag> <bench.py args>      rocprofv3 --kernel-trace --stats of a bench run -> <tag>/
@@ -28,8 +28,12 @@ n=0
 for s in "${STEPS[@]}"; do
   n=$((n + 1))
   read -ra a <<< "$s"
+  # leading KEY=VALUE tokens set the environment of this step only
+  envs=()
+  while [[ ${a[0]} =~ ^[A-Z_][A-Z0-9_]*= ]]; do envs+=("${a[0]}"); a=("${a[@]:1}"); done
   kind=${a[0]}
   args=("${a[@]:1}")
+  for e in "${envs[@]}"; do export "$e"; done
   st "step $n: $s"
   case "$kind" in
     pytest) timeout -k 10 "$TO" python -u -m pytest -x -v --timeout 120 --timeout-method thread "${args[@]}" >> "$O/pytest.log" 2>&1 ;;
@@ -52,6 +56,7 @@ for s in "${STEPS[@]}"; do
     *) st "unknown step kind: $kind"; exit 2 ;;
   esac
   rc=$?
+  for e in "${envs[@]}"; do unset "${e%%=*}"; done
   st "step $n rc=$rc"
   if [ $rc -ne 0 ]; then st "FATAL at step $n"; exit $rc; fi
 done

@@ -31,13 +31,14 @@ def run(C, L, prec):
     stash = [torch.empty(T * Np * 5 * H, device=dev) for _ in range(L)]
     flags = torch.zeros(C.lstm_stack_flag_words(Np), device=dev, dtype=torch.int32)
     seeds = torch.zeros(8, dtype=torch.int64, device=dev)
+    gran = torch.zeros(max(L - 1, 1) * T * Np * H, dtype=torch.int64, device=dev)
 
     def fwd():
         C.lstm_stack_fwd(H, prec, F, x, ws[0::4], ws[1::4], ws[2::4], ws[3::4], hseq, [E] * L, [E] * L, stash, seeds, 0.0,
-                         flags, N, Np, T)
+                         flags, N, Np, T, gran)
 
     dG = [torch.empty((T, Np, 4 * H), device=dev) for _ in range(L)]
-    dX = [torch.empty((T, Np, H), device=dev) for _ in range(L - 1)] + [E]
+    dX = [torch.empty((T, Np, 2 * H), device=dev) for _ in range(L - 1)] + [E]  # granule hand-off
     dh = torch.randn(N, H, device=dev)
 
     inp = [x] + hseq[:-1]
@@ -45,11 +46,11 @@ def run(C, L, prec):
 
     def bwd():
         C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], [], seeds, 0.0, False, flags,
-                         N, Np, T)
+                         N, Np, T, True)
 
     def bwd_fused():
         C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, [], [], seeds, 0.0, False,
-                         flags, N, Np, T)
+                         flags, N, Np, T, True)
 
     def bwd_wgrad():
         bwd()

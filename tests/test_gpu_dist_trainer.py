@@ -70,18 +70,20 @@ def _worker(rank, world, port, model, batch, steps, sync, q, extra_env, trainer=
         tr._configure_optimizers(net)
         net.train()
         info = {"backend": tr.ddp.backend_name, "in_graph": tr._allreduce_in_graph(),
-                "overlap": bool(getattr(tr.ddp, "overlap", False))}
+                "overlap": bool(getattr(tr.ddp, "overlap", False)),
+                "producers": bool(getattr(tr, "grad_producers", False)),
+                "norm_from_allreduce": tr.ddp.norm_parts is not None}
         # the gradient the optimizer sees at step 1 (summed over ranks, times the 1/world it applies) and the clip
         # norm it computes from it: the first step is an eager warm-up step, so the wrapper sees it
         snap = {}
         opt_step = tr.optimizer.step
 
-        def step_and_snapshot(max_norm=0.0, grad_scale=1.0, zero_grad=False):
+        def step_and_snapshot(max_norm=0.0, grad_scale=1.0, zero_grad=False, **kw):
             first = "grad" not in snap
             if first:
                 torch.cuda.synchronize()
                 snap["grad"] = (tr.flat.grad.detach().double() * grad_scale).cpu().numpy().copy()
-            opt_step(max_norm, grad_scale, zero_grad)
+            opt_step(max_norm, grad_scale, zero_grad, **kw)
             if first:
                 snap["norm"] = float(tr.optimizer.grad_norm.item())
 
@@ -134,7 +136,8 @@ def _run(world, model, batch, steps, sync, extra_env=None, timeout=280, trainer=
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("model,trainer,tol", [("small", "fast", 1e-5), ("mlp_small", "gpu_fast", 2e-3),
-                                               ("transformer_encoder", "gpu_fast", 2e-3)])
+                                               ("transformer_encoder", "gpu_fast", 2e-3),
+                                               ("mlp_large", "gpu_fast", 2e-3)])
 def test_step1_summed_gradient_matches_global_batch(model, trainer, tol):
     """The all-reduce checked where it can be checked sharply: the gradient the optimizer receives at step 1 (sum over
     2 ranks x B=1 through the xGMI kernel, times 1/world) against ONE rank on the same 2 windows (B=2), and the clip
@@ -156,6 +159,10 @@ def test_step1_summed_gradient_matches_global_batch(model, trainer, tol):
     assert gref.norm().item() > 0
     assert rel <= tol, rel
     assert nrel <= tol, (i0["norm1"], iref["norm1"])
+    # the clip norm comes from the all-reduce kernel's partials of the reduced gradient (world 2) and the gradient
+    # producers stay on (mlp_large's big weight gradients overwrite their ranges) -- VERDICT r5 next-round #5
+    assert i0["norm_from_allreduce"] and i0["producers"], i0
+    assert iref["producers"], iref
 
 
 @pytest.mark.timeout(600)

@@ -569,12 +569,12 @@ def test_mlp_grad_producers_match_accumulating_path(batch, monkeypatch):
         model.train()
         opt_step = tr.optimizer.step
 
-        def step_and_snapshot(max_norm=0.0, grad_scale=1.0, zero_grad=False, _opt_step=opt_step, _tr=tr):
+        def step_and_snapshot(max_norm=0.0, grad_scale=1.0, zero_grad=False, _opt_step=opt_step, _tr=tr, **kw):
             first = len(grads1) < len(outs) + 1
             if first:
                 torch.cuda.synchronize()
                 grads1.append(_tr.flat.grad.detach().clone())
-            _opt_step(max_norm, grad_scale, zero_grad)
+            _opt_step(max_norm, grad_scale, zero_grad, **kw)
             if first:
                 norms1.append(float(_tr.optimizer.grad_norm.item()))
 

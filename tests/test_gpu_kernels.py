@@ -167,11 +167,10 @@ def test_single_launch_adam_matches_two_launch_and_zeroes_grads(n_params, monkey
 
     torch.manual_seed(6)
     opts = []
-    for two in ("1", "0"):
-        monkeypatch.setenv("MTA_OPTIM_TWO_LAUNCH", two)
+    for single in (False, True):
         ps = [torch.nn.Parameter(torch.full((n_params,), 0.5, device=DEV))]
         flat = FlatParameters(ps)
-        opts.append((flat, FusedAdam(flat, lr=1e-3, weight_decay=1e-5)))
+        opts.append((flat, FusedAdam(flat, lr=1e-3, weight_decay=1e-5, single_launch=single)))
     assert not opts[0][1].single_launch and opts[1][1].single_launch
     for step in range(4):
         g = torch.randn(opts[0][0].padded, device=DEV) * (3.0 if step % 2 else 0.01)

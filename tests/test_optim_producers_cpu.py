@@ -100,7 +100,7 @@ def test_step_hands_packed_partials_after_double_registration(monkeypatch):
 
     class _C:
         def adam_fused(self, *a):
-            seen["cov_s"], seen["cov_e"], seen["ext"] = a[-3], a[-2], a[-1]
+            seen["cov_s"], seen["cov_e"], seen["ext"], seen["ext_only"] = a[-4], a[-3], a[-2], a[-1]
 
     monkeypatch.setattr(O, "lib", lambda *a, **k: _C())
     opt.partials = torch.zeros(4)
@@ -110,3 +110,25 @@ def test_step_hands_packed_partials_after_double_registration(monkeypatch):
     ext = seen["ext"]
     assert ext.numel() == 2 * opt._nparts
     assert float(ext.sum()) == float(opt._nparts)  # B's partials only; A's stale slot zeroed
+    assert seen["ext_only"] is False
+
+
+def test_step_takes_the_norm_from_allreduce_partials(monkeypatch):
+    """world > 1: the xGMI all-reduce's partials of the reduced gradient are the clip norm's only
+    source (ext_only), and the producers' ranges are still handed over so the update leaves them unzeroed."""
+    opt, params = _opt([(8, 4), (4, 4)], monkeypatch)
+    assert opt.register_producer(params[0].grad) is not None
+    seen = {}
+
+    class _C:
+        def adam_fused(self, *a):
+            seen["cov_s"], seen["cov_e"], seen["ext"], seen["ext_only"] = a[-4], a[-3], a[-2], a[-1]
+
+    monkeypatch.setattr(O, "lib", lambda *a, **k: _C())
+    opt.partials = torch.zeros(4)
+    opt.ticket = torch.zeros(1, dtype=torch.int64)
+    sq = torch.ones(256)
+    opt.step(max_norm=5.0, zero_grad=True, ext_norm=sq)
+    assert seen["ext"] is sq and seen["ext_only"] is True
+    assert seen["cov_s"] == [0] and seen["cov_e"] == [8]
+    assert opt.grads_zeroed and opt._plan == {}
