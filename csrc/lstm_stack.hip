@@ -829,8 +829,9 @@ __device__ __forceinline__ void stack_fwd_body(const StackFwdArgs& a, const int 
 // pre-loaded 4 steps ahead: ~10 steps (~13 us) of fill per layer boundary in each direction.
 constexpr int DG = 3;   // gate pre-activation ring (input wave w -> recurrent wave w)
 constexpr int HSL = 3;  // h image slots: h_t in slot (t + 1) % 3 (a wave writing h_t knows every wave read h_{t-2})
-constexpr int XA = 2;   // layers >= 1: an input wave writes its quarter of x_{t+XA} after computing gx_t
-constexpr int DX = XA + 2;  // x image slots (layers >= 1: the four input waves' quarters of x_t)
+constexpr int XS = 3;   // last layer (>= 1): store wave w writes quarter w of x_{t+XS} before it stages step t
+constexpr int XA = 2;   // middle layers: input wave w writes quarter w of x_{t+XA} after computing gx_t
+constexpr int DX = XS + 2;  // x image slots (layers >= 1: the four quarters of x_t)
 constexpr int DS = 3;   // stage slots: step t's fp32 h and BPTT stash in slot t % DS (recurrent wave w -> store wave w)
 enum { SY_H = 0, SY_GX = 1, SY_STG = 2, SY_FREE = 3, SY_XQ = 4, SY_ROWS = 5 };
 
@@ -928,6 +929,75 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
       for (int idx = threadIdx.x; idx < S * ROWB; idx += NW * 192) (&sm.h_lo[0][0][0])[idx] = (__bf16)0.f;
   }
   __syncthreads();  // P0 (the only barrier before the final one)
+  // Layers >= 1: quarter w of x_t (row ls of the tile, units lu .. lu + 3: four granules of the producer layer) goes
+  // into the LDS image every input wave reads its MFMA A operand from.  Written by store wave w XS steps ahead in the
+  // LAST layer (its store waves idle ~2,000 of ~2,750 cycles a step; layer 1 of L=2: forward 77.0 -> 72.7 us), by
+  // input wave w XA steps ahead in a middle layer, whose store waves also produce the next layer's input (a blocking
+  // upstream poll there delays every layer below: L=8 115 -> 129 us), profiles/r6_lstm_decoupled.txt.  (Each wave reading all of x_t
+  // from the granules instead -- 16 scattered 8-byte loads per lane -- took ~3,000 cycles a step and crowded
+  // the memory pipe: L=2 forward 79 -> 140 us, profiles/r6_lstm_decoupled.txt.)
+  const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
+  const unsigned long long* gin = FIRST ? nullptr : a.gran[layer];
+  unsigned long long gq[4];
+  auto issue = [&](int t) {
+    const unsigned long long* p = gin + ((size_t)t * Np + n0 + ls) * H + lu;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gq[e] = gran_load(p + e);
+  };
+  auto tags_ok = [&](int t) -> bool {  // wave-uniform: the in-flight granules of step t have all arrived
+    const unsigned tag = base + (unsigned)(t + 1);
+    bool ok = true;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ok &= (unsigned)(gq[e] >> 32) == tag;
+    return __builtin_amdgcn_ballot_w64(!ok) == 0;
+  };
+  // x_t's quarter: every lane's four tags must carry step t of this launch; reload until they do (bounded)
+  auto ready = [&](int t) -> float4 {
+    const unsigned tag = base + (unsigned)(t + 1);
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ok &= (unsigned)(gq[e] >> 32) == tag;
+      if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+      if (spins >= lim) {
+        if (lane == 0) __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      issue(t);
+    }
+    return make_float4(__builtin_bit_cast(float, (unsigned)gq[0]), __builtin_bit_cast(float, (unsigned)gq[1]),
+                       __builtin_bit_cast(float, (unsigned)gq[2]), __builtin_bit_cast(float, (unsigned)gq[3]));
+  };
+  auto write_x = [&](int t, const float4& xq) {
+    // image slot t % DX last held x_{t-DX}: every input wave has computed gx_{t-DX} from it
+    sy_wait<NW>(&sy[SY_GX][0], t - DX + 1, tmo, lim);
+    const int slot = t % DX;
+    if constexpr (PREC == PREC_F32) {
+      *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
+    } else {
+      const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
+      if constexpr (PREC == PREC_F16X2) {
+        typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+        f16x4_t v4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
+        *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
+      } else {
+        bf16x4 hi4, lo4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          __bf16 hi, lo;
+          split_bf16(xv[e], hi, lo);
+          hi4[e] = hi;
+          lo4[e] = lo;
+        }
+        *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
+        if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
+      }
+    }
+    sy_post(&sy[SY_XQ][w], t + 1);
+  };
 
   if (role == 2) {
     // =========================== store waves ===========================
@@ -942,9 +1012,24 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     const unsigned E = base >> a.eshift;
     if (w == 0 && lane == 0) publish_xcc(a.xcc + layer * a.tr8 + tile, E);
     const bool local = a.xcd_local && !last && partner_local(a.xcc + (layer + 1) * a.tr8 + tile, E, 1u << 14);
+    // (Writing x_{t+1} blocking and x_{t+2..t+XS} only when already arrived measured slower at every depth: L=2
+    // 72.7 -> 83.6 us, r6j)
+    const bool sx = !FIRST && last;  // this role writes the x image (last layer)
+    if (sx) {
+      for (int t = 0; t < XS && t < T; ++t) {
+        issue(t);
+        write_x(t, ready(t));
+      }
+      if (XS < T) issue(XS);
+    }
     SSTAMP_DECL
     for (int t = 0; t < T; ++t) {
       SSTAMP(0)
+      if (sx && t + XS < T) {
+        const float4 xq = ready(t + XS);
+        if (t + XS + 1 < T) issue(t + XS + 1);
+        write_x(t + XS, xq);
+      }
       sy_wait<1>(&sy[SY_STG][w], t + 1, tmo, lim);
       SSTAMP(1)
       const int slot = t % DS;
@@ -1080,65 +1165,6 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
               if constexpr (kWeightLo<PREC>) Xlo[g][kb][e] = lo;
             }
       }
-      // This wave's quarter of x_t (row ls of the tile, units lu .. lu + 3: four granules of the producer layer) goes
-      // into a shared LDS image that every input wave reads its MFMA A operand from.  (Each wave reading all of x_t
-      // from the granules instead -- 16 scattered 8-byte loads per lane -- took ~3,000 cycles a step and crowded
-      // the memory pipe: L=2 forward 79 -> 140 us, profiles/r6_lstm_decoupled.txt.)
-      const int ls = lane >> 2, lu = 16 * w + 4 * (lane & 3);
-      const unsigned long long* gin = a.gran[layer];
-      unsigned long long gq[4];
-      auto issue = [&](int t) {
-        const unsigned long long* p = gin + ((size_t)t * Np + n0 + ls) * H + lu;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) gq[e] = gran_load(p + e);
-      };
-      // x_t's quarter: every lane's four tags must carry step t of this launch; reload until they do (bounded)
-      auto ready = [&](int t) -> float4 {
-        const unsigned tag = base + (unsigned)(t + 1);
-        for (unsigned spins = 0;; ++spins) {
-          bool ok = true;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) ok &= (unsigned)(gq[e] >> 32) == tag;
-          if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-          if (spins >= lim) {
-            if (lane == 0) __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          issue(t);
-        }
-        return make_float4(__builtin_bit_cast(float, (unsigned)gq[0]), __builtin_bit_cast(float, (unsigned)gq[1]),
-                           __builtin_bit_cast(float, (unsigned)gq[2]), __builtin_bit_cast(float, (unsigned)gq[3]));
-      };
-      auto write_x = [&](int t, const float4& xq) {
-        // image slot t % DX last held x_{t-DX}: every input wave has computed gx_{t-DX} from it
-        sy_wait<NW>(&sy[SY_GX][0], t - DX + 1, tmo, lim);
-        const int slot = t % DX;
-        if constexpr (PREC == PREC_F32) {
-          *reinterpret_cast<float4*>(&sm.x_f[slot][ls][lu]) = xq;
-        } else {
-          const float xv[4] = {xq.x, xq.y, xq.z, xq.w};
-          if constexpr (PREC == PREC_F16X2) {
-            typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
-            f16x4_t v4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v4[e] = (_Float16)xv[e];
-            *reinterpret_cast<f16x4_t*>(&sm.x_hi[slot][ls][lu]) = v4;
-          } else {
-            bf16x4 hi4, lo4;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              __bf16 hi, lo;
-              split_bf16(xv[e], hi, lo);
-              hi4[e] = hi;
-              lo4[e] = lo;
-            }
-            *reinterpret_cast<bf16x4*>(&sm.x_hi[slot][ls][lu]) = hi4;
-            if constexpr (PREC == PREC_BF16X3) *reinterpret_cast<bf16x4*>(&sm.x_lo[slot][ls][lu]) = lo4;
-          }
-        }
-        sy_post(&sy[SY_XQ][w], t + 1);
-      };
       auto compute_gx_img = [&](int t) {
         const int xs = t % DX, slot = t % DG;
         f32x4 acc[4];
@@ -1178,16 +1204,16 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
           sm.gxs[slot][4 * q + i][u] = make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
         sy_post(&sy[SY_GX][w], t + 1);
       };
-      // iteration t: gx_t, then x_{t+XA}'s quarter into the image (its granules were issued an iteration ago): the
-      // quarters of x_t were written XA - 1 iterations before they are needed, so one slow input wave does not hold
-      // the other three at the image every step (XA = 1 spent ~1,300 of ~2,560 cycles a step of the layer-1 input
-      // waves in quarter / slot waits, r6 stamps).  (Writing x_{t+1} first whenever its granules had already arrived
-      // measured slower: 82.0 -> 86.1 us, profiles/r6_lstm_decoupled.txt)
-      for (int t = 0; t < XA && t < T; ++t) {
-        issue(t);
-        write_x(t, ready(t));
+      // iteration t: gx_t from x_t's image; a middle layer's input wave then writes its quarter of x_{t+XA} (granules
+      // issued an iteration ago), the last layer's store waves write the image XS steps ahead
+      const bool ix = !last;
+      if (ix) {
+        for (int t = 0; t < XA && t < T; ++t) {
+          issue(t);
+          write_x(t, ready(t));
+        }
+        if (XA < T) issue(XA);
       }
-      if (XA < T) issue(XA);
       SSTAMP_DECL
       for (int t = 0; t < T; ++t) {
         SSTAMP(0)
@@ -1195,7 +1221,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
         SSTAMP(1)
         compute_gx_img(t);
         SSTAMP(2)
-        if (t + XA < T) {
+        if (ix && t + XA < T) {
           const float4 xq = ready(t + XA);
           SSTAMP(3)
           if (t + XA + 1 < T) issue(t + XA + 1);

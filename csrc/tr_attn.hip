@@ -491,7 +491,10 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   // two workgroups per sequence (query halves): 2 x 104 sequences still fit one wave of workgroups on the 256 CUs,
   // and each recomputes only the shared norm / K / V (18.9 -> 16.7 us per launch, transformer B=1 0.576 -> 0.565 ms,
   // profiles/r4_bench_transformer_attn_split_ab.jsonl)
-  a.split = T > 32 ? 1 : 0;
+  // Beyond one wave of workgroups the duplicated norm / QKV work is pure cost (the 131 KB image allows one workgroup
+  // per CU): transformer B=8 (800 sequences) ran 1,600 split workgroups at ~100 us per launch
+  // (profiles/r6_transformer/tr_b8_kernel_stats.csv)
+  a.split = (T > 32 && nseq <= 128) ? 1 : 0;
   tr_attn_fwd_kernel<<<nseq * (a.split ? 2 : 1), ATH, sizeof(AttnFwdSmem), st>>>(a);
   return 0;
 }
