@@ -121,7 +121,7 @@ int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stas
                        const float* const* hseq, const float* const* inp, float* const* g_wih, float* const* g_whh,
                        float* const* g_bih, float* const* g_bhh, const uint32_t* const* mask, float* const* part,
                        uint64_t* seeds, float drop_p, int dropout, unsigned* flags, int N, int Np, int T,
-                       int gran, hipStream_t st);
+                       int form, hipStream_t st);
 long mta_lstm_stack_flag_words(int Np);
 int mta_lstm_stack_epoch_shift(int T);
 // allreduce.hip (one-shot / two-shot all-reduce over xGMI peer memory, one channel per bucket)
@@ -1101,8 +1101,10 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
                     std::vector<at::Tensor> dX, std::vector<at::Tensor> hseq, std::vector<at::Tensor> inp,
                     std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks,
                     std::vector<at::Tensor> parts, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
-                    int64_t N, int64_t Np, int64_t T, bool gran) {
-  // gran: dX[l] hold (T, Np, H) tagged 8-byte granules (2 H floats per row), the decoupled hand-off
+                    int64_t N, int64_t Np, int64_t T, int64_t form) {
+  // form 0: fp32 dX rows + progress words; 1: dX[l] as (T, Np, H) tagged 8-byte granules (2 H floats per row; A/B)
+  TORCH_CHECK(form == 0 || form == 1, "form: 0 fp32 rows + progress words, 1 granules");
+  const bool gran = form == 1;
   const int64_t L = (int64_t)w_hh.size();
   CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");
@@ -1167,7 +1169,7 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
       fused ? g1.data() : nullptr, fused ? g2.data() : nullptr, fused ? g3.data() : nullptr, mk.data(),
       pt.empty() ? nullptr : pt.data(),
       reinterpret_cast<uint64_t*>(seeds.data_ptr<int64_t>()), (float)drop_p, dropout ? 1 : 0,
-      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, gran ? 1 : 0, cur_stream());
+      reinterpret_cast<unsigned*>(flags.data_ptr<int>()), (int)N, (int)Np, (int)T, (int)form, cur_stream());
   TORCH_CHECK(rc == 0, "lstm_stack_bwd: unsupported configuration (rc=", rc, ")");
 }
 

@@ -24,6 +24,16 @@
 #include <cstdlib>
 
 #include "common.h"
+#if MTA_STAMPS == 2
+// diagnostic timeline build: the last weight-gradient workgroup's k-slice starts (0..15), accumulation done (16),
+// atomics issued (17)
+__device__ unsigned long long mta_stack_tls[18];
+#define WG_SLICE_STAMP(k)                                                                                    \
+  do {                                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1 && (k) < 18)                                         \
+      mta_stack_tls[(k)] = __builtin_amdgcn_s_memrealtime();                                                 \
+  } while (0)
+#endif
 #include "lstm_wgrad.h"
 
 // diagnostic builds (csrc/tools/lstm_stack_probe.hip): -DMTA_STAMPS=1 per-segment s_memtime sums, -DMTA_STAMPS=2 the
@@ -35,14 +45,26 @@
 #define STACK_STAMPS (MTA_STAMPS == 1)
 #define STACK_TIMELINE (MTA_STAMPS == 2)
 #if STACK_TIMELINE
+// 100 MHz real-time counter: one clock across XCDs (s_memtime counts per-XCD shader clocks, not aligned)
 __device__ unsigned long long mta_stack_tl[2][64][4];
+// the backward's last 64 weight-gradient workgroups (by block id: the bottom layer's earliest chunks): entry, chunk
+// ready, body done, exit
+__device__ unsigned long long mta_stack_tlw[64][4];
+#define STACK_TLW(k)                                                                                             \
+  do {                                                                                                           \
+    const int _r = (int)(gridDim.x - 1 - blockIdx.x);                                                           \
+    if (threadIdx.x == 0 && _r < 64) mta_stack_tlw[_r][(k)] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
 #define STACK_TL(dir, k)                                                                      \
   do {                                                                                        \
-    if (threadIdx.x == 0 && blockIdx.x < 64) mta_stack_tl[(dir)][blockIdx.x][(k)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && blockIdx.x < 64) mta_stack_tl[(dir)][blockIdx.x][(k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define STACK_TL(dir, k) \
   do {                   \
+  } while (0)
+#define STACK_TLW(k) \
+  do {               \
   } while (0)
 #endif
 // s_sleep units (~64 cycles each) the backward gradient waves wait after a step barrier before their dx MFMA product:
@@ -179,6 +201,28 @@ __device__ __forceinline__ unsigned wait_progress(unsigned* flag, unsigned need,
     }
   }
   // every payload load after this point is sc1 (L1 bypass): only keep the compiler from hoisting them
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return seen;
+}
+
+// wait_progress for a workgroup that waits many steps (the fused weight-gradient chunks: up to T steps, ~240 of
+// them per launch at B = 1, L = 2): the sleep between polls grows with the distance still to go (a step is ~1 us,
+// s_sleep(127) ~4 us), so the pollers do not keep the progress words' lines busy for the pipeline's own hand-offs.
+__device__ __forceinline__ unsigned wait_progress_far(unsigned* flag, unsigned need, unsigned seen, unsigned* tmo,
+                                                      unsigned limit) {
+  unsigned spins = 0;
+  seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  while (!reached(seen, need)) {
+    const unsigned gap = need - seen;  // steps still to go (a previous launch's value: a huge gap)
+    if (gap > 8) __builtin_amdgcn_s_sleep(127);
+    else if (gap > 2) __builtin_amdgcn_s_sleep(24);
+    else __builtin_amdgcn_s_sleep(1);
+    seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (++spins > limit) {
+      __hip_atomic_fetch_add(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      seen = need;
+    }
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   return seen;
 }
@@ -1237,6 +1281,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
 
   // =========================== recurrent waves ===========================
   if (__builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(STACK_PRIO);
+  STACK_TL(0, 0);
   const float* w_hh = a.w_hh[layer];
   const bool stash = a.stash[layer] != nullptr;
   V8 Bhi[4][PREC == PREC_F32 ? 1 : KB], Blo[4][kWeightLo<PREC> ? KB : 1];
@@ -1306,6 +1351,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
       }
     }
   };
+  STACK_TL(0, 1);
   for (int t = 0; t < T; ++t) {
     SSTAMP(0)
     const int hs = t % HSL, hn = (t + 1) % HSL;
@@ -1390,10 +1436,12 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     }
     sy_post(&sy[SY_H][w], (unsigned)(t + 1));
     SSTAMP(5)
+    if (t == T / 2) STACK_TL(0, 2);
   }
   SSTAMP_FLUSH(0, 0, wave == 0)
   stage(T - 1);
   sy_post(&sy[SY_STG][w], (unsigned)T);
+  STACK_TL(0, 3);
   __syncthreads();  // F
 }
 
@@ -1491,7 +1539,7 @@ struct StackBwdArgs {
   mta_wgrad::WgArgs wg[MAXL];
   int wg_nq, wg_per_layer;
   // dX[l] as tagged granules {value, epoch-stamped reverse step} (8 bytes each): no progress word, no drain; the
-  // consumer layer checks the tags (the hand-off of stack_fwd_dec).  0: fp32 rows + progress words (MTA_LSTM_DEC=0)
+  // consumer layer checks the tags (the hand-off of stack_fwd_dec).  0: fp32 rows + progress words
   int gran;
 };
 
@@ -1748,6 +1796,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 
   // =========================== recurrent waves ===========================
   if (__builtin_amdgcn_readfirstlane(wave) < NW) __builtin_amdgcn_s_setprio(STACK_PRIO);
+  STACK_TL(1, 0);
   const float4* stash = reinterpret_cast<const float4*>(a.stash[layer]);
   const float* w_hh = a.w_hh[layer];
   bf16x8 Bhi[PREC == PREC_F32 ? 1 : KB], Blo[PREC == PREC_BF16X3 ? KB : 1];
@@ -1890,12 +1939,15 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
   };
   // steps T-1, T-3, ... use set A; T-2, T-4, ... set B: a loop of exactly two steps per trip (no
   // conditional step inside, so the sets keep their registers across the back-edge), odd T peels step 0
+  STACK_TL(1, 1);
   int t = T - 1;
   for (; t >= 1; t -= 2) {
     step(t, sA, cA);
+    if (t == T / 2 || t - 1 == T / 2) STACK_TL(1, 2);
     step(t - 1, sB, cB);
   }
   if (t == 0) step(0, sA, cA);
+  STACK_TL(1, 3);
   SSTAMP_FLUSH(1, 0, wave == 0)
   store_step(0);
   mta_wait_vmem();
@@ -1928,16 +1980,22 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     const mta_wgrad::WgArgs& w = a.wg[layer];
     const int chunk = w.nchunks - 1 - rem / a.wg_nq, quarter = rem % a.wg_nq;
     const int t_lo = (int)((long)chunk * w.rows_per_chunk / a.Np);  // earliest step of the chunk's rows
-    if (threadIdx.x < a.ntiles)
-      wait_progress(a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + threadIdx.x), base + (unsigned)(a.T - t_lo), base,
-                    a.timeout, a.spin_limit);
-    __syncthreads();
-    mta_wgrad::wgrad_body<PREC, H / 8, true>(w, chunk, quarter, dyn_lds);
+    STACK_TLW(0);
+    auto ready = [&]() {
+      if (threadIdx.x < a.ntiles)
+        wait_progress_far(a.dg_flags + FLAG_STRIDE * (layer * a.tr8 + threadIdx.x), base + (unsigned)(a.T - t_lo),
+                          base, a.timeout, a.spin_limit);
+      __syncthreads();
+      STACK_TLW(1);
+    };
+    mta_wgrad::wgrad_body<PREC, H / 8, true>(w, chunk, quarter, dyn_lds, ready);
+    STACK_TLW(2);
   }
   if (finish_launch(a.ctl, CTL_BWD_EPOCH, CTL_BWD_DONE, base, a.eshift) && a.dropout) {
     // fresh counter-hash masks for the next step (the graph needs no seed-update node)
     for (int l = 0; l < a.L; ++l) a.seeds[l] += 0x9E3779B97F4A7C15ull;
   }
+  if ((int)blockIdx.x >= a.L * a.tr8) STACK_TLW(3);
 }
 
 template <int H, int PREC>
@@ -2091,7 +2149,7 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
                                   const float* const* hseq, const float* const* inp, float* const* g_wih,
                                   float* const* g_whh, float* const* g_bih, float* const* g_bhh,
                                   const uint32_t* const* mask, float* const* part, uint64_t* seeds, float drop_p,
-                                  int dropout, unsigned* flags, int N, int Np, int T, int gran, hipStream_t st) {
+                                  int dropout, unsigned* flags, int N, int Np, int T, int form, hipStream_t st) {
   if (L < 1 || L > MAXL || Np % S || N > Np || N < 1 || (H != 32 && H != 64) || T + 8 >= (1 << MAX_EPOCH_SHIFT)) return -1;
   if (prec == PREC_F16X2) prec = PREC_BF16X3;  // a forward mode: backward products in bf16x3
   StackBwdArgs a{};
@@ -2105,7 +2163,9 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     if (dropout && l > 0 && !a.mask[l]) return -2;
   }
   a.dh_last = dh_last;
-  a.gran = gran;  // dX[l]: (T, Np, H) granules of 8 bytes
+  // form 0: fp32 dX rows + progress words; 1: dX[l] as (T, Np, H) granules of 8 bytes (A/B, measured slower)
+  if (form < 0 || form > 1) return -1;
+  a.gran = form;
   a.seeds = seeds;
   a.drop_p = drop_p;
   a.dropout = dropout;

@@ -6,6 +6,12 @@
 
 #include "common.h"
 
+#ifndef WG_SLICE_STAMP
+#define WG_SLICE_STAMP(k) \
+  do {                    \
+  } while (0)
+#endif
+
 namespace mta_wgrad {
 
 // ---------------------------------------------------------------------------------------------
@@ -106,8 +112,18 @@ __device__ __forceinline__ void wg_store_unit(char* img, int col0, int k0, const
 // One workgroup of NWAVES waves: chunk `chunk` of the rows x c' block `quarter` of CQ = 16 NWAVES gate
 // columns.  SC1A: the dG rows were produced by other workgroups of the same launch (lstm_stack.hip's fused
 // backward) and are read with sc1 loads.
-template <int PREC, int NWAVES, bool SC1A>
-__device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, const int quarter, char* lds) {
+struct WgNoWait {
+  __device__ void operator()() const {}
+};
+
+// wait(): called once by every thread before the first dG (A operand) load -- the fused backward's chunk-ready poll.
+// Chunks of at most four K slices whose units fit one per thread (B = 1..2 windows: a chunk is one step of
+// Np <= 128 rows) take the short path: the B operand ([h_{t-1} | inp], which the backward does not write) is loaded
+// BEFORE the wait, and the A slices all at once after it -- one load round trip after the chunk is ready instead of
+// one per slice (r6 timelines: ~3.5 us per slice, 18.5 us for the chunk of step 0, the whole tail of the backward).
+template <int PREC, int NWAVES, bool SC1A, typename Wait = WgNoWait>
+__device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, const int quarter, char* lds,
+                                           const Wait& wait = Wait()) {
   using I = WgImg<PREC>;
   constexpr int THREADS = 64 * NWAVES;
   constexpr int CQ = 16 * NWAVES;
@@ -241,23 +257,50 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
   // accumulators: this wave's 16 c' x NB columns -> NB/16 tiles (<= 16)
   constexpr int MAX_NT = 16;
   const int NT = NB / 16;
+  // a chunk inside step 0 has h_{t-1} = 0: its W_hh tiles (the first H / 16) are all zero -- skip their products
+  // and atomics (the step-0 chunk is the one that trails the recurrence)
+  const int JT0 = row_end <= a.Np ? H / 16 : 0;
   f32x4 acc[MAX_NT];
 #pragma unroll
   for (int j = 0; j < MAX_NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   WgUnit st0, st1;
-  const bool has0 = u0 < nUnits, has1 = u1 < nUnits;
-  int k0 = row_begin;
-  if (has0) load_unit(d0, u0, k0, st0);
-  if (has1) load_unit(d1, u1, k0, st1);
+  const int nsl = (row_end - row_begin + WG_KS - 1) / WG_KS;
+  const int nB = nUnits - nA;
+  // short path: thread t holds A unit t % nA of slice t / nA and B unit t % nB of slice t / nB
+  const bool shortp = nsl <= 4 && nA * nsl <= THREADS && nB * nsl <= THREADS;
+  const int sa = tid / nA, sb = tid / nB;
+  const int ua = tid % nA, ub = nA + tid % nB;
+  bool has0, has1;
+  if (shortp) {
+    has0 = sa < nsl;
+    has1 = sb < nsl;
+    const Desc da = make_desc(ua), db = make_desc(ub);
+    if (has1) load_unit(db, ub, row_begin + sb * WG_KS, st1);
+    wait();
+    if (has0) load_unit(da, ua, row_begin + sa * WG_KS, st0);
+  } else {
+    has0 = u0 < nUnits;
+    has1 = u1 < nUnits;
+    wait();
+    if (has0) load_unit(d0, u0, row_begin, st0);
+    if (has1) load_unit(d1, u1, row_begin, st1);
+  }
 
-  for (; k0 < row_end; k0 += WG_KS) {
+  int k0 = row_begin;
+  for (int sl = 0; k0 < row_end; k0 += WG_KS, ++sl) {
+    WG_SLICE_STAMP(sl < 16 ? sl : 15);
     __syncthreads();  // previous slice's fragment reads are done
-    if (has0) store_unit(u0, st0);
-    if (has1) store_unit(u1, st1);
+    if (shortp) {
+      if (has0 && sa == sl) store_unit(ua, st0);
+      if (has1 && sb == sl) store_unit(ub, st1);
+    } else {
+      if (has0) store_unit(u0, st0);
+      if (has1) store_unit(u1, st1);
+    }
     __syncthreads();
     const int kn = k0 + WG_KS;
-    if (kn < row_end) {  // next slice in flight during this slice's MFMAs
+    if (!shortp && kn < row_end) {  // next slice in flight during this slice's MFMAs
       if (has0) load_unit(d0, u0, kn, st0);
       if (has1) load_unit(d1, u1, kn, st1);
     }
@@ -270,7 +313,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
         const float av = A[(size_t)am * I::RS + 4 * k4 + (lane >> 4)];
 #pragma unroll
         for (int j = 0; j < MAX_NT; ++j) {
-          if (j < NT) {
+          if (j >= JT0 && j < NT) {
             const float bv = B[(size_t)(16 * j + (lane & 15)) * I::RS + 4 * k4 + (lane >> 4)];
             acc[j] = mfma16x16x4f32(av, bv, acc[j]);
           }
@@ -285,7 +328,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       if constexpr (PREC == PREC_BF16X3) alo = *reinterpret_cast<const bf16x8*>(A + lo_off + (size_t)am * I::RS + 8 * (lane >> 4));
 #pragma unroll
       for (int j = 0; j < MAX_NT; ++j) {
-        if (j < NT) {
+        if (j >= JT0 && j < NT) {
           const size_t bo = (size_t)(16 * j + (lane & 15)) * I::RS + 8 * (lane >> 4);
           const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(B + bo);
           acc[j] = mfma16x16x32(ahi, bhi, acc[j]);
@@ -299,6 +342,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
     }
   }
 
+  WG_SLICE_STAMP(16);
   // ---- partials -> gradients (no-return f32 atomics) ----
   // D layout: lane holds D[4(l>>4)+i][l&15]; local c' = 16*wave + 4(l>>4) + i  ->  gate g = i, unit u
   const int qrow = lane >> 4;
@@ -308,7 +352,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
     const int r = (cp & 3) * H + (cp >> 2);
 #pragma unroll
     for (int j = 0; j < MAX_NT; ++j) {
-      if (j < NT) {
+      if (j < NT && (a.part || j >= JT0)) {  // (deterministic partials: the skipped tiles write their zeros)
         const int col = 16 * j + (lane & 15);
         const float v = acc[j][i];
         if (a.part) {
@@ -321,8 +365,10 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       }
     }
   }
-  // bias: reduce the 4 row-group threads of each A column group (lanes t, t^1, t^2, t^3)
-  if (u0 < nA) {
+  WG_SLICE_STAMP(17);
+  // bias: reduce the 4 row-group threads of each A column group (lanes t, t^1, t^2, t^3; short path: one sum per
+  // slice -- nA is a multiple of 4, so a slice's units stay 4-aligned in the thread index)
+  if (shortp ? has0 : u0 < nA) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float v = bias_acc[c];
@@ -330,8 +376,9 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       v += __shfl_xor(v, 2, 64);
       bias_acc[c] = v;
     }
-    if ((u0 & 3) == 0) {
-      const int cg = u0 >> 2;
+    const int ubias = shortp ? ua : u0;
+    if ((ubias & 3) == 0) {
+      const int cg = ubias >> 2;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const int cp = cq0 + cg * 4 + c;

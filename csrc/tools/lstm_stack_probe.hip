@@ -84,7 +84,10 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
   // decoupled forward (default; DEC=0 in the environment selects the barrier form): (L - 1) x (T, Np, H) granules
   const int dec = getenv("DEC") && atoi(getenv("DEC")) == 0 ? 0 : 1;
-  const int bgran = getenv("BGRAN") && atoi(getenv("BGRAN")) == 1 ? 1 : 0;  // backward granule hand-off (A/B)
+  // backward dX hand-off: 0 fp32 rows + progress words (default), 1 tagged granules (A/B)
+  const int bform = getenv("BFORM") ? atoi(getenv("BFORM")) : 0;
+  const int bgran = bform == 1;
+  const int nowg = getenv("NOWG") && atoi(getenv("NOWG")) == 1;  // 1: no fused weight-gradient workgroups (A/B)
   unsigned long long* gran = nullptr;
   CK(hipMalloc(&gran, (size_t)(L > 1 ? L - 1 : 1) * T * Np * H * 8));
   CK(hipMemset(gran, 0, (size_t)(L > 1 ? L - 1 : 1) * T * Np * H * 8));
@@ -98,9 +101,11 @@ int main(int argc, char** argv) {
   // and the top layer's first tile in the backward (block 0: its gradient waves run the dx MFMAs)
   const int ntiles = Np / 16, tr8 = (ntiles + 7) / 8 * 8;
   const int which = argc > 6 ? atoi(argv[6]) : L - 1;
-  int sb[2] = {which * tr8, 0};
+  // BWDL=<layer> stamps that layer's first tile in the backward (default: the top layer)
+  const int bl = getenv("BWDL") ? atoi(getenv("BWDL")) : L - 1;
+  int sb[2] = {which * tr8, (L - 1 - bl) * tr8};
   CK(hipMemcpyToSymbol(HIP_SYMBOL(mta_stack_stamp_block), sb, sizeof(sb)));
-  printf("stamping forward layer %d (block %d), backward block 0 (top layer)\n", which, sb[0]);
+  printf("stamping forward layer %d (block %d), backward layer %d (block %d)\n", which, sb[0], bl, sb[1]);
 #endif
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -123,9 +128,9 @@ int main(int argc, char** argv) {
     if (mode == 2) continue;
     CK(hipEventRecord(a));
     rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
-                            hseq.data(), inp.data(), gwih.data(), gwhh.data(), gbih.data(), gbhh.data(),
+                            hseq.data(), inp.data(), gwih.data(), nowg ? nullptr : gwhh.data(), gbih.data(), gbhh.data(),
                             const_cast<const uint32_t* const*>(mask.data()), nullptr, seeds, p,
-                            mode == 0 ? 1 : 0, flags, N, Np, T, bgran, 0);
+                            mode == 0 ? 1 : 0, flags, N, Np, T, bform, 0);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     if (rc) {
@@ -137,21 +142,64 @@ int main(int argc, char** argv) {
   }
 #if STACK_TIMELINE
   {
-    // the last forward of the timed loop: per layer, min over tiles of entry / loop start / step T/2 / end
+    constexpr int MAXL_PROBE = 8;
+    // the last forward / backward of the timed loop, per layer: entry / loop start / step T/2 / end, in ns (100 MHz
+    // real-time counter) from the earliest entry of the same tile over its layers, averaged over tiles
     unsigned long long tl[2][64][4];
     CK(hipMemcpyFromSymbol(tl, HIP_SYMBOL(mta_stack_tl), sizeof(tl)));
     const int ntl = Np / 16, tr8l = (ntl + 7) / 8 * 8;
-    unsigned long long t0 = ~0ull;
-    for (int l = 0; l < L; ++l)
-      for (int i = 0; i < ntl && l * tr8l + i < 64; ++i) t0 = tl[0][l * tr8l + i][0] < t0 ? tl[0][l * tr8l + i][0] : t0;
-    for (int l = 0; l < L; ++l) {
-      double v[4] = {0, 0, 0, 0};
-      int cnt = 0;
-      for (int i = 0; i < ntl && l * tr8l + i < 64; ++i, ++cnt)
-        for (int k = 0; k < 4; ++k) v[k] += (double)(tl[0][l * tr8l + i][k] - t0);
-      printf("timeline fwd layer %d (cycles from first entry, mean of %d tiles): entry %.0f start %.0f mid %.0f end %.0f"
-             "  -> pace %.0f cycles/step (second half)\n",
-             l, cnt, v[0] / cnt, v[1] / cnt, v[2] / cnt, v[3] / cnt, (v[3] - v[2]) / cnt / (T - 1 - T / 2));
+    for (int d = 0; d < 2; ++d) {
+      auto blk = [&](int l, int i) { return (d == 0 ? l : L - 1 - l) * tr8l + i; };
+      double v[MAXL_PROBE][4] = {};
+      int cnt[MAXL_PROBE] = {};
+      for (int i = 0; i < ntl; ++i) {
+        unsigned long long t0 = ~0ull;
+        bool ok = true;
+        for (int l = 0; l < L; ++l) {
+          if (blk(l, i) >= 64) { ok = false; break; }
+          t0 = tl[d][blk(l, i)][0] < t0 ? tl[d][blk(l, i)][0] : t0;
+        }
+        if (!ok) continue;
+        for (int l = 0; l < L; ++l) {
+          ++cnt[l];
+          for (int k = 0; k < 4; ++k) v[l][k] += (double)(long long)(tl[d][blk(l, i)][k] - t0);
+        }
+      }
+      for (int l0 = 0; l0 < L; ++l0) {
+        const int l = d == 0 ? l0 : L - 1 - l0;
+        if (!cnt[l]) continue;
+        const double n = cnt[l];
+        const int half = d == 0 ? T - 1 - T / 2 : T / 2;
+        printf("timeline %s layer %d (ns from the tile's first entry, mean of %d tiles): entry %.0f start %.0f mid "
+               "%.0f end %.0f  -> pace %.0f ns/step (second half)\n",
+               d == 0 ? "fwd" : "bwd", l, cnt[l], 10 * v[l][0] / n, 10 * v[l][1] / n, 10 * v[l][2] / n,
+               10 * v[l][3] / n, 10 * (v[l][3] - v[l][2]) / n / half);
+      }
+    }
+    {
+      // the backward's last weight-gradient workgroups (the bottom layer's earliest chunks), ns from the first
+      // recurrence entry of the launch (one real-time clock for the whole chip)
+      unsigned long long tw[64][4];
+      CK(hipMemcpyFromSymbol(tw, HIP_SYMBOL(mta_stack_tlw), sizeof(tw)));
+      unsigned long long r0 = ~0ull, rend = 0;
+      for (int b = 0; b < L * tr8l && b < 64; ++b)
+        if (b % tr8l < ntl) {
+          r0 = tl[1][b][0] < r0 ? tl[1][b][0] : r0;
+          rend = tl[1][b][3] > rend ? tl[1][b][3] : rend;
+        }
+      if (!nowg) {
+        unsigned long long ts[18];
+        CK(hipMemcpyFromSymbol(ts, HIP_SYMBOL(mta_stack_tls), sizeof(ts)));
+        printf("wgrad last block slices (ns from ready):");
+        for (int k = 0; k < 18; ++k)
+          if (ts[k] >= tw[0][1] && ts[k] - tw[0][1] < 10000000ull) printf(" [%d]%.0f", k, 10.0 * (double)(ts[k] - tw[0][1]));
+        printf("\n");
+        printf("wgrad tail: recurrence (%d blocks <64) ends at %.0f ns\n", L * tr8l, 10.0 * (double)(rend - r0));
+        for (int r = 0; r < 12; ++r)
+          printf("  wgrad block last-%d: entry %.0f ready %.0f body_done %.0f exit %.0f ns\n", r,
+                 10.0 * (double)(long long)(tw[r][0] - r0), 10.0 * (double)(long long)(tw[r][1] - r0),
+                 10.0 * (double)(long long)(tw[r][2] - r0), 10.0 * (double)(long long)(tw[r][3] - r0));
+      }
     }
   }
 #endif
@@ -184,6 +232,44 @@ int main(int argc, char** argv) {
     printf("determinism: %ld of %ld h values differ between two identical forwards (max |d| %.3e)\n", bad,
            (long)L * T * N * H, maxd);
   }
+  // backward determinism: 6 backwards of the same forward state must give bitwise-identical dG (the fused weight
+  // gradients' atomics aside); per layer, the first differing step (reverse order) of each rerun
+  if (mode != 2) {
+    std::vector<std::vector<float>> ref(L), again(L);
+    int nbad = 0;
+    for (int pass = 0; pass < 6; ++pass) {
+      CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
+      int rc = mta_lstm_stack_bwd(H, prec, L, FIN, stash.data(), whh.data(), wih.data(), dh_last, dG.data(), dX.data(),
+                                  hseq.data(), inp.data(), gwih.data(), nowg ? nullptr : gwhh.data(), gbih.data(),
+                                  gbhh.data(), const_cast<const uint32_t* const*>(mask.data()), nullptr, seeds, p,
+                                  mode == 0 ? 1 : 0, flags, N, Np, T, bform, 0);
+      CK(hipDeviceSynchronize());
+      if (rc) return 1;
+      char line[512];
+      int off = 0;
+      bool any = false;
+      for (int l = 0; l < L; ++l) {
+        auto& v = pass ? again[l] : ref[l];
+        v.resize((size_t)T * Np * 4 * H);
+        CK(hipMemcpy(v.data(), dG[l], v.size() * 4, hipMemcpyDeviceToHost));
+        if (!pass) continue;
+        int first = -1;
+        for (int t = T - 1; t >= 0 && first < 0; --t)
+          for (int n = 0; n < N && first < 0; ++n)
+            for (int c = 0; c < 4 * H; ++c) {
+              const size_t i = ((size_t)t * Np + n) * 4 * H + c;
+              if (ref[l][i] != again[l][i]) { first = t; break; }
+            }
+        if (first >= 0) any = true;
+        off += snprintf(line + off, sizeof(line) - off, " L%d:%d", l, first);
+      }
+      if (pass) {
+        nbad += any;
+        if (any) printf("bwd determinism: rerun %d differs (first differing step per layer, -1 = none):%s\n", pass, line);
+      }
+    }
+    printf("bwd determinism: %d of 5 reruns differ\n", nbad);
+  }
   // checksums (variants of the kernel must agree): last layer's h at T-1 and layer 0's W_hh gradient after reps runs
   {
     std::vector<float> hl((size_t)Np * H), gw((size_t)4 * H * H);
@@ -197,9 +283,9 @@ int main(int argc, char** argv) {
   }
   unsigned tmo = 0;
   CK(hipMemcpy(&tmo, flags + (nflags - 160), 4, hipMemcpyDeviceToHost));
-  printf("dec=%d bgran=%d mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
+  printf("dec=%d bform=%d mode=%d N=%d L=%d T=%d prec=%d stamps=%d: fwd %.1f us (%.3f us/step)  bwd %.1f us (%.3f us/step)  "
          "timeouts=%u\n",
-         dec, bgran, mode, N, L, T, prec, MTA_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
+         dec, bform, mode, N, L, T, prec, MTA_STAMPS, ms_f * 1e3, ms_f * 1e3 / T, ms_b * 1e3, ms_b * 1e3 / T,
          tmo);
 #if STACK_STAMPS
   unsigned long long acc[2][3][8];

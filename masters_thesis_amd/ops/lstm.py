@@ -219,7 +219,8 @@ def _stack_gran(C, Np: int, L: int, device, T: int, H: int) -> Optional[Tensor]:
 
     if os.environ.get("MTA_LSTM_DEC", "1") == "0":
         return None
-    key = (C.lstm_stack_flag_words(Np), int(L), str(device), int(C.lstm_stack_epoch_shift(int(T))), int(T), int(H))
+    key = (C.lstm_stack_flag_words(Np), int(Np), int(L), str(device), int(C.lstm_stack_epoch_shift(int(T))), int(T),
+           int(H))
     if key not in _GRAN:
         _GRAN[key] = torch.zeros(max(L - 1, 1) * T * Np * H, dtype=torch.int64, device=device)
     return _GRAN[key]
@@ -351,18 +352,17 @@ def pipelined_backward(st: "PipelinedState", dh_last: Tensor) -> None:
         for t in flat:
             t.grad = torch.zeros_like(t)
     dG = [torch.empty((T, Np, 4 * H), device=dev, dtype=torch.float32) for _ in range(L)]
-    # dX hand-off: fp32 rows + progress words.  The kernel also has a tagged-granule form (gran=True: 2 H floats per
-    # row), measured slower at every depth (profiles/r6_lstm_decoupled.txt; the probe's BGRAN=1 A/B)
-    gran = False
-    dX = [torch.empty((T, Np, (2 if gran else 1) * H), device=dev, dtype=torch.float32)
-          for _ in range(L - 1)] + [_empty(dev)]
+    # dX hand-off between layers: fp32 rows + progress words (form 0).  The kernel keeps a tagged-granule form
+    # (form 1, A/B only: slower at every depth, profiles/r6_lstm_decoupled.txt)
+    form = 0
+    dX = [torch.empty((T, Np, H), device=dev, dtype=torch.float32) for _ in range(L - 1)] + [_empty(dev)]
     flags = _stack_flags(C, Np, L, dev, T)
     inp = [st.x] + [st.xdrop[l] if drop else st.hseq[l - 1] for l in range(1, L)]
     grads = [[_grad_buffer(flat[4 * l + k]) for l in range(L)] for k in range(4)]
     parts = _parts(C, True, T, H, [F] + [H] * (L - 1), dev)
     C.lstm_stack_bwd(H, prec, F, list(st.stash), list(flat[1::4]), list(flat[0::4]), dh_last.contiguous(), dG, dX,
                      list(st.hseq), inp, grads, list(st.masks) if drop else [], parts, st.seeds, p, drop, flags, N,
-                     Np, T, gran)
+                     Np, T, form)
     if st.pad is not None:
         real, H0 = st.pad
         idx = _padded_rows_index(H0, H, dev)

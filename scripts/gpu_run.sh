@@ -13,6 +13,7 @@
 #   pmc <tag> <counters> -- <cmd>   one rocprofv3 --pmc pass (its own run, no trace domains) -> <tag>/
 #   probe <N L prec T mode [layer]> tools_bin/stack_s0 + stack_s1 (scripts/build_probes.sh) -> probe.txt
 #   tl <N L prec T mode>            tools_bin/stack_tl timeline build (scripts/build_probes.sh) -> probe.txt
+#   bin <name> <args>               any tools_bin/<name> (diagnostic variants) -> probe.txt
 #   py <script> <args>              python -u <script> <args> -> py.log
 #   smoke                           __graft_entry__.smoke() -> smoke.log
 # STEP_TIMEOUT (s, default 300) bounds every step; PMC passes are killed at 90 s (an over-subscribed counter block
@@ -51,6 +52,8 @@ for s in "${STEPS[@]}"; do
            done
            (exit $prc) ;;
     tl) timeout -k 10 90 ./tools_bin/stack_tl "${args[@]}" >> "$O/probe.txt" 2>&1 ;;
+    bin) b=${args[0]}; echo "== $b ${args[*]:1}" >> "$O/probe.txt"
+         timeout -k 10 90 "./tools_bin/$b" "${args[@]:1}" >> "$O/probe.txt" 2>&1 ;;
     py) timeout -k 10 "$TO" python -u "${args[@]}" >> "$O/py.log" 2>&1 ;;
     smoke) timeout -k 10 "$TO" python -u -c "import __graft_entry__ as g; g.smoke()" >> "$O/smoke.log" 2>&1 ;;
     *) st "unknown step kind: $kind"; exit 2 ;;

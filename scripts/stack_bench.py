@@ -4,6 +4,7 @@
 fixed by the lane-contiguous stash layout and vmcnt-counted waits.)
 """
 import math
+import os
 import sys
 from pathlib import Path
 
@@ -38,7 +39,8 @@ def run(C, L, prec):
                          flags, N, Np, T, gran)
 
     dG = [torch.empty((T, Np, 4 * H), device=dev) for _ in range(L)]
-    dX = [torch.empty((T, Np, 2 * H), device=dev) for _ in range(L - 1)] + [E]  # granule hand-off
+    form = int(os.environ.get("BFORM", "0"))  # 0 fp32 rows + progress words, 1 granule dX
+    dX = [torch.zeros((T, Np, (2 if form != 0 else 1) * H), device=dev) for _ in range(L - 1)] + [E]
     dh = torch.randn(N, H, device=dev)
 
     inp = [x] + hseq[:-1]
@@ -46,11 +48,11 @@ def run(C, L, prec):
 
     def bwd():
         C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, [], [], [], seeds, 0.0, False, flags,
-                         N, Np, T, True)
+                         N, Np, T, form)
 
     def bwd_fused():
         C.lstm_stack_bwd(H, prec, F, stash, ws[1::4], ws[0::4], dh, dG, dX, hseq, inp, grads, [], [], seeds, 0.0, False,
-                         flags, N, Np, T, True)
+                         flags, N, Np, T, form)
 
     def bwd_wgrad():
         bwd()

@@ -97,6 +97,57 @@ def test_pipelined_matches_fp64(prec, N, T, F, H, L):
         assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad w{i}: err {e} (scale {sc})"
 
 
+@pytest.mark.parametrize("prec", ["high", "bf16x3"])
+def test_barrier_forward_matches_fp64(prec, monkeypatch):
+    """MTA_LSTM_DEC=0 (docs/ARCHITECTURE.md knob table): the barrier form of the forward, kept for the A/B; the
+    default decoupled forward runs in every other test of this file."""
+    from masters_thesis_amd.ops import lstm as op
+
+    monkeypatch.setenv("MTA_LSTM_DEC", "0")
+    N, T, F, H, L = 100, 40, 3, 64, 3
+    torch.manual_seed(2)
+    x = torch.randn(N, T, F)
+    ws = _weights(F, H, L, seed=4)
+    R = torch.randn(N, H)
+    ref, w64 = _ref(x, ws, L)
+    (ref * R.double()).sum().backward()
+    wg = [w.to(DEV).requires_grad_(True) for w in ws]
+    out = op.lstm_last_hidden(x.to(DEV), wg, L, 0.0, True, prec)
+    (out * R.to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    tol = TOLS[prec]
+    err = (out.double().cpu() - ref.detach()).abs().max().item()
+    assert err <= tol * max(ref.abs().max().item(), 1.0), f"forward err {err}"
+    for i, (a, b) in enumerate(zip(wg, w64)):
+        sc = b.grad.abs().max().item()
+        e = (a.grad.double().cpu() - b.grad).abs().max().item()
+        assert e <= 4 * tol * max(sc, 1e-3) + 1e-6, f"grad w{i}: err {e} (scale {sc})"
+
+
+@pytest.mark.parametrize("prec", ["high", "bf16x3", "highest"])
+def test_backward_is_run_to_run_stable(prec):
+    """Three backwards of the same batch agree to the fused weight-gradient atomics' ordering noise (~1e-7): an
+    LDS hand-off race in the recurrence shows up as ~1e-4 differences from some reverse step on (r6: the
+    decoupled-backward experiment, profiles/r6_lstm_dec/r6s_bwd_race.txt)."""
+    from masters_thesis_amd.ops import lstm as op
+
+    N, T, F, H, L = 100, 60, 3, 64, 3
+    torch.manual_seed(3)
+    x = torch.randn(N, T, F, device=DEV)
+    ws = [w.to(DEV) for w in _weights(F, H, L, seed=6)]
+    R = torch.randn(N, H, device=DEV)
+    runs = []
+    for _ in range(3):
+        wg = [w.clone().requires_grad_(True) for w in ws]
+        out = op.lstm_last_hidden(x, wg, L, 0.0, True, prec)
+        (out * R).sum().backward()
+        torch.cuda.synchronize()
+        runs.append([w.grad.clone() for w in wg])
+    for other in runs[1:]:
+        for a, b in zip(runs[0], other):
+            assert (a - b).abs().max().item() <= 1e-5 * max(a.abs().max().item(), 1e-3)
+
+
 @pytest.mark.parametrize("N", [2100, 4200])
 def test_pipelined_grid_beyond_one_workgroup_per_cu(N):
     """L x tiles > 256 workgroups (not all co-resident): producers always precede consumers in block order, so
