@@ -1102,9 +1102,9 @@ void lstm_stack_bwd(int64_t H, int64_t prec, int64_t fin, std::vector<at::Tensor
                     std::vector<std::vector<at::Tensor>> grads, std::vector<at::Tensor> masks,
                     std::vector<at::Tensor> parts, at::Tensor seeds, double drop_p, bool dropout, at::Tensor flags,
                     int64_t N, int64_t Np, int64_t T, int64_t form) {
-  // form 0: fp32 dX rows + progress words; 1: dX[l] as (T, Np, H) tagged 8-byte granules (2 H floats per row; A/B)
-  TORCH_CHECK(form == 0 || form == 1, "form: 0 fp32 rows + progress words, 1 granules");
-  const bool gran = form == 1;
+  // form: the dX hand-off, 0 = fp32 rows + progress words (the only form kept)
+  TORCH_CHECK(form == 0, "form: 0 (fp32 rows + progress words)");
+  const bool gran = false;
   const int64_t L = (int64_t)w_hh.size();
   CHECK_F32(dh_last);
   TORCH_CHECK(dh_last.numel() == N * H, "dh_last must be (N, H)");

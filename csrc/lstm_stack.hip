@@ -1538,9 +1538,6 @@ struct StackBwdArgs {
   // fused weight gradients: wg_per_layer workgroups per layer follow the L x tr8 recurrence workgroups
   mta_wgrad::WgArgs wg[MAXL];
   int wg_nq, wg_per_layer;
-  // dX[l] as tagged granules {value, epoch-stamped reverse step} (8 bytes each): no progress word, no drain; the
-  // consumer layer checks the tags (the hand-off of stack_fwd_dec).  0: fp32 rows + progress words
-  int gran;
 };
 
 template <int H, int PREC>
@@ -1560,7 +1557,10 @@ struct BwdSmem {
 // apply this layer's input-dropout mask and hand dH^{(l-1)} to the layer below.
 // Intervals: I(t) = between barriers A(t+1) and A(t); the recurrent waves read dhs[t&1] and write the
 // dG image (t&1) in I(t); the gradient waves write dhs[(t-1)&1] and read image ((t+1)&1) in I(t).
-template <int H, int PREC, bool TOP, bool BOTTOM>
+// DPF: how many intervals before its staging a gradient wave loads dH of the layer above -- 1 (L <= 2: the least
+// fill per layer) or 2 (deeper stacks: the hand-off round trip off every lower layer's interval; L=4 144 -> 132 us,
+// L=8 203 -> 186 us, L=2 92 -> 95 us, profiles/r6_lstm_dec/r6u_probe.txt)
+template <int H, int PREC, bool TOP, bool BOTTOM, int DPF>
 __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int layer, const int tile,
                                                BwdSmem<H, PREC>& sm, const unsigned base) {
   constexpr int G4 = 4 * H;
@@ -1610,44 +1610,17 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
           }
       }
     }
-    float dreg[4] = {0.f, 0.f, 0.f, 0.f};
+    // dH_s of the layer above (4 sequences x unit u) into one of two register sets, loaded DPF intervals before it
+    // is staged
+    float dA[4] = {0.f, 0.f, 0.f, 0.f}, dB[4] = {0.f, 0.f, 0.f, 0.f};
     unsigned seen = base;
-    const bool gr = a.gran != 0;
-    unsigned long long gq[4] = {0, 0, 0, 0};
-    auto load_dh = [&](int t) {  // dH_t rows (4 sequences x unit u) into registers
+    auto load_dh = [&](int t, float (&d)[4]) {
       if constexpr (!TOP) {
-        if (gr) {  // granules: issued now, checked (and re-polled if stale) by complete_dh before they are staged
-          const unsigned long long* g = reinterpret_cast<const unsigned long long*>(dH);
+        seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) gq[i] = gran_load(g + ((size_t)t * Np + n0 + 4 * q + i) * H + u);
-        } else {
-          seen = wait_progress(in_flag, base + (unsigned)(T - t), seen, a.timeout, a.spin_limit);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            dreg[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    };
-    auto complete_dh = [&](int t) {  // granule form: every tag must carry reverse step T - t of this launch
-      if constexpr (!TOP) {
-        if (gr) {
-          const unsigned tag = base + (unsigned)(T - t);
-          for (unsigned spins = 0;; ++spins) {
-            bool ok = true;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ok &= (unsigned)(gq[i] >> 32) == tag;
-            if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-            if (spins >= a.spin_limit) {
-              if (lane == 0) __hip_atomic_fetch_add(a.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            load_dh(t);
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) dreg[i] = __builtin_bit_cast(float, (unsigned)gq[i]);
-        }
+        for (int i = 0; i < 4; ++i)
+          d[i] = __hip_atomic_load(const_cast<float*>(dH) + ((size_t)t * Np + n0 + 4 * q + i) * H + u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     };
     uint32_t mreg = 0x01010101u, mnext = 0x01010101u;
@@ -1657,42 +1630,9 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         if (min) mnext = min[stack_keep_index(t, tile, a.ntiles, ts, H, 16 * w + tc)];
       }
     };
-    auto stage_dh = [&](int t) {
+    auto stage_dh = [&](int t, const float (&d)[4]) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = dreg[i];
-    };
-    // dG_t (fp32, unit-major columns 4u + g) from the LDS image (t&1) -> write-through 16-byte stores: the fused
-    // weight-gradient workgroups read these rows.  Issued by the gradient waves (they wait at the step barrier
-    // for ~1,300 cycles, r3 stamps) instead of the recurrent waves, whose store issue + vmcnt waits were ~500
-    // cycles of every reverse step.  Lane li = 64 w + lane: row li / 16, columns 4 (li % 16) + 64 k.  bf16 images:
-    // dG = hi (+ lo) -- the weight-gradient product splits it into the same hi / lo pair again.
-    // (4 stores per lane for H = 32 and 64: NW waves cover 4 NW rows per pass, G4 / 64 column blocks per row)
-    auto store_dg = [&](int t) {
-      const int buf = t & 1, li = 64 * w + lane, c0 = 4 * (li & 15);
-#pragma unroll
-      for (int pass = 0; pass < 16 / (4 * NW); ++pass)
-#pragma unroll
-      for (int k = 0; k < G4 / 64; ++k) {
-        const int s = (li >> 4) + 4 * NW * pass;
-        float* row = dG + ((size_t)t * Np + n0 + s) * G4;
-        const int c = c0 + 64 * k;  // columns c .. c + 3 = gates 0..3 of unit c / 4
-        f32x4 v;
-        if constexpr (PREC == PREC_F32) {
-          const int uu = c >> 2;
-#pragma unroll
-          for (int g = 0; g < 4; ++g) v[g] = g_f[buf][s][(uu & 3) * KF + g * (H / 4) + (uu >> 2)];
-        } else {
-          const bf16x4 hi4 = *reinterpret_cast<const bf16x4*>(&g_hi[buf][s][c]);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) v[g] = (float)hi4[g];
-          if constexpr (PREC == PREC_BF16X3) {
-            const bf16x4 lo4 = *reinterpret_cast<const bf16x4*>(&g_lo[buf][s][c]);
-#pragma unroll
-            for (int g = 0; g < 4; ++g) v[g] += (float)lo4[g];
-          }
-        }
-        store_sc1_x4(row + c, v);
-      }
+      for (int i = 0; i < 4; ++i) dhs[t & 1][4 * q + i][u] = d[i];
     };
     auto dx_step = [&](int t) {  // dG_t stores and dx_t = dG_t . W_ih from image (t&1) -> masked sc1 stores
       if constexpr (!BOTTOM) {
@@ -1726,68 +1666,76 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] *= ((mreg >> (8 * e)) & 0xFFu) ? keep_scale : 0.f;
         }
-        if (gr) {
-          unsigned long long* g = reinterpret_cast<unsigned long long*>(dXout) + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc;
-          const unsigned tag = base + (unsigned)(T - t);
-          gran_store2(g, o[0], o[1], tag, false);
-          gran_store2(g + 2, o[2], o[3], tag, false);
-        } else {
-          store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
-        }
+        store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
       }
     };
+    // interval I(t) (sets X, Y; they swap every interval -- a loop of exactly two intervals per trip keeps each set
+    // in its registers): DPF 2 stages dH_{t-1} out of X (loaded in I(t+2)) and loads dH_{t-3} into it again; DPF 1
+    // stages dH_{t-1} out of Y (loaded in I(t+1)) and loads dH_{t-2} into X
     if constexpr (!TOP) {
-      load_dh(T - 1);
-      complete_dh(T - 1);
-      stage_dh(T - 1);
-      if (T > 1) load_dh(T - 2);
+      load_dh(T - 1, dA);
+      stage_dh(T - 1, dA);
+      if constexpr (DPF == 2) {
+        if (T > 1) load_dh(T - 2, dA);
+        if (T > 2) load_dh(T - 3, dB);
+      } else {
+        if (T > 1) load_dh(T - 2, dB);
+      }
     }
     __syncthreads();  // B0
     SSTAMP_DECL
-    for (int t = T - 1; t >= 0; --t) {
-      // ---- interval I(t) ----  issue order: [flags, dH loads, keep-byte load, dx store].  The dx product runs
-      // last, while the recurrent waves are in their VALU phase (their dh MFMAs run right after A(t+1); two
-      // MFMA streams on one SIMD serialise, r2 stamp probe), and its store stays in flight across the barrier:
-      // vmcnt(1) waits for this wave's loads of the previous interval and everything older than its dx store.
+    auto interval = [&](int t, float (&X)[4], float (&Y)[4]) {
+      // ---- interval I(t) ----  issue order: [keep-byte load, dH loads, dx store].  The dx product runs last,
+      // while the recurrent waves are in their VALU phase (their dh MFMAs run right after A(t+1); two MFMA streams
+      // on one SIMD serialise, r2 stamp probe), and its store stays in flight across the barrier.
       SSTAMP(0)
-      // the previous interval's dG stores (4 per lane) and dx store stay in flight; every older op (its dH and
-      // keep-byte loads, issued before them) is complete
-      // (granule form: the dx stores need no drain; the dH loads are waited for where complete_dh reads them)
-      if constexpr (BOTTOM) mta_wait_vmem();
-      else if (!gr) mta_wait_vmcnt<1>();
+      // every op older than the previous interval's dx store (DPF 2: its dH loads + dx store) is complete: its keep
+      // word (used now), the dx stores of I(t+2) and earlier (the progress word below)
+      if constexpr (TOP && BOTTOM) mta_wait_vmem();
+      else if constexpr (BOTTOM) mta_wait_vmcnt<DPF == 2 ? 4 : 0>();
+      else if constexpr (TOP) mta_wait_vmcnt<1>();
+      else mta_wait_vmcnt<DPF == 2 ? 5 : 1>();
       mreg = mnext;
       SSTAMP(1)
       // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait at
-      // the top of I(t+1) (which leaves only I(t+2)'s stores in flight), before barrier A(t+1)
-      if (!gr && !BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
+      // the top of I(t+1) (which leaves only I(t+2)'s loads and store in flight), before barrier A(t+1)
+      if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // dG progress: the recurrent waves store dG_{s} in their step s-1 and pass their vmcnt(10) wait at the top of
       // step s-3 only once those stores are complete, before barrier A(s-3): at I(t) (after A(t+1)) every dG_s with
       // s >= t+4 is drained
       if (t + 4 <= T - 1 && wave == NW + 1 && lane == 0)
         __hip_atomic_store(dg_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      load_mask(t);  // for dx_step(t) in I(t-1)
       if constexpr (!TOP) {
-        if (t >= 1) {
-          complete_dh(t - 1);
-          stage_dh(t - 1);
-          if (t >= 2) load_dh(t - 2);
+        if constexpr (DPF == 2) {
+          if (t >= 1) stage_dh(t - 1, X);
+          if (t >= 3) load_dh(t - 3, X);
+        } else {
+          if (t >= 1) stage_dh(t - 1, Y);
+          if (t >= 2) load_dh(t - 2, X);
         }
       }
-      load_mask(t);  // for dx_step(t) in I(t-1)
       SSTAMP(2)
       if (!BOTTOM) __builtin_amdgcn_s_sleep(DX_DELAY);
       if (t + 1 <= T - 1) dx_step(t + 1);
       SSTAMP(3)
       __syncthreads();  // A(t)
       SSTAMP(4)
+    };
+    int t = T - 1;
+    for (; t >= 1; t -= 2) {
+      interval(t, dA, dB);
+      interval(t - 1, dB, dA);
     }
+    if (t == 0) interval(0, dA, dB);
     SSTAMP_FLUSH(1, 1, w == 0)
     mta_wait_vmem();
     mreg = mnext;
     dx_step(0);
     mta_wait_vmem();
     __syncthreads();  // F
-    if (!gr && !BOTTOM && wave == NW && lane == 0)
+    if (!BOTTOM && wave == NW && lane == 0)
       __hip_atomic_store(my_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == NW + 1 && lane == 0)
       __hip_atomic_store(dg_flag, base + (unsigned)T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1967,10 +1915,15 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     if (tile < a.ntiles) {
       const bool top = layer == a.L - 1, bottom = layer == 0;
       auto& sm = *reinterpret_cast<BwdSmem<H, PREC>*>(dyn_lds);
-      if (top && bottom) stack_bwd_body<H, PREC, true, true>(a, layer, tile, sm, base);
-      else if (top) stack_bwd_body<H, PREC, true, false>(a, layer, tile, sm, base);
-      else if (bottom) stack_bwd_body<H, PREC, false, true>(a, layer, tile, sm, base);
-      else stack_bwd_body<H, PREC, false, false>(a, layer, tile, sm, base);
+      if (top && bottom) stack_bwd_body<H, PREC, true, true, 1>(a, layer, tile, sm, base);
+      else if (top) stack_bwd_body<H, PREC, true, false, 1>(a, layer, tile, sm, base);
+      else if (a.L <= 2) {
+        if (bottom) stack_bwd_body<H, PREC, false, true, 1>(a, layer, tile, sm, base);
+        else stack_bwd_body<H, PREC, false, false, 1>(a, layer, tile, sm, base);
+      } else {
+        if (bottom) stack_bwd_body<H, PREC, false, true, 2>(a, layer, tile, sm, base);
+        else stack_bwd_body<H, PREC, false, false, 2>(a, layer, tile, sm, base);
+      }
     }
   } else {
     // fused weight gradient of (layer, time chunk, c' block), top layer and late chunks first (the order
@@ -2163,9 +2116,9 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     if (dropout && l > 0 && !a.mask[l]) return -2;
   }
   a.dh_last = dh_last;
-  // form 0: fp32 dX rows + progress words; 1: dX[l] as (T, Np, H) granules of 8 bytes (A/B, measured slower)
-  if (form < 0 || form > 1) return -1;
-  a.gran = form;
+  // form: the dX hand-off, 0 = fp32 rows + progress words (the tagged-granule form 1 was measured slower at every
+  // depth and removed, profiles/r6_lstm_decoupled.txt)
+  if (form != 0) return -1;
   a.seeds = seeds;
   a.drop_p = drop_p;
   a.dropout = dropout;

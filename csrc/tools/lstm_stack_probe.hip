@@ -84,8 +84,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(seeds, hs.data(), 8 * sizeof(uint64_t), hipMemcpyHostToDevice));
   // decoupled forward (default; DEC=0 in the environment selects the barrier form): (L - 1) x (T, Np, H) granules
   const int dec = getenv("DEC") && atoi(getenv("DEC")) == 0 ? 0 : 1;
-  // backward dX hand-off: 0 fp32 rows + progress words (default), 1 tagged granules (A/B)
-  const int bform = getenv("BFORM") ? atoi(getenv("BFORM")) : 0;
+  const int bform = 0;  // backward dX hand-off: fp32 rows + progress words
   const int bgran = bform == 1;
   const int nowg = getenv("NOWG") && atoi(getenv("NOWG")) == 1;  // 1: no fused weight-gradient workgroups (A/B)
   unsigned long long* gran = nullptr;

@@ -1,5 +1,6 @@
-"""Which part of the decoupled LSTM backward is run-to-run nondeterministic: dG / dX of every layer from the
-recurrence alone (no fused weight gradients), 6 reruns of form 2 (stack_bwd_dec) against form 0 (barrier body).
+"""Run-to-run determinism of the pipelined LSTM backward's recurrence: dG / dX of every layer (no fused weight
+gradients), 6 reruns against the first.
+(r6: this located the decoupled backward's race, profiles/r6_lstm_dec/r6r_bwd_race.txt.)
 Usage: python scripts/debug_bwd_race.py [L] [prec]"""
 import math
 import sys
@@ -48,7 +49,7 @@ def main():
         return dG, dX
 
     ref = bwd(0)
-    for form in (0, 2):
+    for form in (0,):
         for rep in range(6):
             dG, dX = bwd(form)
             msg = []
