@@ -206,6 +206,10 @@ def _stack_flags(C, Np: int, L: int, device, T: int = 60) -> Tensor:
 
 
 _GRAN = {}
+# the decoupled forward wins up to B = 4 windows and loses from B = 8 on (probe, L = 2: N = 200 72.9 vs 81.3 us,
+# 400 73.8 vs 81.1, 800 85.0 vs 83.8, 1,600 102.7 vs 98.3, 6,400 610 vs 447; profiles/r6_lstm_dec/r6w_probe.txt):
+# its input waves' x-image work outweighs the barrier it saves once several tiles share a CU
+DEC_MAX_NP = 512
 
 
 def _stack_gran(C, Np: int, L: int, device, T: int, H: int) -> Optional[Tensor]:
@@ -217,7 +221,7 @@ def _stack_gran(C, Np: int, L: int, device, T: int, H: int) -> Optional[Tensor]:
     older epoch than the one a launch waits for."""
     import os
 
-    if os.environ.get("MTA_LSTM_DEC", "1") == "0":
+    if os.environ.get("MTA_LSTM_DEC", "1") == "0" or Np > DEC_MAX_NP:
         return None
     key = (C.lstm_stack_flag_words(Np), int(Np), int(L), str(device), int(C.lstm_stack_epoch_shift(int(T))), int(T),
            int(H))
