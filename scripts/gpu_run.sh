@@ -35,6 +35,7 @@ for s in "${STEPS[@]}"; do
   kind=${a[0]}
   args=("${a[@]:1}")
   for e in "${envs[@]}"; do export "$e"; done
+  TO=${STEP_TIMEOUT:-300}  # (a step's own STEP_TIMEOUT=... token applies to that step)
   st "step $n: $s"
   case "$kind" in
     pytest) timeout -k 10 "$TO" python -u -m pytest -x -v --timeout 120 --timeout-method thread "${args[@]}" >> "$O/pytest.log" 2>&1 ;;
