@@ -1669,9 +1669,9 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         store_sc1_x4(dXout + ((size_t)t * Np + n0 + ts) * H + 16 * w + tc, o);
       }
     };
-    // interval I(t) (sets X, Y; they swap every interval -- a loop of exactly two intervals per trip keeps each set
-    // in its registers): DPF 2 stages dH_{t-1} out of X (loaded in I(t+2)) and loads dH_{t-3} into it again; DPF 1
-    // stages dH_{t-1} out of Y (loaded in I(t+1)) and loads dH_{t-2} into X
+    // interval I(t) (sets X, Y; DPF 2: they swap every interval -- a loop of exactly two intervals per trip keeps each
+    // set in its registers): DPF 2 stages dH_{t-1} out of X (loaded in I(t+2)) and loads dH_{t-3} into it again;
+    // DPF 1 (X = Y, one set) stages dH_{t-1} (loaded in I(t+1)) and loads dH_{t-2}
     if constexpr (!TOP) {
       load_dh(T - 1, dA);
       stage_dh(T - 1, dA);
@@ -1679,7 +1679,7 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         if (T > 1) load_dh(T - 2, dA);
         if (T > 2) load_dh(T - 3, dB);
       } else {
-        if (T > 1) load_dh(T - 2, dB);
+        if (T > 1) load_dh(T - 2, dA);
       }
     }
     __syncthreads();  // B0
@@ -1723,12 +1723,18 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       __syncthreads();  // A(t)
       SSTAMP(4)
     };
-    int t = T - 1;
-    for (; t >= 1; t -= 2) {
-      interval(t, dA, dB);
-      interval(t - 1, dB, dA);
+    if constexpr (DPF == 2) {
+      int t = T - 1;
+      for (; t >= 1; t -= 2) {
+        interval(t, dA, dB);
+        interval(t - 1, dB, dA);
+      }
+      if (t == 0) interval(0, dA, dB);
+    } else {
+      // one set (staged, then reloaded, in the same interval): no unrolled copy of the interval (the two-interval
+      // loop cost ~2.4 us at L=2, instruction footprint; profiles/r6_lstm_dec/r6x_probe.txt)
+      for (int t = T - 1; t >= 0; --t) interval(t, dA, dA);
     }
-    if (t == 0) interval(0, dA, dB);
     SSTAMP_FLUSH(1, 1, w == 0)
     mta_wait_vmem();
     mreg = mnext;

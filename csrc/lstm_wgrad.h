@@ -186,7 +186,6 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
     return d;
   };
   const int u0 = tid, u1 = tid + THREADS;
-  const Desc d0 = make_desc(u0 < nUnits ? u0 : 0), d1 = make_desc(u1 < nUnits ? u1 : 0);
 
   auto load_unit = [&](const Desc& d, int u, int k0, WgUnit& out) __attribute__((always_inline)) {
     const int r0 = k0 + (u & 3) * 8;
@@ -264,47 +263,8 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
 #pragma unroll
   for (int j = 0; j < MAX_NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  WgUnit st0, st1;
-  const int nsl = (row_end - row_begin + WG_KS - 1) / WG_KS;
-  const int nB = nUnits - nA;
-  // short path: thread t holds A unit t % nA of slice t / nA and B unit t % nB of slice t / nB
-  const bool shortp = nsl <= 4 && nA * nsl <= THREADS && nB * nsl <= THREADS;
-  const int sa = tid / nA, sb = tid / nB;
-  const int ua = tid % nA, ub = nA + tid % nB;
-  bool has0, has1;
-  if (shortp) {
-    has0 = sa < nsl;
-    has1 = sb < nsl;
-    const Desc da = make_desc(ua), db = make_desc(ub);
-    if (has1) load_unit(db, ub, row_begin + sb * WG_KS, st1);
-    wait();
-    if (has0) load_unit(da, ua, row_begin + sa * WG_KS, st0);
-  } else {
-    has0 = u0 < nUnits;
-    has1 = u1 < nUnits;
-    wait();
-    if (has0) load_unit(d0, u0, row_begin, st0);
-    if (has1) load_unit(d1, u1, row_begin, st1);
-  }
-
-  int k0 = row_begin;
-  for (int sl = 0; k0 < row_end; k0 += WG_KS, ++sl) {
-    WG_SLICE_STAMP(sl < 16 ? sl : 15);
-    __syncthreads();  // previous slice's fragment reads are done
-    if (shortp) {
-      if (has0 && sa == sl) store_unit(ua, st0);
-      if (has1 && sb == sl) store_unit(ub, st1);
-    } else {
-      if (has0) store_unit(u0, st0);
-      if (has1) store_unit(u1, st1);
-    }
-    __syncthreads();
-    const int kn = k0 + WG_KS;
-    if (!shortp && kn < row_end) {  // next slice in flight during this slice's MFMAs
-      if (has0) load_unit(d0, u0, kn, st0);
-      if (has1) load_unit(d1, u1, kn, st1);
-    }
-    const int am = wave * 16 + (lane & 15);
+  const int am = wave * 16 + (lane & 15);
+  auto mfma_slice = [&]() __attribute__((always_inline)) {
     if constexpr (PREC == PREC_F32) {
       const float* A = reinterpret_cast<const float*>(imgA);
       const float* B = reinterpret_cast<const float*>(imgB);
@@ -340,6 +300,62 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
         }
       }
     }
+  };
+
+  const int nsl = (row_end - row_begin + WG_KS - 1) / WG_KS;
+  const int nB = nUnits - nA;
+  // short path: thread t holds A unit t % nA of slice t / nA and B unit t % nB of slice t / nB (its own code: with
+  // the pipelined path's descriptors and units live beside its own, the kernel spilled)
+  const bool shortp = nsl <= 4 && nA * nsl <= THREADS && nB * nsl <= THREADS;
+  int ubias;      // this thread's A unit (bias column group) and whether it has one
+  bool hasbias;
+  if (shortp) {
+    const int sa = tid / nA, sb = tid / nB;
+    const int ua = tid % nA, ub = nA + tid % nB;
+    const bool has0 = sa < nsl, has1 = sb < nsl;
+    WgUnit st0, st1;
+    {
+      const Desc db = make_desc(ub);
+      if (has1) load_unit(db, ub, row_begin + sb * WG_KS, st1);
+    }
+    wait();
+    {
+      const Desc da = make_desc(ua);
+      if (has0) load_unit(da, ua, row_begin + sa * WG_KS, st0);
+    }
+    for (int sl = 0; sl < nsl; ++sl) {
+      WG_SLICE_STAMP(sl);
+      __syncthreads();  // previous slice's fragment reads are done
+      if (has0 && sa == sl) store_unit(ua, st0);
+      if (has1 && sb == sl) store_unit(ub, st1);
+      __syncthreads();
+      mfma_slice();
+    }
+    ubias = ua;
+    hasbias = has0;
+  } else {
+    const Desc d0 = make_desc(u0 < nUnits ? u0 : 0), d1 = make_desc(u1 < nUnits ? u1 : 0);
+    const bool has0 = u0 < nUnits, has1 = u1 < nUnits;
+    WgUnit st0, st1;
+    wait();
+    if (has0) load_unit(d0, u0, row_begin, st0);
+    if (has1) load_unit(d1, u1, row_begin, st1);
+    int k0 = row_begin;
+    for (int sl = 0; k0 < row_end; k0 += WG_KS, ++sl) {
+      WG_SLICE_STAMP(sl < 16 ? sl : 15);
+      __syncthreads();  // previous slice's fragment reads are done
+      if (has0) store_unit(u0, st0);
+      if (has1) store_unit(u1, st1);
+      __syncthreads();
+      const int kn = k0 + WG_KS;
+      if (kn < row_end) {  // next slice in flight during this slice's MFMAs
+        if (has0) load_unit(d0, u0, kn, st0);
+        if (has1) load_unit(d1, u1, kn, st1);
+      }
+      mfma_slice();
+    }
+    ubias = u0;
+    hasbias = u0 < nA;
   }
 
   WG_SLICE_STAMP(16);
@@ -368,7 +384,7 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
   WG_SLICE_STAMP(17);
   // bias: reduce the 4 row-group threads of each A column group (lanes t, t^1, t^2, t^3; short path: one sum per
   // slice -- nA is a multiple of 4, so a slice's units stay 4-aligned in the thread index)
-  if (shortp ? has0 : u0 < nA) {
+  if (hasbias) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       float v = bias_acc[c];
@@ -376,7 +392,6 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
       v += __shfl_xor(v, 2, 64);
       bias_acc[c] = v;
     }
-    const int ubias = shortp ? ua : u0;
     if ((ubias & 3) == 0) {
       const int cg = ubias >> 2;
 #pragma unroll
