@@ -40,13 +40,14 @@ sys.path.insert(0, str(REPO))
 
 # vs_baseline: the same-node reference-equivalent PyTorch path at its best -- ``--backend torch`` (nn.LSTM on MIOpen
 # + autograd, heads/loss/optimizer as here) with the whole step captured in a HIP graph, 1 MI355X -- measured by
-# this bench (profiles/r2_bench_same_node_torch_vs_hip.jsonl, hip_graphs=true rows); vs_torch_eager divides by the
-# same path run eagerly (``--no-graphs``).  samples/s per GPU keyed (model, loss, per-GPU batch); weak scaling:
-# the baseline of N GPUs is N x this.
-SAME_NODE_TORCH_GRAPH = {("small", "mse", 1): 508.881, ("medium", "mse", 1): 260.867, ("large", "mse", 1): 132.121,
-                         ("small", "mse", 8): 3090.277, ("small", "mse", 64): 4152.196}
-SAME_NODE_TORCH_EAGER = {("small", "mse", 1): 169.863, ("medium", "mse", 1): 85.333, ("large", "mse", 1): 44.098,
-                         ("small", "mse", 8): 2047.487, ("small", "mse", 64): 4144.375}
+# this bench, re-measured in round 6 (2026-10-18, profiles/r6_bench_same_node_torch.jsonl: lines 1-5 graph-captured,
+# 6-10 ``--no-graphs``; the round-2 figures, profiles/r2_bench_same_node_torch_vs_hip.jsonl, agree to 1-2 %);
+# vs_torch_eager divides by the same path run eagerly.  samples/s per GPU keyed (model, loss, per-GPU batch); weak
+# scaling: the baseline of N GPUs is N x this.
+SAME_NODE_TORCH_GRAPH = {("small", "mse", 1): 515.282, ("medium", "mse", 1): 261.996, ("large", "mse", 1): 132.437,
+                         ("small", "mse", 8): 3152.444, ("small", "mse", 64): 4223.826}
+SAME_NODE_TORCH_EAGER = {("small", "mse", 1): 168.241, ("medium", "mse", 1): 85.289, ("large", "mse", 1): 42.56,
+                         ("small", "mse", 8): 2077.941, ("small", "mse", 64): 4218.843}
 # the 8-vCPU CPU replica of the reference step (BASELINE.md yardstick rows); reported as vs_cpu_yardstick
 YARDSTICK = {("small", "mse", 1): 59.0, ("small", "nll", 1): 58.0, ("small", "combined", 1): 59.0,
              ("medium", "mse", 1): 21.0, ("large", "mse", 1): 14.0, ("small", "mse", 8): 65.0,
