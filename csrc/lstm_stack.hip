@@ -2102,6 +2102,10 @@ extern "C" int mta_lstm_stack_fwd(int H, int prec, int L, int fin, const float* 
 // Np >= 800).  Two parts beat three or more at every measured batch -- more parts mean more partial atomics and
 // more spinning workgroups (profiles/r5_lstm_wgrad_row_split.txt)
 constexpr int WG_FUSED_SPLIT_ROWS = 512;
+// 65-128-row chunks (B = 1: one step of Np = 112 rows) are split in two as well: the chunk of step 0 -- the
+// backward's tail -- is then two 2-slice workgroups instead of one 4-slice one (body 11 -> 7.9 us; L=2 backward
+// 89.3 -> 86.2 us, L=4 129.3 -> 127.5, profiles/r6_lstm_dec/r7a_probe.txt)
+constexpr int WG_SMALL_SPLIT_MIN = 2 * mta_wgrad::WG_KS, WG_SMALL_SPLIT_MAX = 4 * mta_wgrad::WG_KS;
 
 extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* const* stash, const float* const* w_hh,
                                   const float* const* w_ih, const float* dh_last, float* const* dG, float* const* dX,
@@ -2149,7 +2153,8 @@ extern "C" int mta_lstm_stack_bwd(int H, int prec, int L, int fin, const float* 
     // large batches: split a time chunk's rows over two workgroups, so the chunk of the earliest steps
     // (drained last) is not a serial tail of tc * Np rows behind the recurrence
     int rpc = tc * Np;
-    if (!part && rpc > WG_FUSED_SPLIT_ROWS)  // (deterministic mode keeps tc-step chunks: its partials are sized so)
+    if (!part && (rpc > WG_FUSED_SPLIT_ROWS || (rpc > WG_SMALL_SPLIT_MIN && rpc <= WG_SMALL_SPLIT_MAX)))
+      // (deterministic mode keeps tc-step chunks: its partials are sized so)
       rpc = ((rpc + 1) / 2 + mta_wgrad::WG_KS - 1) / mta_wgrad::WG_KS * mta_wgrad::WG_KS;
     for (int l = 0; l < L; ++l) {
       mta_wgrad::WgArgs& w = a.wg[l];
