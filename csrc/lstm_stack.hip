@@ -1698,7 +1698,9 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
       mreg = mnext;
       SSTAMP(1)
       // progress: dx of steps >= t+4 (stored in I(t+3) or earlier) was drained by every gradient wave's wait at
-      // the top of I(t+1) (which leaves only I(t+2)'s loads and store in flight), before barrier A(t+1)
+      // the top of I(t+1) (which leaves only I(t+2)'s loads and store in flight), before barrier A(t+1).  (Publishing
+      // a step earlier from per-wave LDS drain counters + atomic-max progress words was slower at every depth: L=2
+      // 86.3 -> 91.0 us, L=8 192 -> 199, profiles/r6_lstm_dec/r7c_probe.txt)
       if (!BOTTOM && t + 4 <= T - 1 && wave == NW && lane == 0)
         __hip_atomic_store(my_flag, base + (unsigned)(T - t - 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // dG progress: the recurrent waves store dG_{s} in their step s-1 and pass their vmcnt(10) wait at the top of
