@@ -38,7 +38,7 @@ for s in "${STEPS[@]}"; do
   TO=${STEP_TIMEOUT:-300}  # (a step's own STEP_TIMEOUT=... token applies to that step)
   st "step $n: $s"
   case "$kind" in
-    pytest) timeout -k 10 "$TO" python -u -m pytest -x -v --timeout 120 --timeout-method thread "${args[@]}" >> "$O/pytest.log" 2>&1 ;;
+    pytest) timeout -k 10 "$TO" python -u -m pytest -x -v --timeout 300 --timeout-method thread "${args[@]}" >> "$O/pytest.log" 2>&1 ;;
     bench) timeout -k 10 "$TO" python bench.py "${args[@]}" >> "$O/bench.jsonl" 2>> "$O/bench.err" ;;
     prof) tag=${args[0]}
           timeout -k 10 "$TO" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$tag" -o "$tag" -- \
