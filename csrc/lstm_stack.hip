@@ -76,6 +76,10 @@ constexpr int DX_DELAY = 4;
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD: on
 // (fwd 80.0 -> 79.5 us, with DX_DELAY 4 bwd 94.1 us; profiles/r4_lstm_knobs.txt)
 constexpr int STACK_PRIO = 1;
+// diagnostic A/B (probe builds): post a stage slot right after writing it instead of behind the next MFMA chain
+#ifndef STACK_STG_EARLY
+#define STACK_STG_EARLY 0
+#endif
 #if STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
@@ -1375,7 +1379,10 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     }
     SSTAMP(2)
     if constexpr (PREC == PREC_F32) {
-      if (t > 0) stage(t - 1);
+      if (t > 0) {
+        stage(t - 1);
+        if constexpr (STACK_STG_EARLY) sy_post(&sy[SY_STG][w], (unsigned)t);
+      }
       const float* hrow = &sm.h_f[hs][j][q * KF];
 #pragma unroll
       for (int kk = 0; kk < KF; ++kk) {
@@ -1384,7 +1391,10 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
         for (int g = 0; g < 4; ++g) acc[g] = mfma16x16x4f32(av, Bf[g][kk], acc[g]);
       }
     } else {
-      if (t > 0) stage(t - 1);
+      if (t > 0) {
+        stage(t - 1);
+        if constexpr (STACK_STG_EARLY) sy_post(&sy[SY_STG][w], (unsigned)t);
+      }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
@@ -1407,7 +1417,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     }
     // step t-1 staged (posted behind the MFMA chain: its fence then finds the stage writes long complete)
     __builtin_amdgcn_sched_barrier(0);
-    if (t > 0) sy_post(&sy[SY_STG][w], (unsigned)t);
+    if (!STACK_STG_EARLY && t > 0) sy_post(&sy[SY_STG][w], (unsigned)t);
     SSTAMP(3)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

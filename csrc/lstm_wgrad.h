@@ -306,7 +306,8 @@ __device__ __forceinline__ void wgrad_body(const WgArgs& a, const int chunk, con
   const int nB = nUnits - nA;
   // short path: thread t holds A unit t % nA of slice t / nA and B unit t % nB of slice t / nB (its own code: with
   // the pipelined path's descriptors and units live beside its own, the kernel spilled)
-  const bool shortp = nsl <= 4 && nA * nsl <= THREADS && nB * nsl <= THREADS;
+  // (deterministic partials keep the pipelined path: there a slice's bias sum would overwrite another's partial)
+  const bool shortp = !a.part && nsl <= 4 && nA * nsl <= THREADS && nB * nsl <= THREADS;
   int ubias;      // this thread's A unit (bias column group) and whether it has one
   bool hasbias;
   if (shortp) {
