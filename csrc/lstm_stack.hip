@@ -76,10 +76,6 @@ constexpr int DX_DELAY = 4;
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD: on
 // (fwd 80.0 -> 79.5 us, with DX_DELAY 4 bwd 94.1 us; profiles/r4_lstm_knobs.txt)
 constexpr int STACK_PRIO = 1;
-// diagnostic A/B (probe builds): post a stage slot right after writing it instead of behind the next MFMA chain
-#ifndef STACK_STG_EARLY
-#define STACK_STG_EARLY 0
-#endif
 #if STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
@@ -1381,7 +1377,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     if constexpr (PREC == PREC_F32) {
       if (t > 0) {
         stage(t - 1);
-        if constexpr (STACK_STG_EARLY) sy_post(&sy[SY_STG][w], (unsigned)t);
+        sy_post(&sy[SY_STG][w], (unsigned)t);  // (the store waves start on it a whole MFMA chain earlier)
       }
       const float* hrow = &sm.h_f[hs][j][q * KF];
 #pragma unroll
@@ -1393,7 +1389,7 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
     } else {
       if (t > 0) {
         stage(t - 1);
-        if constexpr (STACK_STG_EARLY) sy_post(&sy[SY_STG][w], (unsigned)t);
+        sy_post(&sy[SY_STG][w], (unsigned)t);  // (the store waves start on it a whole MFMA chain earlier)
       }
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb) {
@@ -1415,9 +1411,9 @@ __device__ __forceinline__ void stack_fwd_dec(const StackFwdArgs& a, const int l
         }
       }
     }
-    // step t-1 staged (posted behind the MFMA chain: its fence then finds the stage writes long complete)
+    // (step t-1's stage slot is posted right after it is written, above: posting it behind the MFMA chain cost
+    // 0.3 / 1.0 / 2.0 us at L = 2 / 4 / 8, profiles/r6_lstm_dec/r7d_probe.txt)
     __builtin_amdgcn_sched_barrier(0);
-    if (!STACK_STG_EARLY && t > 0) sy_post(&sy[SY_STG][w], (unsigned)t);
     SSTAMP(3)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
