@@ -72,10 +72,16 @@ __device__ unsigned long long mta_stack_tlw[64][4];
 // SIMD serialise.  4: bwd 98.0 -> 94.5 us at the headline shape; 2: 96, 6: 95.2, 8: 98.2, 12: 104
 // (profiles/r4_lstm_knobs.txt).  The dG rows are stored by the recurrent waves (storing them from the gradient waves
 // measured slower, profiles/r4_lstm_bwd_dg_negative.txt)
-constexpr int DX_DELAY = 4;
+#ifndef DX_DELAY_V  // (diagnostic A/B builds override it)
+#define DX_DELAY_V 4
+#endif
+constexpr int DX_DELAY = DX_DELAY_V;
 // static issue priority of the recurrent waves (fwd and bwd) over the input / gradient waves of their SIMD: on
 // (fwd 80.0 -> 79.5 us, with DX_DELAY 4 bwd 94.1 us; profiles/r4_lstm_knobs.txt)
-constexpr int STACK_PRIO = 1;
+#ifndef STACK_PRIO_V  // (diagnostic A/B builds override it)
+#define STACK_PRIO_V 1
+#endif
+constexpr int STACK_PRIO = STACK_PRIO_V;
 #if STACK_STAMPS
 // Diagnostic build only (csrc/tools/lstm_stack_probe.hip): per-segment s_memtime sums, lane 0 of the first
 // wave of each role of block 0 ([direction][role][segment]; role 0 = recurrent, 1 = input / gradient waves).
