@@ -1949,6 +1949,8 @@ __global__ __launch_bounds__((H / 16) * 128) void lstm_stack_bwd_kernel(StackBwd
     // fused weight gradient of (layer, time chunk, c' block), top layer and late chunks first (the order
     // in which the recurrence drains dG); waits until every tile of the layer has drained the chunk's steps
     const int idx = blockIdx.x - nrec;
+    // layer-major, late chunks first (chunk-major order -- the order chunks become ready -- was slower at every batch
+    // but B=1: B=8 bwd 175 -> 198 us, B=64 1,060 -> 1,203, profiles/r6_lstm_dec/r7g_probe.txt)
     const int layer = a.L - 1 - idx / a.wg_per_layer, rem = idx % a.wg_per_layer;
     const mta_wgrad::WgArgs& w = a.wg[layer];
     const int chunk = w.nchunks - 1 - rem / a.wg_nq, quarter = rem % a.wg_nq;
