@@ -1731,7 +1731,9 @@ __device__ __forceinline__ void stack_bwd_body(const StackBwdArgs& a, const int 
         }
       }
       SSTAMP(2)
-      if (!BOTTOM) __builtin_amdgcn_s_sleep(DX_DELAY);
+      // (stacks of 3+ layers start the dx product at once: L=4 bwd 127.4 -> 123.6 us, L=8 unchanged;
+      // profiles/r6_lstm_dec/r7h_probe.txt)
+      if constexpr (!BOTTOM && DPF == 1) __builtin_amdgcn_s_sleep(DX_DELAY);
       if (t + 1 <= T - 1) dx_step(t + 1);
       SSTAMP(3)
       __syncthreads();  // A(t)
