@@ -21,6 +21,13 @@
 // reads the payload with sc1 loads only.  Stores stay delayed by one step (lstm.hip), so progress is
 // published two steps behind; the consumer keeps a one-step-stale copy of the word so a poll is only
 // paid when it actually waits.  All workgroups (L x tiles <= 8 x 16) are co-resident.
+//
+// Round 6: the forward's default form is stack_fwd_dec (up to 512 padded sequences; ops/lstm.py DEC_MAX_NP): the
+// three wave roles hand LDS ring slots to each other through per-wave step counters instead of one workgroup barrier
+// per step, and the layer hand-off is data-tagged 8-byte granules instead of payload + progress word.  The backward
+// keeps its barrier body (a decoupled backward was slower and not run-to-run stable in bf16; docs/ARCHITECTURE.md),
+// with the gradient waves' dH prefetch distance chosen per depth (stack_bwd_body<..., DPF>) and the fused
+// weight-gradient chunks of one step split over two workgroups at B = 1.
 #include <cstdlib>
 
 #include "common.h"
