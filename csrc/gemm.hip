@@ -1314,13 +1314,24 @@ struct GroupQueue {
   hipStream_t st = nullptr;
 } gq;
 
+// deep-K groups (every problem K >= GROUP_BIG_K: the transformer at B >= 4 windows) run on 128 x 128 tiles: at K =
+// 48,000 (B=8) the 64 x 64 tiles' operand traffic per MFMA bound the two grouped launches (~360 us of a 1.94 ms step)
+constexpr int GROUP_BIG_K = 16384;
+#ifndef GROUP_BIG_TILES  // (diagnostic A/B builds: 0 keeps 64 x 64 tiles at any K)
+#define GROUP_BIG_TILES 1
+#endif
+
 void launch_group(int kind, int first, int count, hipStream_t st) {
   GroupTable t{};
+  int kmin = 1 << 30;
+  for (int q = first; q < first + count; ++q) kmin = std::min(kmin, gq.g[kind][q].K);
+  const bool big = GROUP_BIG_TILES && kmin >= GROUP_BIG_K;
+  const int TB = big ? 128 : 64;
   // one k-chunk for every problem of the launch, sized so that tiles x splits ~ GROUP_WGS
   long work = 0;
   for (int q = first; q < first + count; ++q) {
     const GemmArgs& g = gq.g[kind][q];
-    work += (long)((g.M + 63) / 64) * ((g.N + 63) / 64) * g.K;
+    work += (long)((g.M + TB - 1) / TB) * ((g.N + TB - 1) / TB) * g.K;
   }
   long chunk = (work + GROUP_WGS - 1) / GROUP_WGS;
   chunk = std::max(256L, (chunk + 127) / 128 * 128);
@@ -1333,16 +1344,21 @@ void launch_group(int kind, int first, int count, hipStream_t st) {
     ks = (g.K + kps - 1) / kps;
     g.k_per_split = kps;
     t.g[q] = g;
-    t.nx[q] = (g.N + 63) / 64;
-    t.ny[q] = (g.M + 63) / 64;
+    t.nx[q] = (g.N + TB - 1) / TB;
+    t.ny[q] = (g.M + TB - 1) / TB;
     t.nz[q] = ks;
     t.start[q] = blocks;
     blocks += t.nx[q] * t.ny[q] * ks;
   }
   t.n = count;
   t.start[count] = blocks;
-  if (kind) gemm_group_kernel<64, 64, 128, true><<<blocks, GT, 0, st>>>(t);
-  else gemm_group_kernel<64, 64, 128, false><<<blocks, GT, 0, st>>>(t);
+  if (big) {
+    if (kind) gemm_group_kernel<128, 128, 64, true><<<blocks, GT, 0, st>>>(t);
+    else gemm_group_kernel<128, 128, 64, false><<<blocks, GT, 0, st>>>(t);
+  } else {
+    if (kind) gemm_group_kernel<64, 64, 128, true><<<blocks, GT, 0, st>>>(t);
+    else gemm_group_kernel<64, 64, 128, false><<<blocks, GT, 0, st>>>(t);
+  }
 }
 
 }  // namespace
