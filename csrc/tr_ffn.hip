@@ -106,10 +106,10 @@ struct FfnArgs {
 
 // [features][32] transposed LDS image -> global [features][ldT] at token row0 (16-B pieces; M % 8 == 0)
 template <int NF>
-__device__ __forceinline__ void copy_out_t(const __bf16* img, __bf16* dst, int ldT, int row0, int M) {
+__device__ __forceinline__ void copy_out_t(const __bf16* img, __bf16* dst, int ldT, int row0, int M, int tid) {
 #pragma unroll
   for (int i = 0; i < (NF * 4 + FT - 1) / FT; ++i) {
-    const int idx = threadIdx.x + FT * i, f = idx >> 2, c = idx & 3;
+    const int idx = tid + FT * i, f = idx >> 2, c = idx & 3;
     if (f < NF && row0 + 8 * c < M)
       *reinterpret_cast<uint4*>(dst + (size_t)f * ldT + row0 + 8 * c) = *reinterpret_cast<const uint4*>(img + f * TLD + 8 * c);
   }
@@ -150,33 +150,41 @@ __device__ __forceinline__ bf16x8 afrag(const __bf16* img, int ld, int r0, int k
 
 // [32][width] bf16 LDS image -> global rows row0 .. (16-B pieces, row-contiguous)
 template <int WIDTH, int LD>
-__device__ __forceinline__ void copy_out_bf16(const __bf16* img, __bf16* dst, int row0, int M) {
+__device__ __forceinline__ void copy_out_bf16(const __bf16* img, __bf16* dst, int row0, int M, int tid) {
   constexpr int PER_ROW = WIDTH / 8;
 #pragma unroll
   for (int i = 0; i < FBM * PER_ROW / FT; ++i) {
-    const int idx = threadIdx.x + FT * i, r = idx / PER_ROW, c = idx % PER_ROW;
+    const int idx = tid + FT * i, r = idx / PER_ROW, c = idx % PER_ROW;
     if (row0 + r < M)
       *reinterpret_cast<uint4*>(dst + (size_t)(row0 + r) * WIDTH + 8 * c) =
           *reinterpret_cast<const uint4*>(img + r * LD + 8 * c);
   }
 }
 // [32][128] fp32 LDS image -> global rows
-__device__ __forceinline__ void copy_out_f32(const float* img, float* dst, int row0, int M) {
+__device__ __forceinline__ void copy_out_f32(const float* img, float* dst, int row0, int M, int tid) {
 #pragma unroll
   for (int i = 0; i < FBM * 32 / FT; ++i) {
-    const int idx = threadIdx.x + FT * i, r = idx >> 5, c = idx & 31;
+    const int idx = tid + FT * i, r = idx >> 5, c = idx & 31;
     if (row0 + r < M)
       *reinterpret_cast<float4*>(dst + (size_t)(row0 + r) * FD + 4 * c) =
           *reinterpret_cast<const float4*>(img + r * RLD + 4 * c);
   }
 }
 
+// Both kernels are persistent over 32-row tiles (grid = min(tiles, CUs); each workgroup walks tile, tile + grid, ...):
+// the LDS images allow one 512-thread workgroup per CU, so a one-tile-per-workgroup grid ran B >= 4 windows as
+// serial rounds of load -> compute -> copy out with nothing overlapping them (transformer B=8: 1,500 tiles, ~6
+// rounds).  In the loop a tile's stores drain under the next tile's loads and products; the forward also prefetches
+// the next tile's x1 rows and re-reads each weight-fragment set (L2-resident) for the next tile as soon as this
+// tile's product has consumed it; the backward re-reads its weights with the tile's operands at the tile's start.
+// Register budget: 2 waves per SIMD leave 256 per wave -- weight fragments held across tiles, or the backward's
+// next-tile operands prefetched, spilled.  Every lane-dependent address is re-derived each tile from an opaque copy of
+// the thread index (else the compiler hoists ~100 loop-invariant addresses out of the loop and spills them).
 __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FfnFwdSmem& s = *reinterpret_cast<FfnFwdSmem*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row0 = blockIdx.x * FBM;
-  const int rq = 4 * (lane >> 4), col = lane & 15;
+  const int ntiles = (a.M + FBM - 1) / FBM;
   FSTAMP_RT(0, 10);
   FSTAMP(0, 0);
 
@@ -189,13 +197,15 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     for (int nt = 0; nt < 4; ++nt)
       bw[ks][nt] = bfrag_fm(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
   // x1 rows: 16 threads per row, 8 columns each
-  const int xr = tid >> 4, xc = 8 * (tid & 15);
-  const bool rok = row0 + xr < a.M;
   float4 xv[2];
+  auto load_x = [&](int tile, int t) {
+    const int r = tile * FBM + (t >> 4), xc = 8 * (t & 15);
+    const bool ok = tile < ntiles && r < a.M;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
-                                      : make_float4(1.f, 1.f, 1.f, 1.f);
+    for (int i = 0; i < 2; ++i)
+      xv[i] = ok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)r * FD + xc + 4 * i) : make_float4(1.f, 1.f, 1.f, 1.f);
+  };
+  load_x(blockIdx.x, tid);
   {
     const float v0 = a.b1[tid];
     const float v2 = tid < FD ? a.b2[tid] : 0.f, v3 = tid < FD ? a.g2[tid] : 0.f;
@@ -217,119 +227,140 @@ __global__ __launch_bounds__(FT) void tr_ffn_fwd_kernel(FfnArgs a) {
     dthr = (uint32_t)(a.drop_p * 65536.f + 0.5f);
     dscale = 1.0f / (1.0f - a.drop_p);
   }
-  __syncthreads();  // g2 / biases in LDS
-  FSTAMP(0, 1);
 
-  // ---- RMSNorm2 ----
-  {
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) q += xv[i].x * xv[i].x + xv[i].y * xv[i].y + xv[i].z * xv[i].z + xv[i].w * xv[i].w;
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) q += __shfl_xor(q, off, 64);
-    const float rs = rsqrtf(q * (1.0f / FD) + a.eps);
-    __bf16 yb[8];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float e[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) yb[4 * i + k] = (__bf16)(e[k] * rs * s.g2[xc + 4 * i + k]);
-      *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) = xv[i];
-    }
-    uint4 p0;
-    __builtin_memcpy(&p0, yb, 16);
-    *reinterpret_cast<uint4*>(&s.xn[xr * XLD + xc]) = p0;
-    if (a.xn2T) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s.xnT[(xc + k) * TLD + xr] = yb[k];
-    }
-    if (rok) {
-      if (a.xn2) *reinterpret_cast<uint4*>(a.xn2 + (size_t)(row0 + xr) * FD + xc) = p0;
-      if ((tid & 15) == 0) a.r2[row0 + xr] = rs;
-    }
-  }
-  __syncthreads();  // xn2 image complete
-  FSTAMP(0, 2);
-  if (a.xn2T) copy_out_t<FD>(s.xnT, a.xn2T, a.ldT, row0, a.M);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * FBM;
+    // every lane-dependent address is re-derived from an opaque copy of the thread index each tile: left loop-
+    // invariant, the compiler hoists ~100 of them (64-bit row offsets, LDS offsets, weight-fragment addresses) out
+    // of the tile loop and spills them
+    int tid_l = threadIdx.x;
+    asm volatile("" : "+v"(tid_l));
+    const int tid = tid_l, lane = tid & 63, wave = tid >> 6, xr = tid >> 4, xc = 8 * (tid & 15);
+    const int rq = 4 * (lane >> 4), col = lane & 15;
+    const bool rok = row0 + xr < a.M;
+    __syncthreads();  // g2 / biases in LDS (first tile); the previous tile's x2 image copied out
+    FSTAMP(0, 1);
 
-  // ---- FFN-up: 32 rows x this wave's 64 hidden units, K = 128 ----
-  f32x4 acc[2][4];
+    // ---- RMSNorm2 ----
+    {
+      float q = 0.f;
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+      for (int i = 0; i < 2; ++i) q += xv[i].x * xv[i].x + xv[i].y * xv[i].y + xv[i].z * xv[i].z + xv[i].w * xv[i].w;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int off = 1; off < 16; off <<= 1) q += __shfl_xor(q, off, 64);
+      const float rs = rsqrtf(q * (1.0f / FD) + a.eps);
+      __bf16 yb[8];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const bf16x8 a0 = afrag(s.xn, XLD, 0, 32 * ks, lane), a1 = afrag(s.xn, XLD, 16, 32 * ks, lane);
+      for (int i = 0; i < 2; ++i) {
+        const float e[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
-      acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
-    }
-  }
-  FSTAMP(0, 3);
-  // bias, GELU, dropout (one hash per pair of rows) -> u and pre images
-#pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int j = 64 * wave + 16 * nt + col;
-      const float bias = s.b1[j];
-      uint32_t hp[2] = {0u, 0u};
-      if (a.seed) {
-        const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
-        hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
-        hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
+        for (int k = 0; k < 4; ++k) yb[4 * i + k] = (__bf16)(e[k] * rs * s.g2[xc + 4 * i + k]);
+        *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) = xv[i];
       }
-      bf16x4 ut;
+      uint4 p0;
+      __builtin_memcpy(&p0, yb, 16);
+      *reinterpret_cast<uint4*>(&s.xn[xr * XLD + xc]) = p0;
+      if (a.xn2T) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lr = 16 * mt + rq + r;
-        const float v = acc[mt][nt][r] + bias;
-        float g = mta_gelu(v);
-        if (a.seed) {
-          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
-          g *= u16 >= dthr ? dscale : 0.f;
-        }
-        s.pre[lr * ULD + j] = (__bf16)v;
-        s.u[lr * ULD + j] = (__bf16)g;
-        ut[r] = (__bf16)g;
+        for (int k = 0; k < 8; ++k) s.xnT[(xc + k) * TLD + xr] = yb[k];
       }
-      // four consecutive token rows of hidden unit j: one 8-byte write of the transposed image
-      if (a.uT) *reinterpret_cast<bf16x4*>(&s.uT[j * TLD + 16 * mt + rq]) = ut;
+      if (rok) {
+        if (a.xn2) *reinterpret_cast<uint4*>(a.xn2 + (size_t)(row0 + xr) * FD + xc) = p0;
+        if ((tid & 15) == 0) a.r2[row0 + xr] = rs;
+      }
     }
-  __syncthreads();  // u / pre complete
-  FSTAMP(0, 4);
-  copy_out_bf16<FF, ULD>(s.pre, a.pre, row0, a.M);
-  if (a.u) copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M);
-  if (a.uT) copy_out_t<FF>(s.uT, a.uT, a.ldT, row0, a.M);
+    load_x(tile + gridDim.x, tid);  // the next tile's rows fly under this tile's products
+    __syncthreads();           // xn2 image complete
+    FSTAMP(0, 2);
+    if (a.xn2T) copy_out_t<FD>(s.xnT, a.xn2T, a.ldT, row0, a.M, tid);
 
-  FSTAMP(0, 5);
-  // ---- FFN-down: 32 rows x this wave's 16 output features, K = 512 ----
-  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const bf16x8 a0 = afrag(s.u, ULD, 0, 32 * ks, lane), a1 = afrag(s.u, ULD, 16, 32 * ks, lane);
-    o[0] = mfma16x16x32(a0, bd[ks], o[0]);
-    o[1] = mfma16x16x32(a1, bd[ks], o[1]);
-  }
-  FSTAMP(0, 6);
-  // x2 = x1 + o + b2 into the x image (each wave its own 16 columns: no cross-wave hazard)
-  {
-    const int n = 16 * wave + col;
-    const float bias = s.b2[n];
+    // ---- FFN-up: 32 rows x this wave's 64 hidden units, K = 128 ----
+    f32x4 acc[2][4];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lr = 16 * mt + rq + r;
-        s.x[lr * RLD + n] = (o[mt][r] + bias) + s.x[lr * RLD + n];
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a0 = afrag(s.xn, XLD, 0, 32 * ks, lane), a1 = afrag(s.xn, XLD, 16, 32 * ks, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
+        acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
       }
+    }
+    // the next tile's FFN-up fragments (L2-resident; re-read unconditionally, a branch here made the compiler keep
+    // both copies live) fly under this tile's epilogue and FFN-down
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag_fm(a.w1, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+    FSTAMP(0, 3);
+    // bias, GELU, dropout (one hash per pair of rows) -> u and pre images
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int j = 64 * wave + 16 * nt + col;
+        const float bias = s.b1[j];
+        uint32_t hp[2] = {0u, 0u};
+        if (a.seed) {
+          const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
+          hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
+          hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
+        }
+        bf16x4 ut;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * mt + rq + r;
+          const float v = acc[mt][nt][r] + bias;
+          float g = mta_gelu(v);
+          if (a.seed) {
+            const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+            g *= u16 >= dthr ? dscale : 0.f;
+          }
+          s.pre[lr * ULD + j] = (__bf16)v;
+          s.u[lr * ULD + j] = (__bf16)g;
+          ut[r] = (__bf16)g;
+        }
+        // four consecutive token rows of hidden unit j: one 8-byte write of the transposed image
+        if (a.uT) *reinterpret_cast<bf16x4*>(&s.uT[j * TLD + 16 * mt + rq]) = ut;
+      }
+    __syncthreads();  // u / pre complete
+    FSTAMP(0, 4);
+    copy_out_bf16<FF, ULD>(s.pre, a.pre, row0, a.M, tid);
+    if (a.u) copy_out_bf16<FF, ULD>(s.u, a.u, row0, a.M, tid);
+    if (a.uT) copy_out_t<FF>(s.uT, a.uT, a.ldT, row0, a.M, tid);
+
+    FSTAMP(0, 5);
+    // ---- FFN-down: 32 rows x this wave's 16 output features, K = 512 ----
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const bf16x8 a0 = afrag(s.u, ULD, 0, 32 * ks, lane), a1 = afrag(s.u, ULD, 16, 32 * ks, lane);
+      o[0] = mfma16x16x32(a0, bd[ks], o[0]);
+      o[1] = mfma16x16x32(a1, bd[ks], o[1]);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag_fm(a.w2, FF, 16 * wave, 32 * ks, lane);
+    FSTAMP(0, 6);
+    // x2 = x1 + o + b2 into the x image (each wave its own 16 columns: no cross-wave hazard)
+    {
+      const int n = 16 * wave + col;
+      const float bias = s.b2[n];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * mt + rq + r;
+          s.x[lr * RLD + n] = (o[mt][r] + bias) + s.x[lr * RLD + n];
+        }
+    }
+    __syncthreads();
+    FSTAMP(0, 7);
+    copy_out_f32(s.x, a.x2, row0, a.M, tid);
+    FSTAMP(0, 8);
   }
-  __syncthreads();
-  FSTAMP(0, 7);
-  copy_out_f32(s.x, a.x2, row0, a.M);
-  FSTAMP(0, 8);
   FSTAMP_RT(0, 11);
 }
 
@@ -337,53 +368,28 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   FfnBwdSmem& s = *reinterpret_cast<FfnBwdSmem*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row0 = blockIdx.x * FBM;
-  const int rq = 4 * (lane >> 4), col = lane & 15;
+  const int ntiles = (a.M + FBM - 1) / FBM;
   FSTAMP_RT(1, 10);
   FSTAMP(1, 0);
 
-  // ---- loads: du = dX W2 B fragments (W2^T [512][128]: this wave's 64 hidden units, 4 k-steps); dX (bf16) and
-  // the pre-activation tile into LDS (16-B pieces); x1 and dX rows (fp32, 16 threads per row); r2; g2 ----
-  bf16x8 bw[4][4];
+  // ---- per tile, at its start: the weight fragments, dX (bf16) and the pre-activation tile for LDS, r2, x1 and dX
+  // rows (fp32, 16 threads per row: first used at the tile's end) ----
+  constexpr int PRE_PIECES = FBM * (FF / 8) / FT;
+  uint4 dxp, prep[PRE_PIECES];
+  float rp = 0.f;
+  auto load_tile = [&](int tile, int tid) {  // the LDS operands of a tile: dX (bf16), the pre-activation tile, r2
+    const int row0 = tile * FBM, xr = tid >> 4, xc = 8 * (tid & 15);
+    const bool ok = row0 + xr < a.M;
+    dxp = ok ? *reinterpret_cast<const uint4*>(a.dxb + (size_t)(row0 + xr) * FD + xc) : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag_fm(a.w2, FD, 64 * wave + 16 * nt, 32 * ks, lane);
-  const int xr = tid >> 4, xc = 8 * (tid & 15);
-  const bool rok = row0 + xr < a.M;
-  {
-    const uint4 d0 = rok ? *reinterpret_cast<const uint4*>(a.dxb + (size_t)(row0 + xr) * FD + xc)
-                         : make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(&s.dx[xr * XLD + xc]) = d0;
-    if (a.dxT) {
-      __bf16 e8[8];
-      __builtin_memcpy(e8, &d0, 16);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) s.dxT[(xc + k) * TLD + xr] = e8[k];
+    for (int i = 0; i < PRE_PIECES; ++i) {
+      const int idx = tid + FT * i, r = idx / (FF / 8), c = idx % (FF / 8);
+      prep[i] = row0 + r < a.M ? *reinterpret_cast<const uint4*>(a.prein + (size_t)(row0 + r) * FF + 8 * c)
+                               : make_uint4(0u, 0u, 0u, 0u);
     }
-  }
-  // pre tile [32][512] -> the dpre image (the epilogue reads pre and writes dpre at the same element, same lane)
-#pragma unroll
-  for (int i = 0; i < FBM * (FF / 8) / FT; ++i) {
-    const int idx = tid + FT * i, r = idx / (FF / 8), c = idx % (FF / 8);
-    const uint4 v = row0 + r < a.M ? *reinterpret_cast<const uint4*>(a.prein + (size_t)(row0 + r) * FF + 8 * c)
-                                   : make_uint4(0u, 0u, 0u, 0u);
-    *reinterpret_cast<uint4*>(&s.dpre[r * ULD + 8 * c]) = v;
-  }
-  float4 xv[2], gv[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    xv[i] = rok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
-    gv[i] = rok ? *reinterpret_cast<const float4*>(a.dx + (size_t)(row0 + xr) * FD + xc + 4 * i)
-                : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
+    if (tid < FBM) rp = row0 + tid < a.M ? a.r2in[row0 + tid] : 0.f;
+  };
   if (tid < FD) s.g2[tid] = a.g2[tid];
-  if (tid < FBM) s.r[tid] = row0 + tid < a.M ? a.r2in[row0 + tid] : 0.f;
-  // dxn2 = dpre W1 B fragments (W1^T [128][512]: this wave's 16 features, 16 k-steps)
-  bf16x8 bd[16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag_fm(a.w1, FF, 16 * wave, 32 * ks, lane);
   uint32_t dseed = 0, dthr = 0;
   float dscale = 1.f;
   if (a.seed) {
@@ -392,134 +398,186 @@ __global__ __launch_bounds__(FT) void tr_ffn_bwd_kernel(FfnArgs a) {
     dthr = (uint32_t)(a.drop_p * 65536.f + 0.5f);
     dscale = 1.0f / (1.0f - a.drop_p);
   }
-  __syncthreads();  // dX image, pre tile, g2, r2
-  FSTAMP(1, 1);
+  float dg2_acc = 0.f;  // this workgroup's dg2 column sums over its tiles (tid < FD), one atomic at the end
 
-  // ---- du = dX W2: 32 rows x this wave's 64 hidden units, K = 128 ----
-  f32x4 acc[2][4];
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * FBM;
+    // every lane-dependent address is re-derived from an opaque copy of the thread index each tile: left loop-
+    // invariant, the compiler hoists ~100 of them (64-bit row offsets, LDS offsets, weight-fragment addresses) out
+    // of the tile loop and spills them
+    int tid_l = threadIdx.x;
+    asm volatile("" : "+v"(tid_l));
+    const int tid = tid_l, lane = tid & 63, wave = tid >> 6, xr = tid >> 4, xc = 8 * (tid & 15);
+    const int rq = 4 * (lane >> 4), col = lane & 15;
+    const bool rok = row0 + xr < a.M;
+    // du = dX W2 B fragments (W2^T [512][128]: this wave's 64 hidden units, 4 k-steps) and dxn2 = dpre W1 B fragments
+    // (W1^T [128][512]: this wave's 16 features, 16 k-steps), re-read from L2 every tile with the tile's operands
+    // (held across tiles, or re-read early, they spill: 2 waves per SIMD leave 256 registers)
+    bf16x8 bw[4][4];
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int nt = 0; nt < 4; ++nt) bw[ks][nt] = bfrag_fm(a.w2, FD, 64 * wave + 16 * nt, 32 * ks, lane);
+    load_tile(tile, tid);
+    bf16x8 bd[16];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const bf16x8 a0 = afrag(s.dx, XLD, 0, 32 * ks, lane), a1 = afrag(s.dx, XLD, 16, 32 * ks, lane);
+    for (int ks = 0; ks < 16; ++ks) bd[ks] = bfrag_fm(a.w1, FF, 16 * wave, 32 * ks, lane);
+    // this tile -> LDS (every reader of these images in the previous tile is behind its dxn2 barrier)
+    *reinterpret_cast<uint4*>(&s.dx[xr * XLD + xc]) = dxp;
+    if (a.dxT) {
+      __bf16 e8[8];
+      __builtin_memcpy(e8, &dxp, 16);
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
-      acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
+      for (int k = 0; k < 8; ++k) s.dxT[(xc + k) * TLD + xr] = e8[k];
     }
-  }
-  FSTAMP(1, 2);
-  // dpre = du * keep / (1 - p) * gelu'(pre), in place over the pre tile
+    // pre tile [32][512] -> the dpre image (the epilogue reads pre and writes dpre at the same element, same lane)
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+    for (int i = 0; i < PRE_PIECES; ++i) {
+      const int idx = tid + FT * i, r = idx / (FF / 8), c = idx % (FF / 8);
+      *reinterpret_cast<uint4*>(&s.dpre[r * ULD + 8 * c]) = prep[i];
+    }
+    if (tid < FBM) s.r[tid] = rp;
+    float4 xt[2], gt[2];
+    {
+      const bool ok = row0 + xr < a.M;
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int j = 64 * wave + 16 * nt + col;
-      uint32_t hp[2] = {0u, 0u};
-      if (a.seed) {
-        const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
-        hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
-        hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
+      for (int i = 0; i < 2; ++i) {
+        xt[i] = ok ? *reinterpret_cast<const float4*>(a.x1 + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        gt[i] = ok ? *reinterpret_cast<const float4*>(a.dx + (size_t)(row0 + xr) * FD + xc + 4 * i)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      bf16x4 dt;
+    }
+    __syncthreads();  // dX image, pre tile, g2, r2
+    FSTAMP(1, 1);
+
+    // ---- du = dX W2: 32 rows x this wave's 64 hidden units, K = 128 ----
+    f32x4 acc[2][4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int lr = 16 * mt + rq + r;
-        float v = acc[mt][nt][r];
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 a0 = afrag(s.dx, XLD, 0, 32 * ks, lane), a1 = afrag(s.dx, XLD, 16, 32 * ks, lane);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        acc[0][nt] = mfma16x16x32(a0, bw[ks][nt], acc[0][nt]);
+        acc[1][nt] = mfma16x16x32(a1, bw[ks][nt], acc[1][nt]);
+      }
+    }
+    FSTAMP(1, 2);
+    // dpre = du * keep / (1 - p) * gelu'(pre), in place over the pre tile
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const int j = 64 * wave + 16 * nt + col;
+        uint32_t hp[2] = {0u, 0u};
         if (a.seed) {
-          const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
-          v *= u16 >= dthr ? dscale : 0.f;
+          const uint32_t mp = (uint32_t)(row0 + 16 * mt + rq) >> 1;
+          hp[0] = ffn_pair_hash(dseed, mp, (uint32_t)j);
+          hp[1] = ffn_pair_hash(dseed, mp + 1, (uint32_t)j);
         }
-        v *= mta_gelu_grad((float)s.dpre[lr * ULD + j]);
-        s.dpre[lr * ULD + j] = (__bf16)v;
-        dt[r] = (__bf16)v;
+        bf16x4 dt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int lr = 16 * mt + rq + r;
+          float v = acc[mt][nt][r];
+          if (a.seed) {
+            const uint32_t u16 = (r & 1) ? (hp[r >> 1] >> 16) : (hp[r >> 1] & 0xFFFFu);
+            v *= u16 >= dthr ? dscale : 0.f;
+          }
+          v *= mta_gelu_grad((float)s.dpre[lr * ULD + j]);
+          s.dpre[lr * ULD + j] = (__bf16)v;
+          dt[r] = (__bf16)v;
+        }
+        if (a.dpreT) *reinterpret_cast<bf16x4*>(&s.dpreT[j * TLD + 16 * mt + rq]) = dt;
       }
-      if (a.dpreT) *reinterpret_cast<bf16x4*>(&s.dpreT[j * TLD + 16 * mt + rq]) = dt;
-    }
-  __syncthreads();  // dpre image complete
-  FSTAMP(1, 3);
-  if (a.dpre) copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M);
-  if (a.dpreT) copy_out_t<FF>(s.dpreT, a.dpreT, a.ldT, row0, a.M);
-  if (a.dxT) copy_out_t<FD>(s.dxT, a.dxT, a.ldT, row0, a.M);
+    __syncthreads();  // dpre image complete
+    FSTAMP(1, 3);
+    if (a.dpre) copy_out_bf16<FF, ULD>(s.dpre, a.dpre, row0, a.M, tid);
+    if (a.dpreT) copy_out_t<FF>(s.dpreT, a.dpreT, a.ldT, row0, a.M, tid);
+    if (a.dxT) copy_out_t<FD>(s.dxT, a.dxT, a.ldT, row0, a.M, tid);
 
-  FSTAMP(1, 4);
-  // ---- dxn2 = dpre W1: 32 rows x this wave's 16 features, K = 512 ----
-  f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+    FSTAMP(1, 4);
+    // ---- dxn2 = dpre W1: 32 rows x this wave's 16 features, K = 512 ----
+    f32x4 o[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    const bf16x8 a0 = afrag(s.dpre, ULD, 0, 32 * ks, lane), a1 = afrag(s.dpre, ULD, 16, 32 * ks, lane);
-    o[0] = mfma16x16x32(a0, bd[ks], o[0]);
-    o[1] = mfma16x16x32(a1, bd[ks], o[1]);
-  }
+    for (int ks = 0; ks < 16; ++ks) {
+      const bf16x8 a0 = afrag(s.dpre, ULD, 0, 32 * ks, lane), a1 = afrag(s.dpre, ULD, 16, 32 * ks, lane);
+      o[0] = mfma16x16x32(a0, bd[ks], o[0]);
+      o[1] = mfma16x16x32(a1, bd[ks], o[1]);
+    }
 #pragma unroll
-  for (int mt = 0; mt < 2; ++mt)
+    for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s.g[(16 * mt + rq + r) * RLD + 16 * wave + col] = o[mt][r];
-  __syncthreads();  // dxn2 rows complete
-  FSTAMP(1, 5);
+      for (int r = 0; r < 4; ++r) s.g[(16 * mt + rq + r) * RLD + 16 * wave + col] = o[mt][r];
+    __syncthreads();  // dxn2 rows complete
+    FSTAMP(1, 5);
 
-  // ---- RMSNorm2 backward + residual, 16 threads per row:
-  //   dx1 = dX + r (g2 dy) - x r^3 / d * sum(g2 dy x);  dg2 += dy x r ----
-  {
-    const float r = s.r[xr];
-    float dyv[8], xe[8];
-    float dot = 0.f;
+    // ---- RMSNorm2 backward + residual, 16 threads per row:
+    //   dx1 = dX + r (g2 dy) - x r^3 / d * sum(g2 dy x);  dg2 += dy x r ----
+    {
+      const float r = s.r[xr];
+      float dyv[8], xe[8];
+      float dot = 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float4 dy4 = *reinterpret_cast<const float4*>(&s.g[xr * RLD + xc + 4 * i]);
-      const float e[4] = {dy4.x, dy4.y, dy4.z, dy4.w};
-      const float xx[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
+      for (int i = 0; i < 2; ++i) {
+        const float4 dy4 = *reinterpret_cast<const float4*>(&s.g[xr * RLD + xc + 4 * i]);
+        const float e[4] = {dy4.x, dy4.y, dy4.z, dy4.w};
+        const float xx[4] = {xt[i].x, xt[i].y, xt[i].z, xt[i].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        dyv[4 * i + k] = e[k];
-        xe[4 * i + k] = xx[k];
-        dot = fmaf(s.g2[xc + 4 * i + k] * e[k], xx[k], dot);
+        for (int k = 0; k < 4; ++k) {
+          dyv[4 * i + k] = e[k];
+          xe[4 * i + k] = xx[k];
+          dot = fmaf(s.g2[xc + 4 * i + k] * e[k], xx[k], dot);
+        }
       }
-    }
 #pragma unroll
-    for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
-    const float c = dot * r * r * r * (1.0f / FD);
-    float out[8];
-    __bf16 ob[8];
+      for (int off = 1; off < 16; off <<= 1) dot += __shfl_xor(dot, off, 64);
+      const float c = dot * r * r * r * (1.0f / FD);
+      float out[8];
+      __bf16 ob[8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float gd[4] = {gv[i].x, gv[i].y, gv[i].z, gv[i].w};
+      for (int i = 0; i < 2; ++i) {
+        const float gd[4] = {gt[i].x, gt[i].y, gt[i].z, gt[i].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = 4 * i + k;
-        out[e] = gd[k] + (r * s.g2[xc + e] * dyv[e] - xe[e] * c);
-        ob[e] = (__bf16)out[e];
+        for (int k = 0; k < 4; ++k) {
+          const int e = 4 * i + k;
+          out[e] = gd[k] + (r * s.g2[xc + e] * dyv[e] - xe[e] * c);
+          ob[e] = (__bf16)out[e];
+        }
       }
-    }
-    __syncthreads();  // every row's dy read before the image is reused for dX1
+      __syncthreads();  // every row's dy read before the image is reused for dX1
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<float4*>(&s.g[xr * RLD + xc + 4 * i]) =
-          make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
-    if (rok) {
-      uint4 p0;
-      __builtin_memcpy(&p0, ob, 16);
-      *reinterpret_cast<uint4*>(a.dx1b + (size_t)(row0 + xr) * FD + xc) = p0;
-    }
-    // dg2: per-element dy x r into the x image (x is in registers), column sums after the barrier
+      for (int i = 0; i < 2; ++i)
+        *reinterpret_cast<float4*>(&s.g[xr * RLD + xc + 4 * i]) =
+            make_float4(out[4 * i], out[4 * i + 1], out[4 * i + 2], out[4 * i + 3]);
+      if (rok) {
+        uint4 p0;
+        __builtin_memcpy(&p0, ob, 16);
+        *reinterpret_cast<uint4*>(a.dx1b + (size_t)(row0 + xr) * FD + xc) = p0;
+      }
+      // dg2: per-element dy x r into the x image (x is in registers), column sums after the barrier
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) =
-          make_float4(dyv[4 * i] * xe[4 * i] * r, dyv[4 * i + 1] * xe[4 * i + 1] * r,
-                      dyv[4 * i + 2] * xe[4 * i + 2] * r, dyv[4 * i + 3] * xe[4 * i + 3] * r);
-  }
-  __syncthreads();
-  FSTAMP(1, 6);
-  copy_out_f32(s.g, a.dx1, row0, a.M);
-  if (tid < FD) {
-    float cs = 0.f;
+      for (int i = 0; i < 2; ++i)
+        *reinterpret_cast<float4*>(&s.x[xr * RLD + xc + 4 * i]) =
+            make_float4(dyv[4 * i] * xe[4 * i] * r, dyv[4 * i + 1] * xe[4 * i + 1] * r,
+                        dyv[4 * i + 2] * xe[4 * i + 2] * r, dyv[4 * i + 3] * xe[4 * i + 3] * r);
+    }
+    __syncthreads();
+    FSTAMP(1, 6);
+    copy_out_f32(s.g, a.dx1, row0, a.M, tid);
+    if (tid < FD) {
+      float cs = 0.f;
 #pragma unroll 8
-    for (int rr = 0; rr < FBM; ++rr) cs += s.x[rr * RLD + tid];
-    atomicAdd(a.dg2 + tid, cs);
+      for (int rr = 0; rr < FBM; ++rr) cs += s.x[rr * RLD + tid];
+      dg2_acc += cs;
+    }
+    FSTAMP(1, 7);
   }
-  FSTAMP(1, 7);
+  if (tid < FD && blockIdx.x < ntiles) atomicAdd(a.dg2 + tid, dg2_acc);
   FSTAMP_RT(1, 11);
 }
 
@@ -561,7 +619,14 @@ extern "C" int mta_tr_ffn(int backward, int M, int d, int dff, float eps, const 
   a.dpreT = static_cast<__bf16*>(dpreT);
   a.dxT = static_cast<__bf16*>(dxT);
   a.ldT = M;
-  const int grid = (M + FBM - 1) / FBM;
+  // persistent: one workgroup per CU (the LDS images allow no more), each walking tiles blockIdx.x + k * grid
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int grid = std::min((M + FBM - 1) / FBM, n_cu);
   if (!backward) {
     static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&tr_ffn_fwd_kernel),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,

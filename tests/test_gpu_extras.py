@@ -428,12 +428,14 @@ def test_tr_attn_dx_matches_reference(M):
     assert _rel(dg - 0.5, gr.grad) < 1e-4
 
 
-@pytest.mark.parametrize("dropout,N,T", [(0.0, 100, 60), (0.2, 37, 60), (0.0, 20, 33)])
+@pytest.mark.parametrize("dropout,N,T", [(0.0, 100, 60), (0.2, 37, 60), (0.0, 20, 33), (0.2, 305, 33), (0.0, 600, 33)])
 def test_fused_transformer_ffn_matches_unfused(dropout, N, T):
     """csrc/tr_ffn.hip (the FFN half of every block in one launch forward and one backward, plus split-K weight
     gradients) and csrc/tr_attn.hip (the attention half forward in one launch) against the unfused kernel chain on the
     same inputs, seeds and weights: encoder output and every parameter gradient, plus the fp32 PyTorch reference
-    without dropout.  N = 37: M = 40 x 60 rows, a partial 32-row workgroup at the end; T = 33: padded key masking."""
+    without dropout.  N = 37: M = 40 x 60 rows, a partial 32-row workgroup at the end; T = 33: padded key masking.
+    N = 305 / 600 at T = 33: more 32-row tiles than CUs (the persistent FFN kernels walk 2-3 tiles per workgroup, the
+    last one partial) and, at 600, weight-gradient K >= 16,384 (the grouped launches on 128 x 128 tiles)."""
     from masters_thesis_amd.models.extras import FinancialTransformerMse
     from masters_thesis_amd.ops import extras as X
 
