@@ -329,7 +329,7 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
 // ---- backward tail of the attention half: d(xn) = dqkv Wqkv, then RMSNorm1 backward + residual ----
 // dX = dX1 + rs (g1 o dxn - xhat mean(g1 o dxn o xhat)), xhat = x rs; dg1 += sum over rows of dxn o xhat.  The
 // unfused chain was the input-gradient GEMM (6272 x 128 x 384, ~8.5 us) and the one-wave-per-row norm backward
-// (~5.7 us).  One 512-thread workgroup per 64-row tile (grid-strided): the dqkv tile, x and dX1 rows are staged
+// (~5.7 us).  One 512-thread workgroup per CU walking 32-row tiles, the next tile prefetched into registers: the dqkv tile, x and dX1 rows are staged
 // through LDS by 16-B loads; wave w owns output features 16 w .. 16 w + 15 (Wqkv^T B fragments in registers from a
 // fragment-major image, K = 384); the row statistic crosses the 8 waves once through LDS; dX leaves row-contiguous
 // (fp32 and bf16); the dg1 partial row of each workgroup goes to a deferred norm slot (block-ordered sums).
@@ -370,29 +370,47 @@ __global__ __launch_bounds__(ATH) void tr_attn_dx_kernel(AttnDxArgs a) {
   const float gc = a.g1[c];
   float dg = 0.f;  // this lane's share of dg1[c] (rows 4 (lane >> 4) + r of every tile)
   const int ntiles = (a.M + DXR - 1) / DXR;
+  // a tile's operands are fetched into registers one tile ahead (its dqkv rows, x and dX1 rows, rstd) and written to
+  // the LDS images at the tile's start: the loads of tile i + 1 fly under tile i's product and norm backward
+  constexpr int NQ = DXR * (AQ / 8) / ATH, NX = DXR * (AD / 4) / ATH;
+  uint4 pq[NQ];
+  float4 px[NX], pd[NX];
+  float prs = 0.f;
+  auto fetch = [&](int tile) {
+    const size_t row0 = (size_t)tile * DXR;
+    const bool live = tile < ntiles;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
+      pq[i] = live && row0 + r < (size_t)a.M ? *reinterpret_cast<const uint4*>(a.dqkv + (row0 + r) * AQ + 8 * c8)
+                                             : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
+      const bool ok = live && row0 + r < (size_t)a.M;
+      px[i] = ok ? *reinterpret_cast<const float4*>(a.x + (row0 + r) * AD + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      pd[i] = ok ? *reinterpret_cast<const float4*>(a.dx1 + (row0 + r) * AD + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (tid < DXR) prs = live && row0 + tid < (size_t)a.M ? a.r1[row0 + tid] : 0.f;
+  };
+  fetch(blockIdx.x);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const size_t row0 = (size_t)tile * DXR;
-    // stage: dqkv [64][384] bf16 (3,072 16-B pieces), x and dX1 [64][128] fp32 (2,048 16-B pieces each)
 #pragma unroll
-    for (int i = 0; i < DXR * (AQ / 8) / ATH; ++i) {
+    for (int i = 0; i < NQ; ++i) {
       const int idx = tid + ATH * i, r = idx / (AQ / 8), c8 = idx % (AQ / 8);
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (row0 + r < (size_t)a.M) v = *reinterpret_cast<const uint4*>(a.dqkv + (row0 + r) * AQ + 8 * c8);
-      *reinterpret_cast<uint4*>(&s.dq[r * DQLD + 8 * c8]) = v;
+      *reinterpret_cast<uint4*>(&s.dq[r * DQLD + 8 * c8]) = pq[i];
     }
 #pragma unroll
-    for (int i = 0; i < DXR * (AD / 4) / ATH; ++i) {
+    for (int i = 0; i < NX; ++i) {
       const int idx = tid + ATH * i, r = idx / (AD / 4), c4 = idx % (AD / 4);
-      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), dv = xv;
-      if (row0 + r < (size_t)a.M) {
-        xv = *reinterpret_cast<const float4*>(a.x + (row0 + r) * AD + 4 * c4);
-        dv = *reinterpret_cast<const float4*>(a.dx1 + (row0 + r) * AD + 4 * c4);
-      }
-      *reinterpret_cast<float4*>(&s.x[r * XRLD + 4 * c4]) = xv;
-      *reinterpret_cast<float4*>(&s.dr[r * XRLD + 4 * c4]) = dv;
+      *reinterpret_cast<float4*>(&s.x[r * XRLD + 4 * c4]) = px[i];
+      *reinterpret_cast<float4*>(&s.dr[r * XRLD + 4 * c4]) = pd[i];
     }
-    if (tid < DXR) s.rs[tid] = row0 + tid < (size_t)a.M ? a.r1[row0 + tid] : 0.f;
+    if (tid < DXR) s.rs[tid] = prs;
     __syncthreads();
+    fetch(tile + gridDim.x);
     // dxn tile: 32 rows x this wave's 16 features, K = 384
     constexpr int MT = DXR / 16;
     f32x4 acc[MT];
@@ -510,8 +528,16 @@ extern "C" int mta_tr_attn_dx(int M, const void* dqkv, const void* wqkvt, const 
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                (int)sizeof(AttnDxSmem)) == hipSuccess;
   if (!attr) return 2;
+  // one workgroup per CU is resident (~150 VGPRs at 8 waves: 2 waves per SIMD): a grid of exactly that walks the
+  // tiles with the next tile's operands in flight (the old 1,024-workgroup grid ran B=8 as 4 rounds of 1-2 tiles)
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
   const int tiles = (M + DXR - 1) / DXR;
-  const int grid = tiles < 1024 ? tiles : 1024;
+  const int grid = tiles < n_cu ? tiles : n_cu;
   AttnDxArgs a{};
   int ld = 0;
   long pass = 0;
