@@ -211,81 +211,22 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
   BwdSmem<HD>& s = *reinterpret_cast<BwdSmem<HD>*>(smem_raw);
   const int seq = blockIdx.x / a.heads, h = blockIdx.x % a.heads;
   const int l = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (wave < 3) {
-    __bf16* const rm[3] = {s.q, s.k, s.v};
-    __bf16* const tr[3] = {s.qt, s.kt, nullptr};
-    load_qkv<HD>(a, seq, h, rm, tr, wave);  // wave 0: q, q^T; 1: k, k^T; 2: v
-  } else if (a.dx1) {
-    // wave 3: this head's dO = dX1 rows . Wo^T[head features] (64 x HD, K = D) on the matrix cores -- the output
-    // projection's input-gradient GEMM, fused -- into the dO / dO^T images, then D = rowsum(dO o O)
-    constexpr int RLD = HD + 8;
-    const size_t seqrow = (size_t)seq * a.T;
-    auto put_dO = [&](int tt, const f32x4* acc) {
+  const size_t seqrow0 = (size_t)seq * a.T;
+  auto put_dO = [&](int tt, const f32x4* acc) {
 #pragma unroll
-      for (int dj = 0; dj < HD / 16; ++dj) {
-        f32x4 rb;  // rounded as the unfused chain's bf16 dO tensor
+    for (int dj = 0; dj < HD / 16; ++dj) {
+      f32x4 rb;  // rounded as the unfused chain's bf16 dO tensor
 #pragma unroll
-        for (int r = 0; r < 4; ++r) rb[r] = (float)(__bf16)acc[dj][r];
-        put_rows(s.dO, RLD, 16 * tt, 16 * dj, rb);
-        put_cols(s.dOt, PLD, 16 * tt, 16 * dj, rb);
-      }
-    };
-    if (a.D <= 4 * 32) {
-      // D <= 128 (the transformer: 4 heads of 32): this head's W_o^T fragments once, in registers, and each token
-      // tile's dX1 row pieces (one per k-step) issued together, the next tile's while this one's MFMAs run -- the
-      // one-load-per-k-step chain of this single wave was the attention backward's critical path at B >= 8
-      bf16x8 wf[4][HD / 16];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-        for (int dj = 0; dj < HD / 16; ++dj)
-          wf[kk][dj] = 32 * kk < a.D ? fm_frag(a.wot, a.D, h * HD + 16 * dj, 32 * kk, l) : bf16x8{};
-      bf16x8 af[4];
-      auto fetch = [&](int tt) {
-        const int t = 16 * tt + (l & 15);
-        const bool ok = tt < TP / 16 && t < a.T;
-        const __bf16* arow = a.dx1 + (seqrow + (ok ? t : 0)) * a.D + 8 * (l >> 4);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          af[kk] = ok && 32 * kk < a.D ? *reinterpret_cast<const bf16x8*>(arow + 32 * kk) : bf16x8{};
-      };
-      fetch(0);
-#pragma unroll 1
-      for (int tt = 0; tt < TP / 16; ++tt) {
-        const bf16x8 cur[4] = {af[0], af[1], af[2], af[3]};
-        fetch(tt + 1);
-        f32x4 acc[HD / 16];
-#pragma unroll
-        for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-          for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = mfma16x16x32(cur[kk], wf[kk][dj], acc[dj]);
-        put_dO(tt, acc);
-      }
-    } else {
-#pragma unroll 1
-      for (int tt = 0; tt < TP / 16; ++tt) {
-        f32x4 acc[HD / 16];
-#pragma unroll
-        for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int t = 16 * tt + (l & 15);
-        const bool ok = t < a.T;
-        const __bf16* arow = a.dx1 + (seqrow + (ok ? t : 0)) * a.D + 8 * (l >> 4);
-#pragma unroll 1
-        for (int k0 = 0; k0 < a.D; k0 += 32) {
-          bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + k0);
-          if (!ok) af = bf16x8{};
-#pragma unroll
-          for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = mfma16x16x32(af, fm_frag(a.wot, a.D, h * HD + 16 * dj, k0, l), acc[dj]);
-        }
-        put_dO(tt, acc);
-      }
+      for (int r = 0; r < 4; ++r) rb[r] = (float)(__bf16)acc[dj][r];
+      put_rows(s.dO, RLD, 16 * tt, 16 * dj, rb);
+      put_cols(s.dOt, PLD, 16 * tt, 16 * dj, rb);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dO rows are in LDS for its own lanes
+  };
+  // wave 3 (after dO is in LDS): D = rowsum(dO o O), token t = lane
+  auto dO_rowsum = [&]() {
     const int t = l;
     const bool ok = t < a.T;
-    const __bf16* osrc = a.out + (seqrow + (ok ? t : 0)) * a.D + h * HD;
+    const __bf16* osrc = a.out + (seqrow0 + (ok ? t : 0)) * a.D + h * HD;
     float dsum = 0.f;
 #pragma unroll
     for (int c = 0; c < HD; c += 8) {
@@ -295,7 +236,63 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(AttnArgs a) {
       for (int j = 0; j < 8; ++j) dsum += ok ? (float)dv[j] * (float)ov[j] : 0.f;
     }
     s.rowv[t] = dsum;
-  } else {
+  };
+  if (wave < 3) {
+    __bf16* const rm[3] = {s.q, s.k, s.v};
+    __bf16* const tr[3] = {s.qt, s.kt, nullptr};
+    load_qkv<HD>(a, seq, h, rm, tr, wave);  // wave 0: q, q^T; 1: k, k^T; 2: v
+  }
+  if (a.dx1 && a.D <= 4 * 32) {
+    // this head's dO = dX1 rows . Wo^T[head features] (64 x HD, K = D <= 128: the transformer's 4 heads of 32) on
+    // the matrix cores -- the output projection's input-gradient GEMM, fused: every wave one 16-token tile, its W_o^T
+    // fragments and dX1 row pieces issued together (one wave doing all four tiles, one load round trip per k-step, was
+    // the kernel's critical path at B >= 8), then D = rowsum(dO o O) after a barrier
+    {
+      const int tt = wave;
+      const int t = 16 * tt + (l & 15);
+      const bool ok = t < a.T;
+      const __bf16* arow = a.dx1 + (seqrow0 + (ok ? t : 0)) * a.D + 8 * (l >> 4);
+      bf16x8 wf[4][HD / 16], af[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        af[kk] = ok && 32 * kk < a.D ? *reinterpret_cast<const bf16x8*>(arow + 32 * kk) : bf16x8{};
+#pragma unroll
+        for (int dj = 0; dj < HD / 16; ++dj)
+          wf[kk][dj] = 32 * kk < a.D ? fm_frag(a.wot, a.D, h * HD + 16 * dj, 32 * kk, l) : bf16x8{};
+      }
+      f32x4 acc[HD / 16];
+#pragma unroll
+      for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+        for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = mfma16x16x32(af[kk], wf[kk][dj], acc[dj]);
+      put_dO(tt, acc);
+    }
+    __syncthreads();  // dO complete
+    if (wave == 3) dO_rowsum();
+  } else if (wave == 3 && a.dx1) {
+    // wider D: wave 3 alone, one k-step at a time
+#pragma unroll 1
+    for (int tt = 0; tt < TP / 16; ++tt) {
+      f32x4 acc[HD / 16];
+#pragma unroll
+      for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int t = 16 * tt + (l & 15);
+      const bool ok = t < a.T;
+      const __bf16* arow = a.dx1 + (seqrow0 + (ok ? t : 0)) * a.D + 8 * (l >> 4);
+#pragma unroll 1
+      for (int k0 = 0; k0 < a.D; k0 += 32) {
+        bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + k0);
+        if (!ok) af = bf16x8{};
+#pragma unroll
+        for (int dj = 0; dj < HD / 16; ++dj) acc[dj] = mfma16x16x32(af, fm_frag(a.wot, a.D, h * HD + 16 * dj, k0, l), acc[dj]);
+      }
+      put_dO(tt, acc);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's dO rows are in LDS for its own lanes
+    dO_rowsum();
+  } else if (wave == 3) {
     // wave 3: dO rows (row-major + transposed) and D = rowsum(dO o O)
     const int t = l;
     const bool ok = t < a.T;
