@@ -1320,6 +1320,10 @@ constexpr int GROUP_BIG_K = 16384;
 #ifndef GROUP_BIG_TILES  // (diagnostic A/B builds: 0 keeps 64 x 64 tiles at any K)
 #define GROUP_BIG_TILES 1
 #endif
+#ifndef GROUP_BIG_WGS  // workgroups a deep-K launch is sized to (2 resident per CU at 207 VGPRs; 256 / 1024 slower,
+                       // profiles/r6_groupwgs/)
+#define GROUP_BIG_WGS 512
+#endif
 
 void launch_group(int kind, int first, int count, hipStream_t st) {
   GroupTable t{};
@@ -1333,7 +1337,8 @@ void launch_group(int kind, int first, int count, hipStream_t st) {
     const GemmArgs& g = gq.g[kind][q];
     work += (long)((g.M + TB - 1) / TB) * ((g.N + TB - 1) / TB) * g.K;
   }
-  long chunk = (work + GROUP_WGS - 1) / GROUP_WGS;
+  const long wgs = big ? GROUP_BIG_WGS : GROUP_WGS;
+  long chunk = (work + wgs - 1) / wgs;
   chunk = std::max(256L, (chunk + 127) / 128 * 128);
   int blocks = 0;
   for (int q = 0; q < count; ++q) {
