@@ -46,6 +46,7 @@ struct AttnFwdArgs {
   __bf16 *xn, *qkv, *o;
   float *r1, *lse, *x1;
   int split;  // 1: two workgroups per sequence, one per 32-query half (each recomputes the shared xn / k / v)
+  int nfull;  // split == 0: workgroups below nfull own a whole sequence, the rest split the last sequences in halves
   // first block: the embedding x = in We^T + be computed here from the fp32 input tokens instead of read (in null:
   // x is read); x is then written to x_out (own rows) for the backward
   const float* in;   // [rows_in][F] (rows past rows_in: zero tokens, the padded sequences)
@@ -68,9 +69,10 @@ __global__ __launch_bounds__(ATH) void tr_attn_fwd_kernel(AttnFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   AttnFwdSmem& s = *reinterpret_cast<AttnFwdSmem*>(smem_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool split = a.split != 0;
-  const int seq = split ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, T = a.T;
-  const int qh = split ? (int)(blockIdx.x & 1) : 0;  // query half (split): rows 32 qh .. 32 qh + 31 are this WG's
+  const int b = blockIdx.x, bs = a.split ? b : b - a.nfull;  // bs >= 0: a split workgroup, its index among them
+  const bool split = bs >= 0;
+  const int seq = split ? (a.split ? 0 : a.nfull) + (bs >> 1) : b, T = a.T;
+  const int qh = split ? (bs & 1) : 0;  // query half (split): rows 32 qh .. 32 qh + 31 are this WG's
   auto own = [&](int r) { return !split || (r >> 5) == qh; };
   const size_t grow0 = (size_t)seq * T;
   const int rq = 4 * (lane >> 4), col = lane & 15;
@@ -513,7 +515,19 @@ extern "C" int mta_tr_attn_fwd(int nseq, int T, int d, int heads, const float* x
   // per CU): transformer B=8 (800 sequences) ran 1,600 split workgroups at ~100 us per launch
   // (profiles/r6_transformer/tr_b8_kernel_stats.csv)
   a.split = (T > 32 && nseq <= 128) ? 1 : 0;
-  tr_attn_fwd_kernel<<<nseq * (a.split ? 2 : 1), ATH, sizeof(AttnFwdSmem), st>>>(a);
+  // Above one wave of workgroups the last, partial wave splits its sequences in halves (the workgroups are
+  // dispatched in index order, so those run last): transformer B=8, 832 sequences on 256 CUs, ends on 128 half
+  // workgroups instead of 64 whole ones
+  static const int n_cu = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  const int rem = nseq % n_cu;
+  a.nfull = (!a.split && T > 32 && nseq > n_cu && 2 * rem <= n_cu) ? nseq - rem : nseq;
+  const int grid = a.split ? 2 * nseq : a.nfull + 2 * (nseq - a.nfull);
+  tr_attn_fwd_kernel<<<grid, ATH, sizeof(AttnFwdSmem), st>>>(a);
   return 0;
 }
 
